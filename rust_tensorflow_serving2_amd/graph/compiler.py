@@ -1,0 +1,227 @@
+"""GraphDef -> executable Program.
+
+Pipeline (per signature, per feed/fetch set):
+
+1. **bind variables** — ``VariableV2`` / ``VarHandleOp`` nodes become constants
+   loaded from the TensorBundle (key = node name / ``shared_name``);
+2. **prune** to the sub-graph that the fetches need, with fed tensors as leaves
+   (feeding an interior tensor overrides its producer, as in TF);
+3. **constant-fold** everything that does not depend on a feed;
+4. **fusion passes** (``graph/fused.py``): Conv+BN(+residual)(+ReLU) folding,
+   MatMul+BiasAdd(+act), LayerNorm/GELU/attention pattern matching, softmax+argmax
+   — rewritten into fused ops that run as hand-written HIP kernels on MI355X;
+5. **placement** — weights to the device (bf16 for fused MFMA ops), shape
+   arithmetic stays on the host so a Program can be captured in a HIP graph;
+6. **linearise** into a list of steps over value slots.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Set, Tuple
+
+import numpy as np
+import torch
+
+from ..utils import tensors as T
+from . import ops as O
+from .ir import Graph, Node, fmt_ref, parse_ref
+
+NON_FOLDABLE = {"Placeholder", "PlaceholderWithDefault", "ParseExample", "ParseExampleV2", "NoOp",
+                "RandomUniform", "RandomStandardNormal", "TruncatedNormal", "VariableV2",
+                "VarHandleOp", "SaveV2", "RestoreV2", "Assign", "AssignVariableOp"}
+MAX_FOLD_ELEMS = 1 << 26
+
+
+class CompileError(ValueError):
+    pass
+
+
+def const_value(node: Node):
+    """Decode a Const node's value into a torch tensor (or numpy object array)."""
+    v = node.attrs.get("value")
+    dt = node.attrs.get("dtype", T.DT_FLOAT)
+    if isinstance(v, np.ndarray) and v.dtype == object:
+        return v
+    a = np.asarray(v)
+    if dt == T.DT_BFLOAT16:
+        return torch.from_numpy(a.astype(np.uint16).view(np.int16).copy()).view(torch.bfloat16)
+    if dt == T.DT_STRING:
+        return a.astype(object)
+    t = torch.from_numpy(np.array(a, copy=True))
+    want = O.DT_TO_TORCH.get(dt)
+    if want is not None and t.dtype != want:
+        t = t.to(want)
+    return t
+
+
+def array_to_value(a: np.ndarray, dt: int):
+    if dt == T.DT_BFLOAT16:
+        return torch.from_numpy(np.array(a, dtype=np.uint16).view(np.int16)).view(torch.bfloat16)
+    if dt == T.DT_STRING:
+        return np.asarray(a, dtype=object)
+    return torch.from_numpy(np.array(a, copy=True))
+
+
+def bind_variables(g: Graph, bundle) -> None:
+    for node in list(g.nodes.values()):
+        if node.op in ("VariableV2", "Variable", "VarHandleOp"):
+            key = node.name
+            if node.op == "VarHandleOp":
+                sn = node.sattr("shared_name")
+                if sn and bundle is not None and sn in bundle:
+                    key = sn
+            if bundle is None or key not in bundle:
+                continue  # left unbound: error only if it is actually needed
+            dt = bundle.dtype(key)
+            node.value = [array_to_value(bundle[key], dt)]
+            node.op = "Const"
+            node.attrs = {"dtype": dt, "_variable": key}
+
+
+class Program:
+    """A linearised, device-placed computation (feeds -> fetches)."""
+
+    def __init__(self, steps, n_slots, feed_slots, fetch_slots, const_slots, device, feed_dtypes,
+                 graph: Graph, order: List[str]):
+        self.steps = steps
+        self.n_slots = n_slots
+        self.feed_slots = feed_slots
+        self.fetch_slots = fetch_slots
+        self.const_slots = const_slots
+        self.device = device
+        self.feed_dtypes = feed_dtypes
+        self.graph = graph
+        self.order = order
+        self._ctx = O.Ctx(device)
+
+    def run(self, feeds: Sequence) -> List:
+        vals: List = [None] * self.n_slots
+        for slot, v in self.const_slots:
+            vals[slot] = v
+        for slot, v in zip(self.feed_slots, feeds):
+            vals[slot] = v
+        ctx = self._ctx
+        for fn, node, in_slots, out_slots in self.steps:
+            try:
+                outs = fn(ctx, node, [vals[s] for s in in_slots])
+            except (O.OpError, O.Unsupported):
+                raise
+            except (RuntimeError, ValueError, IndexError, TypeError) as e:
+                raise O.OpError(f"{node.op} node '{node.name}': {e}") from e
+            for s, o in zip(out_slots, outs):
+                if s >= 0:
+                    vals[s] = o
+        return [vals[s] for s in self.fetch_slots]
+
+    def op_histogram(self) -> Dict[str, int]:
+        h: Dict[str, int] = {}
+        for _fn, node, _i, _o in self.steps:
+            h[node.op] = h.get(node.op, 0) + 1
+        return h
+
+
+def _fold(g: Graph, order: List[str], fed: Set[str]) -> None:
+    ctx = O.Ctx(torch.device("cpu"))
+    for name in order:
+        node = g.nodes[name]
+        if node.op == "Const":
+            if node.value is None:
+                node.value = [const_value(node)]
+            continue
+        if name in fed or node.op in NON_FOLDABLE or node.op not in O.OPS:
+            continue
+        if node.ctrl and any(g.nodes[c].op != "Const" for c in node.ctrl):
+            continue
+        if not node.inputs:
+            continue
+        srcs = [g.nodes[s] for s, _ in node.inputs]
+        if not all(s.op == "Const" and s.value is not None and i < len(s.value)
+                   for s, (_, i) in zip(srcs, node.inputs)):
+            continue
+        ins = [s.value[i] for s, (_, i) in zip(srcs, node.inputs)]
+        try:
+            outs = O.OPS[node.op](ctx, node, ins)
+        except Exception:
+            continue  # leave it for run time (and run-time error reporting)
+        if any(isinstance(o, torch.Tensor) and o.numel() > MAX_FOLD_ELEMS for o in outs):
+            continue
+        node.value = list(outs)
+        node.op = "Const"
+        node.inputs = []
+        node.ctrl = []
+
+
+def compile_program(graph: Graph, feeds: Sequence[str], fetches: Sequence[str],
+                    device: torch.device = torch.device("cpu"), passes: Sequence = (),
+                    pass_options: Optional[dict] = None) -> Program:
+    feed_refs = [parse_ref(f) for f in feeds]
+    fetch_refs = [parse_ref(f) for f in fetches]
+    for n, _ in feed_refs + fetch_refs:
+        if n not in graph.nodes:
+            raise CompileError(f"tensor {n!r} not found in graph")
+    fed_nodes = {n for n, _ in feed_refs}
+    # a fed node's other outputs are not computable unless all outputs are fed
+    order = graph.topo([n for n, _ in fetch_refs], stop=fed_nodes)
+    _fold(graph, order, fed_nodes)
+    order = graph.topo([n for n, _ in fetch_refs], stop=fed_nodes)
+    for p in passes:
+        p(graph, order, fed_nodes, fetch_refs, device, pass_options or {})
+        order = graph.topo([n for n, _ in fetch_refs], stop=fed_nodes)
+
+    slot_of: Dict[Tuple[str, int], int] = {}
+
+    def slot(ref):
+        if ref not in slot_of:
+            slot_of[ref] = len(slot_of)
+        return slot_of[ref]
+
+    feed_slots = [slot(r) for r in feed_refs]
+    feed_dtypes = []
+    for n, _ in feed_refs:
+        node = graph.nodes[n]
+        feed_dtypes.append(node.attrs.get("dtype") if node.op == "Placeholder" else None)
+    needed: Dict[str, Set[int]] = {}
+    for name in order:
+        for s, i in graph.nodes[name].inputs:
+            needed.setdefault(s, set()).add(i)
+    for n, i in fetch_refs:
+        needed.setdefault(n, set()).add(i)
+
+    const_slots = []
+    steps = []
+    for name in order:
+        node = graph.nodes[name]
+        if name in fed_nodes:
+            for i in needed.get(name, ()):
+                if (name, i) not in slot_of:
+                    raise CompileError(f"output {i} of fed node {name!r} is needed but not fed")
+            continue
+        if node.op == "Const":
+            if node.value is None:
+                node.value = [const_value(node)]
+            for i in needed.get(name, ()):
+                v = node.value[i]
+                if isinstance(v, torch.Tensor) and device.type != "cpu" and _device_resident(v):
+                    v = v.to(device)
+                    node.value[i] = v
+                const_slots.append((slot((name, i)), v))
+            continue
+        if node.op in ("VariableV2", "Variable", "VarHandleOp"):
+            raise CompileError(f"variable {name!r} has no value in the checkpoint")
+        fn = O.OPS.get(node.op)
+        if fn is None:
+            raise CompileError(f"op {node.op!r} (node {name!r}) is not supported")
+        in_slots = [slot(r) for r in node.inputs]
+        outs = needed.get(name, set())
+        n_out = (max(outs) + 1) if outs else 0
+        out_slots = [slot((name, i)) if i in outs else -1 for i in range(n_out)]
+        steps.append((fn, node, in_slots, out_slots))
+    fetch_slots = [slot(r) for r in fetch_refs]
+    return Program(steps, len(slot_of), feed_slots, fetch_slots, const_slots, device, feed_dtypes,
+                   graph, order)
+
+
+def _device_resident(v: torch.Tensor) -> bool:
+    """Shape-like int tensors stay on the host; everything else goes to the device."""
+    if v.is_floating_point():
+        return True
+    return v.numel() > 64

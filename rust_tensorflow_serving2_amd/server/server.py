@@ -1,0 +1,118 @@
+"""Model server assembly: manager + core + transports (+ batching, metrics, logs).
+
+Equivalent of the stock ``tensorflow/serving`` container the reference starts
+(``serving/rundocker.sh:15``: gRPC 8500, REST 8501, ``MODEL_NAME=resnet``,
+``/models/resnet``), rebuilt MI355X-first: servables run on the local GPU with
+fused HIP kernels; one server process per GPU (``parallel/``) shares the
+listening port via SO_REUSEPORT.
+"""
+from __future__ import annotations
+
+import logging
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+from ..schema import serving
+from . import errors as E
+from .core import ServingCore
+from .manager import ModelManager
+from .servable import Servable, ServableOptions
+
+log = logging.getLogger("tfserve.server")
+
+
+@dataclass
+class ServerOptions:
+    port: int = 8500
+    rest_api_port: int = 0
+    host: str = "0.0.0.0"
+    model_name: str = ""
+    model_base_path: str = ""
+    model_config: Optional[object] = None          # serving.ModelServerConfig
+    device: str = "cpu"
+    enable_batching: bool = False
+    batching_parameters: Optional[object] = None   # serving.BatchingParameters
+    transport: str = "grpc"                        # "grpc" | "native"
+    file_system_poll_wait_seconds: float = 1.0
+    grpc_workers: int = 64
+    servable: ServableOptions = field(default_factory=ServableOptions)
+    monitoring: bool = True
+    weight_source: Optional[object] = None         # parallel.WeightSource for multi-rank loads
+
+
+class ModelServer:
+    def __init__(self, opts: ServerOptions):
+        self.opts = opts
+        opts.servable.device = opts.device
+        self.metrics = None
+        if opts.monitoring:
+            from ..utils.metrics import Metrics
+            self.metrics = Metrics()
+        self.batcher = None
+        if opts.enable_batching:
+            from .batching import BatchingSession
+            self.batcher = BatchingSession(opts.batching_parameters, metrics=self.metrics)
+        from ..utils.request_log import RequestLoggerRegistry
+        self.request_logs = RequestLoggerRegistry()
+        self.manager = ModelManager(self._load, poll_wait_seconds=opts.file_system_poll_wait_seconds)
+        self.core = ServingCore(self.manager, self.batcher, self.request_logs, self.metrics)
+        self.transports = []
+
+    def _load(self, name: str, version: int, path: str, cfg) -> Servable:
+        so = self.opts.servable
+        if self.batcher is not None:
+            so.max_batch_size = self.batcher.max_batch_size
+            so.allowed_batch_sizes = tuple(self.batcher.allowed_batch_sizes)
+        bundle = None
+        if self.opts.weight_source is not None:
+            bundle = self.opts.weight_source.load(name, version, path)
+        s = Servable(name, version, path, so, bundle)
+        s.warmup()
+        if cfg is not None and cfg.HasField("logging_config"):
+            self.request_logs.configure(name, cfg.logging_config)
+        return s
+
+    def initial_config(self):
+        o = self.opts
+        if o.model_config is not None:
+            return o.model_config
+        cfg = serving.ModelServerConfig()
+        if o.model_base_path:
+            mc = cfg.model_config_list.config.add()
+            mc.name = o.model_name or "default"
+            mc.base_path = o.model_base_path
+            mc.model_platform = "tensorflow"
+        return cfg
+
+    def start(self, wait_for_models: bool = True):
+        cfg = self.initial_config()
+        if cfg.WhichOneof("config"):
+            errs = self.manager.apply_config(cfg, wait=wait_for_models)
+            for e in errs:
+                log.error("model load error: %s", e.message)
+        self.manager.start_polling()
+        if self.opts.transport == "native":
+            from .native_transport import NativeTransport
+            t = NativeTransport(self.core, self.opts.port, self.opts.host, batcher=self.batcher)
+        else:
+            from .grpc_transport import GrpcTransport
+            t = GrpcTransport(self.core, self.opts.port, self.opts.host, self.opts.grpc_workers)
+        self.transports.append(t.start())
+        self.port = t.port
+        if self.opts.rest_api_port:
+            from .rest import RestTransport
+            r = RestTransport(self.core, self.opts.rest_api_port, self.opts.host, self.metrics)
+            self.transports.append(r.start())
+            self.rest_port = r.port
+        log.info("serving on port %d", self.port)
+        return self
+
+    def stop(self):
+        for t in self.transports:
+            t.stop()
+        self.transports.clear()
+        if self.batcher is not None:
+            self.batcher.stop()
+        self.manager.stop()
+        self.request_logs.close()
