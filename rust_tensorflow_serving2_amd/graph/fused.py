@@ -1,0 +1,484 @@
+"""Fusion passes: rewrite TF op chains into fused ops backed by gfx950 kernels.
+
+Patterns (matched on the constant-folded IR, only when every intermediate has
+a single consumer and is not fetched):
+
+* ``[Pad] -> Conv2D -> [BiasAdd] -> [FusedBatchNorm*] -> [Add(residual)] -> [Relu]``
+  => ``_FusedConv2D``: BN folded into the weights at load time (w' = w*gamma/
+  sqrt(var+eps), b' = beta - mean*scale), spatial Pad absorbed into the conv's
+  explicit padding, residual add + ReLU in the MFMA kernel's epilogue.  A conv
+  whose input has C % 8 != 0 (the RGB stem) reads the fp32 request tensor
+  directly (ingest cast fused into the operand loads).
+* ``MatMul -> [BiasAdd] -> [Add(residual)] -> [Relu|Tanh|GELU]`` => ``_FusedMatMul``
+  (fp32 output when it feeds a Softmax/ArgMax head or is fetched).
+* ``Mean(NHWC, axes=[1,2])`` => ``_GlobalAvgPool``;  ``MaxPool`` => ``_MaxPool``.
+* ``Softmax(x)`` + ``ArgMax(x, -1)`` on the same logits => ``_SoftmaxArgMax``.
+* BERT: decomposed LayerNorm => ``_LayerNorm``; tanh/erf GELU subgraphs => act
+  of the producing ``_FusedMatMul``; Q/K/V projections + attention core =>
+  ``_FusedQKV`` + ``_Attention`` (see ``bert_passes``).
+
+On a CUDA/HIP device the fused ops launch the ``_hip`` kernels (bf16 operands,
+fp32 accumulate); on the CPU they run an fp32 torch reference of the *same*
+folded parameters, which is how the passes are validated without a GPU.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Set, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..utils import tensors as T
+from . import ops as O
+from .ir import Graph, Node
+
+BF16 = torch.bfloat16
+
+
+# ------------------------------------------------------------------ helpers
+def _const(g: Graph, ref) -> Optional[torch.Tensor]:
+    n = g.nodes.get(ref[0])
+    if n is None or n.op != "Const" or n.value is None:
+        return None
+    v = n.value[ref[1]] if ref[1] < len(n.value) else None
+    return v if isinstance(v, torch.Tensor) else None
+
+
+class _Ctx:
+    def __init__(self, g: Graph, order: List[str], fed: Set[str], fetch_refs, device, opts):
+        self.g = g
+        self.order = order
+        self.fed = fed
+        self.fetch_nodes = {n for n, _ in fetch_refs}
+        self.fetch_refs = set(fetch_refs)
+        self.device = device
+        self.opts = opts
+        self.use_hip = device.type == "cuda"
+        self.cons = g.consumers()
+
+    def only_consumer(self, name: str, idx: int = 0) -> Optional[Node]:
+        """The unique consumer of output ``idx`` of ``name`` (and no other output used)."""
+        if name in self.fetch_nodes:
+            return None
+        cs = self.cons.get(name, [])
+        if len(cs) != 1:
+            return None
+        cname, _pos, oidx = cs[0]
+        if oidx != idx:
+            return None
+        return self.g.nodes[cname]
+
+    def refresh(self):
+        self.cons = self.g.consumers()
+
+
+def _merge_ctrl(nodes: Sequence[Node]) -> List[str]:
+    out: List[str] = []
+    names = {n.name for n in nodes}
+    for n in nodes:
+        for c in n.ctrl:
+            if c not in out and c not in names:
+                out.append(c)
+    return out
+
+
+def _finalize(g: Graph, chain: List[Node], op: str, inputs, attrs) -> Node:
+    last = chain[-1]
+    ctrl = _merge_ctrl(chain)
+    for n in chain[:-1]:
+        del g.nodes[n.name]
+    last.op = op
+    last.inputs = list(inputs)
+    last.ctrl = ctrl
+    last.attrs = attrs
+    last.value = None
+    return last
+
+
+def _pad_k(w_nk: torch.Tensor, mult: int = 64) -> torch.Tensor:
+    n, k = w_nk.shape
+    kp = -(-k // mult) * mult
+    if kp != k:
+        w_nk = torch.cat([w_nk, torch.zeros(n, kp - k, dtype=w_nk.dtype)], dim=1)
+    return w_nk
+
+
+def _to_bf16(x: torch.Tensor) -> torch.Tensor:
+    if x.dtype == BF16:
+        return x
+    if x.dtype == torch.float32 and x.is_cuda and x.is_contiguous():
+        from ..ops import hip
+        return hip().cast_bf16(x)
+    return x.to(BF16).contiguous()
+
+
+# ------------------------------------------------------------------ fused op impls
+class FusedConv:
+    """Conv2D(+folded BN/bias)(+residual)(+act).  Weights: HWIO fp32 (reference)
+    and [Cout][Kpad] bf16 (kernel)."""
+
+    def __init__(self, w_hwio: torch.Tensor, bias: torch.Tensor, strides, padding: str, pads, act: str,
+                 device: torch.device, use_hip: bool, name: str):
+        self.kh, self.kw, self.cin, self.cout = w_hwio.shape
+        self.sh, self.sw = strides
+        self.padding = padding          # "SAME" | "VALID" | "EXPLICIT"
+        self.pads = pads                # (pt, pb, pl, pr) for EXPLICIT
+        self.act = act
+        self.use_hip = use_hip
+        self.name = name
+        self.device = device
+        if use_hip:
+            k = self.kh * self.kw * self.cin
+            w_nk = w_hwio.permute(3, 0, 1, 2).reshape(self.cout, k)
+            self.w = _pad_k(w_nk).to(BF16).contiguous().to(device)
+            self.b = bias.float().contiguous().to(device)
+        else:
+            self.w_ref = w_hwio.float().to(device)
+            self.b_ref = bias.float().to(device)
+
+    def pads_for(self, h, w):
+        if self.padding == "SAME":
+            return O.tf_same_pads(h, self.kh, self.sh) + O.tf_same_pads(w, self.kw, self.sw)
+        if self.padding == "EXPLICIT":
+            return tuple(self.pads)
+        return (0, 0, 0, 0)
+
+    def __call__(self, ctx, node, ins):
+        x = O.to_torch(ins[0])
+        res = O.to_torch(ins[1]) if len(ins) > 1 else None
+        pt, pb, pl, pr = self.pads_for(x.shape[1], x.shape[2])
+        if not self.use_hip:
+            y = F.conv2d(F.pad(x.float().permute(0, 3, 1, 2), [pl, pr, pt, pb]),
+                         self.w_ref.permute(3, 2, 0, 1), stride=(self.sh, self.sw))
+            y = y.permute(0, 2, 3, 1) + self.b_ref
+            if res is not None:
+                y = y + res.float()
+            return [_ref_act(y, self.act).contiguous()]
+        from ..ops import ACT, hip, tuned_config
+        if self.cin % 8 != 0:
+            x = x.float().contiguous()            # stem: fp32 operand gather + cast in-kernel
+        else:
+            x = _to_bf16(x).contiguous()
+        if res is not None:
+            res = _to_bf16(res).contiguous()
+        H = hip()
+        n, h, w, _ = x.shape
+        ho = (h + pt + pb - self.kh) // self.sh + 1
+        wo = (w + pl + pr - self.kw) // self.sw + 1
+        M = n * ho * wo
+        args = (x, self.w, self.b, res, self.kh, self.kw, self.sh, self.sw, pt, pb, pl, pr, ACT[self.act])
+        out = torch.empty((n, ho, wo, self.cout), device=x.device, dtype=BF16)
+        key = ("conv", tuple(x.shape), x.dtype, self.cout, self.kh, self.kw, self.sh, res is not None)
+        cfg = tuned_config(key, M, self.cout, lambda c: H.conv2d(*args, cfg=c, out=out))
+        return [H.conv2d(*args, cfg=cfg, out=out)]
+
+
+class FusedMatMul:
+    def __init__(self, w_kn: torch.Tensor, bias: Optional[torch.Tensor], act: str, out_f32: bool,
+                 device, use_hip: bool, name: str):
+        self.k, self.n = w_kn.shape
+        self.act = act
+        self.out_f32 = out_f32
+        self.use_hip = use_hip and self.k % 8 == 0
+        self.name = name
+        b = bias if bias is not None else torch.zeros(self.n)
+        if self.use_hip:
+            self.w = _pad_k(w_kn.t().contiguous(), 8).to(BF16).contiguous().to(device)
+            self.b = b.float().contiguous().to(device)
+        else:
+            self.w_ref = w_kn.float().to(device)
+            self.b_ref = b.float().to(device)
+
+    def __call__(self, ctx, node, ins):
+        x = O.to_torch(ins[0])
+        res = O.to_torch(ins[1]) if len(ins) > 1 else None
+        if not self.use_hip:
+            y = x.float() @ self.w_ref.to(x.device) + self.b_ref.to(x.device)
+            if res is not None:
+                y = y + res.float()
+            y = _ref_act(y, self.act)
+            return [y if self.out_f32 or not x.is_cuda else y.to(BF16)]
+        from ..ops import ACT, hip, tuned_config
+        H = hip()
+        x = _to_bf16(x).contiguous()
+        if res is not None:
+            res = _to_bf16(res).contiguous()
+        M = x.numel() // self.k
+        shape = list(x.shape[:-1]) + [self.n]
+        out = torch.empty(shape, device=x.device, dtype=torch.float32 if self.out_f32 else BF16)
+        key = ("mm", M, self.n, self.k, res is not None, self.out_f32)
+        run = lambda c: H.linear(x, self.w, self.b, res, ACT[self.act], c, self.out_f32, 1.0, out)  # noqa: E731
+        cfg = tuned_config(key, M, self.n, run)
+        return [run(cfg)]
+
+
+def _ref_act(y, act):
+    if act == "relu":
+        return torch.relu(y)
+    if act == "tanh":
+        return torch.tanh(y)
+    if act == "gelu_tanh":
+        return F.gelu(y, approximate="tanh")
+    if act == "gelu_erf":
+        return F.gelu(y)
+    return y
+
+
+def _impl_op(ctx, node, ins):
+    return node.attrs["_impl"](ctx, node, ins)
+
+
+for _op in ("_FusedConv2D", "_FusedMatMul", "_GlobalAvgPool", "_MaxPool", "_SoftmaxArgMax", "_LayerNorm",
+            "_FusedQKV", "_Attention", "_EmbedLN"):
+    O.OPS[_op] = _impl_op
+
+
+class GlobalAvgPool:
+    def __init__(self, keep_dims: bool, use_hip: bool):
+        self.keep = keep_dims
+        self.use_hip = use_hip
+
+    def __call__(self, ctx, node, ins):
+        x = O.to_torch(ins[0])
+        if self.use_hip and x.is_cuda and x.shape[-1] % 8 == 0:
+            from ..ops import hip
+            y = hip().global_avgpool(_to_bf16(x).contiguous())
+        else:
+            y = x.float().mean(dim=(1, 2))
+        return [y.reshape(y.shape[0], 1, 1, -1) if self.keep else y]
+
+
+class MaxPool:
+    def __init__(self, ksize, strides, padding, use_hip):
+        self.kh, self.kw = ksize
+        self.sh, self.sw = strides
+        self.padding = padding
+        self.use_hip = use_hip
+
+    def __call__(self, ctx, node, ins):
+        x = O.to_torch(ins[0])
+        h, w = x.shape[1], x.shape[2]
+        if self.padding == "SAME":
+            (pt, pb), (pl, pr) = O.tf_same_pads(h, self.kh, self.sh), O.tf_same_pads(w, self.kw, self.sw)
+        else:
+            pt = pb = pl = pr = 0
+        if self.use_hip and x.is_cuda and x.shape[-1] % 8 == 0:
+            from ..ops import hip
+            return [hip().maxpool(_to_bf16(x).contiguous(), self.kh, self.kw, self.sh, self.sw, pt, pb, pl, pr)]
+        xc = F.pad(x.permute(0, 3, 1, 2), [pl, pr, pt, pb], value=float("-inf"))
+        return [F.max_pool2d(xc, (self.kh, self.kw), (self.sh, self.sw)).permute(0, 2, 3, 1).contiguous()]
+
+
+class SoftmaxArgMax:
+    def __init__(self, use_hip, classes_dtype):
+        self.use_hip = use_hip
+        self.cdt = classes_dtype
+
+    def __call__(self, ctx, node, ins):
+        x = O.to_torch(ins[0])
+        if self.use_hip and x.is_cuda and x.dim() == 2 and x.dtype in (torch.float32, BF16):
+            from ..ops import hip
+            probs, cls = hip().softmax_argmax(x.contiguous(), True, True)
+        else:
+            probs = torch.softmax(x.float(), dim=-1)
+            cls = torch.argmax(x.float(), dim=-1)
+        return [probs, cls if self.cdt == torch.int64 else cls.to(self.cdt)]
+
+
+# ------------------------------------------------------------------ passes
+def fuse_conv(g, order, fed, fetch_refs, device, opts):
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    for name in order:
+        n = g.nodes.get(name)
+        if n is None or n.op != "Conv2D" or n.sattr("data_format", "NHWC") != "NHWC":
+            continue
+        dil = n.attr("dilations", [1, 1, 1, 1]) or [1, 1, 1, 1]
+        if any(d != 1 for d in dil):
+            continue
+        w = _const(g, n.inputs[1])
+        if w is None or w.dim() != 4:
+            continue
+        x_ref = n.inputs[0]
+        padding = n.sattr("padding", "VALID")
+        pads = (0, 0, 0, 0)
+        chain: List[Node] = []
+        if padding == "EXPLICIT":
+            ep = n.attr("explicit_paddings", [])
+            if ep[0] or ep[1] or ep[6] or ep[7]:
+                continue
+            pads = (ep[2], ep[3], ep[4], ep[5])
+        prod = g.nodes.get(x_ref[0])
+        if (padding == "VALID" and prod is not None and prod.op == "Pad" and x_ref[1] == 0
+                and c.only_consumer(prod.name) is n):
+            pv = _const(g, prod.inputs[1])
+            if pv is not None:
+                p = [int(v) for v in pv.reshape(-1).tolist()]
+                if p[0] == p[1] == p[6] == p[7] == 0 and min(p) >= 0:
+                    chain.append(prod)
+                    x_ref = prod.inputs[0]
+                    padding, pads = "EXPLICIT", (p[2], p[3], p[4], p[5])
+        strides = n.attr("strides", [1, 1, 1, 1])
+        w = w.float()
+        cout = w.shape[3]
+        bias = torch.zeros(cout)
+        chain.append(n)
+        cur = n
+        residual = None
+        act = "none"
+        nxt = c.only_consumer(cur.name)
+        if nxt is not None and nxt.op == "BiasAdd" and nxt.inputs[0] == (cur.name, 0):
+            b = _const(g, nxt.inputs[1])
+            if b is not None and b.numel() == cout:
+                bias = bias + b.float()
+                chain.append(nxt)
+                cur = nxt
+                nxt = c.only_consumer(cur.name)
+        if (nxt is not None and nxt.op in ("FusedBatchNorm", "FusedBatchNormV2", "FusedBatchNormV3")
+                and not nxt.attr("is_training", False) and nxt.sattr("data_format", "NHWC") == "NHWC"
+                and nxt.inputs[0] == (cur.name, 0)):
+            params = [_const(g, r) for r in nxt.inputs[1:5]]
+            outs_used = {i for _c, _p, i in c.cons.get(nxt.name, [])}
+            if all(p is not None for p in params) and outs_used <= {0} and nxt.name not in c.fetch_nodes:
+                gamma, beta, mean, var = (p.float() for p in params)
+                scale = gamma * torch.rsqrt(var + float(nxt.attr("epsilon", 1e-3)))
+                w = w * scale
+                bias = (bias - mean) * scale + beta
+                chain.append(nxt)
+                cur = nxt
+                nxt = c.only_consumer(cur.name)
+        if nxt is not None and nxt.op in ("Add", "AddV2") and len(nxt.inputs) == 2:
+            other = nxt.inputs[1] if nxt.inputs[0] == (cur.name, 0) else nxt.inputs[0]
+            if other != (cur.name, 0) and _const(g, other) is None:
+                residual = other
+                chain.append(nxt)
+                cur = nxt
+                nxt = c.only_consumer(cur.name)
+        if nxt is not None and nxt.op == "Relu":
+            act = "relu"
+            chain.append(nxt)
+            cur = nxt
+        impl = FusedConv(w, bias, (strides[1], strides[2]), padding, pads, act, device, c.use_hip, cur.name)
+        inputs = [x_ref] + ([residual] if residual is not None else [])
+        _finalize(g, chain, "_FusedConv2D", inputs, {"_impl": impl})
+        c.refresh()
+
+
+def _feeds_head(c: _Ctx, name: str, depth: int = 0) -> bool:
+    if name in c.fetch_nodes:
+        return True
+    if depth > 3:
+        return False
+    for cname, _p, _i in c.cons.get(name, []):
+        cn = c.g.nodes[cname]
+        if cn.op in ("Softmax", "ArgMax", "_SoftmaxArgMax", "LogSoftmax", "TopKV2", "Sigmoid"):
+            return True
+        if cn.op in ("Identity", "Squeeze", "Reshape") and _feeds_head(c, cname, depth + 1):
+            return True
+    return False
+
+
+GELU_ACTS = ("gelu_tanh", "gelu_erf")
+
+
+def fuse_matmul(g, order, fed, fetch_refs, device, opts):
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    for name in order:
+        n = g.nodes.get(name)
+        if n is None or n.op != "MatMul" or n.attr("transpose_a", False):
+            continue
+        w = _const(g, n.inputs[1])
+        if w is None or w.dim() != 2:
+            continue
+        w = w.float()
+        if n.attr("transpose_b", False):
+            w = w.t()
+        kdim, ndim = w.shape
+        chain = [n]
+        cur = n
+        bias = None
+        residual = None
+        act = "none"
+        nxt = c.only_consumer(cur.name)
+        if nxt is not None and nxt.op in ("BiasAdd", "Add", "AddV2") and nxt.inputs[0] == (cur.name, 0):
+            b = _const(g, nxt.inputs[1])
+            if b is not None and b.numel() == ndim:
+                bias = b.float().reshape(-1)
+                chain.append(nxt)
+                cur = nxt
+                nxt = c.only_consumer(cur.name)
+        gelu = match_gelu(g, c, cur.name)
+        if gelu is not None:
+            act, gnodes, out_node = gelu
+            chain += gnodes + [out_node]
+            cur = out_node
+        elif nxt is not None and nxt.op in ("Relu", "Tanh"):
+            act = nxt.op.lower()
+            chain.append(nxt)
+            cur = nxt
+        elif nxt is not None and nxt.op in ("Add", "AddV2") and len(nxt.inputs) == 2:
+            other = nxt.inputs[1] if nxt.inputs[0] == (cur.name, 0) else nxt.inputs[0]
+            if other != (cur.name, 0) and _const(g, other) is None:
+                residual = other
+                chain.append(nxt)
+                cur = nxt
+        out_f32 = _feeds_head(c, cur.name)
+        impl = FusedMatMul(w, bias, act, out_f32, device, c.use_hip, cur.name)
+        _finalize(g, chain, "_FusedMatMul", [n.inputs[0]] + ([residual] if residual else []), {"_impl": impl})
+        c.refresh()
+
+
+def match_gelu(g: Graph, c: _Ctx, src: str):
+    """Match GELU applied to ``src`` (exactly-once uses):
+    erf form:  0.5 * x * (1 + erf(x / sqrt(2)))   (any association order)
+    tanh form: 0.5 * x * (1 + tanh(sqrt(2/pi) * (x + 0.044715 * x^3)))
+    Returns (act, interior nodes, output node) or None."""
+    from .patterns import match_gelu_subgraph
+    return match_gelu_subgraph(g, c, src)
+
+
+def fuse_pools(g, order, fed, fetch_refs, device, opts):
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    for name in order:
+        n = g.nodes.get(name)
+        if n is None:
+            continue
+        if n.op == "Mean":
+            ax = _const(g, n.inputs[1])
+            if ax is not None and sorted(int(a) for a in ax.reshape(-1).tolist()) in ([1, 2], [-3, -2]):
+                n.op = "_GlobalAvgPool"
+                n.attrs = {"_impl": GlobalAvgPool(bool(n.attr("keep_dims", False)), c.use_hip)}
+                n.inputs = [n.inputs[0]]
+        elif n.op == "MaxPool" and n.sattr("data_format", "NHWC") == "NHWC":
+            k, s = n.attr("ksize"), n.attr("strides")
+            n.op = "_MaxPool"
+            n.attrs = {"_impl": MaxPool((k[1], k[2]), (s[1], s[2]), n.sattr("padding", "VALID"), c.use_hip)}
+
+
+def fuse_softmax_argmax(g, order, fed, fetch_refs, device, opts):
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    by_input: Dict[tuple, Dict[str, Node]] = {}
+    for name in order:
+        n = g.nodes.get(name)
+        if n is None or not n.inputs:
+            continue
+        if n.op == "Softmax":
+            by_input.setdefault(n.inputs[0], {})["sm"] = n
+        elif n.op == "ArgMax":
+            ax = _const(g, n.inputs[1])
+            if ax is not None and ax.numel() == 1 and int(ax.reshape(-1)[0]) in (1, -1):
+                by_input.setdefault(n.inputs[0], {})["am"] = n
+    for src, d in by_input.items():
+        if "sm" in d and "am" in d:
+            sm, am = d["sm"], d["am"]
+            cdt = O.DT_TO_TORCH.get(am.attrs.get("output_type", T.DT_INT64), torch.int64)
+            sm.op = "_SoftmaxArgMax"
+            sm.attrs = {"_impl": SoftmaxArgMax(c.use_hip, cdt)}
+            am.op = "Identity"
+            am.inputs = [(sm.name, 1)]
+            am.attrs = {}
+
+
+def default_passes(options=None):
+    from .patterns import bert_passes
+    return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_matmul]

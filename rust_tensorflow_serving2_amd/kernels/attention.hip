@@ -1,0 +1,166 @@
+// Fused multi-head self-attention for encoder models (BERT), gfx950.
+//
+// Input is the packed output of ONE fused QKV GEMM: qkv[B][S][3*H*D] (bf16,
+// Q | K | V column blocks, head h at columns h*D).  One 256-thread workgroup
+// per (batch, head, 64-query block); each wave64 owns 16 query rows against
+// all S keys:
+//   scores = Q K^T          v_mfma_f32_16x16x32_bf16, K row-major in LDS
+//                           (XOR-swizzled 16-B chunks: conflict-free b128 reads)
+//   P = softmax(scores*scale + mask_bias)   in registers: each lane holds 4 rows
+//                           x S/16 columns; row max/sum via 16-lane xor shuffles
+//   ctx = P V               P re-laid out through a per-wave LDS strip into the
+//                           A-operand layout; V stored transposed (Vt[d][key],
+//                           rows padded by 16 B) so B fragments are 16-B reads
+// S <= 256, S % 32 == 0, D == 64.  The S x S matrix never touches HBM.
+#include "common.h"
+#include "launch.h"
+
+namespace tfsk {
+
+namespace {
+
+constexpr int D = 64;
+constexpr int QB = 64;       // query rows per workgroup (4 waves x 16)
+
+template <int S>
+__global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restrict__ qkv,
+                                                        const float* __restrict__ mask_bias,
+                                                        uint16_t* __restrict__ ctx, int H, float scale) {
+  constexpr int VT_LD = S + 8;           // Vt row stride (elements): +16 B pad
+  constexpr int P_LD = S + 8;
+  constexpr int NT = S / 16;             // key tiles
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);          // [S][64] swizzled
+  uint16_t* Vt = Ks + S * D;                                  // [64][VT_LD]
+  uint16_t* Ps = Vt + D * VT_LD;                              // [4][16][P_LD]
+
+  const int qblocks = S / QB;
+  const int bid = blockIdx.x;
+  const int qb = bid % qblocks;
+  const int h = (bid / qblocks) % H;
+  const int b = bid / (qblocks * H);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const long row_stride = 3L * H * D;
+  const uint16_t* base = qkv + long(b) * S * row_stride;
+
+  // ---- stage K (row-major, swizzled) and V (transposed) for this (b, h)
+  for (int c = tid; c < S * 8; c += 256) {
+    const int key = c >> 3, ch = c & 7;
+    const uint4 kv = *reinterpret_cast<const uint4*>(base + long(key) * row_stride + H * D + h * D + ch * 8);
+    *reinterpret_cast<uint4*>(Ks + key * D + ((ch ^ (key & 7)) * 8)) = kv;
+    const uint4 vv = *reinterpret_cast<const uint4*>(base + long(key) * row_stride + 2 * H * D + h * D + ch * 8);
+    const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      Vt[(ch * 8 + 2 * e) * VT_LD + key] = uint16_t(w[e] & 0xffff);
+      Vt[(ch * 8 + 2 * e + 1) * VT_LD + key] = uint16_t(w[e] >> 16);
+    }
+  }
+  // ---- Q fragments straight from global (A operand: row = fr, k = 8*fq + j)
+  const int q0 = qb * QB + wid * 16;
+  bf16x8 qf[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+    qf[kk] = *reinterpret_cast<const bf16x8*>(base + long(q0 + fr) * row_stride + h * D + kk * 32 + fq * 8);
+  __syncthreads();
+
+  // ---- scores
+  f32x4 s[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int key = nt * 16 + fr;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + fq;
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + key * D + ((ch ^ (key & 7)) * 8));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[kk], kf, acc, 0, 0, 0);
+    }
+    s[nt] = acc;
+  }
+  // ---- softmax (rows fq*4 + r, columns nt*16 + fr)
+  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const float mb = mask_bias ? mask_bias[long(b) * S + nt * 16 + fr] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = s[nt][r] * scale + mb;
+      s[nt][r] = v;
+      mx[r] = fmaxf(mx[r], v);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
+  float sum[4] = {0.f, 0.f, 0.f, 0.f};
+  uint16_t* pw = Ps + wid * 16 * P_LD;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = __expf(s[nt][r] - mx[r]);
+      sum[r] += e;
+      pw[(fq * 4 + r) * P_LD + nt * 16 + fr] = f32_to_bf16(e);
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
+  __syncthreads();   // P strip (wave-private) + nothing else pending; cheap at this size
+
+  // ---- ctx = P V
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < S / 32; ++ks) {
+    const bf16x8 pa = *reinterpret_cast<const bf16x8*>(pw + fr * P_LD + ks * 32 + fq * 8);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vt + (dt * 16 + fr) * VT_LD + ks * 32 + fq * 8);
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[dt], 0, 0, 0);
+    }
+  }
+  // ---- normalise + store: rows q0 + fq*4 + r, cols h*D + dt*16 + fr
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float inv = 1.f / sum[r];
+    uint16_t* orow = ctx + (long(b) * S + q0 + fq * 4 + r) * (long(H) * D) + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) orow[dt * 16 + fr] = f32_to_bf16(o[dt][r] * inv);
+  }
+}
+
+template <int S>
+hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, int H, float scale, hipStream_t st) {
+  constexpr int lds = (S * D + D * (S + 8) + 4 * 16 * (S + 8)) * 2;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<S>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int grid = B * H * (S / QB);
+  hipLaunchKernelGGL((attention_kernel<S>), dim3(grid), dim3(256), lds, st, qkv, mb, ctx, H, scale);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t attention_launch(const uint16_t* qkv, const float* mask_bias, uint16_t* ctx, int B, int S, int H,
+                            int Dh, float scale, hipStream_t st) {
+  if (Dh != D) return hipErrorInvalidValue;
+  switch (S) {
+    case 64: return launch_s<64>(qkv, mask_bias, ctx, B, H, scale, st);
+    case 128: return launch_s<128>(qkv, mask_bias, ctx, B, H, scale, st);
+    case 192: return launch_s<192>(qkv, mask_bias, ctx, B, H, scale, st);
+    case 256: return launch_s<256>(qkv, mask_bias, ctx, B, H, scale, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace tfsk

@@ -1,0 +1,274 @@
+// torch bindings of the gfx950 kernels (`_hip`).  Every op launches on the
+// caller's current HIP stream, allocates nothing inside the launch function
+// beyond the output tensor (so callers can capture them in HIP graphs with
+// pre-allocated outputs via the `out=` forms), and validates shapes on the host
+// before anything touches the GPU.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "launch.h"
+
+namespace {
+
+using torch::Tensor;
+
+hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
+}
+
+void need(const Tensor& t, at::ScalarType st, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+const uint16_t* bf16p(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* bf16p_mut(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+// x: NHWC bf16 (or fp32 when stem=true), w: [Cout][ldb] bf16, bias: [Cout] f32
+Tensor conv2d(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
+              const c10::optional<Tensor>& residual, int64_t KH, int64_t KW, int64_t SH, int64_t SW,
+              int64_t PT, int64_t PB, int64_t PL, int64_t PR, int64_t act, int64_t cfg,
+              const c10::optional<Tensor>& out, bool out_f32) {
+  const bool stem = x.scalar_type() == at::kFloat;
+  need(x, stem ? at::kFloat : at::kBFloat16, "x");
+  need(w, at::kBFloat16, "w");
+  TORCH_CHECK(x.dim() == 4, "x must be NHWC");
+  c10::hip::HIPGuard guard(x.device());
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = (H + PT + PB - KH) / SH + 1, Wo = (W + PL + PR - KW) / SW + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty conv output");
+  const int Cout = w.size(0), ldb = w.size(1);
+  const int K = KH * KW * C;
+  TORCH_CHECK(ldb >= K && ldb % 8 == 0, "weight rows must hold K=", K, " (padded to a multiple of 8)");
+  int a_mode;
+  if (stem) {
+    a_mode = tfsk::kAStemF32;
+  } else {
+    TORCH_CHECK(C % 8 == 0, "conv input channels must be a multiple of 8 (got ", C, ")");
+    a_mode = (KH == 1 && KW == 1 && SH == 1 && SW == 1 && PT == 0 && PL == 0) ? tfsk::kADense : tfsk::kAIm2col;
+  }
+  Tensor y = out.has_value() ? *out
+                             : torch::empty({N, Ho, Wo, Cout}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  need(y, out_f32 ? at::kFloat : at::kBFloat16, "out");
+  TORCH_CHECK(y.numel() == int64_t(N) * Ho * Wo * Cout, "out has the wrong size");
+  tfsk::IGemmArgs a{};
+  a.a = x.data_ptr();
+  a.b = bf16p(w);
+  a.M = N * Ho * Wo; a.N = Cout; a.K = K; a.lda = C; a.ldb = ldb;
+  a.H = H; a.W = W; a.C = C; a.KH = KH; a.KW = KW; a.SH = SH; a.SW = SW; a.PT = PT; a.PL = PL;
+  a.Ho = Ho; a.Wo = Wo;
+  if (bias.has_value()) {
+    need(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == Cout, "bias size");
+    a.bias = bias->data_ptr<float>();
+  }
+  if (residual.has_value()) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->numel() == y.numel(), "residual shape must match the output");
+    a.residual = bf16p(*residual);
+    a.ldr = Cout;
+  }
+  a.act = act; a.out = y.data_ptr(); a.ldc = Cout; a.out_f32 = out_f32; a.alpha = 1.f;
+  TORCH_CHECK(cfg >= 0 && cfg < tfsk::kNumIGemmConfigs, "bad tile config");
+  check(tfsk::igemm_launch(a, a_mode, cfg, cur_stream(x)), "igemm");
+  return y;
+}
+
+// x: [M][K] bf16 (any leading dims), w: [N][ldb] bf16 -> [.., N]
+Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
+              const c10::optional<Tensor>& residual, int64_t act, int64_t cfg, bool out_f32, double alpha,
+              const c10::optional<Tensor>& out) {
+  need(x, at::kBFloat16, "x");
+  need(w, at::kBFloat16, "w");
+  c10::hip::HIPGuard guard(x.device());
+  const int K = x.size(-1);
+  const int M = x.numel() / K;
+  const int N = w.size(0), ldb = w.size(1);
+  TORCH_CHECK(ldb >= K && K % 8 == 0 && ldb % 8 == 0, "linear: K must be a multiple of 8 and fit in w");
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  Tensor y = out.has_value() ? *out : torch::empty(sizes, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  need(y, out_f32 ? at::kFloat : at::kBFloat16, "out");
+  TORCH_CHECK(y.numel() == int64_t(M) * N, "out has the wrong size");
+  tfsk::IGemmArgs a{};
+  a.a = x.data_ptr(); a.b = bf16p(w);
+  a.M = M; a.N = N; a.K = K; a.lda = K; a.ldb = ldb;
+  if (bias.has_value()) {
+    need(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == N, "bias size");
+    a.bias = bias->data_ptr<float>();
+  }
+  if (residual.has_value()) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->numel() == y.numel(), "residual shape must match the output");
+    a.residual = bf16p(*residual);
+    a.ldr = N;
+  }
+  a.act = act; a.out = y.data_ptr(); a.ldc = N; a.out_f32 = out_f32; a.alpha = float(alpha);
+  TORCH_CHECK(cfg >= 0 && cfg < tfsk::kNumIGemmConfigs, "bad tile config");
+  check(tfsk::igemm_launch(a, tfsk::kADense, cfg, cur_stream(x)), "igemm(linear)");
+  return y;
+}
+
+Tensor maxpool(const Tensor& x, int64_t KH, int64_t KW, int64_t SH, int64_t SW, int64_t PT, int64_t PB,
+               int64_t PL, int64_t PR, const c10::optional<Tensor>& out) {
+  need(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "maxpool: NHWC with C % 8 == 0");
+  c10::hip::HIPGuard guard(x.device());
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = (H + PT + PB - KH) / SH + 1, Wo = (W + PL + PR - KW) / SW + 1;
+  Tensor y = out.has_value() ? *out : torch::empty({N, Ho, Wo, C}, x.options());
+  need(y, at::kBFloat16, "out");
+  TORCH_CHECK(y.numel() == int64_t(N) * Ho * Wo * C, "out has the wrong size");
+  check(tfsk::maxpool_nhwc_launch(bf16p(x), bf16p_mut(y), N, H, W, C, KH, KW, SH, SW, PT, PL, Ho, Wo,
+                                  cur_stream(x)), "maxpool");
+  return y;
+}
+
+Tensor global_avgpool(const Tensor& x, const c10::optional<Tensor>& out) {
+  need(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "global_avgpool: NHWC with C % 8 == 0");
+  c10::hip::HIPGuard guard(x.device());
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  Tensor y = out.has_value() ? *out : torch::empty({N, C}, x.options());
+  need(y, at::kBFloat16, "out");
+  check(tfsk::global_avgpool_nhwc_launch(bf16p(x), bf16p_mut(y), N, HW, C, cur_stream(x)), "gap");
+  return y;
+}
+
+std::vector<Tensor> softmax_argmax(const Tensor& logits, bool want_probs, bool want_classes,
+                                   const c10::optional<Tensor>& probs_out,
+                                   const c10::optional<Tensor>& classes_out) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous(), "logits must be contiguous GPU");
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "logits must be f32 or bf16");
+  c10::hip::HIPGuard guard(logits.device());
+  const int cols = logits.size(-1);
+  const int rows = logits.numel() / cols;
+  Tensor probs, classes;
+  if (want_probs) {
+    probs = probs_out.has_value() ? *probs_out : torch::empty(logits.sizes(), logits.options().dtype(at::kFloat));
+    need(probs, at::kFloat, "probs");
+  }
+  if (want_classes) {
+    auto sz = logits.sizes().vec();
+    sz.pop_back();
+    classes = classes_out.has_value() ? *classes_out : torch::empty(sz, logits.options().dtype(at::kLong));
+    need(classes, at::kLong, "classes");
+  }
+  check(tfsk::softmax_argmax_launch(logits.data_ptr(), bf, want_probs ? probs.data_ptr<float>() : nullptr,
+                                    want_classes ? classes.data_ptr<int64_t>() : nullptr, rows, cols,
+                                    cur_stream(logits)), "softmax_argmax");
+  return {probs, classes};
+}
+
+Tensor cast_bf16(const Tensor& x, const c10::optional<Tensor>& out) {
+  need(x, at::kFloat, "x");
+  c10::hip::HIPGuard guard(x.device());
+  Tensor y = out.has_value() ? *out : torch::empty(x.sizes(), x.options().dtype(at::kBFloat16));
+  need(y, at::kBFloat16, "out");
+  check(tfsk::cast_f32_bf16_launch(x.data_ptr<float>(), bf16p_mut(y), x.numel(), cur_stream(x)), "cast");
+  return y;
+}
+
+Tensor layernorm(const Tensor& x, const c10::optional<Tensor>& residual, const Tensor& gamma, const Tensor& beta,
+                 double eps, const c10::optional<Tensor>& out) {
+  need(x, at::kBFloat16, "x");
+  need(gamma, at::kFloat, "gamma");
+  need(beta, at::kFloat, "beta");
+  c10::hip::HIPGuard guard(x.device());
+  const int cols = x.size(-1);
+  TORCH_CHECK(cols % 8 == 0 && gamma.numel() == cols && beta.numel() == cols, "layernorm shapes");
+  const int rows = x.numel() / cols;
+  const uint16_t* r = nullptr;
+  if (residual.has_value()) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->numel() == x.numel(), "residual shape");
+    r = bf16p(*residual);
+  }
+  Tensor y = out.has_value() ? *out : torch::empty_like(x);
+  need(y, at::kBFloat16, "out");
+  check(tfsk::layernorm_launch(bf16p(x), r, gamma.data_ptr<float>(), beta.data_ptr<float>(), bf16p_mut(y), rows,
+                               cols, float(eps), cur_stream(x)), "layernorm");
+  return y;
+}
+
+Tensor embed_ln(const Tensor& ids, const c10::optional<Tensor>& type_ids, const Tensor& word, const Tensor& pos,
+                const Tensor& type, const Tensor& gamma, const Tensor& beta, double eps) {
+  need(ids, at::kLong, "ids");
+  need(word, at::kBFloat16, "word");
+  need(pos, at::kBFloat16, "pos");
+  need(type, at::kBFloat16, "type");
+  need(gamma, at::kFloat, "gamma");
+  need(beta, at::kFloat, "beta");
+  TORCH_CHECK(ids.dim() == 2, "ids must be [batch, seq]");
+  c10::hip::HIPGuard guard(ids.device());
+  const int B = ids.size(0), S = ids.size(1), Hd = word.size(1);
+  TORCH_CHECK(Hd % 8 == 0 && pos.size(1) == Hd && type.size(1) == Hd && pos.size(0) >= S, "embedding shapes");
+  const int64_t* tt = nullptr;
+  if (type_ids.has_value()) {
+    need(*type_ids, at::kLong, "type_ids");
+    TORCH_CHECK(type_ids->numel() == ids.numel(), "type_ids shape");
+    tt = type_ids->data_ptr<int64_t>();
+  }
+  Tensor y = torch::empty({B, S, Hd}, word.options());
+  check(tfsk::embed_ln_launch(ids.data_ptr<int64_t>(), tt, bf16p(word), bf16p(pos), bf16p(type),
+                              gamma.data_ptr<float>(), beta.data_ptr<float>(), bf16p_mut(y), B * S, S, Hd,
+                              word.size(0), type.size(0), float(eps), cur_stream(ids)), "embed_ln");
+  return y;
+}
+
+Tensor attention(const Tensor& qkv, const c10::optional<Tensor>& mask_bias, int64_t heads, double scale,
+                 const c10::optional<Tensor>& out) {
+  need(qkv, at::kBFloat16, "qkv");
+  TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, S, 3*H*D]");
+  c10::hip::HIPGuard guard(qkv.device());
+  const int B = qkv.size(0), S = qkv.size(1), HD3 = qkv.size(2);
+  TORCH_CHECK(HD3 % (3 * heads) == 0, "qkv width must be 3*heads*head_dim");
+  const int D = HD3 / (3 * heads);
+  TORCH_CHECK(D == 64, "attention kernel supports head_dim 64");
+  const float* mb = nullptr;
+  if (mask_bias.has_value()) {
+    need(*mask_bias, at::kFloat, "mask_bias");
+    TORCH_CHECK(mask_bias->numel() == int64_t(B) * S, "mask_bias must be [B, S]");
+    mb = mask_bias->data_ptr<float>();
+  }
+  Tensor y = out.has_value() ? *out : torch::empty({B, S, heads * D}, qkv.options());
+  need(y, at::kBFloat16, "out");
+  check(tfsk::attention_launch(bf16p(qkv), mb, bf16p_mut(y), B, S, heads, D, float(scale), cur_stream(qkv)),
+        "attention");
+  return y;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 HIP kernels (MFMA implicit-GEMM conv/GEMM, attention, norms, pooling)";
+  m.def("conv2d", &conv2d, "NHWC implicit-GEMM conv (+bias +residual +act)", py::arg("x"), py::arg("w"),
+        py::arg("bias"), py::arg("residual"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
+        py::arg("pt"), py::arg("pb"), py::arg("pl"), py::arg("pr"), py::arg("act") = 0, py::arg("cfg") = 0,
+        py::arg("out") = py::none(), py::arg("out_f32") = false);
+  m.def("linear", &linear, "x @ w^T (+bias +residual +act)", py::arg("x"), py::arg("w"), py::arg("bias"),
+        py::arg("residual") = py::none(), py::arg("act") = 0, py::arg("cfg") = 0, py::arg("out_f32") = false,
+        py::arg("alpha") = 1.0, py::arg("out") = py::none());
+  m.def("maxpool", &maxpool, py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
+        py::arg("pt"), py::arg("pb"), py::arg("pl"), py::arg("pr"), py::arg("out") = py::none());
+  m.def("global_avgpool", &global_avgpool, py::arg("x"), py::arg("out") = py::none());
+  m.def("softmax_argmax", &softmax_argmax, py::arg("logits"), py::arg("want_probs") = true,
+        py::arg("want_classes") = true, py::arg("probs_out") = py::none(), py::arg("classes_out") = py::none());
+  m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("out") = py::none());
+  m.def("layernorm", &layernorm, py::arg("x"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
+        py::arg("eps"), py::arg("out") = py::none());
+  m.def("embed_ln", &embed_ln, py::arg("ids"), py::arg("type_ids"), py::arg("word"), py::arg("pos"),
+        py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("eps"));
+  m.def("attention", &attention, py::arg("qkv"), py::arg("mask_bias"), py::arg("heads"), py::arg("scale"),
+        py::arg("out") = py::none());
+  m.def("num_configs", []() { return tfsk::kNumIGemmConfigs; });
+  m.def("config_tile", [](int cfg) { return std::make_pair(tfsk::igemm_config_bm(cfg), tfsk::igemm_config_bn(cfg)); });
+}

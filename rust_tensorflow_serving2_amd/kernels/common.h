@@ -1,0 +1,66 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace tfsk {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef uint16_t bf16_t;   // storage type on the host-visible side
+
+constexpr int kWave = 64;
+constexpr int kNumXcd = 8;
+
+enum Act : int { kActNone = 0, kActRelu = 1, kActGeluTanh = 2, kActGeluErf = 3, kActTanh = 4 };
+
+__device__ __forceinline__ float bf16_to_f32(bf16_t v) {
+  return __uint_as_float(uint32_t(v) << 16);
+}
+
+// round-to-nearest-even f32 -> bf16 (NaN preserved)
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return bf16_t((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return bf16_t(u >> 16);
+}
+
+__device__ __forceinline__ float apply_act(float x, int act) {
+  switch (act) {
+    case kActRelu: return x > 0.f ? x : 0.f;
+    case kActGeluTanh: {
+      const float c = 0.7978845608028654f;
+      float u = c * (x + 0.044715f * x * x * x);
+      return 0.5f * x * (1.f + tanhf(u));
+    }
+    case kActGeluErf: return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+    case kActTanh: return tanhf(x);
+    default: return x;
+  }
+}
+
+// Bijective XCD-aware remap (MI355X: 8 XCDs, blocks dealt round-robin):
+// blocks that share an XCD get a contiguous range of logical tile ids, so
+// neighbouring tiles (which share A rows / B columns) hit the same L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / kNumXcd, r = nwg % kNumXcd;
+  const int xcd = bid % kNumXcd, idx = bid / kNumXcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace tfsk

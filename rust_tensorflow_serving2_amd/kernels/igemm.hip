@@ -1,0 +1,324 @@
+// Implicit-GEMM convolution / GEMM for MI355X (gfx950), bf16 in, fp32 MFMA accumulate.
+//
+// C[M][N] = epilogue( A[M][K] * B[N][K]^T )
+//   A: NHWC activations gathered on the fly (im2col never materialised), a dense
+//      row-major matrix, or (stem) the fp32 request tensor itself — the ingest
+//      fp32->bf16 cast is fused into the stem conv's operand load.
+//   B: weights [Cout][K] bf16 (BN scale folded in at load time).
+//   epilogue: *alpha + bias[n] (+ residual[m][n]) -> act -> bf16/f32 store.
+//
+// CDNA4 mapping:
+//   * 256-thread workgroups = 4 wave64s in a 2x2 grid; each wave owns a
+//     (BM/2)x(BN/2) sub-tile built from v_mfma_f32_16x16x32_bf16 tiles.
+//   * BK = 64: each tile row is 128 B; 16-B chunks are XOR-swizzled by
+//     (row & 7) so the ds_read_b128 fragment reads of a 16-lane group hit 16
+//     distinct 16-B bank slots (conflict-free; see MI355X LDS banking).
+//   * register-staged double-buffered LDS: the global loads of k-tile t+1 are
+//     issued before the MFMAs of tile t and written to the other LDS buffer
+//     after them -> one barrier per k-tile.
+//   * bijective XCD-aware block remap + GROUP_M tile ordering so tiles that
+//     share operand panels run on the same XCD (shared 4 MB L2).
+//   * epilogue staged through LDS as fp32 so bias/residual/activation work on
+//     coalesced 16-B row chunks (residual read once, output written once).
+#include "common.h"
+#include "launch.h"
+
+namespace tfsk {
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int kThreads = 256;
+constexpr int kGroupM = 8;
+
+template <int BM, int BN, int AMODE>
+struct IGemm {
+  static constexpr int WM = BM / 2, WN = BN / 2;
+  static constexpr int TM = WM / 16, TN = WN / 16;
+  static constexpr int A_CHUNKS = BM * BK / 8 / kThreads;
+  static constexpr int B_CHUNKS = BN * BK / 8 / kThreads;
+  static constexpr int LDS_MAIN = 2 * (BM + BN) * BK * 2;
+  static constexpr int CS_LD = BN + 4;
+  static constexpr int LDS_EPI = BM * CS_LD * 4;
+  static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
+
+template <int BM, int BN, int AMODE>
+__global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
+  using G = IGemm<BM, BN, AMODE>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* As = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* Bs = As + 2 * BM * BK;
+
+  const int M = p.M, N = p.N, K = p.K;
+  const int nbm = (M + BM - 1) / BM, nbn = (N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = kGroupM * nbn;
+  const int group = wg / per_group;
+  const int first_m = group * kGroupM;
+  const int gsz = min(nbm - first_m, kGroupM);
+  const int bm = first_m + (wg % per_group) % gsz;
+  const int bn = (wg % per_group) / gsz;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int chunk = tid & 7;
+  const int row_base = tid >> 3;   // 0..31
+
+  // ---- per-thread A row descriptors
+  int a_off[G::A_CHUNKS];     // element offset of the row's base (dense: m*lda; im2col: image base)
+  int a_hi[G::A_CHUNKS], a_wi[G::A_CHUNKS];
+  bool a_ok[G::A_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < G::A_CHUNKS; ++i) {
+    const int m = m0 + row_base + 32 * i;
+    a_ok[i] = m < M;
+    const int mm = a_ok[i] ? m : 0;
+    if (AMODE == kADense) {
+      a_off[i] = mm * p.lda;
+      a_hi[i] = a_wi[i] = 0;
+    } else {
+      const int hw = p.Ho * p.Wo;
+      const int n = mm / hw, r = mm - n * hw;
+      const int ho = r / p.Wo, wo = r - ho * p.Wo;
+      a_off[i] = n * p.H * p.W * p.C;
+      a_hi[i] = ho * p.SH - p.PT;
+      a_wi[i] = wo * p.SW - p.PL;
+    }
+  }
+
+  uint4 ra[G::A_CHUNKS], rb[G::B_CHUNKS];
+  const uint16_t* __restrict__ Bg = p.b;
+
+  auto gload = [&](int kt) {
+    const int k0 = kt * BK;
+    if (AMODE == kADense) {
+      const uint16_t* __restrict__ Ag = static_cast<const uint16_t*>(p.a);
+      const int k = k0 + chunk * 8;
+#pragma unroll
+      for (int i = 0; i < G::A_CHUNKS; ++i) {
+        if (a_ok[i] && k < K) ra[i] = *reinterpret_cast<const uint4*>(Ag + a_off[i] + k);
+        else ra[i] = make_uint4(0, 0, 0, 0);
+      }
+    } else if (AMODE == kAIm2col) {
+      const uint16_t* __restrict__ Ag = static_cast<const uint16_t*>(p.a);
+      // C % 8 == 0, so a 16-B chunk never straddles two filter taps
+      const int k = k0 + chunk * 8;
+      const int tap = k / p.C;
+      const int ci = k - tap * p.C;
+      const int kh = tap / p.KW, kw = tap - kh * p.KW;
+      const bool kok = k < K;
+#pragma unroll
+      for (int i = 0; i < G::A_CHUNKS; ++i) {
+        const int hi = a_hi[i] + kh, wi = a_wi[i] + kw;
+        const bool ok = kok && a_ok[i] && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+        if (ok) ra[i] = *reinterpret_cast<const uint4*>(Ag + a_off[i] + (hi * p.W + wi) * p.C + ci);
+        else ra[i] = make_uint4(0, 0, 0, 0);
+      }
+    } else {  // kAStemF32: fp32 NHWC, tiny C, element gather + cast
+      const float* __restrict__ Ag = static_cast<const float*>(p.a);
+#pragma unroll
+      for (int i = 0; i < G::A_CHUNKS; ++i) {
+        uint16_t v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = k0 + chunk * 8 + e;
+          float x = 0.f;
+          if (a_ok[i] && k < K) {
+            const int tap = k / p.C, c = k - tap * p.C;
+            const int kh = tap / p.KW, kw = tap - kh * p.KW;
+            const int hi = a_hi[i] + kh, wi = a_wi[i] + kw;
+            if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+              x = Ag[a_off[i] + (hi * p.W + wi) * p.C + c];
+          }
+          v[e] = f32_to_bf16(x);
+        }
+        ra[i] = make_uint4(v[0] | (uint32_t(v[1]) << 16), v[2] | (uint32_t(v[3]) << 16),
+                           v[4] | (uint32_t(v[5]) << 16), v[6] | (uint32_t(v[7]) << 16));
+      }
+    }
+    {
+      const int k = k0 + chunk * 8;
+#pragma unroll
+      for (int i = 0; i < G::B_CHUNKS; ++i) {
+        const int n = n0 + row_base + 32 * i;
+        if (n < N && k < p.ldb) rb[i] = *reinterpret_cast<const uint4*>(Bg + size_t(n) * p.ldb + k);
+        else rb[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+
+  auto sstore = [&](int buf) {
+    uint16_t* as = As + buf * BM * BK;
+    uint16_t* bs = Bs + buf * BN * BK;
+#pragma unroll
+    for (int i = 0; i < G::A_CHUNKS; ++i) {
+      const int row = row_base + 32 * i;
+      *reinterpret_cast<uint4*>(as + row * BK + swz(row, chunk) * 8) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < G::B_CHUNKS; ++i) {
+      const int row = row_base + 32 * i;
+      *reinterpret_cast<uint4*>(bs + row * BK + swz(row, chunk) * 8) = rb[i];
+    }
+  };
+
+  f32x4 acc[G::TM][G::TN];
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K + BK - 1) / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const uint16_t* as = As + cur * BM * BK;
+    const uint16_t* bs = Bs + cur * BN * BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + fq;
+      bf16x8 af[G::TM], bfr[G::TN];
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i) {
+        const int row = wm * G::WM + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(as + row * BK + swz(row, ch) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j) {
+        const int row = wn * G::WN + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + row * BK + swz(row, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage fp32 tile in LDS, then coalesced 8-wide row chunks
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * G::WM + i * 16 + fq * 4 + r) * G::CS_LD + wn * G::WN + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+
+  const float alpha = p.alpha;
+  const bool vec_ok = (N % 8 == 0) && (p.ldc % 8 == 0) && (!p.residual || p.ldr % 8 == 0);
+  constexpr int CPR = BN / 8;   // chunks per row
+  for (int c = tid; c < BM * CPR; c += kThreads) {
+    const int row = c / CPR, col = (c - row * CPR) * 8;
+    const int m = m0 + row, n = n0 + col;
+    if (m >= M || n >= N) continue;
+    const float4 lo = *reinterpret_cast<const float4*>(Cs + row * G::CS_LD + col);
+    const float4 hi = *reinterpret_cast<const float4*>(Cs + row * G::CS_LD + col + 4);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    if (vec_ok && n + 8 <= N) {
+      float bv[8];
+      if (p.bias) {
+        const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+        const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+        bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+        bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+      }
+      float rv[8];
+      if (p.residual) {
+        const uint4 rr = *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
+        const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          rv[2 * e] = bf16_to_f32(uint16_t(w[e] & 0xffff));
+          rv[2 * e + 1] = bf16_to_f32(uint16_t(w[e] >> 16));
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rv[e] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e] * alpha + bv[e] + rv[e], p.act);
+      if (p.out_f32) {
+        float* o = static_cast<float*>(p.out) + size_t(m) * p.ldc + n;
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        uint16_t b[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) b[e] = f32_to_bf16(v[e]);
+        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.out) + size_t(m) * p.ldc + n) =
+            make_uint4(b[0] | (uint32_t(b[1]) << 16), b[2] | (uint32_t(b[3]) << 16),
+                       b[4] | (uint32_t(b[5]) << 16), b[6] | (uint32_t(b[7]) << 16));
+      }
+    } else {
+      for (int e = 0; e < 8 && n + e < N; ++e) {
+        float x = v[e] * alpha;
+        if (p.bias) x += p.bias[n + e];
+        if (p.residual) x += bf16_to_f32(p.residual[size_t(m) * p.ldr + n + e]);
+        x = apply_act(x, p.act);
+        if (p.out_f32) static_cast<float*>(p.out)[size_t(m) * p.ldc + n + e] = x;
+        else static_cast<uint16_t*>(p.out)[size_t(m) * p.ldc + n + e] = f32_to_bf16(x);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int AMODE>
+hipError_t launch_cfg(const IGemmArgs& a, hipStream_t s) {
+  using G = IGemm<BM, BN, AMODE>;
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  if (tiles == 0) return hipSuccess;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<BM, BN, AMODE>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE>), dim3(tiles), dim3(kThreads), G::LDS, s, a);
+  return hipGetLastError();
+}
+
+template <int AMODE>
+hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
+  switch (cfg) {
+    case 0: return launch_cfg<128, 128, AMODE>(a, s);
+    case 1: return launch_cfg<128, 64, AMODE>(a, s);
+    case 2: return launch_cfg<64, 128, AMODE>(a, s);
+    case 3: return launch_cfg<64, 64, AMODE>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+int igemm_config_bm(int cfg) { const int t[] = {128, 128, 64, 64}; return t[cfg]; }
+int igemm_config_bn(int cfg) { const int t[] = {128, 64, 128, 64}; return t[cfg]; }
+
+hipError_t igemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) {
+  switch (a_mode) {
+    case kADense: return launch_mode<kADense>(a, cfg, s);
+    case kAIm2col: return launch_mode<kAIm2col>(a, cfg, s);
+    case kAStemF32: return launch_mode<kAStemF32>(a, cfg, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace tfsk

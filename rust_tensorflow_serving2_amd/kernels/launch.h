@@ -1,0 +1,65 @@
+// Host-side launchers of the HIP kernels (torch-free; bindings.cpp wraps them).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tfsk {
+
+// Implicit-GEMM geometry.  GEMM view: C[M][N] = A[M][K] * B[N][K]^T where
+//   A = im2col(x) of an NHWC input (or a dense row-major matrix),
+//   B = weights [Cout][ldb] with k = (kh*KW + kw)*C + c (zero padded to ldb).
+struct IGemmArgs {
+  const void* a;        // bf16 NHWC / dense [M][lda] (fp32 NHWC for the stem mode)
+  const uint16_t* b;    // bf16 [N][ldb]
+  int M, N, K;
+  int lda, ldb;
+  // conv geometry (a_mode 1/2)
+  int H, W, C, KH, KW, SH, SW, PT, PL, Ho, Wo;
+  // epilogue
+  const float* bias;    // [N] or nullptr
+  const uint16_t* residual;  // bf16 [M][ldr] or nullptr
+  int ldr;
+  int act;
+  void* out;            // bf16 or f32 [M][ldc]
+  int ldc;
+  int out_f32;
+  float alpha;          // scale applied to the accumulator before bias
+};
+
+enum AMode : int { kADense = 0, kAIm2col = 1, kAStemF32 = 2 };
+
+// Tile configs (BMxBN): 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64
+constexpr int kNumIGemmConfigs = 4;
+int igemm_config_bm(int cfg);
+int igemm_config_bn(int cfg);
+hipError_t igemm_launch(const IGemmArgs& args, int a_mode, int cfg, hipStream_t stream);
+
+// NHWC bf16 max-pool (TF SAME/VALID padding given explicitly).
+hipError_t maxpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int H, int W, int C,
+                               int KH, int KW, int SH, int SW, int PT, int PL, int Ho, int Wo,
+                               hipStream_t stream);
+// Mean over H,W of NHWC bf16 -> [N][C] (bf16).
+hipError_t global_avgpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int HW, int C,
+                                      hipStream_t stream);
+// Row softmax (fp32 in) -> probs f32 + argmax int64 (the classifier head).
+hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, int64_t* classes,
+                                 int rows, int cols, hipStream_t stream);
+// fp32 -> bf16 cast (vectorized).
+hipError_t cast_f32_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t stream);
+hipError_t cast_bf16_f32_launch(const uint16_t* x, float* y, int64_t n, hipStream_t stream);
+
+// LayerNorm over the last dim (bf16 in/out, f32 gamma/beta), optional fused residual add:
+// y = LN(x + r) ; if `sum_out` != nullptr the pre-norm sum is also written.
+hipError_t layernorm_launch(const uint16_t* x, const uint16_t* r, const float* gamma, const float* beta,
+                            uint16_t* y, int rows, int cols, float eps, hipStream_t stream);
+// Embedding: y[t] = LN(word[ids[t]] + pos[t % S] + type[tt[t]]) (bf16 tables, f32 LN params)
+hipError_t embed_ln_launch(const int64_t* ids, const int64_t* type_ids, const uint16_t* word,
+                           const uint16_t* pos, const uint16_t* type, const float* gamma,
+                           const float* beta, uint16_t* y, int tokens, int seq, int hidden,
+                           int vocab, int ntypes, float eps, hipStream_t stream);
+// Fused multi-head attention over a packed QKV buffer [B*S][3*H*D] (bf16):
+// ctx[b,s,h,:] = softmax(Q K^T * scale + mask_bias[b, :]) V ; mask_bias f32 [B][S] (0 / -1e4 style)
+hipError_t attention_launch(const uint16_t* qkv, const float* mask_bias, uint16_t* ctx, int B, int S,
+                            int H, int D, float scale, hipStream_t stream);
+
+}  // namespace tfsk

@@ -1,0 +1,273 @@
+// Memory-bound companion kernels (gfx950): pooling, classifier head, casts,
+// LayerNorm, embedding+LN.  All bf16 traffic is 16-B vectorised (8 elements
+// per lane), reductions are wave64 shuffles.
+#include "common.h"
+#include "launch.h"
+
+namespace tfsk {
+
+namespace {
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[2 * e] = bf16_to_f32(uint16_t(w[e] & 0xffff));
+    f[2 * e + 1] = bf16_to_f32(uint16_t(w[e] >> 16));
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint16_t b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b[e] = f32_to_bf16(f[e]);
+  return make_uint4(b[0] | (uint32_t(b[1]) << 16), b[2] | (uint32_t(b[3]) << 16),
+                    b[4] | (uint32_t(b[5]) << 16), b[6] | (uint32_t(b[7]) << 16));
+}
+
+// ---------------------------------------------------------------- max pool
+__global__ __launch_bounds__(256) void maxpool_nhwc_kernel(const uint16_t* __restrict__ x,
+                                                           uint16_t* __restrict__ y, int N, int H, int W,
+                                                           int C, int KH, int KW, int SH, int SW, int PT,
+                                                           int PL, int Ho, int Wo) {
+  const int C8 = C / 8;
+  const long total = long(N) * Ho * Wo * C8;
+  for (long i = blockIdx.x * long(blockDim.x) + threadIdx.x; i < total; i += long(gridDim.x) * blockDim.x) {
+    const int c8 = int(i % C8);
+    long t = i / C8;
+    const int wo = int(t % Wo); t /= Wo;
+    const int ho = int(t % Ho);
+    const int n = int(t / Ho);
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int hi = ho * SH - PT + kh;
+      if ((unsigned)hi >= (unsigned)H) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int wi = wo * SW - PL + kw;
+        if ((unsigned)wi >= (unsigned)W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + ((long(n) * H + hi) * W + wi) * C + c8 * 8), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
+      }
+    }
+    *reinterpret_cast<uint4*>(y + i * 8) = pack8(m);
+  }
+}
+
+// ---------------------------------------------------------------- global avg pool
+__global__ __launch_bounds__(256) void gap_nhwc_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                       int N, int HW, int C) {
+  const int C8 = C / 8;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C8) return;
+  const int n = i / C8, c8 = i - n * C8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint16_t* p = x + long(n) * HW * C + c8 * 8;
+  for (int h = 0; h < HW; ++h) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(p + long(h) * C), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] += f[e];
+  }
+  const float inv = 1.f / float(HW);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] *= inv;
+  *reinterpret_cast<uint4*>(y + long(n) * C + c8 * 8) = pack8(s);
+}
+
+// ---------------------------------------------------------------- softmax + argmax
+// One wave per row.  ArgMax ties resolve to the smallest index (TF semantics).
+__global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restrict__ logits, int in_bf16,
+                                                             float* __restrict__ probs,
+                                                             int64_t* __restrict__ classes, int rows, int cols) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  auto ld = [&](int c) -> float {
+    return in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * cols + c])
+                   : static_cast<const float*>(logits)[long(row) * cols + c];
+  };
+  float mx = -INFINITY;
+  int arg = 0x7fffffff;
+  for (int c = lane; c < cols; c += 64) {
+    const float v = ld(c);
+    if (v > mx || (v == mx && c < arg)) { mx = v; arg = c; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(arg, o, 64);
+    if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+  }
+  float s = 0.f;
+  for (int c = lane; c < cols; c += 64) s += __expf(ld(c) - mx);
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  if (probs)
+    for (int c = lane; c < cols; c += 64) probs[long(row) * cols + c] = __expf(ld(c) - mx) * inv;
+  if (classes && lane == 0) classes[row] = arg;
+}
+
+// ---------------------------------------------------------------- casts
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, long n) {
+  const long n8 = n / 8;
+  for (long i = blockIdx.x * long(blockDim.x) + threadIdx.x; i < n8; i += long(gridDim.x) * blockDim.x) {
+    const float4 a = reinterpret_cast<const float4*>(x)[2 * i];
+    const float4 b = reinterpret_cast<const float4*>(x)[2 * i + 1];
+    const float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    reinterpret_cast<uint4*>(y)[i] = pack8(f);
+  }
+  for (long i = n8 * 8 + blockIdx.x * long(blockDim.x) + threadIdx.x; i < n; i += long(gridDim.x) * blockDim.x)
+    y[i] = f32_to_bf16(x[i]);
+}
+
+__global__ void cast_bf16_f32_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, long n) {
+  for (long i = blockIdx.x * long(blockDim.x) + threadIdx.x; i < n; i += long(gridDim.x) * blockDim.x)
+    y[i] = bf16_to_f32(x[i]);
+}
+
+// ---------------------------------------------------------------- LayerNorm
+// One wave per row; two passes over the (L2-resident) row; fp32 statistics.
+__global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restrict__ x,
+                                                        const uint16_t* __restrict__ r,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta,
+                                                        uint16_t* __restrict__ y, int rows, int cols, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const uint16_t* xr = x + long(row) * cols;
+  const uint16_t* rr = r ? r + long(row) * cols : nullptr;
+  float s = 0.f, ss = 0.f;
+  for (int c = lane * 8; c < cols; c += 512) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
+    if (rr) {
+      float g[8];
+      unpack8(*reinterpret_cast<const uint4*>(rr + c), g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += g[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s += f[e]; ss += f[e] * f[e]; }
+  }
+  s = wave_sum(s);
+  ss = wave_sum(ss);
+  const float mean = s / cols;
+  const float var = fmaxf(ss / cols - mean * mean, 0.f);
+  const float inv = rsqrtf(var + eps);
+  for (int c = lane * 8; c < cols; c += 512) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
+    if (rr) {
+      float g[8];
+      unpack8(*reinterpret_cast<const uint4*>(rr + c), g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += g[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = (f[e] - mean) * inv * gamma[c + e] + beta[c + e];
+    *reinterpret_cast<uint4*>(y + long(row) * cols + c) = pack8(f);
+  }
+}
+
+// ---------------------------------------------------------------- embedding + LN
+__global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* __restrict__ ids,
+                                                       const int64_t* __restrict__ tids,
+                                                       const uint16_t* __restrict__ word,
+                                                       const uint16_t* __restrict__ pos,
+                                                       const uint16_t* __restrict__ type,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, uint16_t* __restrict__ y,
+                                                       int tokens, int seq, int hidden, int vocab, int ntypes,
+                                                       float eps) {
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= tokens) return;
+  long id = ids[t];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  long tt = tids ? tids[t] : 0;
+  tt = tt < 0 ? 0 : (tt >= ntypes ? ntypes - 1 : tt);
+  const int p = t % seq;
+  float s = 0.f, ss = 0.f;
+  for (int c = lane * 8; c < hidden; c += 512) {
+    float a[8], b[8], d[8];
+    unpack8(*reinterpret_cast<const uint4*>(word + id * hidden + c), a);
+    unpack8(*reinterpret_cast<const uint4*>(pos + long(p) * hidden + c), b);
+    unpack8(*reinterpret_cast<const uint4*>(type + tt * hidden + c), d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float v = a[e] + b[e] + d[e]; s += v; ss += v * v; }
+  }
+  s = wave_sum(s);
+  ss = wave_sum(ss);
+  const float mean = s / hidden;
+  const float inv = rsqrtf(fmaxf(ss / hidden - mean * mean, 0.f) + eps);
+  for (int c = lane * 8; c < hidden; c += 512) {
+    float a[8], b[8], d[8];
+    unpack8(*reinterpret_cast<const uint4*>(word + id * hidden + c), a);
+    unpack8(*reinterpret_cast<const uint4*>(pos + long(p) * hidden + c), b);
+    unpack8(*reinterpret_cast<const uint4*>(type + tt * hidden + c), d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = (a[e] + b[e] + d[e] - mean) * inv * gamma[c + e] + beta[c + e];
+    *reinterpret_cast<uint4*>(y + long(t) * hidden + c) = pack8(a);
+  }
+}
+
+int grid_for(long work, int block) {
+  long g = (work + block - 1) / block;
+  if (g > 256 * 16) g = 256 * 16;
+  return int(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+hipError_t maxpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int KH, int KW,
+                               int SH, int SW, int PT, int PL, int Ho, int Wo, hipStream_t s) {
+  const long work = long(N) * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_nhwc_kernel, dim3(grid_for(work, 256)), dim3(256), 0, s, x, y, N, H, W, C, KH, KW,
+                     SH, SW, PT, PL, Ho, Wo);
+  return hipGetLastError();
+}
+
+hipError_t global_avgpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s) {
+  const int work = N * (C / 8);
+  hipLaunchKernelGGL(gap_nhwc_kernel, dim3((work + 255) / 256), dim3(256), 0, s, x, y, N, HW, C);
+  return hipGetLastError();
+}
+
+hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, int64_t* classes, int rows,
+                                 int cols, hipStream_t s) {
+  hipLaunchKernelGGL(softmax_argmax_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, logits, in_bf16, probs, classes,
+                     rows, cols);
+  return hipGetLastError();
+}
+
+hipError_t cast_f32_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n / 8 + 1, 256)), dim3(256), 0, s, x, y, long(n));
+  return hipGetLastError();
+}
+
+hipError_t cast_bf16_f32_launch(const uint16_t* x, float* y, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, y, long(n));
+  return hipGetLastError();
+}
+
+hipError_t layernorm_launch(const uint16_t* x, const uint16_t* r, const float* gamma, const float* beta,
+                            uint16_t* y, int rows, int cols, float eps, hipStream_t s) {
+  hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, r, gamma, beta, y, rows, cols,
+                     eps);
+  return hipGetLastError();
+}
+
+hipError_t embed_ln_launch(const int64_t* ids, const int64_t* type_ids, const uint16_t* word, const uint16_t* pos,
+                           const uint16_t* type, const float* gamma, const float* beta, uint16_t* y, int tokens,
+                           int seq, int hidden, int vocab, int ntypes, float eps, hipStream_t s) {
+  hipLaunchKernelGGL(embed_ln_kernel, dim3((tokens + 3) / 4), dim3(256), 0, s, ids, type_ids, word, pos, type,
+                     gamma, beta, y, tokens, seq, hidden, vocab, ntypes, eps);
+  return hipGetLastError();
+}
+
+}  // namespace tfsk

@@ -1,0 +1,157 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references of the same op (MI355X).
+
+Inputs are bf16-rounded first so the only differences are accumulation order
+and the final bf16 rounding of outputs."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from rust_tensorflow_serving2_amd.ops import ACT, hip  # noqa: E402
+
+DEV = torch.device("cuda:0")
+BF = torch.bfloat16
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale)
+
+
+def pack_w(w_hwio):
+    kh, kw, cin, cout = w_hwio.shape
+    k = kh * kw * cin
+    kp = -(-k // 64) * 64
+    w = w_hwio.permute(3, 0, 1, 2).reshape(cout, k)
+    w = torch.cat([w, torch.zeros(cout, kp - k)], 1)
+    return w.to(BF).contiguous().to(DEV)
+
+
+def ref_conv(x, w_hwio, bias, stride, pads, res=None, act="none"):
+    pt, pb, pl, pr = pads
+    y = F.conv2d(F.pad(x.float().permute(0, 3, 1, 2), [pl, pr, pt, pb]), w_hwio.float().permute(3, 2, 0, 1),
+                 stride=stride).permute(0, 2, 3, 1) + bias
+    if res is not None:
+        y = y + res.float()
+    return torch.relu(y) if act == "relu" else y
+
+
+CONV_SHAPES = [
+    # N, H, W, Cin, Cout, k, stride, pads            (ResNet-50 layers, small batch)
+    (2, 56, 56, 64, 64, 1, 1, (0, 0, 0, 0)),
+    (2, 56, 56, 64, 64, 3, 1, (1, 1, 1, 1)),
+    (2, 56, 56, 64, 256, 1, 1, (0, 0, 0, 0)),
+    (2, 56, 56, 256, 128, 1, 1, (0, 0, 0, 0)),
+    (2, 56, 56, 128, 128, 3, 2, (1, 1, 1, 1)),
+    (2, 56, 56, 256, 512, 1, 2, (0, 0, 0, 0)),
+    (3, 14, 14, 256, 256, 3, 1, (1, 1, 1, 1)),
+    (1, 7, 7, 512, 2048, 1, 1, (0, 0, 0, 0)),
+    (1, 9, 9, 24, 40, 3, 2, (0, 1, 0, 1)),   # odd channels (C % 64 != 0), asymmetric SAME pads
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_conv_matches_fp32(shape, cfg):
+    n, h, w, cin, cout, k, s, pads = shape
+    x = rnd(n, h, w, cin, seed=1).to(BF)
+    wt = rnd(k, k, cin, cout, scale=1 / math.sqrt(k * k * cin), seed=2).to(BF).float()
+    b = rnd(cout, scale=0.1, seed=3)
+    ho = (h + pads[0] + pads[1] - k) // s + 1
+    wo = (w + pads[2] + pads[3] - k) // s + 1
+    res = rnd(n, ho, wo, cout, seed=4).to(BF)
+    y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), k, k, s, s, *pads, act=ACT["relu"], cfg=cfg)
+    ref = ref_conv(x, wt, b, s, pads, res, "relu")
+    torch.cuda.synchronize()
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert y.shape == (n, ho, wo, cout)
+    assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
+
+
+def test_stem_conv_fp32_input():
+    x = torch.rand(2, 32, 32, 3)                      # fp32 request tensor, C=3
+    wt = rnd(7, 7, 3, 64, scale=0.1, seed=5).to(BF).float()
+    b = rnd(64, scale=0.1, seed=6)
+    y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), None, 7, 7, 2, 2, 2, 3, 2, 3, act=ACT["relu"], cfg=1)
+    ref = ref_conv(x.to(BF).float(), wt, b, 2, (2, 3, 2, 3), None, "relu")
+    assert (y.float().cpu() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+
+def test_asymmetric_identity_gemm():
+    """A = I, asymmetric B: catches a transposed C write (guide §3)."""
+    m = n = 64
+    a = torch.eye(m, 128)[:, :128].to(BF)
+    bmat = torch.arange(n * 128, dtype=torch.float32).reshape(n, 128) % 17 - 8
+    y = hip().linear(a.to(DEV), bmat.to(BF).to(DEV), None, None, 0, 3, True)
+    ref = a.float() @ bmat.t()
+    assert torch.equal(y.cpu(), ref)
+
+
+@pytest.mark.parametrize("m,n,k,act", [(32, 1001, 2048, "none"), (256, 2304, 768, "none"),
+                                       (256, 3072, 768, "gelu_tanh"), (256, 768, 3072, "none"),
+                                       (8, 768, 768, "tanh"), (100, 72, 40, "gelu_erf")])
+@pytest.mark.parametrize("cfg", [0, 3])
+def test_linear_matches_fp32(m, n, k, act, cfg):
+    x = rnd(m, k, seed=7).to(BF)
+    w = rnd(n, k, scale=1 / math.sqrt(k), seed=8).to(BF)
+    b = rnd(n, scale=0.1, seed=9)
+    res = rnd(m, n, seed=10).to(BF) if act == "none" else None
+    out_f32 = n % 8 != 0
+    y = hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), None if res is None else res.to(DEV), ACT[act], cfg, out_f32)
+    ref = x.float() @ w.float().t() + b
+    if res is not None:
+        ref = ref + res.float()
+    ref = {"none": ref, "gelu_tanh": F.gelu(ref, approximate="tanh"), "gelu_erf": F.gelu(ref),
+           "tanh": torch.tanh(ref)}[act]
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
+
+
+def test_pools_and_head():
+    x = rnd(4, 112, 112, 64, seed=11).to(BF)
+    y = hip().maxpool(x.to(DEV), 3, 3, 2, 2, 0, 1, 0, 1)
+    ref = F.max_pool2d(F.pad(x.float().permute(0, 3, 1, 2), [0, 1, 0, 1], value=-1e30), 3, 2).permute(0, 2, 3, 1)
+    assert torch.equal(y.float().cpu(), ref)
+    g = rnd(4, 7, 7, 2048, seed=12).to(BF)
+    gy = hip().global_avgpool(g.to(DEV))
+    assert (gy.float().cpu() - g.float().mean((1, 2))).abs().max() < 1e-2
+    logits = rnd(37, 1001, scale=3, seed=13)
+    logits[5, 7] = logits[5, 9] = 100.0          # tie -> smallest index (TF ArgMax)
+    p, c = hip().softmax_argmax(logits.to(DEV))
+    assert torch.allclose(p.cpu(), torch.softmax(logits, -1), atol=1e-6)
+    assert torch.equal(c.cpu(), torch.argmax(logits, -1)) and c[5].item() == 7
+
+
+def test_layernorm_and_embedding():
+    x = rnd(300, 768, seed=14).to(BF)
+    r = rnd(300, 768, seed=15).to(BF)
+    gm, bt = rnd(768, seed=16), rnd(768, seed=17)
+    y = hip().layernorm(x.to(DEV), r.to(DEV), gm.to(DEV), bt.to(DEV), 1e-12)
+    ref = F.layer_norm(x.float() + r.float(), (768,), gm, bt, 1e-12)
+    assert (y.float().cpu() - ref).abs().max() < 5e-2
+    ids = torch.randint(0, 1000, (3, 128))
+    tt = torch.randint(0, 2, (3, 128))
+    word, pos, typ = rnd(1000, 768, seed=18).to(BF), rnd(512, 768, seed=19).to(BF), rnd(2, 768, seed=20).to(BF)
+    e = hip().embed_ln(ids.to(DEV), tt.to(DEV), word.to(DEV), pos.to(DEV), typ.to(DEV), gm.to(DEV), bt.to(DEV),
+                       1e-12)
+    ref = F.layer_norm(word.float()[ids] + pos.float()[:128] + typ.float()[tt], (768,), gm, bt, 1e-12)
+    assert (e.float().cpu() - ref).abs().max() < 5e-2
+
+
+@pytest.mark.parametrize("s", [64, 128, 256])
+def test_attention_matches_fp32(s):
+    b, h, d = 3, 12, 64
+    qkv = rnd(b, s, 3 * h * d, seed=21).to(BF)
+    mask = torch.zeros(b, s)
+    mask[1, s // 2:] = -10000.0
+    y = hip().attention(qkv.to(DEV), mask.to(DEV), h, 1 / math.sqrt(d))
+    q, k, v = qkv.float().reshape(b, s, 3, h, d).permute(2, 0, 3, 1, 4)
+    att = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(d) + mask[:, None, None, :], -1)
+    ref = (att @ v).permute(0, 2, 1, 3).reshape(b, s, h * d)
+    assert (y.float().cpu() - ref).abs().max() < 3e-2
