@@ -1,11 +1,12 @@
-// torch bindings of the gfx950 kernels (`_hip`).  Every op launches on the
+// torch bindings of the gfx950 kernels (`_hip`).  (ROCm torch exposes HIP
+// devices as "cuda": guards/streams use the MasqueradingAsCUDA variants.)  Every op launches on the
 // caller's current HIP stream, allocates nothing inside the launch function
 // beyond the output tensor (so callers can capture them in HIP graphs with
 // pre-allocated outputs via the `out=` forms), and validates shapes on the host
 // before anything touches the GPU.
 #include <torch/extension.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include "launch.h"
 
@@ -14,7 +15,7 @@ namespace {
 using torch::Tensor;
 
 hipStream_t cur_stream(const Tensor& t) {
-  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 
 void check(hipError_t e, const char* what) {
@@ -39,7 +40,7 @@ Tensor conv2d(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   need(x, stem ? at::kFloat : at::kBFloat16, "x");
   need(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4, "x must be NHWC");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int Ho = (H + PT + PB - KH) / SH + 1, Wo = (W + PL + PR - KW) / SW + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty conv output");
@@ -86,7 +87,7 @@ Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
               const c10::optional<Tensor>& out) {
   need(x, at::kBFloat16, "x");
   need(w, at::kBFloat16, "w");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int K = x.size(-1);
   const int M = x.numel() / K;
   const int N = w.size(0), ldb = w.size(1);
@@ -120,7 +121,7 @@ Tensor maxpool(const Tensor& x, int64_t KH, int64_t KW, int64_t SH, int64_t SW, 
                int64_t PL, int64_t PR, const c10::optional<Tensor>& out) {
   need(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "maxpool: NHWC with C % 8 == 0");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int Ho = (H + PT + PB - KH) / SH + 1, Wo = (W + PL + PR - KW) / SW + 1;
   Tensor y = out.has_value() ? *out : torch::empty({N, Ho, Wo, C}, x.options());
@@ -134,7 +135,7 @@ Tensor maxpool(const Tensor& x, int64_t KH, int64_t KW, int64_t SH, int64_t SW, 
 Tensor global_avgpool(const Tensor& x, const c10::optional<Tensor>& out) {
   need(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "global_avgpool: NHWC with C % 8 == 0");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
   Tensor y = out.has_value() ? *out : torch::empty({N, C}, x.options());
   need(y, at::kBFloat16, "out");
@@ -148,7 +149,7 @@ std::vector<Tensor> softmax_argmax(const Tensor& logits, bool want_probs, bool w
   TORCH_CHECK(logits.is_cuda() && logits.is_contiguous(), "logits must be contiguous GPU");
   const bool bf = logits.scalar_type() == at::kBFloat16;
   TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "logits must be f32 or bf16");
-  c10::hip::HIPGuard guard(logits.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
   const int cols = logits.size(-1);
   const int rows = logits.numel() / cols;
   Tensor probs, classes;
@@ -170,7 +171,7 @@ std::vector<Tensor> softmax_argmax(const Tensor& logits, bool want_probs, bool w
 
 Tensor cast_bf16(const Tensor& x, const c10::optional<Tensor>& out) {
   need(x, at::kFloat, "x");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   Tensor y = out.has_value() ? *out : torch::empty(x.sizes(), x.options().dtype(at::kBFloat16));
   need(y, at::kBFloat16, "out");
   check(tfsk::cast_f32_bf16_launch(x.data_ptr<float>(), bf16p_mut(y), x.numel(), cur_stream(x)), "cast");
@@ -182,7 +183,7 @@ Tensor layernorm(const Tensor& x, const c10::optional<Tensor>& residual, const T
   need(x, at::kBFloat16, "x");
   need(gamma, at::kFloat, "gamma");
   need(beta, at::kFloat, "beta");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int cols = x.size(-1);
   TORCH_CHECK(cols % 8 == 0 && gamma.numel() == cols && beta.numel() == cols, "layernorm shapes");
   const int rows = x.numel() / cols;
@@ -208,7 +209,7 @@ Tensor embed_ln(const Tensor& ids, const c10::optional<Tensor>& type_ids, const 
   need(gamma, at::kFloat, "gamma");
   need(beta, at::kFloat, "beta");
   TORCH_CHECK(ids.dim() == 2, "ids must be [batch, seq]");
-  c10::hip::HIPGuard guard(ids.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(ids.device());
   const int B = ids.size(0), S = ids.size(1), Hd = word.size(1);
   TORCH_CHECK(Hd % 8 == 0 && pos.size(1) == Hd && type.size(1) == Hd && pos.size(0) >= S, "embedding shapes");
   const int64_t* tt = nullptr;
@@ -228,7 +229,7 @@ Tensor attention(const Tensor& qkv, const c10::optional<Tensor>& mask_bias, int6
                  const c10::optional<Tensor>& out) {
   need(qkv, at::kBFloat16, "qkv");
   TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, S, 3*H*D]");
-  c10::hip::HIPGuard guard(qkv.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   const int B = qkv.size(0), S = qkv.size(1), HD3 = qkv.size(2);
   TORCH_CHECK(HD3 % (3 * heads) == 0, "qkv width must be 3*heads*head_dim");
   const int D = HD3 / (3 * heads);
