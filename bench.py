@@ -1,0 +1,174 @@
+"""Headline benchmark: Predict RPCs/sec (+ p50 latency), ResNet-50 v1.5, MI355X.
+
+BASELINE.json metric: "Predict RPCs/sec + p50 latency, ResNet-50 batch=1/32 at
+1/2/4/8 MI355X".  One rank per GPU (torchrun sets RANK/LOCAL_RANK/WORLD_SIZE);
+each rank is a full model server on its GPU:
+
+* rank 0 writes a random-init ResNet-50 v1.5 SavedModel (no network: synthetic
+  weights of the real architecture); every rank loads it through the RCCL
+  weight broadcast (parallel/weights.py) when WORLD_SIZE > 1;
+* the server is the native HTTP/2 gRPC front end with the Predict fast path:
+  C++ decode -> pinned batch slots -> fused gfx950 kernels in a HIP graph ->
+  C++ encode (dynamic batching: --batch requests per GPU batch);
+* load: the native gRPC load generator (C++, separate threads, real TCP
+  loopback connections, HTTP/2 framing) sends batch-1 PredictRequests exactly
+  as the reference Rust client builds them (alias "input", DT_FLOAT float_val,
+  224x224x3; src/lib.rs:229-263), drawn from 64 distinct synthetic images.
+
+A *step* = ``--batch`` Predict RPCs (one full GPU batch per rank).  W warmup
+steps are untimed; then exactly K steps are timed between barriers with
+``torch.cuda.synchronize()`` on both sides; the max time over ranks is used
+and ``value`` = total RPCs of all ranks / that time (weak scaling: fixed work
+per GPU).  Extra fields report p50/p99 latency.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Predict RPCs/sec + p50 latency, ResNet-50 batch=1/32 at 1/2/4/8 MI355X"
+PREDICT = "/tensorflow.serving.PredictionService/Predict"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=32, help="server batch size (requests per GPU batch)")
+    ap.add_argument("--request-batch", type=int, default=1, help="images per Predict request")
+    ap.add_argument("--concurrency", type=int, default=0, help="in-flight RPCs per rank (default 4*batch)")
+    ap.add_argument("--connections", type=int, default=16)
+    ap.add_argument("--client-threads", type=int, default=4)
+    ap.add_argument("--io-threads", type=int, default=6)
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--transport", default="native", choices=["native", "grpc"])
+    ap.add_argument("--batch-timeout-us", type=int, default=2000)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=device)
+    logging.basicConfig(level=logging.WARNING)
+
+    from rust_tensorflow_serving2_amd import _C, native
+    from rust_tensorflow_serving2_amd.models import resnet
+    from rust_tensorflow_serving2_amd.server.server import ModelServer, ServerOptions
+    from rust_tensorflow_serving2_amd.server.servable import ServableOptions
+
+    base = os.path.join(tempfile.gettempdir(), f"tfserve_bench_{os.environ.get('MASTER_PORT', 'solo')}", "resnet")
+    if rank == 0 and not os.path.exists(os.path.join(base, "1", "saved_model.pb")):
+        resnet.export(os.path.join(base, "1"), seed=0, image_size=args.image_size)
+    if world > 1:
+        dist.barrier()
+
+    weight_source = None
+    if world > 1:
+        from rust_tensorflow_serving2_amd.parallel.weights import RcclWeightSource
+        weight_source = RcclWeightSource(device=device)
+    sopts = ServableOptions(device=str(device), max_batch_size=args.batch,
+                            allowed_batch_sizes=tuple(sorted({1, 2, 4, 8, 16, args.batch})))
+    port = (args.port + local) if args.port else 0
+    server = ModelServer(ServerOptions(port=port, host="127.0.0.1", model_name="resnet", model_base_path=base,
+                                       device=str(device), transport=args.transport, servable=sopts,
+                                       file_system_poll_wait_seconds=0, weight_source=weight_source,
+                                       monitoring=False))
+    t_load = time.perf_counter()
+    server.start()
+    t_load = time.perf_counter() - t_load
+    if args.transport == "native":
+        tr = server.transports[0]
+        # wait for the fast-path endpoint (registered by the manager listener)
+        for _ in range(600):
+            if tr.stats().get("endpoints"):
+                break
+            time.sleep(0.1)
+
+    # requests exactly as the reference client builds them
+    rng = np.random.default_rng(1234 + rank)
+    bodies = []
+    for _ in range(64):
+        img = rng.random((args.request_batch, args.image_size, args.image_size, 3), dtype=np.float32)
+        bodies.append(native.encode_predict_request(native.spec_tuple("resnet", None, None, "serving_default"),
+                                                    {"input": img}))
+    conc = args.concurrency or 4 * args.batch
+    per_step = max(1, args.batch // args.request_batch)
+
+    def drive(n):
+        return _C.run_loadgen("127.0.0.1", server.port, PREDICT, bodies, n, conc, args.connections,
+                              args.client_threads, 600.0)
+
+    w = drive(max(per_step, args.warmup * per_step))
+    if w["errors"]:
+        raise SystemExit(f"warmup errors: {w['first_error']}")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = drive(args.steps * per_step)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lat = np.asarray(r["latency_us"], dtype=np.float64)
+    mine = torch.tensor([elapsed, float(r["ok"]), float(r["errors"]), np.percentile(lat, 50) if lat.size else 0,
+                         np.percentile(lat, 99) if lat.size else 0], dtype=torch.float64, device=device)
+    if world > 1:
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        allv = torch.stack(allv).cpu().numpy()
+    else:
+        allv = mine.cpu().numpy()[None]
+    stats = server.transports[0].stats() if args.transport == "native" else {}
+    if rank == 0:
+        t_max = float(allv[:, 0].max())
+        total_ok = float(allv[:, 1].sum())
+        value = total_ok / t_max
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "Predict RPCs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * t_max / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic 224x224x3 f32 images (float_val, batch-1 PredictRequests as the Rust client "
+                    "sends), random-init ResNet-50 v1.5 weights",
+            "config": {"model": "ResNet-50 v1.5", "global_batch": args.batch * world, "seq_len": None,
+                       "parallelism": f"dp{world}", "server_batch": args.batch,
+                       "request_batch": args.request_batch, "image_size": args.image_size,
+                       "transport": args.transport, "concurrency_per_gpu": conc},
+            "images_per_s": round(value * args.request_batch, 1),
+            "p50_latency_ms": round(float(np.median(allv[:, 3])) / 1e3, 3),
+            "p99_latency_ms": round(float(allv[:, 4].max()) / 1e3, 3),
+            "errors": int(allv[:, 2].sum()),
+            "load_s": round(t_load, 2),
+            "fast_path_share": round(stats.get("fast_path", 0) / max(1, stats.get("requests", 1)), 3) if stats else None,
+        }
+        print(json.dumps(out), flush=True)
+    server.stop()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -76,6 +76,16 @@ def _py_includes():
     return [f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}"]
 
 
+def _nghttp2_lib() -> str:
+    """libnghttp2 runtime (no -dev package in the image: link the .so.N directly)."""
+    for d in ("/usr/lib/x86_64-linux-gnu", "/usr/lib64", "/usr/lib", "/lib/x86_64-linux-gnu"):
+        for name in ("libnghttp2.so", "libnghttp2.so.14"):
+            p = os.path.join(d, name)
+            if os.path.exists(p):
+                return p
+    raise RuntimeError("libnghttp2 not found")
+
+
 def build_cpu(jobs: int = 8, verbose: bool = False) -> str:
     out = os.path.join(PKG, "_C" + EXT)
     sources = sorted(glob.glob(os.path.join(CSRC, "*.cpp")))
@@ -84,7 +94,8 @@ def build_cpu(jobs: int = 8, verbose: bool = False) -> str:
              "-Wall", "-Wno-unused-function", "-pthread"] + _py_includes()
     objs, changed = _compile_all(os.environ.get("CXX", "g++"), sources, headers, flags, "cpu", jobs)
     if changed or not os.path.exists(out):
-        _run([os.environ.get("CXX", "g++"), "-shared", "-pthread", "-o", out + ".tmp"] + objs + ["-ldl"])
+        _run([os.environ.get("CXX", "g++"), "-shared", "-pthread", "-o", out + ".tmp"] + objs +
+             [_nghttp2_lib(), "-ldl"])
         os.replace(out + ".tmp", out)
     if verbose:
         print("built", out)

@@ -1,0 +1,303 @@
+// Predict fast path + dynamic batching into pinned slots (see batcher.h).
+#include "batcher.h"
+
+#include <cstring>
+
+namespace tfs {
+
+static const char* kPredictPath = "/tensorflow.serving.PredictionService/Predict";
+
+Endpoint::Endpoint(int id_, std::string model_, int64_t version_, std::string signature_,
+                   std::vector<TensorSpecC> inputs_, std::vector<TensorSpecC> outputs_, int max_rows_,
+                   int64_t timeout_us_, int max_wait_ms_)
+    : id(id_), model(std::move(model_)), version(version_), signature(std::move(signature_)),
+      inputs(std::move(inputs_)), outputs(std::move(outputs_)), max_rows(max_rows_), timeout_us(timeout_us_),
+      max_wait_ms(max_wait_ms_) {}
+
+void Endpoint::set_slot_buffers(int slot, std::vector<uint8_t*> in_base, std::vector<const uint8_t*> out_base) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (slot >= int(slots_.size())) slots_.resize(slot + 1);
+  slots_[slot].in_base = std::move(in_base);
+  slots_[slot].out_base = std::move(out_base);
+}
+
+int Endpoint::open_slot_locked(int n) {
+  if (open_ >= 0) {
+    Slot& s = slots_[open_];
+    if (s.reserved + n <= max_rows) return open_;
+    s.state = kReady;
+    open_ = -1;
+    cv_ready_.notify_all();
+  }
+  const int N = int(slots_.size());
+  for (int k = 0; k < N; ++k) {
+    const int idx = (next_ + k) % N;
+    if (slots_[idx].state == kFree && !slots_[idx].in_base.empty()) {
+      Slot& s = slots_[idx];
+      s.state = kOpen;
+      s.first = Clock::now();
+      s.reserved = s.copied = 0;
+      open_ = idx;
+      next_ = (idx + 1) % N;
+      return idx;
+    }
+  }
+  return -1;
+}
+
+int Endpoint::offer(std::unique_ptr<Call>& call, const PredictRequestView& req) {
+  if (req.inputs.size() != inputs.size()) return 1;
+  // match aliases (inputs sorted by alias on registration)
+  std::vector<const TensorView*> tv(inputs.size(), nullptr);
+  for (auto& kv : req.inputs) {
+    bool found = false;
+    for (size_t i = 0; i < inputs.size(); ++i) {
+      if (inputs[i].alias == kv.first) {
+        tv[i] = &kv.second;
+        found = true;
+        break;
+      }
+    }
+    if (!found) return 1;
+  }
+  int n = -1;
+  for (size_t i = 0; i < inputs.size(); ++i) {
+    const TensorView& t = *tv[i];
+    const TensorSpecC& s = inputs[i];
+    if (t.dtype != s.dtype || t.shape.size() != s.row_shape.size() + 1) return 1;
+    if (t.storage != Storage::kView && t.storage != Storage::kOwned) return 1;
+    for (size_t d = 0; d < s.row_shape.size(); ++d)
+      if (t.shape[d + 1] != s.row_shape[d]) return 1;
+    const int64_t rows = t.shape[0];
+    if (rows < 1 || rows > max_rows) return 1;
+    if (n < 0) n = int(rows);
+    if (rows != n) return 1;
+    if (t.count != size_t(rows) * s.row_elems) return 1;
+    if (t.nbytes != size_t(rows) * s.row_bytes) return 1;
+  }
+  std::vector<int> outs;
+  for (auto& a : req.output_filter) {
+    int found = -1;
+    for (size_t j = 0; j < outputs.size(); ++j)
+      if (outputs[j].alias == a) found = int(j);
+    if (found < 0) return 1;
+    for (int o : outs)
+      if (o == found) return 1;   // duplicate alias -> python reports it
+    outs.push_back(found);
+  }
+
+  // the Call is heap-allocated and its body is never modified again, so this
+  // pointer stays valid after the unique_ptr moves into the slot
+  const uint8_t* body = reinterpret_cast<const uint8_t*>(call->body.data());
+  int slot = -1, r0 = 0;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (closed_) return 1;
+    auto deadline = Clock::now() + std::chrono::milliseconds(max_wait_ms);
+    while ((slot = open_slot_locked(n)) < 0) {
+      if (cv_free_.wait_until(lk, deadline) == std::cv_status::timeout && (slot = open_slot_locked(n)) < 0) {
+        st_.rejected++;
+        return 2;
+      }
+      if (closed_) return 1;
+    }
+    Slot& s = slots_[slot];
+    r0 = s.reserved;
+    s.reserved += n;
+    Pending p;
+    p.row0 = r0;
+    p.n = n;
+    p.outs = std::move(outs);
+    p.call = std::move(call);
+    s.reqs.push_back(std::move(p));
+    st_.requests++;
+    if (s.reserved == max_rows) {
+      s.state = kReady;
+      open_ = -1;
+    }
+  }
+  // copy outside the lock: IO threads fill different rows of a slot in parallel
+  Slot& s = slots_[slot];
+  for (size_t i = 0; i < inputs.size(); ++i) {
+    const TensorView& t = *tv[i];
+    const uint8_t* src = t.storage == Storage::kView ? body + t.offset
+                                                     : reinterpret_cast<const uint8_t*>(t.owned.data());
+    std::memcpy(s.in_base[i] + size_t(r0) * inputs[i].row_bytes, src, t.nbytes);
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    s.copied += n;
+    if (s.copied == s.reserved) cv_ready_.notify_all();
+  }
+  return 0;
+}
+
+int Endpoint::acquire(int slot, int timeout_ms) {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (slot < 0 || slot >= int(slots_.size())) return -1;
+  const auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (!closed_) {
+    Slot& s = slots_[slot];
+    const auto now = Clock::now();
+    if (s.state == kReady && s.reserved > 0 && s.copied == s.reserved) {
+      s.state = kRunning;
+      st_.batches++;
+      st_.rows += s.reserved;
+      return s.reserved;
+    }
+    if (s.state == kOpen && s.reserved > 0) {
+      const auto due = s.first + std::chrono::microseconds(timeout_us);
+      if (now >= due) {
+        s.state = kReady;
+        if (open_ == slot) open_ = -1;
+        continue;
+      }
+      if (now >= deadline) return 0;
+      cv_ready_.wait_until(lk, std::min(due, deadline));
+      continue;
+    }
+    if (now >= deadline) return 0;
+    cv_ready_.wait_until(lk, deadline);
+  }
+  return -1;
+}
+
+void Endpoint::complete(int slot, Server& srv) {
+  Slot& s = slots_[slot];
+  ModelSpecView spec;
+  spec.name = model;
+  spec.has_version = true;
+  spec.version = version;
+  spec.signature_name = signature;
+  std::vector<OutTensor> outs;
+  for (auto& p : s.reqs) {
+    outs.clear();
+    const size_t nout = p.outs.empty() ? outputs.size() : p.outs.size();
+    for (size_t k = 0; k < nout; ++k) {
+      const int j = p.outs.empty() ? int(k) : p.outs[k];
+      const TensorSpecC& o = outputs[j];
+      OutTensor t;
+      t.alias = o.alias;
+      t.dtype = o.dtype;
+      t.shape.push_back(p.n);
+      t.shape.insert(t.shape.end(), o.row_shape.begin(), o.row_shape.end());
+      t.data = s.out_base[j] + size_t(p.row0) * o.row_bytes;
+      t.count = size_t(p.n) * o.row_elems;
+      outs.push_back(std::move(t));
+    }
+    std::string body = encode_predict_response(&spec, outs, false);
+    srv.respond(*p.call, 0, std::string(), std::move(body));
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  s.reqs.clear();
+  s.reserved = s.copied = 0;
+  s.state = kFree;
+  cv_free_.notify_all();
+}
+
+void Endpoint::fail(int slot, Server& srv, int code, const std::string& msg) {
+  Slot& s = slots_[slot];
+  for (auto& p : s.reqs) srv.respond(*p.call, code, msg, std::string());
+  std::lock_guard<std::mutex> g(mu_);
+  s.reqs.clear();
+  s.reserved = s.copied = 0;
+  s.state = kFree;
+  cv_free_.notify_all();
+}
+
+void Endpoint::close() {
+  std::lock_guard<std::mutex> g(mu_);
+  closed_ = true;
+  cv_ready_.notify_all();
+  cv_free_.notify_all();
+}
+
+EndpointStats Endpoint::stats() {
+  std::lock_guard<std::mutex> g(mu_);
+  return st_;
+}
+
+// ---------------------------------------------------------------- FastPath
+static std::string route_key(const std::string& m, const std::string& s, int64_t v) {
+  std::string k = m;
+  k.push_back('\0');
+  k += s;
+  k.push_back('\0');
+  k += v < 0 ? std::string("L") : std::to_string(v);
+  return k;
+}
+
+bool FastPath::try_dispatch(std::unique_ptr<Call>& call) {
+  if (call->method != kPredictPath) return false;
+  PredictRequestView req;
+  try {
+    parse_predict_request(reinterpret_cast<const uint8_t*>(call->body.data()), call->body.size(), req);
+  } catch (const std::exception&) {
+    return false;   // python path reports the precise error
+  }
+  if (!req.has_spec || req.spec.has_label) return false;
+  const std::string sig = req.spec.signature_name.empty() ? "serving_default" : req.spec.signature_name;
+  std::shared_ptr<Endpoint> ep;
+  {
+    std::shared_lock<std::shared_mutex> g(mu_);
+    auto it = routes_.find(route_key(req.spec.name, sig, req.spec.has_version ? req.spec.version : -1));
+    if (it == routes_.end()) return false;
+    auto e = eps_.find(it->second);
+    if (e == eps_.end()) return false;
+    ep = e->second;
+  }
+  const int r = ep->offer(call, req);
+  if (r == 0) return true;
+  if (r == 2) {
+    srv_->respond(*call, 14 /*UNAVAILABLE*/, "The batch scheduling queue is full", std::string());
+    return true;
+  }
+  return false;
+}
+
+int FastPath::add_endpoint(std::shared_ptr<Endpoint> ep) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  eps_[ep->id] = ep;
+  return ep->id;
+}
+
+std::shared_ptr<Endpoint> FastPath::endpoint(int id) {
+  std::shared_lock<std::shared_mutex> g(mu_);
+  auto it = eps_.find(id);
+  return it == eps_.end() ? nullptr : it->second;
+}
+
+void FastPath::remove_endpoint(int id) {
+  std::shared_ptr<Endpoint> ep;
+  {
+    std::unique_lock<std::shared_mutex> g(mu_);
+    for (auto it = routes_.begin(); it != routes_.end();) {
+      if (it->second == id) it = routes_.erase(it);
+      else ++it;
+    }
+    auto it = eps_.find(id);
+    if (it != eps_.end()) {
+      ep = it->second;
+      eps_.erase(it);
+    }
+  }
+  if (ep) ep->close();
+}
+
+void FastPath::set_route(const std::string& model, const std::string& signature, int64_t version, int ep_id) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  const std::string k = route_key(model, signature, version);
+  if (ep_id < 0) routes_.erase(k);
+  else routes_[k] = ep_id;
+}
+
+void FastPath::clear_routes(const std::string& model) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  const std::string prefix = model + std::string(1, '\0');
+  for (auto it = routes_.begin(); it != routes_.end();) {
+    if (it->first.compare(0, prefix.size(), prefix) == 0) it = routes_.erase(it);
+    else ++it;
+  }
+}
+
+}  // namespace tfs

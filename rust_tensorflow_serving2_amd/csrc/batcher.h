@@ -1,0 +1,114 @@
+// Predict fast path + dynamic batching into pinned GPU staging slots.
+//
+// Python registers an *endpoint* per (model, version, signature) whose inputs
+// all have a leading batch dimension and static per-row shapes.  For each
+// Predict call the IO thread: decodes the request with the native codec (no
+// Python, no GIL), validates it against the endpoint, reserves rows in the
+// currently open batch *slot* and memcpy's the tensor bytes straight into
+// that slot's pinned host buffer (parallel across IO threads).  A GPU worker
+// (one per slot/lane) waits until its slot is full or the batch timeout
+// expires, runs the device program on the rows, and calls complete(): the
+// per-request PredictResponses are encoded from the pinned output buffers and
+// posted back to the IO threads.  Anything the fast path does not handle
+// (labels, fill-rule tensors, mismatched aliases/shapes, output filters with
+// unknown aliases, ...) falls through to the Python core, which produces the
+// exact TF-Serving error or result.
+#pragma once
+#include <map>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "http2.h"
+#include "wire.h"
+
+namespace tfs {
+
+struct TensorSpecC {
+  std::string alias;
+  int dtype = 0;
+  std::vector<int64_t> row_shape;
+  size_t row_elems = 1;
+  size_t row_bytes = 0;
+};
+
+struct Pending {
+  std::unique_ptr<Call> call;
+  int row0 = 0, n = 0;
+  std::vector<int> outs;   // output indices to encode (empty = all)
+};
+
+enum SlotState : int { kFree = 0, kOpen = 1, kReady = 2, kRunning = 3 };
+
+struct Slot {
+  std::vector<uint8_t*> in_base;     // per input: pinned [max_rows][row]
+  std::vector<const uint8_t*> out_base;
+  int reserved = 0;
+  int copied = 0;
+  int state = kFree;
+  Clock::time_point first;
+  std::vector<Pending> reqs;
+};
+
+struct EndpointStats {
+  uint64_t requests = 0, batches = 0, rows = 0, rejected = 0;
+};
+
+class Endpoint {
+ public:
+  Endpoint(int id, std::string model, int64_t version, std::string signature, std::vector<TensorSpecC> inputs,
+           std::vector<TensorSpecC> outputs, int max_rows, int64_t timeout_us, int max_wait_ms);
+  void set_slot_buffers(int slot, std::vector<uint8_t*> in_base, std::vector<const uint8_t*> out_base);
+  // IO thread.  Returns 0 if accepted, 1 if not applicable (slow path), 2 if rejected (queue full).
+  int offer(std::unique_ptr<Call>& call, const PredictRequestView& req);
+  // GPU worker side.
+  int acquire(int slot, int timeout_ms);
+  void complete(int slot, Server& srv);
+  void fail(int slot, Server& srv, int code, const std::string& msg);
+  void close();
+
+  const int id;
+  const std::string model;
+  const int64_t version;
+  const std::string signature;
+  std::vector<TensorSpecC> inputs, outputs;
+  const int max_rows;
+  const int64_t timeout_us;
+  const int max_wait_ms;
+  EndpointStats stats();
+
+ private:
+  int open_slot_locked(int n);
+  std::mutex mu_;
+  std::condition_variable cv_ready_, cv_free_;
+  std::vector<Slot> slots_;
+  int open_ = -1;
+  int next_ = 0;
+  bool closed_ = false;
+  EndpointStats st_;
+};
+
+class FastPath {
+ public:
+  explicit FastPath(Server* srv) : srv_(srv) {}
+  bool try_dispatch(std::unique_ptr<Call>& call);
+  int add_endpoint(std::shared_ptr<Endpoint> ep);
+  std::shared_ptr<Endpoint> endpoint(int id);
+  void remove_endpoint(int id);
+  // route (model, signature) [+version] to an endpoint; version < 0 = "latest"
+  void set_route(const std::string& model, const std::string& signature, int64_t version, int ep_id);
+  void clear_routes(const std::string& model);
+  int next_id() { return ++ids_; }
+  Server* server() { return srv_; }
+
+ private:
+  Server* srv_;
+  std::shared_mutex mu_;
+  std::map<int, std::shared_ptr<Endpoint>> eps_;
+  std::map<std::string, int> routes_;   // key = model \0 signature \0 version|"L"
+  int ids_ = 0;
+};
+
+}  // namespace tfs

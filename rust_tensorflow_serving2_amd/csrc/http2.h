@@ -1,0 +1,105 @@
+// Native gRPC-over-HTTP/2 front end (server) and load generator (client).
+//
+// Replaces the transport layer the reference leaves to tonic/hyper/h2 on the
+// client side (src/lib.rs:132-138; Cargo.lock tonic 0.1 / h2 0.2) and to the
+// external TF-Serving container on the server side (serving/rundocker.sh:15).
+// Design: N epoll IO threads, each with its own SO_REUSEPORT listening socket
+// (kernel load-balances connections across threads *and* across server
+// processes, one per GPU); libnghttp2 for framing/HPACK/flow control; request
+// bodies assembled per stream and dispatched either to the C++ Predict fast
+// path (batcher.h) or to a queue drained by Python control-plane threads.
+// Responses from any thread are posted to the owning IO thread (eventfd).
+#pragma once
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace tfs {
+
+using Clock = std::chrono::steady_clock;
+
+// One completed unary request waiting for its answer.
+struct Call {
+  uint64_t conn_id = 0;
+  int io_index = 0;
+  int32_t stream_id = 0;
+  std::string method;      // ":path", e.g. /tensorflow.serving.PredictionService/Predict
+  std::string body;        // protobuf message (gRPC 5-byte prefix stripped)
+  Clock::time_point arrival;
+  int64_t timeout_us = 0;  // grpc-timeout, 0 = none
+};
+
+class Server;
+
+// Fast-path hook: return true when the call was taken (it will be answered
+// later through Server::respond).
+using FastDispatch = std::function<bool(std::unique_ptr<Call>&)>;
+
+struct ServerStats {
+  std::atomic<uint64_t> connections{0}, requests{0}, fast_path{0}, slow_path{0}, responses{0}, errors{0};
+  std::atomic<uint64_t> bytes_in{0}, bytes_out{0};
+};
+
+class IoThread;
+
+class Server {
+ public:
+  Server(const std::string& host, int port, int io_threads, size_t max_message);
+  ~Server();
+  void start();
+  void stop();
+  int port() const { return port_; }
+
+  void set_fast_dispatch(FastDispatch fn) { fast_ = std::move(fn); }
+  // Answer a call (thread-safe).  status = grpc code; body ignored unless OK.
+  void respond(uint64_t conn_id, int io_index, int32_t stream_id, int status, std::string message,
+               std::string body);
+  void respond(const Call& c, int status, std::string message, std::string body) {
+    respond(c.conn_id, c.io_index, c.stream_id, status, std::move(message), std::move(body));
+  }
+  // Slow path queue for the Python control plane.
+  std::unique_ptr<Call> next_call(int timeout_ms);
+  void push_call(std::unique_ptr<Call> c);
+
+  // Called by IO threads when a request is complete.
+  void dispatch(std::unique_ptr<Call> c);
+  size_t max_message() const { return max_message_; }
+  ServerStats stats;
+
+ private:
+  std::string host_;
+  int port_;
+  size_t max_message_;
+  std::vector<std::unique_ptr<IoThread>> io_;
+  FastDispatch fast_;
+  std::mutex qmu_;
+  std::condition_variable qcv_;
+  std::deque<std::unique_ptr<Call>> queue_;
+  std::atomic<bool> running_{false};
+};
+
+// ---------------------------------------------------------------- load generator
+struct LoadGenResult {
+  uint64_t ok = 0, errors = 0;
+  double elapsed_s = 0;
+  std::vector<double> latency_us;   // per successful request
+  std::string first_error;
+  uint64_t bytes_sent = 0, bytes_recv = 0;
+};
+
+// Drive `total` unary calls of `method` against host:port with `concurrency`
+// streams in flight spread over `connections` HTTP/2 connections served by
+// `threads` client threads.  Bodies are used round-robin (pre-serialised).
+LoadGenResult run_loadgen(const std::string& host, int port, const std::string& method,
+                          const std::vector<std::string>& bodies, uint64_t total, int concurrency,
+                          int connections, int threads, double timeout_s);
+
+}  // namespace tfs

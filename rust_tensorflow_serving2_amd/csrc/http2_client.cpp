@@ -1,0 +1,338 @@
+// Native gRPC load generator (HTTP/2 client on libnghttp2), GIL-free.
+//
+// The benchmark client of the serving stack: pre-serialised
+// request bodies (e.g. the exact PredictRequest the reference client builds,
+// src/lib.rs:244-263) are fired over `connections` HTTP/2 connections with
+// `concurrency` unary calls in flight; per-call latency is recorded from
+// submit to end-of-stream (trailers) on the client clock.
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+#include "http2.h"
+#include "nghttp2_min.h"
+#include "wire.h"
+
+namespace tfs {
+
+namespace {
+
+struct Shared {
+  std::vector<std::string> framed;
+  std::string path, authority;
+  uint64_t total;
+  std::atomic<uint64_t> issued{0};
+  std::atomic<uint64_t> finished{0};
+  Clock::time_point deadline;
+};
+
+struct Req {
+  const std::string* body;
+  size_t off = 0;
+  Clock::time_point t0;
+  int http_status = 0;
+  int grpc_status = -1;
+  std::string grpc_message;
+  size_t bytes = 0;
+};
+
+struct ClientConn {
+  int fd = -1;
+  nghttp2_session* sess = nullptr;
+  Shared* sh = nullptr;
+  int inflight = 0;
+  int target = 0;
+  bool dead = false;
+  std::string wbuf;
+  size_t wpos = 0;
+  bool want_out = false;
+  uint64_t next_body = 0;
+  // results
+  std::vector<double>* lat;
+  uint64_t* ok;
+  uint64_t* err;
+  std::string* first_error;
+  uint64_t* bytes_sent;
+  uint64_t* bytes_recv;
+};
+
+ssize_t read_body(nghttp2_session*, int32_t, uint8_t* buf, size_t length, uint32_t* flags,
+                  nghttp2_data_source* src, void*) {
+  Req* r = static_cast<Req*>(src->ptr);
+  const size_t n = std::min(length, r->body->size() - r->off);
+  memcpy(buf, r->body->data() + r->off, n);
+  r->off += n;
+  if (r->off == r->body->size()) *flags |= NGHTTP2_DATA_FLAG_EOF;
+  return ssize_t(n);
+}
+
+int on_header(nghttp2_session* s, const nghttp2_frame* f, const uint8_t* name, size_t nl, const uint8_t* value,
+              size_t vl, uint8_t, void*) {
+  Req* r = static_cast<Req*>(nghttp2_session_get_stream_user_data(s, f->hd.stream_id));
+  if (!r) return 0;
+  std::string n((const char*)name, nl);
+  if (n == ":status") r->http_status = atoi(std::string((const char*)value, vl).c_str());
+  else if (n == "grpc-status") r->grpc_status = atoi(std::string((const char*)value, vl).c_str());
+  else if (n == "grpc-message") r->grpc_message.assign((const char*)value, vl);
+  return 0;
+}
+
+int on_data(nghttp2_session* s, uint8_t, int32_t sid, const uint8_t*, size_t len, void*) {
+  Req* r = static_cast<Req*>(nghttp2_session_get_stream_user_data(s, sid));
+  if (r) r->bytes += len;
+  return 0;
+}
+
+bool submit_one(ClientConn* c);
+
+int on_close(nghttp2_session* s, int32_t sid, uint32_t err, void* ud) {
+  ClientConn* c = static_cast<ClientConn*>(ud);
+  Req* r = static_cast<Req*>(nghttp2_session_get_stream_user_data(s, sid));
+  if (!r) return 0;
+  const double us = std::chrono::duration<double, std::micro>(Clock::now() - r->t0).count();
+  *c->bytes_recv += r->bytes;
+  if (err == 0 && r->http_status == 200 && r->grpc_status == 0) {
+    (*c->ok)++;
+    c->lat->push_back(us);
+  } else {
+    (*c->err)++;
+    if (c->first_error->empty())
+      *c->first_error = "http " + std::to_string(r->http_status) + " grpc-status " + std::to_string(r->grpc_status) +
+                        " " + r->grpc_message + (err ? " rst " + std::to_string(err) : "");
+  }
+  delete r;
+  c->inflight--;
+  c->sh->finished++;
+  submit_one(c);
+  return 0;
+}
+
+bool submit_one(ClientConn* c) {
+  Shared* sh = c->sh;
+  if (c->inflight >= c->target) return false;
+  const uint64_t k = sh->issued.fetch_add(1);
+  if (k >= sh->total) {
+    sh->issued.fetch_sub(1);
+    return false;
+  }
+  Req* r = new Req();
+  r->body = &sh->framed[(c->next_body++) % sh->framed.size()];
+  r->t0 = Clock::now();
+  static const std::string m = ":method", post = "POST", sc = ":scheme", http = "http", pa = ":path",
+                           au = ":authority", ct = "content-type", grpc = "application/grpc", te = "te",
+                           tr = "trailers";
+  nghttp2_nv nv[] = {
+      {(uint8_t*)m.data(), (uint8_t*)post.data(), m.size(), post.size(), 0},
+      {(uint8_t*)sc.data(), (uint8_t*)http.data(), sc.size(), http.size(), 0},
+      {(uint8_t*)pa.data(), (uint8_t*)sh->path.data(), pa.size(), sh->path.size(), 0},
+      {(uint8_t*)au.data(), (uint8_t*)sh->authority.data(), au.size(), sh->authority.size(), 0},
+      {(uint8_t*)ct.data(), (uint8_t*)grpc.data(), ct.size(), grpc.size(), 0},
+      {(uint8_t*)te.data(), (uint8_t*)tr.data(), te.size(), tr.size(), 0},
+  };
+  nghttp2_data_provider prd;
+  prd.source.ptr = r;
+  prd.read_callback = read_body;
+  int32_t sid = nghttp2_submit_request(c->sess, nullptr, nv, 6, &prd, r);
+  if (sid < 0) {
+    delete r;
+    sh->issued.fetch_sub(1);
+    c->dead = true;
+    return false;
+  }
+  *c->bytes_sent += r->body->size();
+  c->inflight++;
+  return true;
+}
+
+int connect_to(const std::string& host, int port) {
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) != 0 || !res)
+    throw std::runtime_error("cannot resolve " + host);
+  int fd = socket(AF_INET, SOCK_STREAM, 0);
+  if (connect(fd, res->ai_addr, res->ai_addrlen) != 0) {
+    int e = errno;
+    freeaddrinfo(res);
+    ::close(fd);
+    throw std::runtime_error(std::string("connect failed: ") + strerror(e));
+  }
+  freeaddrinfo(res);
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  int sz = 4 << 20;
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+  fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK);
+  return fd;
+}
+
+bool cflush(ClientConn* c, int ep, uint64_t tag) {
+  for (;;) {
+    if (c->wpos < c->wbuf.size()) {
+      ssize_t n = send(c->fd, c->wbuf.data() + c->wpos, c->wbuf.size() - c->wpos, MSG_NOSIGNAL);
+      if (n < 0) {
+        if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+        return false;
+      }
+      c->wpos += size_t(n);
+      continue;
+    }
+    c->wbuf.clear();
+    c->wpos = 0;
+    const uint8_t* data;
+    ssize_t n = nghttp2_session_mem_send(c->sess, &data);
+    if (n < 0) return false;
+    if (n == 0) break;
+    ssize_t w = send(c->fd, data, size_t(n), MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno != EAGAIN && errno != EWOULDBLOCK) return false;
+      w = 0;
+    }
+    if (w < n) c->wbuf.assign((const char*)data + w, size_t(n - w));
+  }
+  const bool pending = c->wpos < c->wbuf.size();
+  if (pending != c->want_out) {
+    epoll_event ev{};
+    ev.events = EPOLLIN | (pending ? EPOLLOUT : 0);
+    ev.data.u64 = tag;
+    epoll_ctl(ep, EPOLL_CTL_MOD, c->fd, &ev);
+    c->want_out = pending;
+  }
+  return true;
+}
+
+void client_thread(Shared* sh, const std::string& host, int port, int nconn, int per_conn, LoadGenResult* out) {
+  nghttp2_session_callbacks* cbs;
+  nghttp2_session_callbacks_new(&cbs);
+  nghttp2_session_callbacks_set_on_header_callback(cbs, on_header);
+  nghttp2_session_callbacks_set_on_data_chunk_recv_callback(cbs, on_data);
+  nghttp2_session_callbacks_set_on_stream_close_callback(cbs, on_close);
+  int ep = epoll_create1(0);
+  std::vector<std::unique_ptr<ClientConn>> conns;
+  for (int i = 0; i < nconn; ++i) {
+    auto c = std::make_unique<ClientConn>();
+    try {
+      c->fd = connect_to(host, port);
+    } catch (const std::exception& e) {
+      if (out->first_error.empty()) out->first_error = e.what();
+      out->errors++;
+      continue;
+    }
+    c->sh = sh;
+    c->target = per_conn;
+    c->lat = &out->latency_us;
+    c->ok = &out->ok;
+    c->err = &out->errors;
+    c->first_error = &out->first_error;
+    c->bytes_sent = &out->bytes_sent;
+    c->bytes_recv = &out->bytes_recv;
+    c->next_body = uint64_t(i) * 7919;
+    nghttp2_session_client_new(&c->sess, cbs, c.get());
+    nghttp2_settings_entry iv[] = {{NGHTTP2_SETTINGS_MAX_CONCURRENT_STREAMS, 4096},
+                                   {NGHTTP2_SETTINGS_INITIAL_WINDOW_SIZE, 16u << 20}};
+    nghttp2_submit_settings(c->sess, NGHTTP2_FLAG_NONE, iv, 2);
+    nghttp2_session_set_local_window_size(c->sess, NGHTTP2_FLAG_NONE, 0, 1 << 30);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = conns.size();
+    epoll_ctl(ep, EPOLL_CTL_ADD, c->fd, &ev);
+    conns.push_back(std::move(c));
+  }
+  for (size_t i = 0; i < conns.size(); ++i) {
+    while (submit_one(conns[i].get())) {}
+    if (!cflush(conns[i].get(), ep, i)) conns[i]->dead = true;
+  }
+  std::vector<uint8_t> rbuf(1 << 20);
+  std::vector<epoll_event> evs(64);
+  for (;;) {
+    bool any_live = false;
+    for (auto& c : conns)
+      if (!c->dead && (c->inflight > 0)) any_live = true;
+    if (!any_live) break;
+    if (Clock::now() > sh->deadline) {
+      if (out->first_error.empty()) out->first_error = "load generator timed out";
+      break;
+    }
+    int n = epoll_wait(ep, evs.data(), int(evs.size()), 100);
+    for (int i = 0; i < n; ++i) {
+      const uint64_t idx = evs[i].data.u64;
+      ClientConn* c = conns[idx].get();
+      if (c->dead) continue;
+      if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) {
+        for (;;) {
+          ssize_t r = recv(c->fd, rbuf.data(), rbuf.size(), 0);
+          if (r > 0) {
+            if (nghttp2_session_mem_recv(c->sess, rbuf.data(), size_t(r)) < 0) { c->dead = true; break; }
+            if (size_t(r) < rbuf.size()) break;
+            continue;
+          }
+          if (r == 0 || (errno != EAGAIN && errno != EWOULDBLOCK)) c->dead = true;
+          break;
+        }
+      }
+      if (!c->dead && !cflush(c, ep, idx)) c->dead = true;
+      if (c->dead && out->first_error.empty()) out->first_error = "connection lost";
+    }
+  }
+  for (auto& c : conns) {
+    out->errors += uint64_t(std::max(0, c->inflight));
+    if (c->sess) nghttp2_session_del(c->sess);
+    if (c->fd >= 0) ::close(c->fd);
+  }
+  ::close(ep);
+  nghttp2_session_callbacks_del(cbs);
+}
+
+}  // namespace
+
+LoadGenResult run_loadgen(const std::string& host, int port, const std::string& method,
+                          const std::vector<std::string>& bodies, uint64_t total, int concurrency, int connections,
+                          int threads, double timeout_s) {
+  if (bodies.empty()) throw std::invalid_argument("no request bodies");
+  Shared sh;
+  sh.path = method;
+  sh.authority = host + ":" + std::to_string(port);
+  sh.total = total;
+  sh.deadline = Clock::now() + std::chrono::microseconds(int64_t(timeout_s * 1e6));
+  for (auto& b : bodies) {
+    std::string f(5 + b.size(), '\0');
+    grpc_frame_header(reinterpret_cast<uint8_t*>(&f[0]), uint32_t(b.size()));
+    memcpy(&f[5], b.data(), b.size());
+    sh.framed.push_back(std::move(f));
+  }
+  threads = std::max(1, std::min(threads, connections));
+  connections = std::max(connections, threads);
+  const int per_conn = std::max(1, concurrency / connections);
+  std::vector<LoadGenResult> parts(threads);
+  std::vector<std::thread> ts;
+  const auto t0 = Clock::now();
+  for (int t = 0; t < threads; ++t) {
+    const int nconn = connections / threads + (t < connections % threads ? 1 : 0);
+    ts.emplace_back(client_thread, &sh, host, port, nconn, per_conn, &parts[t]);
+  }
+  for (auto& t : ts) t.join();
+  LoadGenResult res;
+  res.elapsed_s = std::chrono::duration<double>(Clock::now() - t0).count();
+  for (auto& p : parts) {
+    res.ok += p.ok;
+    res.errors += p.errors;
+    res.bytes_sent += p.bytes_sent;
+    res.bytes_recv += p.bytes_recv;
+    res.latency_us.insert(res.latency_us.end(), p.latency_us.begin(), p.latency_us.end());
+    if (res.first_error.empty()) res.first_error = p.first_error;
+  }
+  return res;
+}
+
+}  // namespace tfs

@@ -5,16 +5,19 @@
 * Requests are padded up to a *batch bucket* (``allowed_batch_sizes``, else
   powers of two up to ``max_batch_size``).  Each bucket is warmed up eagerly
   once (kernel tile autotuning happens here), then captured into a HIP graph
-  with static input/output buffers; serving a batch is one H2D copy into the
-  static inputs, one ``graph.replay()``, one D2H copy of the outputs.
-* ``lanes`` independent (stream, buffers, graphs) sets let the H2D copy and
-  compute of consecutive batches overlap (one lane in flight per stream).
+  with static device input/output buffers.
+* ``lanes`` independent sets of {HIP stream, pinned host staging buffers sized
+  for the largest bucket, per-bucket graphs} let the H2D copy, compute and D2H
+  of consecutive batches overlap.  The pinned input buffers of a lane double as
+  the native fast path's batch *slot*: IO threads memcpy request tensors
+  directly into them (server/native_transport.py), so a batch costs one H2D
+  copy, one ``graph.replay()`` and one D2H copy.
 """
 from __future__ import annotations
 
 import logging
 import threading
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -37,6 +40,15 @@ def buckets_for(max_batch: int, allowed: Sequence[int] = ()) -> List[int]:
     return sorted(set(out))
 
 
+def _torch_dtype(dt: int) -> torch.dtype:
+    from ..graph.ops import DT_TO_TORCH
+    if dt == T.DT_BFLOAT16:
+        return torch.bfloat16
+    if dt in DT_TO_TORCH:
+        return DT_TO_TORCH[dt]
+    raise E.unimplemented(f"dtype {T.DT_NAMES.get(dt, dt)} is not supported on the GPU runtime")
+
+
 class _Lane:
     def __init__(self, device):
         self.stream = torch.cuda.Stream(device=device)
@@ -44,12 +56,13 @@ class _Lane:
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.static_in: Dict[int, List[torch.Tensor]] = {}
         self.static_out: Dict[int, List[torch.Tensor]] = {}
-        self.host_in: Dict[int, List[torch.Tensor]] = {}
-        self.host_out: Dict[int, List[torch.Tensor]] = {}
+        self.host_in: List[torch.Tensor] = []      # pinned [max_bucket, ...]
+        self.host_out: List[torch.Tensor] = []     # pinned [max_bucket, ...]
+        self.done = torch.cuda.Event()
 
 
 class GpuRunner:
-    def __init__(self, servable, in_specs, out_specs, lanes: int = 2):
+    def __init__(self, servable, in_specs, out_specs, lanes: int = 3):
         self.servable = servable
         self.in_specs = in_specs
         self.out_specs = out_specs
@@ -63,28 +76,65 @@ class GpuRunner:
                            all(d >= 0 for d in s.shape[1:]) and s.dtype != T.DT_STRING for s in in_specs)
         self.use_graphs = opts.hip_graphs and self.batched
         self.buckets = buckets_for(opts.max_batch_size, opts.allowed_batch_sizes)
-        self.lanes = [_Lane(self.device) for _ in range(max(1, lanes))]
+        self._out_dt = [s.dtype for s in out_specs]
         self._rr = 0
         self._rr_lock = threading.Lock()
-        self._out_dt = [s.dtype for s in out_specs]
+        self.lanes: List[_Lane] = []
+        if self.batched:
+            with torch.cuda.device(self.device):
+                self.lanes = [_Lane(self.device) for _ in range(max(1, lanes))]
+                for lane in self.lanes:
+                    self._alloc_host(lane)
+
+    # ------------------------------------------------------------ buffers
+    def _alloc_host(self, lane: _Lane):
+        bmax = self.buckets[-1]
+        for s in self.in_specs:
+            lane.host_in.append(torch.zeros([bmax] + list(s.shape[1:]), dtype=_torch_dtype(s.dtype),
+                                            pin_memory=True))
+        self._out_shapes: Optional[List[Tuple[int, ...]]] = None
+
+    def _ensure_host_out(self, lane: _Lane, outs: List[torch.Tensor]):
+        if lane.host_out:
+            return
+        bmax = self.buckets[-1]
+        for o in outs:
+            lane.host_out.append(torch.zeros([bmax] + list(o.shape[1:]), dtype=o.dtype, pin_memory=True))
+
+    def lane_host_pointers(self, lane_idx: int) -> Tuple[List[int], List[int]]:
+        """Pinned buffers of a lane (for the native fast path): capture the largest
+        bucket first so the output buffers exist with their final dtypes."""
+        lane = self.lanes[lane_idx]
+        with lane.lock:
+            # capture every bucket up front: no graph capture while serving traffic
+            for b in reversed(self.buckets):
+                if b not in lane.graphs:
+                    with torch.cuda.device(self.device):
+                        self._capture(lane, b)
+        return [t.data_ptr() for t in lane.host_in], [t.data_ptr() for t in lane.host_out]
 
     # ------------------------------------------------------------ helpers
-    def _to_device_dtype(self, spec, arr: np.ndarray) -> torch.Tensor:
-        from .servable import _np_to_torch
-        return _np_to_torch(arr, spec.dtype)
-
     def _finish(self, outs: List) -> List:
         res = []
         for v, dt in zip(outs, self._out_dt):
-            if isinstance(v, torch.Tensor) and v.dtype == torch.bfloat16 and dt == T.DT_FLOAT:
-                v = v.float()
+            if isinstance(v, torch.Tensor):
+                want = _torch_dtype(dt) if dt != T.DT_STRING else None
+                if want is not None and v.dtype != want:
+                    v = v.to(want)
             res.append(v)
         return res
 
-    def _eager(self, feeds: List) -> List:
+    def _eager(self, inputs: Sequence) -> List:
+        from .servable import _np_to_torch
         with torch.cuda.device(self.device):
-            dev_feeds = [f.to(self.device, non_blocking=True) if isinstance(f, torch.Tensor) else f for f in feeds]
-            outs = self._finish(self.program.run(dev_feeds))
+            feeds = []
+            for s, v in zip(self.in_specs, inputs):
+                if isinstance(v, np.ndarray) and v.dtype == object:
+                    feeds.append(v)
+                    continue
+                t = v if isinstance(v, torch.Tensor) else _np_to_torch(v, s.dtype)
+                feeds.append(t.to(self.device, non_blocking=True))
+            outs = self._finish(self.program.run(feeds))
             return [o.cpu() if isinstance(o, torch.Tensor) else o for o in outs]
 
     def _bucket(self, n: int) -> Optional[int]:
@@ -101,59 +151,62 @@ class GpuRunner:
 
     def _capture(self, lane: _Lane, b: int) -> None:
         dev = self.device
-        ins = []
-        hosts = []
-        for s in self.in_specs:
-            shape = [b] + list(s.shape[1:])
-            tdt = T.np_dtype(s.dtype)
-            t = torch.zeros(shape, dtype=torch.from_numpy(np.zeros(0, tdt)).dtype, device=dev)
-            ins.append(t)
-            hosts.append(torch.zeros(shape, dtype=t.dtype, pin_memory=True))
+        ins = [torch.zeros([b] + list(s.shape[1:]), dtype=_torch_dtype(s.dtype), device=dev) for s in self.in_specs]
         # eager warm-up on the lane's stream (autotunes kernel tiles for this shape)
         with torch.cuda.stream(lane.stream):
             self._finish(self.program.run(ins))
-            self._finish(self.program.run(ins))
+            outs = self._finish(self.program.run(ins))
         lane.stream.synchronize()
+        self._ensure_host_out(lane, outs)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=lane.stream):
+        with torch.cuda.graph(graph, stream=lane.stream, capture_error_mode="thread_local"):
             outs = self._finish(self.program.run(ins))
         lane.graphs[b] = graph
         lane.static_in[b] = ins
         lane.static_out[b] = outs
-        lane.host_in[b] = hosts
-        lane.host_out[b] = [torch.empty(o.shape, dtype=o.dtype, pin_memory=True) for o in outs]
         log.info("captured HIP graph: %s bucket=%d (%d steps)", self.servable.name, b, len(self.program.steps))
 
+    def _launch(self, lane: _Lane, n: int) -> int:
+        """H2D rows [0, b) of the lane's pinned inputs, replay, D2H; returns b."""
+        b = self._bucket(n)
+        if b not in lane.graphs:
+            with torch.cuda.device(self.device):
+                self._capture(lane, b)
+        with torch.cuda.stream(lane.stream):
+            for h, d in zip(lane.host_in, lane.static_in[b]):
+                d.copy_(h[:b], non_blocking=True)
+            lane.graphs[b].replay()
+            for so, ho in zip(lane.static_out[b], lane.host_out):
+                ho[:b].copy_(so, non_blocking=True)
+            lane.done.record(lane.stream)
+        lane.done.synchronize()
+        return b
+
     # ------------------------------------------------------------ run
+    def run_lane(self, lane_idx: int, n: int) -> None:
+        """Fast path: rows [0, n) are already in the lane's pinned inputs."""
+        lane = self.lanes[lane_idx]
+        with lane.lock:
+            self._launch(lane, n)
+
     def run(self, inputs: Sequence) -> List:
         if not self.use_graphs:
-            feeds = [v if (isinstance(v, np.ndarray) and v.dtype == object) or isinstance(v, torch.Tensor)
-                     else self._to_device_dtype(s, v) for s, v in zip(self.in_specs, inputs)]
-            return self._eager(feeds)
+            return self._eager(inputs)
         n = int(inputs[0].shape[0])
         for v in inputs:
             if int(v.shape[0]) != n:
                 raise E.invalid("all inputs must have the same batch size (dim 0)")
-        b = self._bucket(n)
-        if b is None:
-            # larger than the biggest bucket: split into bucket-sized chunks
+        if n == 0:
+            return self._eager(inputs)
+        if self._bucket(n) is None:
             big = self.buckets[-1]
             parts = [self.run([v[i:i + big] for v in inputs]) for i in range(0, n, big)]
             return [np.concatenate([p[k] for p in parts]) for k in range(len(self.out_specs))]
+        from .servable import _np_to_torch
         lane = self._pick_lane()
         with lane.lock:
-            if b not in lane.graphs:
-                with torch.cuda.device(self.device):
-                    self._capture(lane, b)
-            hin, sin = lane.host_in[b], lane.static_in[b]
-            for h, v, s in zip(hin, inputs, self.in_specs):
-                src = v if isinstance(v, torch.Tensor) else self._to_device_dtype(s, v)
+            for h, v, s in zip(lane.host_in, inputs, self.in_specs):
+                src = v if isinstance(v, torch.Tensor) else _np_to_torch(v, s.dtype)
                 h[:n].copy_(src.reshape(h[:n].shape))
-            with torch.cuda.stream(lane.stream):
-                for h, d in zip(hin, sin):
-                    d.copy_(h, non_blocking=True)
-                lane.graphs[b].replay()
-                for so, ho in zip(lane.static_out[b], lane.host_out[b]):
-                    ho.copy_(so, non_blocking=True)
-            lane.stream.synchronize()
-            return [ho[:n].numpy().copy() if ho.dim() else ho.numpy().copy() for ho in lane.host_out[b]]
+            self._launch(lane, n)
+            return [ho[:n].numpy().copy() for ho in lane.host_out]

@@ -1,0 +1,213 @@
+"""Native HTTP/2 gRPC transport (``_C.Http2Server``) + Predict fast path.
+
+* IO threads (C++, epoll, libnghttp2) terminate gRPC; each owns an
+  SO_REUSEPORT listener so connections spread over threads and over the
+  per-GPU server processes sharing the port.
+* Predict calls that match a registered *endpoint* never touch Python per
+  request: decoded + validated + copied into a pinned batch slot on the IO
+  thread, batched, executed by a GPU lane worker (one HIP-graph replay per
+  batch), encoded and answered from C++.
+* Every other call (control plane, Classify/Regress, unusual Predicts) is
+  queued to Python worker threads that run :class:`~.core.ServingCore`.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from .. import native  # noqa: F401  (loads _C)
+from .. import _C
+from . import errors as E
+from .manager import AVAILABLE, END, UNLOADING
+from .servable import PREDICT_METHOD
+
+log = logging.getLogger("tfserve.native")
+
+
+class FastEndpoint:
+    """A (servable, signature) served by the C++ fast path on the GPU runner's lanes."""
+
+    def __init__(self, transport: "NativeTransport", servable, sig_name: str, timeout_us: int):
+        self.t = transport
+        self.servable = servable
+        self.sig = sig_name
+        srv = transport.srv
+        sig = servable.signatures[sig_name]
+        in_specs = servable.input_specs(sig_name)
+        out_specs = servable.output_specs(sig_name)
+        in_aliases = sorted(in_specs)
+        out_aliases = sorted(out_specs)
+        self.runner = servable.runner(sig_name, in_aliases, out_aliases)
+        self.max_rows = self.runner.buckets[-1]
+        ins = [(a, in_specs[a].dtype, list(in_specs[a].shape[1:])) for a in in_aliases]
+        outs = [(a, out_specs[a].dtype, list(out_specs[a].shape[1:])) for a in out_aliases]
+        self.id = srv.add_endpoint(servable.name, servable.version, sig_name, ins, outs, self.max_rows, timeout_us)
+        io_in, io_out = srv.endpoint_io_order(self.id)
+        assert list(io_in) == in_aliases and list(io_out) == out_aliases
+        self.workers: List[threading.Thread] = []
+        self._stop = threading.Event()
+        for lane_idx in range(len(self.runner.lanes)):
+            in_ptrs, out_ptrs = self.runner.lane_host_pointers(lane_idx)
+            srv.set_slot_buffers(self.id, lane_idx, in_ptrs, out_ptrs)
+        for lane_idx in range(len(self.runner.lanes)):
+            th = threading.Thread(target=self._work, args=(lane_idx,), daemon=True,
+                                  name=f"tfs-gpu-{servable.name}-{lane_idx}")
+            th.start()
+            self.workers.append(th)
+
+    def _work(self, lane_idx: int):
+        srv = self.t.srv
+        while not self._stop.is_set():
+            n = srv.acquire(self.id, lane_idx, 100)
+            if n < 0:
+                return
+            if n == 0:
+                continue
+            try:
+                self.runner.run_lane(lane_idx, n)
+            except Exception as e:  # report to every caller of the batch
+                log.exception("fast-path batch failed")
+                srv.fail(self.id, lane_idx, E.INTERNAL, f"{type(e).__name__}: {e}")
+                continue
+            srv.complete(self.id, lane_idx)
+            if self.t.metrics is not None:
+                self.t.metrics.observe_batch(n, 0.0, str(self.servable.options.device))
+
+    def close(self):
+        self._stop.set()
+        self.t.srv.remove_endpoint(self.id)
+        for th in self.workers:
+            th.join(timeout=5)
+
+
+class NativeTransport:
+    def __init__(self, core, port: int, host: str = "0.0.0.0", batcher=None, io_threads: int = 4,
+                 py_workers: int = 16, fast_path: bool = True, batch_timeout_us: int = 2000,
+                 max_message: int = 2 ** 31 - 1, metrics=None):
+        self.core = core
+        self.srv = _C.Http2Server(host, port, io_threads, max_message)
+        self.port = self.srv.port
+        self.metrics = metrics if metrics is not None else getattr(core, "metrics", None)
+        self.fast_path = fast_path
+        self.batch_timeout_us = batch_timeout_us
+        if batcher is not None:
+            self.batch_timeout_us = int(getattr(batcher, "timeout_us", batch_timeout_us))
+        self._workers = [threading.Thread(target=self._serve, daemon=True, name=f"tfs-py-{i}")
+                         for i in range(py_workers)]
+        self._stop = threading.Event()
+        self._eps: Dict[tuple, FastEndpoint] = {}
+        self._eps_lock = threading.Lock()
+
+    # ------------------------------------------------------------ slow path
+    def _serve(self):
+        srv, core = self.srv, self.core
+        while not self._stop.is_set():
+            call = srv.next_call(100)
+            if call is None:
+                continue
+            try:
+                body = core.handle(call.method, call.body)
+                srv.respond(call, 0, "", body)
+            except E.ServingError as e:
+                srv.respond(call, e.code, e.message, b"")
+            except Exception as e:  # pragma: no cover - defensive
+                srv.respond(call, E.INTERNAL, str(e), b"")
+
+    # ------------------------------------------------------------ fast path wiring
+    def _on_state(self, name: str, version: int, state: int):
+        if not self.fast_path:
+            return
+        if state == AVAILABLE:
+            threading.Thread(target=self._register, args=(name, version), daemon=True).start()
+        elif state in (UNLOADING, END):
+            self._unregister(name, version)
+
+    def _register(self, name: str, version: int):
+        mgr = self.core.manager
+        try:
+            servable = mgr.resolve(name, version)
+        except E.ServingError:
+            return
+        try:
+            if not servable.options.is_gpu:
+                return
+            for sig_name, sig in servable.signatures.items():
+                if sig.method_name != PREDICT_METHOD:
+                    continue
+                ins = servable.input_specs(sig_name)
+                if not all(s.shape and s.shape[0] == -1 and all(d >= 0 for d in s.shape[1:]) for s in ins.values()):
+                    continue
+                outs = servable.output_specs(sig_name)
+                if not all(s.shape and s.shape[0] == -1 and all(d >= 0 for d in s.shape[1:]) for s in outs.values()):
+                    continue
+                try:
+                    ep = FastEndpoint(self, servable, sig_name, self.batch_timeout_us)
+                except Exception:
+                    log.exception("fast path unavailable for %s/%s", name, sig_name)
+                    continue
+                with self._eps_lock:
+                    self._eps[(name, version, sig_name)] = ep
+                self.srv.set_route(name, sig_name, version, ep.id)
+                log.info("fast path: %s v%d %s -> endpoint %d", name, version, sig_name, ep.id)
+            self._refresh_latest(name)
+        finally:
+            servable.release()
+
+    def _refresh_latest(self, name: str):
+        with self._eps_lock:
+            versions = sorted({v for (n, v, _s) in self._eps if n == name})
+            sigs = {}
+            for (n, v, s), ep in self._eps.items():
+                if n == name:
+                    sigs.setdefault(s, {})[v] = ep
+        latest_avail = max((v for n, v, _ in self.core.manager.available() if n == name), default=None)
+        for s, byv in sigs.items():
+            if latest_avail is not None and latest_avail in byv:
+                self.srv.set_route(name, s, -1, byv[latest_avail].id)
+            else:
+                self.srv.set_route(name, s, -1, -1)   # latest not fast-pathable: python decides
+
+    def _unregister(self, name: str, version: int):
+        with self._eps_lock:
+            keys = [k for k in self._eps if k[0] == name and k[1] == version]
+            eps = [self._eps.pop(k) for k in keys]
+        for k, ep in zip(keys, eps):
+            self.srv.set_route(name, k[2], version, -1)
+        self._refresh_latest(name)
+        for ep in eps:
+            ep.close()
+
+    # ------------------------------------------------------------ lifecycle
+    def start(self):
+        self.srv.start()
+        for w in self._workers:
+            w.start()
+        mgr = self.core.manager
+        mgr.listeners.append(self._on_state)
+        for name, version, _s in mgr.available():
+            self._register(name, version)
+        return self
+
+    def stop(self, grace: Optional[float] = 1.0):
+        self._stop.set()
+        with self._eps_lock:
+            eps = list(self._eps.values())
+            self._eps.clear()
+        for ep in eps:
+            ep.close()
+        self.srv.stop()
+        for w in self._workers:
+            w.join(timeout=2)
+        try:
+            self.core.manager.listeners.remove(self._on_state)
+        except ValueError:
+            pass
+
+    def stats(self) -> dict:
+        d = dict(self.srv.stats())
+        with self._eps_lock:
+            d["endpoints"] = {f"{k[0]}/v{k[1]}/{k[2]}": self.srv.endpoint_stats(ep.id) for k, ep in self._eps.items()}
+        return d

@@ -1,0 +1,67 @@
+"""Native HTTP/2 front end: wire interop with grpcio's C-core client, error
+statuses, concurrency, and the native load generator (CPU, half_plus_two)."""
+import asyncio
+
+import numpy as np
+import pytest
+
+from rust_tensorflow_serving2_amd import _C, native
+from rust_tensorflow_serving2_amd.client import TensorflowServing, TFServingError, unpack_signature_defs
+from rust_tensorflow_serving2_amd.server.server import ModelServer, ServerOptions
+
+import grpc
+
+
+@pytest.fixture(scope="module")
+def nserver(hpt_path):
+    srv = ModelServer(ServerOptions(port=0, host="127.0.0.1", model_name="hpt", model_base_path=hpt_path,
+                                    transport="native", file_system_poll_wait_seconds=0)).start()
+    yield srv
+    srv.stop()
+
+
+def test_grpcio_client_interop(nserver):
+    async def go():
+        c = await TensorflowServing.new().hostname("127.0.0.1").port(nserver.port).build()
+        st = await c.model_status("hpt")
+        assert st.model_version_status[0].state == 30
+        assert "serving_default" in unpack_signature_defs(await c.model_metadata("hpt"))
+        out = await c.predict_tensors("hpt", {"x": np.array([[1.0], [3.0]], np.float32)})
+        np.testing.assert_allclose(out["y"].reshape(-1), [2.5, 3.5])
+        with pytest.raises(TFServingError) as ei:
+            await c.model_status("missing")
+        assert ei.value.code == grpc.StatusCode.NOT_FOUND
+        res = await asyncio.gather(*[c.clone().predict_tensors("hpt", {"x": np.full((1, 1), i, np.float32)})
+                                     for i in range(40)])
+        np.testing.assert_allclose([r["y"][0, 0] for r in res], [0.5 * i + 2 for i in range(40)])
+        await c.close()
+    asyncio.run(go())
+
+
+def test_unknown_method_and_large_message(nserver):
+    async def go():
+        ch = grpc.aio.insecure_channel(f"127.0.0.1:{nserver.port}",
+                                       options=[("grpc.max_send_message_length", 64 << 20),
+                                                ("grpc.max_receive_message_length", 64 << 20)])
+        with pytest.raises(grpc.aio.AioRpcError) as ei:
+            await ch.unary_unary("/tensorflow.serving.PredictionService/Nope")(b"")
+        assert ei.value.code() == grpc.StatusCode.UNIMPLEMENTED
+        # 20 MB request (a client-side batch of 32 images) is accepted (raised limits)
+        x = np.zeros((5_000_000, 1), np.float32)
+        body = native.encode_predict_request(native.spec_tuple("hpt", None, None, ""), {"x": x})
+        raw = await ch.unary_unary("/tensorflow.serving.PredictionService/Predict")(body)
+        assert len(raw) > 20_000_000
+        await ch.close()
+    asyncio.run(go())
+
+
+def test_native_loadgen(nserver):
+    body = native.encode_predict_request(native.spec_tuple("hpt", None, None, ""), {"x": np.ones((1, 1), np.float32)})
+    r = _C.run_loadgen("127.0.0.1", nserver.port, "/tensorflow.serving.PredictionService/Predict", [body],
+                       300, 16, 4, 2, 60.0)
+    assert r["ok"] == 300 and r["errors"] == 0, r["first_error"]
+    assert len(r["latency_us"]) == 300
+    bad = native.encode_predict_request(native.spec_tuple("nope", None, None, ""), {"x": np.ones((1, 1), np.float32)})
+    r = _C.run_loadgen("127.0.0.1", nserver.port, "/tensorflow.serving.PredictionService/Predict", [bad],
+                       10, 4, 1, 1, 60.0)
+    assert r["errors"] == 10 and "grpc-status 5" in r["first_error"]
