@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--transport", default="native", choices=["native", "grpc"])
     ap.add_argument("--batch-timeout-us", type=int, default=2000)
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "tiny"],
+                    help="tiny = same 224x224x3 payload, negligible compute (transport ceiling probe; "
+                         "NOT the headline config)")
     return ap.parse_args()
 
 
@@ -78,9 +81,14 @@ def main():
     from rust_tensorflow_serving2_amd.server.server import ModelServer, ServerOptions
     from rust_tensorflow_serving2_amd.server.servable import ServableOptions
 
-    base = os.path.join(tempfile.gettempdir(), f"tfserve_bench_{os.environ.get('MASTER_PORT', 'solo')}", "resnet")
+    base = os.path.join(tempfile.gettempdir(), f"tfserve_bench_{os.environ.get('MASTER_PORT', 'solo')}",
+                        "resnet" if args.model == "resnet50" else "tiny")
     if rank == 0 and not os.path.exists(os.path.join(base, "1", "saved_model.pb")):
-        resnet.export(os.path.join(base, "1"), seed=0, image_size=args.image_size)
+        if args.model == "resnet50":
+            resnet.export(os.path.join(base, "1"), seed=0, image_size=args.image_size)
+        else:
+            resnet.export(os.path.join(base, "1"), seed=0, image_size=args.image_size, blocks=(1, 1, 1, 1),
+                          width=8, num_classes=1001)
     if world > 1:
         dist.barrier()
 
@@ -93,6 +101,7 @@ def main():
     port = (args.port + local) if args.port else 0
     server = ModelServer(ServerOptions(port=port, host="127.0.0.1", model_name="resnet", model_base_path=base,
                                        device=str(device), transport=args.transport, servable=sopts,
+                                       io_threads=args.io_threads, batch_timeout_us=args.batch_timeout_us,
                                        file_system_poll_wait_seconds=0, weight_source=weight_source,
                                        monitoring=False))
     t_load = time.perf_counter()
@@ -152,7 +161,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic 224x224x3 f32 images (float_val, batch-1 PredictRequests as the Rust client "
                     "sends), random-init ResNet-50 v1.5 weights",
-            "config": {"model": "ResNet-50 v1.5", "global_batch": args.batch * world, "seq_len": None,
+            "config": {"model": "ResNet-50 v1.5" if args.model == "resnet50" else "tiny-transport-probe",
+                       "global_batch": args.batch * world, "seq_len": None,
                        "parallelism": f"dp{world}", "server_batch": args.batch,
                        "request_batch": args.request_batch, "image_size": args.image_size,
                        "transport": args.transport, "concurrency_per_gpu": conc},

@@ -36,6 +36,8 @@ class ServerOptions:
     transport: str = "grpc"                        # "grpc" | "native"
     file_system_poll_wait_seconds: float = 1.0
     grpc_workers: int = 64
+    io_threads: int = 4                            # native transport epoll threads
+    batch_timeout_us: int = 2000                   # native fast-path batch window
     servable: ServableOptions = field(default_factory=ServableOptions)
     monitoring: bool = True
     weight_source: Optional[object] = None         # parallel.WeightSource for multi-rank loads
@@ -94,7 +96,8 @@ class ModelServer:
         self.manager.start_polling()
         if self.opts.transport == "native":
             from .native_transport import NativeTransport
-            t = NativeTransport(self.core, self.opts.port, self.opts.host, batcher=self.batcher)
+            t = NativeTransport(self.core, self.opts.port, self.opts.host, batcher=self.batcher,
+                                io_threads=self.opts.io_threads, batch_timeout_us=self.opts.batch_timeout_us)
         else:
             from .grpc_transport import GrpcTransport
             t = GrpcTransport(self.core, self.opts.port, self.opts.host, self.opts.grpc_workers)

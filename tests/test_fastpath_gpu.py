@@ -1,0 +1,108 @@
+"""Native Predict fast path on the GPU: results must equal the Python slow path
+(same servable), partial batches / mixed request batch sizes / output_filter,
+and fall-through for requests the fast path does not take (labels, bad shapes)."""
+import asyncio
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import grpc  # noqa: E402
+
+from rust_tensorflow_serving2_amd import _C, native  # noqa: E402
+from rust_tensorflow_serving2_amd.schema import serving  # noqa: E402
+from rust_tensorflow_serving2_amd.server.server import ModelServer, ServerOptions  # noqa: E402
+from rust_tensorflow_serving2_amd.server.servable import ServableOptions  # noqa: E402
+
+PREDICT = "/tensorflow.serving.PredictionService/Predict"
+
+
+@pytest.fixture(scope="module")
+def gpu_server(tmp_path_factory):
+    from rust_tensorflow_serving2_amd.models import resnet
+    base = str(tmp_path_factory.mktemp("fp") / "resnet")
+    resnet.export(os.path.join(base, "1"), blocks=(1, 1, 1, 1), width=16, num_classes=10, image_size=32, seed=5)
+    so = ServableOptions(device="cuda:0", max_batch_size=8, allowed_batch_sizes=(1, 2, 4, 8))
+    srv = ModelServer(ServerOptions(port=0, host="127.0.0.1", model_name="resnet", model_base_path=base,
+                                    device="cuda:0", transport="native", servable=so,
+                                    file_system_poll_wait_seconds=0, batch_timeout_us=500)).start()
+    tr = srv.transports[0]
+    import time
+    for _ in range(300):
+        if tr.stats().get("endpoints"):
+            break
+        time.sleep(0.05)
+    assert tr.stats()["endpoints"], "fast path endpoint not registered"
+    yield srv
+    srv.stop()
+
+
+def _call(port, body):
+    async def go():
+        async with grpc.aio.insecure_channel(f"127.0.0.1:{port}") as ch:
+            return await ch.unary_unary(PREDICT)(body)
+    return asyncio.run(go())
+
+
+def test_fast_path_matches_slow_path(gpu_server):
+    x = np.random.default_rng(0).random((3, 32, 32, 3), dtype=np.float32)
+    spec = native.spec_tuple("resnet", None, None, "serving_default")
+    fast = serving.PredictResponse.FromString(_call(gpu_server.port, native.encode_predict_request(spec, {"input": x})))
+    slow = serving.PredictResponse.FromString(
+        gpu_server.core.predict(native.encode_predict_request(spec, {"input": x})))
+    for k in ("probabilities", "classes"):
+        a = np.array(fast.outputs[k].float_val or fast.outputs[k].int64_val)
+        b = np.array(slow.outputs[k].float_val or slow.outputs[k].int64_val)
+        np.testing.assert_allclose(a, b, atol=1e-5)
+    assert fast.model_spec.version.value == 1 and fast.model_spec.signature_name == "serving_default"
+    assert list(d.size for d in fast.outputs["probabilities"].tensor_shape.dim) == [3, 10]
+    st = gpu_server.transports[0].stats()
+    assert st["fast_path"] >= 1
+
+
+def test_many_concurrent_rows_are_routed_back_correctly(gpu_server):
+    """Each request gets ITS rows back even when batched with others."""
+    rng = np.random.default_rng(1)
+    xs = [rng.random((1 + (i % 3), 32, 32, 3), dtype=np.float32) for i in range(24)]
+    spec = native.spec_tuple("resnet", None, None, "")
+    bodies = [native.encode_predict_request(spec, {"input": x}) for x in xs]
+
+    async def go():
+        async with grpc.aio.insecure_channel(f"127.0.0.1:{gpu_server.port}") as ch:
+            stub = ch.unary_unary(PREDICT)
+            return await asyncio.gather(*[stub(b) for b in bodies])
+    outs = asyncio.run(go())
+    for x, raw in zip(xs, outs):
+        ref = serving.PredictResponse.FromString(
+            gpu_server.core.predict(native.encode_predict_request(spec, {"input": x})))
+        got = np.array(serving.PredictResponse.FromString(raw).outputs["probabilities"].float_val)
+        np.testing.assert_allclose(got, np.array(ref.outputs["probabilities"].float_val), atol=1e-5)
+
+
+def test_output_filter_and_fallthrough(gpu_server):
+    x = np.random.default_rng(2).random((1, 32, 32, 3), dtype=np.float32)
+    body = native.encode_predict_request(native.spec_tuple("resnet", 1, None, "serving_default"), {"input": x},
+                                         ["classes"])
+    r = serving.PredictResponse.FromString(_call(gpu_server.port, body))
+    assert list(r.outputs) == ["classes"]
+    # wrong image size -> not fast-pathable -> python path returns INVALID_ARGUMENT
+    bad = native.encode_predict_request(native.spec_tuple("resnet", None, None, ""),
+                                        {"input": np.zeros((1, 31, 32, 3), np.float32)})
+    with pytest.raises(grpc.aio.AioRpcError) as ei:
+        _call(gpu_server.port, bad)
+    assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+
+
+def test_loadgen_against_fast_path(gpu_server):
+    spec = native.spec_tuple("resnet", None, None, "")
+    bodies = [native.encode_predict_request(spec, {"input": np.random.default_rng(i).random((1, 32, 32, 3),
+                                                                                           dtype=np.float32)})
+              for i in range(8)]
+    r = _C.run_loadgen("127.0.0.1", gpu_server.port, PREDICT, bodies, 400, 32, 4, 2, 120.0)
+    assert r["ok"] == 400 and r["errors"] == 0, r["first_error"]
