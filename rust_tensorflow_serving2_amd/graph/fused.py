@@ -128,9 +128,17 @@ class FusedConv:
         self.use_hip = use_hip
         self.name = name
         self.device = device
+        # RGB(A) stems: input re-laid out as bf16 RGBA by ingest_c4, weights as
+        # [Cout][kh][8 taps][4 ch] so the kernel's operand gather is 8-B vector loads
+        self.c4 = use_hip and self.cin <= 4 and self.kw <= 8
         if use_hip:
-            k = self.kh * self.kw * self.cin
-            w_nk = w_hwio.permute(3, 0, 1, 2).reshape(self.cout, k)
+            if self.c4:
+                w4 = torch.zeros(self.kh, 8, 4, self.cout)
+                w4[:, :self.kw, :self.cin, :] = w_hwio.float()
+                w_nk = w4.permute(3, 0, 1, 2).reshape(self.cout, self.kh * 32)
+            else:
+                k = self.kh * self.kw * self.cin
+                w_nk = w_hwio.permute(3, 0, 1, 2).reshape(self.cout, k)
             self.w = _pad_k(w_nk).to(BF16).contiguous().to(device)
             self.b = bias.float().contiguous().to(device)
         else:
@@ -156,8 +164,10 @@ class FusedConv:
                 y = y + res.float()
             return [_ref_act(y, self.act).contiguous()]
         from ..ops import ACT, hip, tuned_config
-        if self.cin % 8 != 0:
-            x = x.float().contiguous()            # stem: fp32 operand gather + cast in-kernel
+        if self.c4:
+            x = hip().ingest_c4(x.float().contiguous())   # fp32 RGB request -> bf16 RGBA
+        elif self.cin % 8 != 0:
+            x = x.float().contiguous()            # generic: fp32 operand gather + cast in-kernel
         else:
             x = _to_bf16(x).contiguous()
         if res is not None:
@@ -170,8 +180,9 @@ class FusedConv:
         args = (x, self.w, self.b, res, self.kh, self.kw, self.sh, self.sw, pt, pb, pl, pr, ACT[self.act])
         out = torch.empty((n, ho, wo, self.cout), device=x.device, dtype=BF16)
         key = ("conv", tuple(x.shape), x.dtype, self.cout, self.kh, self.kw, self.sh, res is not None)
-        cfg = tuned_config(key, M, self.cout, lambda c: H.conv2d(*args, cfg=c, out=out))
-        return [H.conv2d(*args, cfg=cfg, out=out)]
+        K = self.kh * 32 if self.c4 else self.kh * self.kw * self.cin
+        cfg, splits = tuned_config(key, M, self.cout, lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s), K)
+        return [H.conv2d(*args, cfg=cfg, out=out, splits=splits)]
 
 
 class FusedMatMul:
@@ -208,9 +219,9 @@ class FusedMatMul:
         shape = list(x.shape[:-1]) + [self.n]
         out = torch.empty(shape, device=x.device, dtype=torch.float32 if self.out_f32 else BF16)
         key = ("mm", M, self.n, self.k, res is not None, self.out_f32)
-        run = lambda c: H.linear(x, self.w, self.b, res, ACT[self.act], c, self.out_f32, 1.0, out)  # noqa: E731
-        cfg = tuned_config(key, M, self.n, run)
-        return [run(cfg)]
+        run = lambda c, s: H.linear(x, self.w, self.b, res, ACT[self.act], c, self.out_f32, 1.0, out, s)  # noqa
+        cfg, splits = tuned_config(key, M, self.n, run, self.k)
+        return [run(cfg, splits)]
 
 
 def _ref_act(y, act):

@@ -22,6 +22,28 @@ void check(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
 }
 
+// Launch with optional split-K: raw fp32 slabs in a workspace + reduce/epilogue kernel.
+void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, const Tensor& like, hipStream_t st) {
+  TORCH_CHECK(cfg >= 0 && cfg < tfsk::kNumIGemmConfigs, "bad tile config");
+  const int nk = (a.K + 63) / 64;
+  if (splits > nk) splits = nk;
+  if (splits <= 1) {
+    a.splits = 1;
+    a.kt_per_split = nk;
+    a.ws = nullptr;
+    TORCH_CHECK(tfsk::igemm_launch(a, a_mode, cfg, st) == hipSuccess, "igemm launch failed");
+    return;
+  }
+  const int per = (nk + splits - 1) / splits;
+  splits = (nk + per - 1) / per;
+  Tensor ws = torch::empty({splits * int64_t(a.M) * a.N}, like.options().dtype(at::kFloat));
+  a.splits = int(splits);
+  a.kt_per_split = per;
+  a.ws = ws.data_ptr<float>();
+  TORCH_CHECK(tfsk::igemm_launch(a, a_mode, cfg, st) == hipSuccess, "igemm(split-K) launch failed");
+  TORCH_CHECK(tfsk::splitk_reduce_launch(a, st) == hipSuccess, "split-K reduce launch failed");
+}
+
 void need(const Tensor& t, at::ScalarType st, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
@@ -35,7 +57,7 @@ uint16_t* bf16p_mut(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data
 Tensor conv2d(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
               const c10::optional<Tensor>& residual, int64_t KH, int64_t KW, int64_t SH, int64_t SW,
               int64_t PT, int64_t PB, int64_t PL, int64_t PR, int64_t act, int64_t cfg,
-              const c10::optional<Tensor>& out, bool out_f32) {
+              const c10::optional<Tensor>& out, bool out_f32, int64_t splits) {
   const bool stem = x.scalar_type() == at::kFloat;
   need(x, stem ? at::kFloat : at::kBFloat16, "x");
   need(w, at::kBFloat16, "w");
@@ -45,11 +67,15 @@ Tensor conv2d(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   const int Ho = (H + PT + PB - KH) / SH + 1, Wo = (W + PL + PR - KW) / SW + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty conv output");
   const int Cout = w.size(0), ldb = w.size(1);
-  const int K = KH * KW * C;
+  const bool c4 = !stem && C == 4;
+  TORCH_CHECK(!c4 || KW <= 8, "4-channel (RGBA) conv supports KW <= 8");
+  const int K = c4 ? KH * 32 : KH * KW * C;   // c4 weights: [Cout][kh][8 taps][4 ch]
   TORCH_CHECK(ldb >= K && ldb % 8 == 0, "weight rows must hold K=", K, " (padded to a multiple of 8)");
   int a_mode;
   if (stem) {
-    a_mode = tfsk::kAStemF32;
+    a_mode = (C == 3 && KH == 7 && KW == 7) ? tfsk::kAStem7x7x3 : tfsk::kAStemF32;
+  } else if (c4) {
+    a_mode = tfsk::kAC4;
   } else {
     TORCH_CHECK(C % 8 == 0, "conv input channels must be a multiple of 8 (got ", C, ")");
     a_mode = (KH == 1 && KW == 1 && SH == 1 && SW == 1 && PT == 0 && PL == 0) ? tfsk::kADense : tfsk::kAIm2col;
@@ -76,15 +102,14 @@ Tensor conv2d(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
     a.ldr = Cout;
   }
   a.act = act; a.out = y.data_ptr(); a.ldc = Cout; a.out_f32 = out_f32; a.alpha = 1.f;
-  TORCH_CHECK(cfg >= 0 && cfg < tfsk::kNumIGemmConfigs, "bad tile config");
-  check(tfsk::igemm_launch(a, a_mode, cfg, cur_stream(x)), "igemm");
+  run_igemm(a, a_mode, cfg, splits, x, cur_stream(x));
   return y;
 }
 
 // x: [M][K] bf16 (any leading dims), w: [N][ldb] bf16 -> [.., N]
 Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
               const c10::optional<Tensor>& residual, int64_t act, int64_t cfg, bool out_f32, double alpha,
-              const c10::optional<Tensor>& out) {
+              const c10::optional<Tensor>& out, int64_t splits) {
   need(x, at::kBFloat16, "x");
   need(w, at::kBFloat16, "w");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -112,8 +137,7 @@ Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
     a.ldr = N;
   }
   a.act = act; a.out = y.data_ptr(); a.ldc = N; a.out_f32 = out_f32; a.alpha = float(alpha);
-  TORCH_CHECK(cfg >= 0 && cfg < tfsk::kNumIGemmConfigs, "bad tile config");
-  check(tfsk::igemm_launch(a, tfsk::kADense, cfg, cur_stream(x)), "igemm(linear)");
+  run_igemm(a, tfsk::kADense, cfg, splits, x, cur_stream(x));
   return y;
 }
 
@@ -167,6 +191,17 @@ std::vector<Tensor> softmax_argmax(const Tensor& logits, bool want_probs, bool w
                                     want_classes ? classes.data_ptr<int64_t>() : nullptr, rows, cols,
                                     cur_stream(logits)), "softmax_argmax");
   return {probs, classes};
+}
+
+Tensor ingest_c4(const Tensor& x, const c10::optional<Tensor>& out) {
+  need(x, at::kFloat, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) <= 4, "ingest_c4: NHWC with C <= 4");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = out.has_value() ? *out : torch::empty({x.size(0), x.size(1), x.size(2), 4}, x.options().dtype(at::kBFloat16));
+  need(y, at::kBFloat16, "out");
+  check(tfsk::ingest_c4_launch(x.data_ptr<float>(), bf16p_mut(y), x.numel() / x.size(3), x.size(3), cur_stream(x)),
+        "ingest_c4");
+  return y;
 }
 
 Tensor cast_bf16(const Tensor& x, const c10::optional<Tensor>& out) {
@@ -254,16 +289,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d", &conv2d, "NHWC implicit-GEMM conv (+bias +residual +act)", py::arg("x"), py::arg("w"),
         py::arg("bias"), py::arg("residual"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
         py::arg("pt"), py::arg("pb"), py::arg("pl"), py::arg("pr"), py::arg("act") = 0, py::arg("cfg") = 0,
-        py::arg("out") = py::none(), py::arg("out_f32") = false);
+        py::arg("out") = py::none(), py::arg("out_f32") = false, py::arg("splits") = 1);
   m.def("linear", &linear, "x @ w^T (+bias +residual +act)", py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("residual") = py::none(), py::arg("act") = 0, py::arg("cfg") = 0, py::arg("out_f32") = false,
-        py::arg("alpha") = 1.0, py::arg("out") = py::none());
+        py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("splits") = 1);
   m.def("maxpool", &maxpool, py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
         py::arg("pt"), py::arg("pb"), py::arg("pl"), py::arg("pr"), py::arg("out") = py::none());
   m.def("global_avgpool", &global_avgpool, py::arg("x"), py::arg("out") = py::none());
   m.def("softmax_argmax", &softmax_argmax, py::arg("logits"), py::arg("want_probs") = true,
         py::arg("want_classes") = true, py::arg("probs_out") = py::none(), py::arg("classes_out") = py::none());
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("out") = py::none());
+  m.def("ingest_c4", &ingest_c4, "fp32 NHWC (C<=4) -> bf16 NHWC C=4", py::arg("x"), py::arg("out") = py::none());
   m.def("layernorm", &layernorm, py::arg("x"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("out") = py::none());
   m.def("embed_ln", &embed_ln, py::arg("ids"), py::arg("type_ids"), py::arg("word"), py::arg("pos"),

@@ -119,6 +119,46 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
         if (ok) ra[i] = *reinterpret_cast<const uint4*>(Ag + a_off[i] + (hi * p.W + wi) * p.C + ci);
         else ra[i] = make_uint4(0, 0, 0, 0);
       }
+    } else if (AMODE == kAC4) {
+      const uint16_t* __restrict__ Ag = static_cast<const uint16_t*>(p.a);
+      const int k = k0 + chunk * 8;
+      const int kh = k >> 5, kw = (k & 31) >> 2;   // kw even: taps kw, kw+1
+      const bool kok = kh < p.KH;
+      const bool t1ok = kw + 1 < p.KW;
+#pragma unroll
+      for (int i = 0; i < G::A_CHUNKS; ++i) {
+        const int hi = a_hi[i] + kh, wi = a_wi[i] + kw;
+        const bool rok = kok && a_ok[i] && (unsigned)hi < (unsigned)p.H;
+        const uint16_t* rowp = Ag + a_off[i] + hi * p.W * 4;
+        uint2 t0 = make_uint2(0, 0), t1 = make_uint2(0, 0);
+        if (rok && kw < p.KW && (unsigned)wi < (unsigned)p.W) t0 = *reinterpret_cast<const uint2*>(rowp + wi * 4);
+        if (rok && t1ok && (unsigned)(wi + 1) < (unsigned)p.W)
+          t1 = *reinterpret_cast<const uint2*>(rowp + (wi + 1) * 4);
+        ra[i] = make_uint4(t0.x, t0.y, t1.x, t1.y);
+      }
+    } else if (AMODE == kAStem7x7x3) {
+      // k = kh*21 + j, j = kw*3 + c: for a fixed kh the 21 operands of one output
+      // pixel are 21 *contiguous* floats of input row hi (cols wi0..wi0+6, 3 ch),
+      // so only kh needs a (constant) division and one bounds test per element.
+      const float* __restrict__ Ag = static_cast<const float*>(p.a);
+      const int W3 = p.W * 3;
+#pragma unroll
+      for (int i = 0; i < G::A_CHUNKS; ++i) {
+        uint16_t v[8];
+        const float* rowp = Ag + a_off[i] + a_wi[i] * 3;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = k0 + chunk * 8 + e;
+          const int kh = k / 21, j = k - kh * 21;
+          const int hi = a_hi[i] + kh, wi = a_wi[i] + j / 3;
+          float x = 0.f;
+          if (a_ok[i] && k < 147 && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+            x = rowp[hi * W3 + j];
+          v[e] = f32_to_bf16(x);
+        }
+        ra[i] = make_uint4(v[0] | (uint32_t(v[1]) << 16), v[2] | (uint32_t(v[3]) << 16),
+                           v[4] | (uint32_t(v[5]) << 16), v[6] | (uint32_t(v[7]) << 16));
+      }
     } else {  // kAStemF32: fp32 NHWC, tiny C, element gather + cast
       const float* __restrict__ Ag = static_cast<const float*>(p.a);
 #pragma unroll
@@ -173,15 +213,17 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
 #pragma unroll
     for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + BK - 1) / BK;
-  gload(0);
+  const int nk_all = (K + BK - 1) / BK;
+  const int kt0 = p.splits > 1 ? blockIdx.y * p.kt_per_split : 0;
+  const int nk = p.splits > 1 ? min(nk_all, kt0 + p.kt_per_split) - kt0 : nk_all;
+  gload(kt0);
   sstore(0);
   __syncthreads();
 
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
+    if (kt + 1 < nk) gload(kt0 + kt + 1);
     const uint16_t* as = As + cur * BM * BK;
     const uint16_t* bs = Bs + cur * BN * BK;
 #pragma unroll
@@ -220,8 +262,31 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   __syncthreads();
 
   const float alpha = p.alpha;
-  const bool vec_ok = (N % 8 == 0) && (p.ldc % 8 == 0) && (!p.residual || p.ldr % 8 == 0);
   constexpr int CPR = BN / 8;   // chunks per row
+  if (p.splits > 1) {
+    // raw partial slab of this K split; splitk_reduce applies the epilogue
+    float* ws = p.ws + size_t(blockIdx.y) * M * N;
+    const bool v4 = (N % 4 == 0);
+    for (int c = tid; c < BM * CPR; c += kThreads) {
+      const int row = c / CPR, col = (c - row * CPR) * 8;
+      const int m = m0 + row, n = n0 + col;
+      if (m >= M || n >= N) continue;
+      const float* src = Cs + row * G::CS_LD + col;
+      float* dst = ws + size_t(m) * N + n;
+      if (v4 && n + 8 <= N) {
+        float4 a = *reinterpret_cast<const float4*>(src);
+        float4 b = *reinterpret_cast<const float4*>(src + 4);
+        a.x *= alpha; a.y *= alpha; a.z *= alpha; a.w *= alpha;
+        b.x *= alpha; b.y *= alpha; b.z *= alpha; b.w *= alpha;
+        *reinterpret_cast<float4*>(dst) = a;
+        *reinterpret_cast<float4*>(dst + 4) = b;
+      } else {
+        for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = src[e] * alpha;
+      }
+    }
+    return;
+  }
+  const bool vec_ok = (N % 8 == 0) && (p.ldc % 8 == 0) && (!p.residual || p.ldr % 8 == 0);
   for (int c = tid; c < BM * CPR; c += kThreads) {
     const int row = c / CPR, col = (c - row * CPR) * 8;
     const int m = m0 + row, n = n0 + col;
@@ -292,8 +357,40 @@ hipError_t launch_cfg(const IGemmArgs& a, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE>), dim3(tiles), dim3(kThreads), G::LDS, s, a);
+  const int splits = a.splits > 1 ? a.splits : 1;
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE>), dim3(tiles, splits), dim3(kThreads), G::LDS, s, a);
   return hipGetLastError();
+}
+
+// Sum the split-K slabs (fixed order -> deterministic) + epilogue; 8 columns per thread.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(IGemmArgs p) {
+  const int M = p.M, N = p.N;
+  const int cpr = (N + 7) / 8;
+  const long total = long(M) * cpr;
+  const size_t slab = size_t(M) * N;
+  for (long c = blockIdx.x * long(blockDim.x) + threadIdx.x; c < total; c += long(gridDim.x) * blockDim.x) {
+    const int m = int(c / cpr), n = int(c - long(m) * cpr) * 8;
+    const int ne = min(8, N - n);
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < p.splits; ++s) {
+      const float* src = p.ws + s * slab + size_t(m) * N + n;
+      if (ne == 8 && (N % 4 == 0)) {
+        const float4 a = *reinterpret_cast<const float4*>(src);
+        const float4 b = *reinterpret_cast<const float4*>(src + 4);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      } else {
+        for (int e = 0; e < ne; ++e) v[e] += src[e];
+      }
+    }
+    for (int e = 0; e < ne; ++e) {
+      float x = v[e];
+      if (p.bias) x += p.bias[n + e];
+      if (p.residual) x += bf16_to_f32(p.residual[size_t(m) * p.ldr + n + e]);
+      x = apply_act(x, p.act);
+      if (p.out_f32) static_cast<float*>(p.out)[size_t(m) * p.ldc + n + e] = x;
+      else static_cast<uint16_t*>(p.out)[size_t(m) * p.ldc + n + e] = f32_to_bf16(x);
+    }
+  }
 }
 
 template <int AMODE>
@@ -317,8 +414,18 @@ hipError_t igemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) 
     case kADense: return launch_mode<kADense>(a, cfg, s);
     case kAIm2col: return launch_mode<kAIm2col>(a, cfg, s);
     case kAStemF32: return launch_mode<kAStemF32>(a, cfg, s);
+    case kAStem7x7x3: return launch_mode<kAStem7x7x3>(a, cfg, s);
+    case kAC4: return launch_mode<kAC4>(a, cfg, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t splitk_reduce_launch(const IGemmArgs& a, hipStream_t s) {
+  const long work = long(a.M) * ((a.N + 7) / 8);
+  long g = (work + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(int(g < 1 ? 1 : g)), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 }  // namespace tfsk

@@ -24,9 +24,26 @@ struct IGemmArgs {
   int ldc;
   int out_f32;
   float alpha;          // scale applied to the accumulator before bias
+  // split-K: gridDim.y = splits; split s covers k-tiles [s*kt_per_split, ...).
+  // With splits > 1 the kernel stores raw fp32 partials to ws[s][M][N] and
+  // splitk_reduce applies the epilogue.
+  int splits;
+  int kt_per_split;
+  float* ws;
 };
 
-enum AMode : int { kADense = 0, kAIm2col = 1, kAStemF32 = 2 };
+// kAStem7x7x3: fp32 NHWC input with C == 3 and a 7-wide filter (the ResNet
+// stem) — compile-time geometry for the operand gather.
+// kAC4: bf16 NHWC with exactly 4 channels (RGB + zero pad, written by
+// ingest_c4) and KW <= 8; k = kh*32 + kw*4 + c, so one 16-B operand chunk is
+// two 8-B filter taps and kh = k >> 5 (no division in the gather).
+enum AMode : int { kADense = 0, kAIm2col = 1, kAStemF32 = 2, kAStem7x7x3 = 3, kAC4 = 4 };
+
+// fp32 NHWC with C <= 4 channels -> bf16 NHWC with 4 channels (zero padded).
+hipError_t ingest_c4_launch(const float* x, uint16_t* y, int64_t pixels, int C, hipStream_t stream);
+
+// Sum split-K partial slabs and apply the epilogue (bias, residual, act, store).
+hipError_t splitk_reduce_launch(const IGemmArgs& args, hipStream_t stream);
 
 // Tile configs (BMxBN): 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64
 constexpr int kNumIGemmConfigs = 4;

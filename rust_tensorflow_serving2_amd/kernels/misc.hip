@@ -216,6 +216,16 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* __restrict
   }
 }
 
+// fp32 NHWC (C <= 4) -> bf16 NHWC C = 4 (zero padded): one pixel per thread,
+// one 8-B store; feeds the kAC4 stem gather.
+__global__ void ingest_c4_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, long pixels, int C) {
+  for (long i = blockIdx.x * long(blockDim.x) + threadIdx.x; i < pixels; i += long(gridDim.x) * blockDim.x) {
+    uint16_t v[4] = {0, 0, 0, 0};
+    for (int c = 0; c < C; ++c) v[c] = f32_to_bf16(x[i * C + c]);
+    reinterpret_cast<uint2*>(y)[i] = make_uint2(v[0] | (uint32_t(v[1]) << 16), v[2] | (uint32_t(v[3]) << 16));
+  }
+}
+
 int grid_for(long work, int block) {
   long g = (work + block - 1) / block;
   if (g > 256 * 16) g = 256 * 16;
@@ -247,6 +257,11 @@ hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, 
 
 hipError_t cast_f32_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t s) {
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n / 8 + 1, 256)), dim3(256), 0, s, x, y, long(n));
+  return hipGetLastError();
+}
+
+hipError_t ingest_c4_launch(const float* x, uint16_t* y, int64_t pixels, int C, hipStream_t s) {
+  hipLaunchKernelGGL(ingest_c4_kernel, dim3(grid_for(pixels, 256)), dim3(256), 0, s, x, y, long(pixels), C);
   return hipGetLastError();
 }
 

@@ -66,32 +66,59 @@ def heuristic_config(M: int, N: int) -> int:
     return 3
 
 
-def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int], None]) -> int:
-    """Pick the fastest tile config for ``key`` by timing each once (eager only —
-    never during HIP-graph capture; falls back to the heuristic there)."""
-    cfg = _TUNED.get(key)
-    if cfg is not None:
-        return cfg
+TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+
+
+def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
+    bm, bn = TILES[cfg]
+    tiles = -(-M // bm) * -(-N // bn)
+    nk = -(-K // 64)
+    s = 1
+    while tiles * s < 256 and nk // (s * 2) >= 4 and s < 16:
+        s *= 2
+    return s
+
+
+def candidates(M: int, N: int, K: int):
+    """(tile config, split-K) pairs worth timing for an M x N x K problem."""
+    nk = -(-K // 64)
+    out = []
+    for cfg, (bm, bn) in TILES.items():
+        tiles = -(-M // bm) * -(-N // bn)
+        for s in (1, 2, 4, 8, 16):
+            if s > 1 and (nk // s < 2 or tiles >= 1024 or tiles * s > 4096):
+                continue
+            out.append((cfg, s))
+    return out
+
+
+def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64) -> Tuple[int, int]:
+    """Pick the fastest (tile config, split-K) for ``key`` by timing each
+    candidate (eager only — never during HIP-graph capture, where the
+    heuristic is used)."""
+    hit = _TUNED.get(key)
+    if hit is not None:
+        return hit
     if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
-        return heuristic_config(M, N)
+        c = heuristic_config(M, N)
+        return c, heuristic_splits(M, N, K, c)
     with _TUNE_LOCK:
-        cfg = _TUNED.get(key)
-        if cfg is not None:
-            return cfg
-        n = hip().num_configs()
-        best, best_t = heuristic_config(M, N), float("inf")
-        for c in range(n):
-            launch(c)   # warm (also sets the kernel's LDS attribute)
+        hit = _TUNED.get(key)
+        if hit is not None:
+            return hit
+        best, best_t = None, float("inf")
+        for c, s in candidates(M, N, K):
+            launch(c, s)   # warm (also sets the kernel's LDS attribute)
             start = torch.cuda.Event(enable_timing=True)
             end = torch.cuda.Event(enable_timing=True)
             start.record()
             for _ in range(3):
-                launch(c)
+                launch(c, s)
             end.record()
             end.synchronize()
             t = start.elapsed_time(end)
             if t < best_t:
-                best, best_t = c, t
+                best, best_t = (c, s), t
         _TUNED[key] = best
         return best
 

@@ -30,9 +30,8 @@ def main():
     for b in args.batch:
         x = np.random.default_rng(0).random((b, 224, 224, 3), dtype=np.float32)
         r.run([x])  # capture
-        lane = r.lanes[0]
         bucket = r._bucket(b)
-        g = lane.graphs[bucket]
+        g = next(l.graphs[bucket] for l in r.lanes if bucket in l.graphs)
         torch.cuda.synchronize()
         for _ in range(5):
             g.replay()

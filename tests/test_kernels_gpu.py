@@ -57,8 +57,8 @@ CONV_SHAPES = [
 
 
 @pytest.mark.parametrize("shape", CONV_SHAPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
-def test_conv_matches_fp32(shape, cfg):
+@pytest.mark.parametrize("cfg,splits", [(0, 1), (1, 1), (2, 1), (3, 1), (3, 3), (1, 4)])
+def test_conv_matches_fp32(shape, cfg, splits):
     n, h, w, cin, cout, k, s, pads = shape
     x = rnd(n, h, w, cin, seed=1).to(BF)
     wt = rnd(k, k, cin, cout, scale=1 / math.sqrt(k * k * cin), seed=2).to(BF).float()
@@ -66,7 +66,8 @@ def test_conv_matches_fp32(shape, cfg):
     ho = (h + pads[0] + pads[1] - k) // s + 1
     wo = (w + pads[2] + pads[3] - k) // s + 1
     res = rnd(n, ho, wo, cout, seed=4).to(BF)
-    y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), k, k, s, s, *pads, act=ACT["relu"], cfg=cfg)
+    y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), k, k, s, s, *pads, act=ACT["relu"], cfg=cfg,
+                     splits=splits)
     ref = ref_conv(x, wt, b, s, pads, res, "relu")
     torch.cuda.synchronize()
     err = (y.float().cpu() - ref).abs().max().item()
@@ -74,13 +75,38 @@ def test_conv_matches_fp32(shape, cfg):
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
 
 
-def test_stem_conv_fp32_input():
-    x = torch.rand(2, 32, 32, 3)                      # fp32 request tensor, C=3
-    wt = rnd(7, 7, 3, 64, scale=0.1, seed=5).to(BF).float()
+@pytest.mark.parametrize("k,c,cfg", [(7, 3, 1), (7, 3, 0), (3, 3, 3), (5, 4, 1)])
+def test_stem_conv_fp32_input(k, c, cfg):
+    """fp32 request tensor with few channels: the ingest cast is fused into the
+    operand gather (7x7x3 = specialised ResNet stem loader; others generic)."""
+    x = torch.rand(2, 33, 31, c)
+    wt = rnd(k, k, c, 64, scale=0.1, seed=5).to(BF).float()
     b = rnd(64, scale=0.1, seed=6)
-    y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), None, 7, 7, 2, 2, 2, 3, 2, 3, act=ACT["relu"], cfg=1)
-    ref = ref_conv(x.to(BF).float(), wt, b, 2, (2, 3, 2, 3), None, "relu")
+    pads = (k // 2 - 1, k // 2, k // 2 - 1, k // 2)
+    y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), None, k, k, 2, 2, *pads, act=ACT["relu"], cfg=cfg)
+    ref = ref_conv(x.to(BF).float(), wt, b, 2, pads, None, "relu")
+    assert y.shape == ref.shape
     assert (y.float().cpu() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("k,c", [(7, 3), (3, 3), (5, 4), (7, 1)])
+def test_rgba_stem_path(k, c):
+    """ingest_c4 (fp32 RGB -> bf16 RGBA) + kAC4 gather with [Cout][kh][8][4] weights."""
+    x = torch.rand(3, 37, 29, c)
+    wt = rnd(k, k, c, 64, scale=0.1, seed=7).to(BF).float()
+    b = rnd(64, scale=0.1, seed=8)
+    w4 = torch.zeros(k, 8, 4, 64)
+    w4[:, :k, :c, :] = wt
+    wp = w4.permute(3, 0, 1, 2).reshape(64, k * 32)
+    kp = -(-k * 32 // 64) * 64
+    wp = torch.cat([wp, torch.zeros(64, kp - k * 32)], 1).to(BF).contiguous().to(DEV)
+    x4 = hip().ingest_c4(x.to(DEV))
+    assert x4.shape == (3, 37, 29, 4) and torch.equal(x4[..., :c].float().cpu(), x.to(BF).float())
+    pads = (k // 2 - 1, k // 2, k // 2 - 1, k // 2) if k > 1 else (0, 0, 0, 0)
+    for cfg in (1, 3):
+        y = hip().conv2d(x4, wp, b.to(DEV), None, k, k, 2, 2, *pads, act=ACT["relu"], cfg=cfg)
+        ref = ref_conv(x.to(BF).float(), wt, b, 2, pads, None, "relu")
+        assert (y.float().cpu() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
 
 
 def test_asymmetric_identity_gemm():
@@ -96,14 +122,15 @@ def test_asymmetric_identity_gemm():
 @pytest.mark.parametrize("m,n,k,act", [(32, 1001, 2048, "none"), (256, 2304, 768, "none"),
                                        (256, 3072, 768, "gelu_tanh"), (256, 768, 3072, "none"),
                                        (8, 768, 768, "tanh"), (100, 72, 40, "gelu_erf")])
-@pytest.mark.parametrize("cfg", [0, 3])
-def test_linear_matches_fp32(m, n, k, act, cfg):
+@pytest.mark.parametrize("cfg,splits", [(0, 1), (3, 1), (3, 8), (1, 3)])
+def test_linear_matches_fp32(m, n, k, act, cfg, splits):
     x = rnd(m, k, seed=7).to(BF)
     w = rnd(n, k, scale=1 / math.sqrt(k), seed=8).to(BF)
     b = rnd(n, scale=0.1, seed=9)
     res = rnd(m, n, seed=10).to(BF) if act == "none" else None
     out_f32 = n % 8 != 0
-    y = hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), None if res is None else res.to(DEV), ACT[act], cfg, out_f32)
+    y = hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), None if res is None else res.to(DEV), ACT[act], cfg, out_f32,
+                     splits=splits)
     ref = x.float() @ w.float().t() + b
     if res is not None:
         ref = ref + res.float()

@@ -33,7 +33,8 @@ def test_resnet50_gpu_matches_cpu(resnet50):
     assert err < 5e-3, err
     # run again (HIP-graph replay path, different batch inside the same bucket)
     g2 = gpu.run("serving_default", {"input": x[:3]}, ["classes", "probabilities"])
-    np.testing.assert_allclose(g2["probabilities"], g["probabilities"][:3], atol=1e-5)
+    # bucket 4 vs bucket 8 may pick different tile/split-K configs -> fp32 summation order differs
+    np.testing.assert_allclose(g2["probabilities"], g["probabilities"][:3], atol=2e-4)
     runner = next(iter(gpu._runners.values()))
     hist = runner.program.op_histogram()
     assert hist.get("_FusedConv2D") == 53 and "Conv2D" not in hist
