@@ -55,9 +55,10 @@ def parse():
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--transport", default="native", choices=["native", "grpc"])
     ap.add_argument("--batch-timeout-us", type=int, default=2000)
-    ap.add_argument("--model", default="resnet50", choices=["resnet50", "tiny"],
-                    help="tiny = same 224x224x3 payload, negligible compute (transport ceiling probe; "
-                         "NOT the headline config)")
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "tiny", "bert-base"],
+                    help="resnet50 = headline config; bert-base = BASELINE config 3 (seq 128); "
+                         "tiny = same 224x224x3 payload, negligible compute (transport ceiling probe)")
+    ap.add_argument("--seq-len", type=int, default=128)
     return ap.parse_args()
 
 
@@ -81,11 +82,15 @@ def main():
     from rust_tensorflow_serving2_amd.server.server import ModelServer, ServerOptions
     from rust_tensorflow_serving2_amd.server.servable import ServableOptions
 
+    model_name = "bert" if args.model == "bert-base" else "resnet"
     base = os.path.join(tempfile.gettempdir(), f"tfserve_bench_{os.environ.get('MASTER_PORT', 'solo')}",
-                        "resnet" if args.model == "resnet50" else "tiny")
+                        args.model)
     if rank == 0 and not os.path.exists(os.path.join(base, "1", "saved_model.pb")):
         if args.model == "resnet50":
             resnet.export(os.path.join(base, "1"), seed=0, image_size=args.image_size)
+        elif args.model == "bert-base":
+            from rust_tensorflow_serving2_amd.models import bert
+            bert.export(os.path.join(base, "1"), bert.BertConfig(seq_len=args.seq_len), seed=0)
         else:
             resnet.export(os.path.join(base, "1"), seed=0, image_size=args.image_size, blocks=(1, 1, 1, 1),
                           width=8, num_classes=1001)
@@ -99,7 +104,7 @@ def main():
     sopts = ServableOptions(device=str(device), max_batch_size=args.batch,
                             allowed_batch_sizes=tuple(sorted({1, 2, 4, 8, 16, args.batch})))
     port = (args.port + local) if args.port else 0
-    server = ModelServer(ServerOptions(port=port, host="127.0.0.1", model_name="resnet", model_base_path=base,
+    server = ModelServer(ServerOptions(port=port, host="127.0.0.1", model_name=model_name, model_base_path=base,
                                        device=str(device), transport=args.transport, servable=sopts,
                                        io_threads=args.io_threads, batch_timeout_us=args.batch_timeout_us,
                                        file_system_poll_wait_seconds=0, weight_source=weight_source,
@@ -118,10 +123,20 @@ def main():
     # requests exactly as the reference client builds them
     rng = np.random.default_rng(1234 + rank)
     bodies = []
+    spec = native.spec_tuple(model_name, None, None, "serving_default")
     for _ in range(64):
-        img = rng.random((args.request_batch, args.image_size, args.image_size, 3), dtype=np.float32)
-        bodies.append(native.encode_predict_request(native.spec_tuple("resnet", None, None, "serving_default"),
-                                                    {"input": img}))
+        rb = args.request_batch
+        if args.model == "bert-base":
+            S = args.seq_len
+            ids = rng.integers(0, 30522, (rb, S)).astype(np.int32)
+            mask = np.ones((rb, S), np.int32)
+            mask[:, int(rng.integers(S // 2, S + 1)):] = 0
+            seg = np.zeros((rb, S), np.int32)
+            seg[:, S // 2:] = 1
+            feeds = {"input_ids": ids, "input_mask": mask, "segment_ids": seg}
+        else:
+            feeds = {"input": rng.random((rb, args.image_size, args.image_size, 3), dtype=np.float32)}
+        bodies.append(native.encode_predict_request(spec, feeds))
     conc = args.concurrency or 4 * args.batch
     per_step = max(1, args.batch // args.request_batch)
 
@@ -155,14 +170,21 @@ def main():
         t_max = float(allv[:, 0].max())
         total_ok = float(allv[:, 1].sum())
         value = total_ok / t_max
+        metric = METRIC if args.model != "bert-base" else \
+            f"Predict RPCs/sec + p50 latency, BERT-base seq={args.seq_len} dynamic batching on MI355X"
+        model_label = {"resnet50": "ResNet-50 v1.5", "tiny": "tiny-transport-probe",
+                       "bert-base": f"BERT-base seq {args.seq_len}"}[args.model]
+        data = ("synthetic 224x224x3 f32 images (float_val, batch-1 PredictRequests as the Rust client sends), "
+                "random-init ResNet-50 v1.5 weights") if args.model != "bert-base" else \
+            "synthetic int32 token ids / masks, random-init BERT-base weights"
         out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "Predict RPCs/s", "n_gpus": world,
+            "metric": metric, "value": round(value, 1), "unit": "Predict RPCs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * t_max / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic 224x224x3 f32 images (float_val, batch-1 PredictRequests as the Rust client "
-                    "sends), random-init ResNet-50 v1.5 weights",
-            "config": {"model": "ResNet-50 v1.5" if args.model == "resnet50" else "tiny-transport-probe",
-                       "global_batch": args.batch * world, "seq_len": None,
+            "data": data,
+            "config": {"model": model_label,
+                       "global_batch": args.batch * world,
+                       "seq_len": args.seq_len if args.model == "bert-base" else None,
                        "parallelism": f"dp{world}", "server_batch": args.batch,
                        "request_batch": args.request_batch, "image_size": args.image_size,
                        "transport": args.transport, "concurrency_per_gpu": conc},

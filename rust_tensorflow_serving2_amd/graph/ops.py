@@ -459,12 +459,20 @@ def _gather(ctx, n, ins):
     batch_dims = int(n.attr("batch_dims", 0))
     if batch_dims:
         raise Unsupported("GatherV2 with batch_dims")
-    idx = idx.to(params.device).long()
     if ax < 0:
         ax += params.dim()
-    if idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= params.shape[ax]):
+    if idx.device.type == "cpu" and idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= params.shape[ax]):
         raise OpError(f"{n.name}: indices out of range [0, {params.shape[ax]})")
-    out = torch.index_select(params, ax, idx.reshape(-1))
+    idx = idx.to(params.device).long()
+    if params.is_cuda:
+        # no host sync (HIP-graph capturable): out-of-range rows read as zeros, as TF's GPU kernel does
+        n_ax = params.shape[ax]
+        valid = (idx >= 0) & (idx < n_ax)
+        out = torch.index_select(params, ax, idx.clamp(0, n_ax - 1).reshape(-1))
+        vshape = [1] * ax + [idx.numel()] + [1] * (params.dim() - ax - 1)
+        out = out * valid.reshape(vshape).to(out.dtype)
+    else:
+        out = torch.index_select(params, ax, idx.reshape(-1))
     shape = list(params.shape[:ax]) + list(idx.shape) + list(params.shape[ax + 1:])
     return [out.reshape(shape)]
 

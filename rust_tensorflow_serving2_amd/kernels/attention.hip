@@ -25,7 +25,8 @@ constexpr int QB = 64;       // query rows per workgroup (4 waves x 16)
 template <int S>
 __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restrict__ qkv,
                                                         const float* __restrict__ mask_bias,
-                                                        uint16_t* __restrict__ ctx, int H, float scale) {
+                                                        uint16_t* __restrict__ ctx, int H, float scale,
+                                                        long mask_bstride, long mask_qstride) {
   constexpr int VT_LD = S + 8;           // Vt row stride (elements): +16 B pad
   constexpr int P_LD = S + 8;
   constexpr int NT = S / 16;             // key tiles
@@ -81,11 +82,12 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
   }
   // ---- softmax (rows fq*4 + r, columns nt*16 + fr)
   float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  const float* mrow = mask_bias ? mask_bias + long(b) * mask_bstride + long(q0 + fq * 4) * mask_qstride : nullptr;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
-    const float mb = mask_bias ? mask_bias[long(b) * S + nt * 16 + fr] : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      const float mb = mrow ? mrow[long(r) * mask_qstride + nt * 16 + fr] : 0.f;
       const float v = s[nt][r] * scale + mb;
       s[nt][r] = v;
       mx[r] = fmaxf(mx[r], v);
@@ -135,7 +137,8 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
 }
 
 template <int S>
-hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, int H, float scale, hipStream_t st) {
+hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, int H, float scale, long bs, long qs,
+                    hipStream_t st) {
   constexpr int lds = (S * D + D * (S + 8) + 4 * 16 * (S + 8)) * 2;
   static bool attr = false;
   if (!attr) {
@@ -145,20 +148,21 @@ hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, 
     attr = true;
   }
   const int grid = B * H * (S / QB);
-  hipLaunchKernelGGL((attention_kernel<S>), dim3(grid), dim3(256), lds, st, qkv, mb, ctx, H, scale);
+  hipLaunchKernelGGL((attention_kernel<S>), dim3(grid), dim3(256), lds, st, qkv, mb, ctx, H, scale, bs, qs);
   return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t attention_launch(const uint16_t* qkv, const float* mask_bias, uint16_t* ctx, int B, int S, int H,
-                            int Dh, float scale, hipStream_t st) {
+                            int Dh, float scale, long mask_bstride, long mask_qstride, hipStream_t st) {
   if (Dh != D) return hipErrorInvalidValue;
+  const long bs = mask_bstride, qs = mask_qstride;
   switch (S) {
-    case 64: return launch_s<64>(qkv, mask_bias, ctx, B, H, scale, st);
-    case 128: return launch_s<128>(qkv, mask_bias, ctx, B, H, scale, st);
-    case 192: return launch_s<192>(qkv, mask_bias, ctx, B, H, scale, st);
-    case 256: return launch_s<256>(qkv, mask_bias, ctx, B, H, scale, st);
+    case 64: return launch_s<64>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
+    case 128: return launch_s<128>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
+    case 192: return launch_s<192>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
+    case 256: return launch_s<256>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
     default: return hipErrorInvalidValue;
   }
 }

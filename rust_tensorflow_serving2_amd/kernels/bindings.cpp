@@ -261,7 +261,7 @@ Tensor embed_ln(const Tensor& ids, const c10::optional<Tensor>& type_ids, const 
 }
 
 Tensor attention(const Tensor& qkv, const c10::optional<Tensor>& mask_bias, int64_t heads, double scale,
-                 const c10::optional<Tensor>& out) {
+                 const c10::optional<Tensor>& out, int64_t mask_bstride, int64_t mask_qstride) {
   need(qkv, at::kBFloat16, "qkv");
   TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, S, 3*H*D]");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
@@ -269,15 +269,20 @@ Tensor attention(const Tensor& qkv, const c10::optional<Tensor>& mask_bias, int6
   TORCH_CHECK(HD3 % (3 * heads) == 0, "qkv width must be 3*heads*head_dim");
   const int D = HD3 / (3 * heads);
   TORCH_CHECK(D == 64, "attention kernel supports head_dim 64");
+  TORCH_CHECK(S == 64 || S == 128 || S == 192 || S == 256, "attention kernel supports S in {64,128,192,256}");
   const float* mb = nullptr;
   if (mask_bias.has_value()) {
     need(*mask_bias, at::kFloat, "mask_bias");
-    TORCH_CHECK(mask_bias->numel() == int64_t(B) * S, "mask_bias must be [B, S]");
+    // largest index the kernel reads must be inside the mask tensor
+    const int64_t last = int64_t(B - 1) * mask_bstride + int64_t(S - 1) * mask_qstride + (S - 1);
+    TORCH_CHECK(mask_bstride >= 0 && mask_qstride >= 0 && last < mask_bias->numel(),
+                "mask strides exceed the mask tensor");
     mb = mask_bias->data_ptr<float>();
   }
   Tensor y = out.has_value() ? *out : torch::empty({B, S, heads * D}, qkv.options());
   need(y, at::kBFloat16, "out");
-  check(tfsk::attention_launch(bf16p(qkv), mb, bf16p_mut(y), B, S, heads, D, float(scale), cur_stream(qkv)),
+  check(tfsk::attention_launch(bf16p(qkv), mb, bf16p_mut(y), B, S, heads, D, float(scale), mask_bstride,
+                               mask_qstride, cur_stream(qkv)),
         "attention");
   return y;
 }
@@ -305,7 +310,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_ln", &embed_ln, py::arg("ids"), py::arg("type_ids"), py::arg("word"), py::arg("pos"),
         py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("eps"));
   m.def("attention", &attention, py::arg("qkv"), py::arg("mask_bias"), py::arg("heads"), py::arg("scale"),
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("mask_bstride") = 0, py::arg("mask_qstride") = 0);
   m.def("num_configs", []() { return tfsk::kNumIGemmConfigs; });
   m.def("config_tile", [](int cfg) { return std::make_pair(tfsk::igemm_config_bm(cfg), tfsk::igemm_config_bn(cfg)); });
 }

@@ -75,8 +75,10 @@ hipError_t embed_ln_launch(const int64_t* ids, const int64_t* type_ids, const ui
                            const float* beta, uint16_t* y, int tokens, int seq, int hidden,
                            int vocab, int ntypes, float eps, hipStream_t stream);
 // Fused multi-head attention over a packed QKV buffer [B*S][3*H*D] (bf16):
-// ctx[b,s,h,:] = softmax(Q K^T * scale + mask_bias[b, :]) V ; mask_bias f32 [B][S] (0 / -1e4 style)
+// ctx[b,q,h,:] = softmax(Q K^T * scale + mask[b*bstride + q*qstride + key]) V
+// (additive f32 mask; strides 0 broadcast, e.g. BERT's [B,1,S,S] adder or a [B,S] key mask)
 hipError_t attention_launch(const uint16_t* qkv, const float* mask_bias, uint16_t* ctx, int B, int S,
-                            int H, int D, float scale, hipStream_t stream);
+                            int H, int D, float scale, long mask_bstride, long mask_qstride,
+                            hipStream_t stream);
 
 }  // namespace tfsk

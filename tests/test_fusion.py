@@ -1,0 +1,79 @@
+"""Fusion passes on CPU: fused graph (fp32 reference of the fused ops, same
+folded parameters the HIP kernels use) == unfused reference interpreter, and
+the expected patterns were actually matched."""
+import os
+
+import numpy as np
+import pytest
+
+from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
+
+
+@pytest.fixture(scope="module")
+def tiny_bert(models_dir):
+    from rust_tensorflow_serving2_amd.models import bert
+    cfg = bert.BertConfig(vocab_size=100, hidden=64, layers=2, heads=2, intermediate=128, max_position=64, seq_len=32)
+    path = os.path.join(str(models_dir), "tiny_bert", "1")
+    bert.export(path, cfg, seed=3)
+    return path
+
+
+def _pair(path):
+    return (Servable("m", 1, path, ServableOptions(device="cpu")),
+            Servable("m", 1, path, ServableOptions(device="cpu", fuse=True)))
+
+
+def test_resnet_fusion_exact(tiny_resnet_path):
+    ref, fused = _pair(os.path.join(tiny_resnet_path, "1"))
+    x = np.random.default_rng(0).random((3, 32, 32, 3), dtype=np.float32)
+    a = ref.run("serving_default", {"input": x}, ["classes", "probabilities"])
+    b = fused.run("serving_default", {"input": x}, ["classes", "probabilities"])
+    np.testing.assert_allclose(a["probabilities"], b["probabilities"], atol=1e-5)
+    np.testing.assert_array_equal(a["classes"], b["classes"])
+    hist = fused.runner("serving_default", ["input"], ["classes", "probabilities"]).program.op_histogram()
+    assert hist["_FusedConv2D"] == 17 and "Conv2D" not in hist and "FusedBatchNormV3" not in hist
+    assert hist["_SoftmaxArgMax"] == 1 and hist["_GlobalAvgPool"] == 1 and hist["_MaxPool"] == 1
+
+
+def test_bert_fusion_exact(tiny_bert):
+    ref, fused = _pair(tiny_bert)
+    rng = np.random.default_rng(0)
+    ids = rng.integers(0, 100, (3, 32)).astype(np.int32)
+    mask = np.ones((3, 32), np.int32)
+    mask[1, 20:] = 0
+    seg = np.zeros((3, 32), np.int32)
+    seg[:, 16:] = 1
+    feeds = {"input_ids": ids, "input_mask": mask, "segment_ids": seg}
+    outs = ["pooled_output", "probabilities"]
+    a, b = ref.run("serving_default", feeds, outs), fused.run("serving_default", feeds, outs)
+    for k in outs:
+        np.testing.assert_allclose(a[k], b[k], atol=1e-5)
+    hist = fused.runner("serving_default", sorted(feeds), outs).program.op_histogram()
+    assert hist["_LayerNorm"] == 5 and hist["_Attention"] == 2 and hist["_FusedQKV"] == 2
+    assert hist["_FusedMatMul"] == 8 and "MatMul" not in hist and "BatchMatMulV2" not in hist
+    assert "Rsqrt" not in hist and "Pow" not in hist and "Tanh" not in hist
+
+
+def test_gelu_erf_form_matches():
+    """Keras-style erf GELU subgraph is recognised too."""
+    import torch
+    from rust_tensorflow_serving2_amd.graph.builder import DType, GraphBuilder
+    from rust_tensorflow_serving2_amd.graph.compiler import compile_program
+    from rust_tensorflow_serving2_amd.graph.fused import default_passes
+    from rust_tensorflow_serving2_amd.graph.ir import from_graph_def
+    from rust_tensorflow_serving2_amd.utils import tensors as T
+    f32 = DType(T.DT_FLOAT)
+    g = GraphBuilder()
+    x = g.placeholder("x", T.DT_FLOAT, [-1, 16])
+    w = g.const("w", np.random.default_rng(0).standard_normal((16, 24)).astype(np.float32))
+    y = g.node("MatMul", "mm", [x, w], T=f32)
+    half = g.node("Mul", "half", [y, g.const("c05", np.float32(0.5))], T=f32)
+    d = g.node("RealDiv", "div", [y, g.const("sq2", np.float32(np.sqrt(2)))], T=f32)
+    e = g.node("Erf", "erf", [d], T=f32)
+    a = g.node("AddV2", "add", [g.const("one", np.float32(1.0)), e], T=f32)
+    out = g.node("Mul", "gelu", [half, a], T=f32)
+    xs = torch.randn(5, 16)
+    p0 = compile_program(from_graph_def(g.graph), ["x:0"], [out + ":0"])
+    p1 = compile_program(from_graph_def(g.graph), ["x:0"], [out + ":0"], passes=default_passes())
+    assert p1.op_histogram() == {"_FusedMatMul": 1}
+    torch.testing.assert_close(p0.run([xs])[0], p1.run([xs])[0], atol=1e-5, rtol=1e-5)

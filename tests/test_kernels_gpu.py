@@ -177,8 +177,14 @@ def test_attention_matches_fp32(s):
     qkv = rnd(b, s, 3 * h * d, seed=21).to(BF)
     mask = torch.zeros(b, s)
     mask[1, s // 2:] = -10000.0
-    y = hip().attention(qkv.to(DEV), mask.to(DEV), h, 1 / math.sqrt(d))
+    y = hip().attention(qkv.to(DEV), mask.to(DEV), h, 1 / math.sqrt(d), None, s, 0)   # [B, S] key mask
     q, k, v = qkv.float().reshape(b, s, 3, h, d).permute(2, 0, 3, 1, 4)
     att = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(d) + mask[:, None, None, :], -1)
     ref = (att @ v).permute(0, 2, 1, 3).reshape(b, s, h * d)
     assert (y.float().cpu() - ref).abs().max() < 3e-2
+    # full per-query mask [B, 1, S, S] (BERT adder layout), causal-style pattern
+    full = torch.triu(torch.full((s, s), -10000.0), 1).expand(b, 1, s, s).contiguous()
+    y2 = hip().attention(qkv.to(DEV), full.to(DEV), h, 1 / math.sqrt(d), None, s * s, s)
+    att2 = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(d) + full, -1)
+    ref2 = (att2 @ v).permute(0, 2, 1, 3).reshape(b, s, h * d)
+    assert (y2.float().cpu() - ref2).abs().max() < 3e-2
