@@ -87,6 +87,9 @@ Tensor conv2d(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   tfsk::IGemmArgs a{};
   a.a = x.data_ptr();
   a.b = bf16p(w);
+  a.a_bytes = x.numel() * x.element_size();
+  a.b_bytes = w.numel() * 2;
+  TORCH_CHECK(a.a_bytes < 0x7ffffff0LL && a.b_bytes < 0x7ffffff0LL, "conv operands must be < 2 GiB");
   a.M = N * Ho * Wo; a.N = Cout; a.K = K; a.lda = C; a.ldb = ldb;
   a.H = H; a.W = W; a.C = C; a.KH = KH; a.KW = KW; a.SH = SH; a.SW = SW; a.PT = PT; a.PL = PL;
   a.Ho = Ho; a.Wo = Wo;
@@ -124,6 +127,9 @@ Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   TORCH_CHECK(y.numel() == int64_t(M) * N, "out has the wrong size");
   tfsk::IGemmArgs a{};
   a.a = x.data_ptr(); a.b = bf16p(w);
+  a.a_bytes = x.numel() * 2;
+  a.b_bytes = w.numel() * 2;
+  TORCH_CHECK(a.a_bytes < 0x7ffffff0LL && a.b_bytes < 0x7ffffff0LL, "linear operands must be < 2 GiB");
   a.M = M; a.N = N; a.K = K; a.lda = K; a.ldb = ldb;
   if (bias.has_value()) {
     need(*bias, at::kFloat, "bias");

@@ -64,10 +64,16 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   const int m0 = bm * BM, n0 = bn * BN;
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int chunk = tid & 7;
   const int row_base = tid >> 3;   // 0..31
+  // Direct-to-LDS staging (dense / im2col operands): each wave instruction
+  // DMAs 64 lanes x 16 B = 8 rows x 128 B into a lane-linear LDS image, so
+  // lane l fills row (l>>3) at 16-B slot (l&7); the XOR swizzle is applied to
+  // the *source* chunk instead (logical chunk = slot ^ (row & 7)).
+  constexpr bool GL = (AMODE == kADense || AMODE == kAIm2col);
+  const int gl_chunk = (lane & 7) ^ ((lane >> 3) & 7);
 
   // ---- per-thread A row descriptors
   int a_off[G::A_CHUNKS];     // element offset of the row's base (dense: m*lda; im2col: image base)
@@ -75,7 +81,8 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   bool a_ok[G::A_CHUNKS];
 #pragma unroll
   for (int i = 0; i < G::A_CHUNKS; ++i) {
-    const int m = m0 + row_base + 32 * i;
+    const int rloc = GL ? wid * (BM / 4) + i * 8 + (lane >> 3) : row_base + 32 * i;
+    const int m = m0 + rloc;
     a_ok[i] = m < M;
     const int mm = a_ok[i] ? m : 0;
     if (AMODE == kADense) {
@@ -192,6 +199,48 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
     }
   };
 
+  // buffer descriptors: out-of-range offsets read as 0 (conv padding, M/N/K tails)
+  constexpr uint32_t kOOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.a), 0, int(p.a_bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(p.b), 0, int(p.b_bytes), 0x00020000);
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+  auto gstage = [&](int buf, int kt) {
+    const int kc = kt * BK + gl_chunk * 8;
+    uint16_t* as = As + buf * BM * BK;
+    uint16_t* bs = Bs + buf * BN * BK;
+    if (AMODE == kADense) {
+#pragma unroll
+      for (int i = 0; i < G::A_CHUNKS; ++i) {
+        const uint32_t off = (a_ok[i] && kc < K) ? uint32_t(a_off[i] + kc) * 2u : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(as + (wid * (BM / 4) + i * 8) * BK), 16, off,
+                                                 0, 0, 0);
+      }
+    } else {
+      const int tap = kc / p.C;
+      const int ci = kc - tap * p.C;
+      const int kh = tap / p.KW, kw = tap - kh * p.KW;
+      const bool kok = kc < K;
+#pragma unroll
+      for (int i = 0; i < G::A_CHUNKS; ++i) {
+        const int hi = a_hi[i] + kh, wi = a_wi[i] + kw;
+        const bool ok = kok && a_ok[i] && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+        const uint32_t off = ok ? uint32_t(a_off[i] + (hi * p.W + wi) * p.C + ci) * 2u : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(as + (wid * (BM / 4) + i * 8) * BK), 16, off,
+                                                 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < G::B_CHUNKS; ++i) {
+      const int n = n0 + wid * (BN / 4) + i * 8 + (lane >> 3);
+      const uint32_t off = (n < N && kc < p.ldb) ? (uint32_t(n) * uint32_t(p.ldb) + uint32_t(kc)) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_ptr_t)(bs + (wid * (BN / 4) + i * 8) * BK), 16, off,
+                                               0, 0, 0);
+    }
+  };
+
   auto sstore = [&](int buf) {
     uint16_t* as = As + buf * BM * BK;
     uint16_t* bs = Bs + buf * BN * BK;
@@ -216,14 +265,24 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   const int nk_all = (K + BK - 1) / BK;
   const int kt0 = p.splits > 1 ? blockIdx.y * p.kt_per_split : 0;
   const int nk = p.splits > 1 ? min(nk_all, kt0 + p.kt_per_split) - kt0 : nk_all;
-  gload(kt0);
-  sstore(0);
+  if (GL) {
+    gstage(0, kt0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    gload(kt0);
+    sstore(0);
+  }
   __syncthreads();
 
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt0 + kt + 1);
+    if (GL) {
+      // DMA of tile kt+1 into the other buffer runs under this tile's MFMAs
+      if (kt + 1 < nk) gstage(cur ^ 1, kt0 + kt + 1);
+    } else if (kt + 1 < nk) {
+      gload(kt0 + kt + 1);
+    }
     const uint16_t* as = As + cur * BM * BK;
     const uint16_t* bs = Bs + cur * BN * BK;
 #pragma unroll
@@ -246,7 +305,12 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
         for (int j = 0; j < G::TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) sstore(cur ^ 1);
+    if (GL) {
+      // retire this wave's DMA, then the barrier makes every wave's DMA visible
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (kt + 1 < nk) {
+      sstore(cur ^ 1);
+    }
     __syncthreads();
   }
 

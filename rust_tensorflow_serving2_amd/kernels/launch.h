@@ -30,6 +30,10 @@ struct IGemmArgs {
   int splits;
   int kt_per_split;
   float* ws;
+  // byte extents of A and B (buffer-descriptor bounds for the direct-to-LDS
+  // loads; must be < 2^31)
+  int64_t a_bytes;
+  int64_t b_bytes;
 };
 
 // kAStem7x7x3: fp32 NHWC input with C == 3 and a 7-wide filter (the ResNet
