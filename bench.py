@@ -99,8 +99,8 @@ def main():
 
     weight_source = None
     if world > 1:
-        from rust_tensorflow_serving2_amd.parallel.weights import RcclWeightSource
-        weight_source = RcclWeightSource(device=device)
+        from rust_tensorflow_serving2_amd.parallel.weights import ReplicatedWeightSource
+        weight_source = ReplicatedWeightSource(dist.distributed_c10d._get_default_store(), device=device)
     sopts = ServableOptions(device=str(device), max_batch_size=args.batch,
                             allowed_batch_sizes=tuple(sorted({1, 2, 4, 8, 16, args.batch})))
     port = (args.port + local) if args.port else 0

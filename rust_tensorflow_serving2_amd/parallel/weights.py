@@ -1,18 +1,33 @@
 """Multi-GPU model loading: read the SavedModel once, broadcast over RCCL.
 
 One server process per GPU (``torch.distributed``, backend ``nccl`` == RCCL on
-ROCm).  Rank ``root`` reads ``saved_model.pb`` + the TensorBundle from disk,
-packs every variable into ONE contiguous byte blob on its GPU and
-``broadcast``s it over xGMI (a single large collective, ring/tree-pipelined
-by RCCL: ResNet-50's 102 MB fp32 blob ~ 1 ms at link rate), then every rank
-rebuilds an in-memory bundle with the same API as
-:class:`~..savedmodel.bundle.Bundle`.  The graph proto (small) is broadcast
-as bytes with the object collective on the same group.
+ROCm; ``gloo`` for CPU replicas in tests).  The leader rank reads
+``saved_model.pb`` + the TensorBundle from disk, packs every variable into ONE
+contiguous byte blob on its device and ``broadcast``s it (a single large
+collective, ring/tree-pipelined by RCCL over xGMI: ResNet-50's 102 MB fp32
+blob is ~1 ms at link rate, BERT-base's 440 MB ~4 ms); every rank rebuilds an
+in-memory bundle with the same API as :class:`~..savedmodel.bundle.Bundle`.
+The small graph proto travels with the object collective on the same group.
+
+Collective ordering.  Each rank's model manager decides *when* to load on its
+own (file-system polling, reload RPCs arriving on any rank), but collectives
+must be issued in the same order everywhere.  So only the leader initiates:
+its loader takes a process-wide lock, publishes ``(seq, name, version, path)``
+to the control store and then broadcasts; every follower has ONE event thread
+that consumes leader events strictly in ``seq`` order, joins each broadcast
+and hands the bundle to the local manager's pending load (or parks it until
+the local manager asks for it).  The reference has no multi-GPU path at all
+(one TF Serving container, ``serving/rundocker.sh:15``).
 """
 from __future__ import annotations
 
-import os
-from typing import Dict, Optional
+import json
+import logging
+import threading
+import time
+from concurrent.futures import Future
+from concurrent.futures import TimeoutError as FutureTimeout
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 import torch
@@ -21,6 +36,8 @@ import torch.distributed as dist
 from ..savedmodel import saved_model as sm
 from ..schema import tf
 from ..utils import tensors as T
+
+log = logging.getLogger("tfserve.weights")
 
 
 class MemoryBundle:
@@ -46,53 +63,172 @@ class MemoryBundle:
         return self._a[k]
 
 
-class RcclWeightSource:
-    """Loads a servable version on every rank with one RCCL broadcast of the weights."""
+class LoadError(RuntimeError):
+    pass
 
-    def __init__(self, group=None, root: int = 0, device: Optional[torch.device] = None):
-        self.group = group
-        self.root = root
-        self.rank = dist.get_rank(group)
-        self.device = device or torch.device("cuda", torch.cuda.current_device())
-        self.last_broadcast_bytes = 0
-        self.last_broadcast_s = 0.0
 
-    def load(self, name: str, version: int, path: str) -> sm.SavedModelBundle:
-        meta = [None]
-        if self.rank == self.root:
+def _sync(device: torch.device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def broadcast_bundle(path: Optional[str], root: int, group, device: torch.device,
+                     stats: Optional[dict] = None) -> sm.SavedModelBundle:
+    """Collective: root reads ``path`` and every rank returns the same bundle.
+
+    A load failure on the root is broadcast as an error so followers never
+    block on a blob that is not coming.
+    """
+    rank = dist.get_rank(group)
+    meta = [None]
+    b = None
+    if rank == root:
+        try:
             b = sm.load(path)
             names = sorted(b.bundle.keys()) if b.bundle is not None else []
             entries = [(n, b.bundle.dtype(n), list(b.bundle.shape(n))) for n in names]
-            meta[0] = (b.meta_graph.SerializeToString(), entries, list(b.tags))
-        dist.broadcast_object_list(meta, src=self.root, group=self.group)
-        mg_bytes, entries, tags = meta[0]
-        sizes = []
-        for _n, dt, shape in entries:
-            sizes.append(int(np.prod(shape)) * np.dtype(T.np_dtype(dt)).itemsize if shape else
-                         np.dtype(T.np_dtype(dt)).itemsize)
-        total = int(sum(sizes))
-        blob = torch.empty(total, dtype=torch.uint8, device=self.device)
-        if self.rank == self.root:
-            host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
-            off = 0
-            for (n, dt, shape), sz in zip(entries, sizes):
-                a = np.require(b.bundle[n], requirements="C")
-                host[off:off + sz].numpy()[:] = a.reshape(-1).view(np.uint8)
-                off += sz
-            blob.copy_(host, non_blocking=True)
-        torch.cuda.synchronize(self.device)
-        import time
-        t0 = time.perf_counter()
-        dist.broadcast(blob, src=self.root, group=self.group)
-        torch.cuda.synchronize(self.device)
-        self.last_broadcast_s = time.perf_counter() - t0
-        self.last_broadcast_bytes = total
-        cpu = blob.cpu().numpy()
-        arrays, dtypes = {}, {}
+            meta[0] = ("ok", b.meta_graph.SerializeToString(), entries, list(b.tags))
+        except Exception as e:    # propagated to every rank
+            meta[0] = ("error", f"{type(e).__name__}: {e}", None, None)
+    dist.broadcast_object_list(meta, src=root, group=group,
+                               device=device if device.type == "cuda" else None)
+    status, mg_bytes, entries, tags = meta[0]
+    if status != "ok":
+        raise LoadError(mg_bytes)
+    sizes = []
+    for _n, dt, shape in entries:
+        item = np.dtype(T.np_dtype(dt)).itemsize
+        sizes.append(int(np.prod(shape)) * item if shape else item)
+    total = int(sum(sizes))
+    blob = torch.empty(max(total, 1), dtype=torch.uint8, device=device)
+    if rank == root:
+        host = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=device.type == "cuda")
+        hv = host.numpy()
         off = 0
-        for (n, dt, shape), sz in zip(entries, sizes):
-            arrays[n] = cpu[off:off + sz].view(T.np_dtype(dt)).reshape(shape)
-            dtypes[n] = dt
+        for (n, _dt, _shape), sz in zip(entries, sizes):
+            a = np.require(b.bundle[n], requirements="C")
+            hv[off:off + sz] = a.reshape(-1).view(np.uint8)
             off += sz
-        mg = tf.MetaGraphDef.FromString(mg_bytes)
-        return sm.SavedModelBundle(path, mg, MemoryBundle(arrays, dtypes), tags)
+        blob.copy_(host, non_blocking=True)
+    _sync(device)
+    t0 = time.perf_counter()
+    dist.broadcast(blob, src=root, group=group)
+    _sync(device)
+    if stats is not None:
+        stats["broadcast_s"] = time.perf_counter() - t0
+        stats["broadcast_bytes"] = total
+    cpu = blob.cpu().numpy()
+    arrays, dtypes = {}, {}
+    off = 0
+    for (n, dt, shape), sz in zip(entries, sizes):
+        arrays[n] = cpu[off:off + sz].view(T.np_dtype(dt)).reshape(shape)
+        dtypes[n] = dt
+        off += sz
+    mg = tf.MetaGraphDef.FromString(mg_bytes)
+    return sm.SavedModelBundle(path or "", mg, MemoryBundle(arrays, dtypes), tags)
+
+
+class ReplicatedWeightSource:
+    """``load(name, version, path)`` for every replica, with leader-ordered collectives.
+
+    ``store`` is a ``torch.distributed.Store`` shared by the replicas (the
+    default group's TCPStore works); ``group`` the process group the weight
+    broadcast runs on (nccl/RCCL for GPUs, gloo for CPU replicas).
+    """
+
+    def __init__(self, store, group=None, device: Optional[torch.device] = None, leader: int = 0,
+                 load_timeout: float = 900.0, prefix: str = "tfs/wev"):
+        self.store = store
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.leader = leader
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+                else torch.device("cpu")
+        self.device = device
+        self.load_timeout = load_timeout
+        self.prefix = prefix
+        self.stats: dict = {}
+        self._lock = threading.Lock()           # leader: one collective at a time, seq order
+        self._seq = 0
+        self._pending: Dict[Tuple[str, int], Future] = {}
+        self._parked: Dict[Tuple[str, int], Tuple[float, object]] = {}
+        self._stop = threading.Event()
+        self._thread = None
+        if self.rank != leader:
+            self._thread = threading.Thread(target=self._follow, name="tfs-wev", daemon=True)
+            self._thread.start()
+
+    @property
+    def is_leader(self) -> bool:
+        return self.rank == self.leader
+
+    # ------------------------------------------------------------ leader
+    def _publish_and_broadcast(self, name: str, version: int, path: str):
+        with self._lock:
+            self._seq += 1
+            self.store.set(f"{self.prefix}/{self._seq}", json.dumps([name, int(version), path]))
+            return broadcast_bundle(path, self.leader, self.group, self.device, self.stats)
+
+    # ------------------------------------------------------------ follower
+    def _follow(self):
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        seq = 1
+        while not self._stop.is_set():
+            key = f"{self.prefix}/{seq}"
+            if not self.store.check([key]):     # non-blocking poll (lets close() end the thread)
+                self._stop.wait(0.02)
+                continue
+            name, version, path = json.loads(self.store.get(key).decode())
+            seq += 1
+            try:
+                res = broadcast_bundle(None, self.leader, self.group, self.device, self.stats)
+                err = None
+            except Exception as e:
+                res, err = None, e
+            k = (name, version)
+            with self._lock:
+                fut = self._pending.pop(k, None)
+                if fut is None:
+                    self._parked[k] = (time.time(), err if err is not None else res)
+                    self._expire()
+            if fut is not None:
+                if err is not None:
+                    fut.set_exception(err)
+                else:
+                    fut.set_result(res)
+
+    def _expire(self, ttl: float = 600.0):
+        now = time.time()
+        for k in [k for k, (t, _) in self._parked.items() if now - t > ttl]:
+            del self._parked[k]
+
+    # ------------------------------------------------------------ API
+    def load(self, name: str, version: int, path: str):
+        if self.is_leader:
+            return self._publish_and_broadcast(name, version, path)
+        k = (name, int(version))
+        with self._lock:
+            parked = self._parked.pop(k, None)
+            if parked is None:
+                fut = self._pending.get(k)
+                if fut is None:
+                    fut = self._pending[k] = Future()
+        if parked is not None:
+            if isinstance(parked[1], Exception):
+                raise parked[1]
+            return parked[1]
+        try:
+            return fut.result(timeout=self.load_timeout)
+        except FutureTimeout:
+            with self._lock:
+                self._pending.pop(k, None)
+            raise LoadError(f"timed out waiting for the leader rank to broadcast {name} version {version}")
+
+    def close(self):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5)
+

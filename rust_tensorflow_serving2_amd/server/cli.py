@@ -1,0 +1,170 @@
+"""``python -m rust_tensorflow_serving2_amd.server`` — the model server binary.
+
+Replaces the stock container the reference starts with
+``docker run -p 9000:8500 -p 9001:8501 -v $(pwd)/models:/models/resnet
+-e MODEL_NAME=resnet tensorflow/serving`` (``serving/rundocker.sh:15``).  Flag
+names follow TensorFlow Serving's ``tensorflow_model_server`` so existing
+launch scripts keep working::
+
+    python -m rust_tensorflow_serving2_amd.server --port=8500 --rest_api_port=8501 \\
+        --model_name=resnet --model_base_path=/models/resnet --num_gpus=8
+
+``--num_gpus N`` (N > 1, or 0 = every visible GPU) starts one replica process
+per GPU (``parallel/replicas.py``): all replicas share the gRPC/REST ports via
+SO_REUSEPORT, weights are read once and broadcast over RCCL, and reload
+requests are replicated to every GPU.  The same entry point runs under
+``torchrun`` (it honours RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import signal
+import sys
+import threading
+import time
+from typing import List, Optional
+
+log = logging.getLogger("tfserve.cli")
+
+
+def _bool(v: str) -> bool:
+    return str(v).lower() in ("1", "true", "yes", "on")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="python -m rust_tensorflow_serving2_amd.server",
+                                 description="MI355X-native TensorFlow-Serving-compatible model server")
+    a = ap.add_argument
+    a("--port", type=int, default=8500, help="gRPC port (PredictionService + ModelService)")
+    a("--rest_api_port", type=int, default=0, help="REST/HTTP port (0 = disabled)")
+    a("--host", "--grpc_host", default="0.0.0.0", dest="host")
+    a("--model_name", default="default")
+    a("--model_base_path", default="")
+    a("--model_config_file", default="", help="text-format ModelServerConfig (supersedes --model_name/base_path)")
+    a("--model_config_file_poll_wait_seconds", type=float, default=0.0)
+    a("--file_system_poll_wait_seconds", type=float, default=1.0)
+    a("--enable_batching", type=_bool, nargs="?", const=True, default=False)
+    a("--batching_parameters_file", default="", help="text-format BatchingParameters")
+    a("--enable_model_warmup", type=_bool, nargs="?", const=True, default=True)
+    a("--monitoring", type=_bool, nargs="?", const=True, default=True,
+      help="Prometheus metrics at /monitoring/prometheus/metrics on the REST port")
+    # MI355X-specific
+    a("--device", default="auto", help="auto | cpu | cuda[:i] (replicas always use cuda:LOCAL_RANK)")
+    a("--num_gpus", type=int, default=1, help="replica processes, one per GPU (0 = all visible GPUs)")
+    a("--transport", default="native", choices=["native", "grpc"],
+      help="native = C++ HTTP/2 front end with the Predict fast path; grpc = grpcio server")
+    a("--io_threads", type=int, default=4, help="native transport epoll threads (per replica)")
+    a("--batch_timeout_us", type=int, default=2000, help="fast-path batch window when batching params unset")
+    a("--max_batch_size", type=int, default=32, help="fast-path GPU batch (HIP-graph bucket) limit")
+    a("--hip_graphs", type=_bool, nargs="?", const=True, default=True)
+    a("--log_level", default="INFO")
+    return ap
+
+
+def _read_text_proto(path: str, msg):
+    from google.protobuf import text_format
+    with open(path) as f:
+        text_format.Parse(f.read(), msg)
+    return msg
+
+
+def make_server(args, rank: int = 0, world: int = 1):
+    """Build a ModelServer for this process (replica ``rank`` of ``world``)."""
+    import torch
+    from ..schema import serving
+    from .servable import ServableOptions
+    from .server import ModelServer, ServerOptions
+
+    if world > 1:
+        device = f"cuda:{int(os.environ.get('LOCAL_RANK', rank))}" if args.device in ("auto", "cuda") or \
+            args.device.startswith("cuda") else "cpu"
+    elif args.device == "auto":
+        device = "cuda:0" if torch.cuda.is_available() else "cpu"
+    elif args.device == "cuda":
+        device = "cuda:0"
+    else:
+        device = args.device
+    batching = None
+    if args.enable_batching and args.batching_parameters_file:
+        batching = _read_text_proto(args.batching_parameters_file, serving.BatchingParameters())
+    weight_source = replicas = None
+    if world > 1:
+        import torch.distributed as dist
+        from ..parallel.replicas import ReplicaControl
+        from ..parallel.weights import ReplicatedWeightSource
+        dev = torch.device(device)
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if dev.type == "cuda":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group("gloo")
+        store = dist.distributed_c10d._get_default_store()
+        weight_source = ReplicatedWeightSource(store, device=dev)
+        replicas = ReplicaControl(store, rank, world)
+    sopts = ServableOptions(device=device, hip_graphs=args.hip_graphs, warmup=args.enable_model_warmup,
+                            max_batch_size=args.max_batch_size)
+    opts = ServerOptions(port=args.port, rest_api_port=args.rest_api_port, host=args.host,
+                         model_name=args.model_name, model_base_path=args.model_base_path,
+                         model_config_file=args.model_config_file,
+                         model_config_file_poll_wait_seconds=args.model_config_file_poll_wait_seconds,
+                         device=device, enable_batching=args.enable_batching, batching_parameters=batching,
+                         transport=args.transport, file_system_poll_wait_seconds=args.file_system_poll_wait_seconds,
+                         io_threads=args.io_threads, batch_timeout_us=args.batch_timeout_us, servable=sopts,
+                         monitoring=args.monitoring, weight_source=weight_source, replicas=replicas)
+    return ModelServer(opts)
+
+
+def serve(args, rank: int = 0, world: int = 1, ready: Optional[threading.Event] = None,
+          stop: Optional[threading.Event] = None) -> int:
+    server = make_server(args, rank, world)
+    server.start()
+    log.info("replica %d/%d serving gRPC on %s:%d%s", rank, world, args.host, server.port,
+             f", REST on {server.rest_port}" if getattr(server, "rest_port", None) else "")
+    print(f"[tfserve] replica {rank}/{world} ready: grpc={server.port}"
+          + (f" rest={server.rest_port}" if getattr(server, "rest_port", None) else ""), flush=True)
+    stop = stop or threading.Event()
+    signalled = []
+    if threading.current_thread() is threading.main_thread():
+        # the handler only flips a flag: Event.set() from a signal handler can
+        # deadlock against the main thread's own Event.wait() (same lock)
+        for s in (signal.SIGINT, signal.SIGTERM):
+            signal.signal(s, lambda *_: signalled.append(1))
+    if ready is not None:
+        ready.set()
+    while not signalled and not stop.is_set():
+        time.sleep(0.1)
+    server.stop()
+    if world > 1:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    return 0
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    import faulthandler
+    faulthandler.register(signal.SIGUSR1, all_threads=True)     # `kill -USR1 <pid>` dumps stacks
+    args = build_parser().parse_args(argv)
+    logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env > 1:                       # a replica (launched by us or by torchrun)
+        return serve(args, int(os.environ.get("RANK", "0")), world_env)
+    n = args.num_gpus
+    if n == 0:
+        import torch                         # device_count() does not initialise the GPU
+        n = max(1, torch.cuda.device_count())
+    if n > 1:
+        from ..parallel.replicas import launch
+        return launch(argv, n)
+    return serve(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

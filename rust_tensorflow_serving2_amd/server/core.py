@@ -56,6 +56,7 @@ class ServingCore:
         self.batcher = batcher
         self.request_logger = request_logger
         self.metrics = metrics
+        self.replicas = None          # parallel.replicas.ReplicaControl when serving N GPU replicas
         self.handlers = {
             METHOD_PREFIX_P + "Predict": self.predict,
             METHOD_PREFIX_P + "Classify": self.classify,
@@ -365,7 +366,12 @@ class ServingCore:
     def handle_reload_config(self, request: bytes) -> bytes:
         req = _parse(serving.ReloadConfigRequest, request)
         resp = serving.ReloadConfigResponse()
-        errs = self.manager.apply_config(req.config, wait=True)
+        if self.replicas is not None:
+            # validate here (fail fast, nothing published), then apply on every replica
+            self.manager.validate_config(req.config)
+            errs = self.replicas.reload(req.config)
+        else:
+            errs = self.manager.apply_config(req.config, wait=True)
         if errs:
             resp.status.error_code = errs[0].code
             resp.status.error_message = "; ".join(e.message for e in errs)

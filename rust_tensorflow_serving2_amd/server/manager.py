@@ -112,8 +112,9 @@ class ModelManager:
             e = self._models.get(name)
             return None if e is None or e.removed else e.config
 
-    def apply_config(self, server_config, wait: bool = True, timeout: float = 600.0) -> List[E.ServingError]:
-        """Make the running set match ``server_config`` (supersedes previous config)."""
+    @staticmethod
+    def validate_config(server_config) -> Dict[str, object]:
+        """Check a ModelServerConfig; returns {name: ModelConfig} (raises INVALID_ARGUMENT)."""
         kind = server_config.WhichOneof("config")
         if kind != "model_config_list":
             raise E.invalid("ModelServerConfig: only model_config_list is supported "
@@ -129,6 +130,11 @@ class ModelManager:
             if mc.model_platform and mc.model_platform not in ("tensorflow", "tf", "savedmodel"):
                 raise E.invalid(f"ModelConfig {mc.name}: unsupported model_platform {mc.model_platform!r}")
             new[mc.name] = mc
+        return new
+
+    def apply_config(self, server_config, wait: bool = True, timeout: float = 600.0) -> List[E.ServingError]:
+        """Make the running set match ``server_config`` (supersedes previous config)."""
+        new = self.validate_config(server_config)
         with self._lock:
             for name, entry in self._models.items():
                 if name not in new and not entry.removed:

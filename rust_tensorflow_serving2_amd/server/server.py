@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import logging
 import os
+import threading
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -25,7 +26,7 @@ log = logging.getLogger("tfserve.server")
 @dataclass
 class ServerOptions:
     port: int = 8500
-    rest_api_port: int = 0
+    rest_api_port: int = 0                         # 0 = off, -1 = ephemeral
     host: str = "0.0.0.0"
     model_name: str = ""
     model_base_path: str = ""
@@ -40,7 +41,10 @@ class ServerOptions:
     batch_timeout_us: int = 2000                   # native fast-path batch window
     servable: ServableOptions = field(default_factory=ServableOptions)
     monitoring: bool = True
-    weight_source: Optional[object] = None         # parallel.WeightSource for multi-rank loads
+    weight_source: Optional[object] = None         # parallel.weights.ReplicatedWeightSource (N replicas)
+    replicas: Optional[object] = None              # parallel.replicas.ReplicaControl (N replicas)
+    model_config_file: str = ""                    # text-format ModelServerConfig
+    model_config_file_poll_wait_seconds: float = 0.0
 
 
 class ModelServer:
@@ -59,7 +63,11 @@ class ModelServer:
         self.request_logs = RequestLoggerRegistry()
         self.manager = ModelManager(self._load, poll_wait_seconds=opts.file_system_poll_wait_seconds)
         self.core = ServingCore(self.manager, self.batcher, self.request_logs, self.metrics)
+        self.core.replicas = opts.replicas
         self.transports = []
+        self._cfg_thread = None
+        self._cfg_stop = threading.Event()
+        self._cfg_text = None
 
     def _load(self, name: str, version: int, path: str, cfg) -> Servable:
         so = self.opts.servable
@@ -75,10 +83,38 @@ class ModelServer:
             self.request_logs.configure(name, cfg.logging_config)
         return s
 
+    def _read_config_file(self):
+        from google.protobuf import text_format
+        with open(self.opts.model_config_file) as f:
+            text = f.read()
+        cfg = serving.ModelServerConfig()
+        try:
+            text_format.Parse(text, cfg)
+        except text_format.ParseError as e:
+            raise E.invalid(f"could not parse --model_config_file {self.opts.model_config_file}: {e}") from None
+        return text, cfg
+
+    def _poll_config_file(self):
+        """TF Serving's --model_config_file_poll_wait_seconds: re-apply the file when it changes."""
+        while not self._cfg_stop.wait(self.opts.model_config_file_poll_wait_seconds):
+            try:
+                text, cfg = self._read_config_file()
+            except (OSError, E.ServingError) as e:
+                log.error("model config file poll: %s", e)
+                continue
+            if text != self._cfg_text:
+                self._cfg_text = text
+                log.info("model config file changed; applying")
+                for err in self.manager.apply_config(cfg, wait=True):
+                    log.error("model load error: %s", err.message)
+
     def initial_config(self):
         o = self.opts
         if o.model_config is not None:
             return o.model_config
+        if o.model_config_file:
+            self._cfg_text, cfg = self._read_config_file()
+            return cfg
         cfg = serving.ModelServerConfig()
         if o.model_base_path:
             mc = cfg.model_config_list.config.add()
@@ -94,6 +130,11 @@ class ModelServer:
             for e in errs:
                 log.error("model load error: %s", e.message)
         self.manager.start_polling()
+        if self.opts.replicas is not None:
+            self.opts.replicas.attach(self.manager)
+        if self.opts.model_config_file and self.opts.model_config_file_poll_wait_seconds > 0:
+            self._cfg_thread = threading.Thread(target=self._poll_config_file, name="tfs-cfgfile", daemon=True)
+            self._cfg_thread.start()
         if self.opts.transport == "native":
             from .native_transport import NativeTransport
             t = NativeTransport(self.core, self.opts.port, self.opts.host, batcher=self.batcher,
@@ -105,13 +146,19 @@ class ModelServer:
         self.port = t.port
         if self.opts.rest_api_port:
             from .rest import RestTransport
-            r = RestTransport(self.core, self.opts.rest_api_port, self.opts.host, self.metrics)
+            # 0 = disabled (TF Serving convention); -1 = any free port (tests)
+            r = RestTransport(self.core, max(0, self.opts.rest_api_port), self.opts.host, self.metrics)
             self.transports.append(r.start())
             self.rest_port = r.port
         log.info("serving on port %d", self.port)
         return self
 
     def stop(self):
+        self._cfg_stop.set()
+        if self.opts.replicas is not None:
+            self.opts.replicas.close()
+        if self.opts.weight_source is not None and hasattr(self.opts.weight_source, "close"):
+            self.opts.weight_source.close()
         for t in self.transports:
             t.stop()
         self.transports.clear()

@@ -1,0 +1,116 @@
+"""Data-parallel replicas on CPU (gloo, world_size 2): leader-ordered weight
+broadcast (parallel/weights.py), config replication (parallel/replicas.py) and
+the multi-replica server binary sharing one port via SO_REUSEPORT."""
+import asyncio
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _weights_worker(rank, world, port, model_dir, out_q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from rust_tensorflow_serving2_amd.parallel.weights import LoadError, ReplicatedWeightSource
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    store = dist.distributed_c10d._get_default_store()
+    ws = ReplicatedWeightSource(store, device=torch.device("cpu"), load_timeout=60)
+    res = {}
+    if rank == 0:
+        time.sleep(0.5)                         # followers ask first: they must wait for the leader
+    b = ws.load("m", 1, os.path.join(model_dir, "1"))
+    res["keys"] = sorted(b.bundle.keys())
+    res["sum"] = float(sum(np.asarray(b.bundle[k], np.float64).sum() for k in res["keys"]))
+    res["sigs"] = sorted(b.signatures)
+    try:
+        ws.load("m", 2, os.path.join(model_dir, "does_not_exist"))
+        res["err"] = None
+    except LoadError as e:
+        res["err"] = str(e)
+    ws.close()
+    dist.barrier()
+    dist.destroy_process_group()
+    out_q.put((rank, res))
+
+
+def test_replicated_weight_source_gloo(tiny_resnet_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_weights_worker, args=(r, 2, port, tiny_resnet_path, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0]["keys"] == out[1]["keys"] and len(out[0]["keys"]) > 10
+    assert out[0]["sum"] == pytest.approx(out[1]["sum"])
+    assert out[0]["sigs"] == out[1]["sigs"]
+    assert out[0]["err"] and out[1]["err"] and out[0]["err"] == out[1]["err"]
+
+
+async def _predict(port, model, x):
+    from rust_tensorflow_serving2_amd.client import TensorflowServing
+    c = await TensorflowServing.new().hostname("127.0.0.1").port(port).build()
+    return await c.predict_tensors(model, {"x": x})
+
+
+def test_cli_two_replicas_shared_port_and_reload(hpt_path, tmp_path):
+    """`--num_gpus 2` on CPU: two replica processes on one port; a reload sent to
+    whichever replica owns the connection is applied on both."""
+    from rust_tensorflow_serving2_amd.client import TensorflowServing
+    from rust_tensorflow_serving2_amd.schema import serving
+    port = _free_port()
+    logf = str(tmp_path / "replicas.log")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("WORLD_SIZE", None)
+    proc = subprocess.Popen([sys.executable, "-m", "rust_tensorflow_serving2_amd.server", f"--port={port}",
+                             "--model_name=a", f"--model_base_path={hpt_path}", "--num_gpus=2", "--device=cpu",
+                             "--host=127.0.0.1", "--file_system_poll_wait_seconds=0", "--log_level=WARNING"],
+                            env=env, stdout=open(logf, "w"), stderr=subprocess.STDOUT, text=True,
+                            start_new_session=True)
+    try:
+        deadline = time.time() + 180
+        while time.time() < deadline and proc.poll() is None:
+            if open(logf).read().count("ready:") >= 2:
+                break
+            time.sleep(0.2)
+        assert open(logf).read().count("ready:") == 2, open(logf).read()[-3000:]
+        x = np.array([[2.0]], np.float32)
+        for _ in range(8):          # fresh connections spread over both replicas
+            assert asyncio.run(_predict(port, "a", x))["y"].reshape(-1).tolist() == [3.0]
+
+        async def reload():
+            c = await TensorflowServing.new().hostname("127.0.0.1").port(port).build()
+            cfg = serving.ModelConfig(name="b", base_path=hpt_path, model_platform="tensorflow")
+            return await c.reload([cfg])
+        resp = asyncio.run(reload())
+        assert resp.status.error_code == 0, resp.status.error_message
+        for _ in range(16):         # both replicas now serve "b" and no longer "a"
+            assert asyncio.run(_predict(port, "b", x))["y"].reshape(-1).tolist() == [3.0]
+        from rust_tensorflow_serving2_amd.client import TFServingError
+        with pytest.raises(TFServingError):
+            asyncio.run(_predict(port, "a", x))
+    finally:
+        os.killpg(proc.pid, 15)
+        try:
+            proc.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, 9)
+            proc.wait()
