@@ -59,7 +59,26 @@ def parse():
                     help="resnet50 = headline config; bert-base = BASELINE config 3 (seq 128); "
                          "tiny = same 224x224x3 payload, negligible compute (transport ceiling probe)")
     ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--cpu-report", action="store_true",
+                    help="add per-thread-group CPU seconds of the timed window (from /proc) to the JSON")
     return ap.parse_args()
+
+
+def thread_cpu() -> dict:
+    """{thread name: cpu seconds} of this process (utime+stime from /proc)."""
+    tick = os.sysconf("SC_CLK_TCK")
+    out = {}
+    base = f"/proc/{os.getpid()}/task"
+    for tid in os.listdir(base):
+        try:
+            with open(f"{base}/{tid}/comm") as f:
+                name = f.read().strip()
+            with open(f"{base}/{tid}/stat") as f:
+                fields = f.read().rsplit(")", 1)[1].split()
+            out[name] = out.get(name, 0.0) + (int(fields[11]) + int(fields[12])) / tick
+        except (FileNotFoundError, ProcessLookupError, IndexError):
+            continue
+    return out
 
 
 def main():
@@ -150,12 +169,24 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    cpu0 = thread_cpu() if args.cpu_report else None
+    ru0 = os.times()
     t0 = time.perf_counter()
     r = drive(args.steps * per_step)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    cpu_report = None
+    if cpu0 is not None:
+        cpu1 = thread_cpu()
+        groups = {}
+        for k, v in cpu1.items():
+            g = k.rstrip("0123456789")
+            groups[g] = groups.get(g, 0.0) + v - cpu0.get(k, 0.0)
+        cpu_report = {k: round(v / elapsed, 2) for k, v in sorted(groups.items(), key=lambda x: -x[1]) if v > 0.01}
+        ru1 = os.times()
+        cpu_report["process_total"] = round((ru1.user + ru1.system - ru0.user - ru0.system) / elapsed, 2)
     lat = np.asarray(r["latency_us"], dtype=np.float64)
     mine = torch.tensor([elapsed, float(r["ok"]), float(r["errors"]), np.percentile(lat, 50) if lat.size else 0,
                          np.percentile(lat, 99) if lat.size else 0], dtype=torch.float64, device=device)
@@ -193,6 +224,7 @@ def main():
             "p99_latency_ms": round(float(allv[:, 4].max()) / 1e3, 3),
             "errors": int(allv[:, 2].sum()),
             "load_s": round(t_load, 2),
+            "cpu_cores_by_thread": cpu_report,
             "fast_path_share": round(stats.get("fast_path", 0) / max(1, stats.get("requests", 1)), 3) if stats else None,
         }
         print(json.dumps(out), flush=True)

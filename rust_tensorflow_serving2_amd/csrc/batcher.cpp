@@ -45,10 +45,10 @@ int Endpoint::open_slot_locked(int n) {
   return -1;
 }
 
-int Endpoint::offer(std::unique_ptr<Call>& call, const PredictRequestView& req) {
+int Endpoint::offer(std::unique_ptr<Call>& call, PredictRequestView& req) {
   if (req.inputs.size() != inputs.size()) return 1;
   // match aliases (inputs sorted by alias on registration)
-  std::vector<const TensorView*> tv(inputs.size(), nullptr);
+  std::vector<TensorView*> tv(inputs.size(), nullptr);
   for (auto& kv : req.inputs) {
     bool found = false;
     for (size_t i = 0; i < inputs.size(); ++i) {
@@ -86,20 +86,41 @@ int Endpoint::offer(std::unique_ptr<Call>& call, const PredictRequestView& req) 
     outs.push_back(found);
   }
 
-  // the Call is heap-allocated and its body is never modified again, so this
-  // pointer stays valid after the unique_ptr moves into the slot
-  const uint8_t* body = reinterpret_cast<const uint8_t*>(call->body.data());
+  // the Call is heap-allocated and its body is never modified again, so these
+  // pointers stay valid after the unique_ptr moves into a slot or the queue
+  const uint8_t* body = call->data();
+  std::vector<const uint8_t*> src(inputs.size());
+  std::vector<std::string> owned;
+  owned.reserve(inputs.size());   // no reallocation: src may point into (SSO) strings
+  for (size_t i = 0; i < inputs.size(); ++i) {
+    TensorView& t = *tv[i];
+    if (t.storage == Storage::kView) {
+      src[i] = body + t.offset;
+    } else {
+      owned.push_back(std::move(t.owned));
+      src[i] = reinterpret_cast<const uint8_t*>(owned.back().data());
+    }
+  }
   int slot = -1, r0 = 0;
   {
-    std::unique_lock<std::mutex> lk(mu_);
+    std::lock_guard<std::mutex> lk(mu_);
     if (closed_) return 1;
-    auto deadline = Clock::now() + std::chrono::milliseconds(max_wait_ms);
-    while ((slot = open_slot_locked(n)) < 0) {
-      if (cv_free_.wait_until(lk, deadline) == std::cv_status::timeout && (slot = open_slot_locked(n)) < 0) {
+    // FIFO: once anything is queued, later requests queue behind it
+    if (!queue_.empty() || (slot = open_slot_locked(n)) < 0) {
+      const size_t cap = max_queue_ ? max_queue_ : size_t(max_rows) * 64;
+      if (queue_.size() >= cap) {
         st_.rejected++;
         return 2;
       }
-      if (closed_) return 1;
+      Queued q;
+      q.call = std::move(call);
+      q.n = n;
+      q.outs = std::move(outs);
+      q.owned = std::move(owned);   // vector move steals the element buffer: src stays valid
+      q.src = std::move(src);
+      queue_.push_back(std::move(q));
+      st_.requests++;
+      return 0;
     }
     Slot& s = slots_[slot];
     r0 = s.reserved;
@@ -117,19 +138,50 @@ int Endpoint::offer(std::unique_ptr<Call>& call, const PredictRequestView& req) 
     }
   }
   // copy outside the lock: IO threads fill different rows of a slot in parallel
-  Slot& s = slots_[slot];
-  for (size_t i = 0; i < inputs.size(); ++i) {
-    const TensorView& t = *tv[i];
-    const uint8_t* src = t.storage == Storage::kView ? body + t.offset
-                                                     : reinterpret_cast<const uint8_t*>(t.owned.data());
-    std::memcpy(s.in_base[i] + size_t(r0) * inputs[i].row_bytes, src, t.nbytes);
-  }
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    s.copied += n;
-    if (s.copied == s.reserved) cv_ready_.notify_all();
-  }
+  copy_rows(slot, r0, n, src);
   return 0;
+}
+
+void Endpoint::copy_rows(int slot, int r0, int n, const std::vector<const uint8_t*>& src) {
+  Slot& s = slots_[slot];
+  for (size_t i = 0; i < inputs.size(); ++i)
+    std::memcpy(s.in_base[i] + size_t(r0) * inputs[i].row_bytes, src[i], size_t(n) * inputs[i].row_bytes);
+  std::lock_guard<std::mutex> g(mu_);
+  s.copied += n;
+  if (s.copied == s.reserved) cv_ready_.notify_all();
+}
+
+void Endpoint::drain_queue() {
+  struct Job {
+    int slot, r0, n;
+    std::vector<const uint8_t*> src;
+    std::vector<std::string> owned;
+  };
+  std::vector<Job> jobs;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    while (!queue_.empty() && !closed_) {
+      Queued& q = queue_.front();
+      const int slot = open_slot_locked(q.n);
+      if (slot < 0) break;
+      Slot& s = slots_[slot];
+      Job j{slot, s.reserved, q.n, std::move(q.src), std::move(q.owned)};
+      s.reserved += q.n;
+      Pending p;
+      p.row0 = j.r0;
+      p.n = q.n;
+      p.outs = std::move(q.outs);
+      p.call = std::move(q.call);
+      s.reqs.push_back(std::move(p));
+      if (s.reserved == max_rows) {
+        s.state = kReady;
+        open_ = -1;
+      }
+      queue_.pop_front();
+      jobs.push_back(std::move(j));
+    }
+  }
+  for (auto& j : jobs) copy_rows(j.slot, j.r0, j.n, j.src);
 }
 
 int Endpoint::acquire(int slot, int timeout_ms) {
@@ -188,28 +240,40 @@ void Endpoint::complete(int slot, Server& srv) {
     std::string body = encode_predict_response(&spec, outs, false);
     srv.respond(*p.call, 0, std::string(), std::move(body));
   }
-  std::lock_guard<std::mutex> g(mu_);
-  s.reqs.clear();
-  s.reserved = s.copied = 0;
-  s.state = kFree;
-  cv_free_.notify_all();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    s.reqs.clear();
+    s.reserved = s.copied = 0;
+    s.state = kFree;
+    cv_free_.notify_all();
+  }
+  drain_queue();
 }
 
 void Endpoint::fail(int slot, Server& srv, int code, const std::string& msg) {
   Slot& s = slots_[slot];
   for (auto& p : s.reqs) srv.respond(*p.call, code, msg, std::string());
-  std::lock_guard<std::mutex> g(mu_);
-  s.reqs.clear();
-  s.reserved = s.copied = 0;
-  s.state = kFree;
-  cv_free_.notify_all();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    s.reqs.clear();
+    s.reserved = s.copied = 0;
+    s.state = kFree;
+    cv_free_.notify_all();
+  }
+  drain_queue();
 }
 
-void Endpoint::close() {
-  std::lock_guard<std::mutex> g(mu_);
-  closed_ = true;
-  cv_ready_.notify_all();
-  cv_free_.notify_all();
+void Endpoint::close(Server* srv) {
+  std::deque<Queued> left;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    closed_ = true;
+    left.swap(queue_);
+    cv_ready_.notify_all();
+    cv_free_.notify_all();
+  }
+  if (srv)
+    for (auto& q : left) srv->respond(*q.call, 14 /*UNAVAILABLE*/, "Servable is being unloaded", std::string());
 }
 
 EndpointStats Endpoint::stats() {
@@ -231,7 +295,7 @@ bool FastPath::try_dispatch(std::unique_ptr<Call>& call) {
   if (call->method != kPredictPath) return false;
   PredictRequestView req;
   try {
-    parse_predict_request(reinterpret_cast<const uint8_t*>(call->body.data()), call->body.size(), req);
+    parse_predict_request(call->data(), call->size(), req);
   } catch (const std::exception&) {
     return false;   // python path reports the precise error
   }
@@ -281,7 +345,7 @@ void FastPath::remove_endpoint(int id) {
       eps_.erase(it);
     }
   }
-  if (ep) ep->close();
+  if (ep) ep->close(srv_);
 }
 
 void FastPath::set_route(const std::string& model, const std::string& signature, int64_t version, int ep_id) {

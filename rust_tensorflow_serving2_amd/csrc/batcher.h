@@ -14,6 +14,7 @@
 // unknown aliases, ...) falls through to the Python core, which produces the
 // exact TF-Serving error or result.
 #pragma once
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -40,6 +41,17 @@ struct Pending {
   std::vector<int> outs;   // output indices to encode (empty = all)
 };
 
+// A validated request waiting for a batch slot (every slot busy on the GPU).
+// IO threads never block: they park the request here and move on; the lane
+// worker that frees a slot moves queued requests into it.
+struct Queued {
+  std::unique_ptr<Call> call;
+  int n = 0;
+  std::vector<int> outs;
+  std::vector<const uint8_t*> src;     // per input: row data (views into call->body or `owned`)
+  std::vector<std::string> owned;      // kOwned tensors (non-packed encodings)
+};
+
 enum SlotState : int { kFree = 0, kOpen = 1, kReady = 2, kRunning = 3 };
 
 struct Slot {
@@ -61,13 +73,15 @@ class Endpoint {
   Endpoint(int id, std::string model, int64_t version, std::string signature, std::vector<TensorSpecC> inputs,
            std::vector<TensorSpecC> outputs, int max_rows, int64_t timeout_us, int max_wait_ms);
   void set_slot_buffers(int slot, std::vector<uint8_t*> in_base, std::vector<const uint8_t*> out_base);
-  // IO thread.  Returns 0 if accepted, 1 if not applicable (slow path), 2 if rejected (queue full).
-  int offer(std::unique_ptr<Call>& call, const PredictRequestView& req);
+  // IO thread, never blocks.  Returns 0 if accepted (batched or queued), 1 if
+  // not applicable (slow path), 2 if rejected (queue full).
+  int offer(std::unique_ptr<Call>& call, PredictRequestView& req);
   // GPU worker side.
   int acquire(int slot, int timeout_ms);
   void complete(int slot, Server& srv);
   void fail(int slot, Server& srv, int code, const std::string& msg);
-  void close();
+  // Responds UNAVAILABLE to requests still queued when `srv` is given.
+  void close(Server* srv = nullptr);
 
   const int id;
   const std::string model;
@@ -81,7 +95,17 @@ class Endpoint {
 
  private:
   int open_slot_locked(int n);
+  // Move queued requests into open slots; copies run outside the lock.
+  void drain_queue();
+  struct CopyJob {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t bytes;
+  };
+  void copy_rows(int slot, int r0, int n, const std::vector<const uint8_t*>& src);
   std::mutex mu_;
+  std::deque<Queued> queue_;
+  size_t max_queue_ = 0;
   std::condition_variable cv_ready_, cv_free_;
   std::vector<Slot> slots_;
   int open_ = -1;

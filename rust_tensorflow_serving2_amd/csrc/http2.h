@@ -32,7 +32,12 @@ struct Call {
   int io_index = 0;
   int32_t stream_id = 0;
   std::string method;      // ":path", e.g. /tensorflow.serving.PredictionService/Predict
-  std::string body;        // protobuf message (gRPC 5-byte prefix stripped)
+  // gRPC message as received: the 5-byte length prefix is kept (skipped via
+  // `off`) so the 602 KB request buffer moves into the Call without a copy
+  std::string body;
+  size_t off = 0;
+  const uint8_t* data() const { return reinterpret_cast<const uint8_t*>(body.data()) + off; }
+  size_t size() const { return body.size() - off; }
   Clock::time_point arrival;
   int64_t timeout_us = 0;  // grpc-timeout, 0 = none
 };

@@ -1,4 +1,5 @@
 // gRPC/HTTP2 server: epoll IO threads + libnghttp2 sessions (see http2.h).
+#include <pthread.h>
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -146,6 +147,7 @@ class IoThread {
     nghttp2_session_callbacks_set_on_frame_recv_callback(cbs_, &IoThread::on_frame_recv);
     nghttp2_session_callbacks_set_on_data_chunk_recv_callback(cbs_, &IoThread::on_data_chunk);
     nghttp2_session_callbacks_set_on_stream_close_callback(cbs_, &IoThread::on_stream_close);
+    nghttp2_session_callbacks_set_data_source_read_length_callback(cbs_, &IoThread::read_length);
   }
 
   ~IoThread() {
@@ -162,7 +164,10 @@ class IoThread {
 
   void start() {
     running_ = true;
-    th_ = std::thread([this] { loop(); });
+    th_ = std::thread([this] {
+      pthread_setname_np(pthread_self(), "tfs-h2io");
+      loop();
+    });
   }
 
   void stop() {
@@ -208,6 +213,13 @@ class IoThread {
       st->bad_content_type = v.rfind("application/grpc", 0) != 0;
     }
     return 0;
+  }
+
+  // large responses go out in frames as big as the peer allows (not 16 KB)
+  static ssize_t read_length(nghttp2_session*, uint8_t, int32_t, int32_t session_window, int32_t stream_window,
+                             uint32_t max_frame, void*) {
+    int64_t n = std::min<int64_t>(std::min<int64_t>(session_window, stream_window), max_frame);
+    return ssize_t(std::max<int64_t>(n, 1));
   }
 
   static int on_data_chunk(nghttp2_session* s, uint8_t, int32_t sid, const uint8_t* data, size_t len, void* ud) {
@@ -287,12 +299,13 @@ class IoThread {
     call->io_index = index_;
     call->stream_id = st->id;
     call->method = st->path;
-    call->body.assign(st->body, 5, std::string::npos);
+    call->body = std::move(st->body);   // no copy: the prefix is skipped via `off`
+    call->off = 5;
     std::string().swap(st->body);
     call->arrival = Clock::now();
     call->timeout_us = st->timeout_us;
     srv_->stats.requests++;
-    srv_->stats.bytes_in += call->body.size();
+    srv_->stats.bytes_in += call->size();
     srv_->dispatch(std::move(call));
   }
 

@@ -2,6 +2,7 @@
 //   wire codec (PredictRequest/PredictResponse), crc32c, LevelDB tables
 //   (TensorBundle index), mmap'd bundle shards, the HTTP/2 gRPC front end
 //   and the dynamic batcher (see server.cpp / batcher.cpp).
+#include <pthread.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -156,6 +157,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("encode_predict_request", &encode_request, py::arg("spec"), py::arg("inputs"),
         py::arg("output_filter") = py::list(), py::arg("use_tensor_content") = false);
 
+  m.def("set_thread_name", [](const std::string& name) {
+    // OS-level thread name (<= 15 chars), visible in /proc/<pid>/task/*/comm
+    pthread_setname_np(pthread_self(), name.substr(0, 15).c_str());
+  });
   m.def("crc32c", [](const py::buffer& b, uint32_t init) {
     ConstBuf cb = get_buf(b);
     py::gil_scoped_release nogil;

@@ -60,6 +60,13 @@ typedef int (*nghttp2_on_frame_recv_callback)(nghttp2_session*, const nghttp2_fr
 typedef int (*nghttp2_on_data_chunk_recv_callback)(nghttp2_session*, uint8_t flags, int32_t stream_id,
                                                    const uint8_t* data, size_t len, void*);
 typedef int (*nghttp2_on_stream_close_callback)(nghttp2_session*, int32_t stream_id, uint32_t error_code, void*);
+typedef ssize_t (*nghttp2_send_callback)(nghttp2_session*, const uint8_t* data, size_t length, int flags, void*);
+typedef int (*nghttp2_send_data_callback)(nghttp2_session*, nghttp2_frame* frame, const uint8_t* framehd,
+                                          size_t length, nghttp2_data_source* source, void*);
+typedef ssize_t (*nghttp2_data_source_read_length_callback)(nghttp2_session*, uint8_t frame_type, int32_t stream_id,
+                                                            int32_t session_remote_window_size,
+                                                            int32_t stream_remote_window_size,
+                                                            uint32_t remote_max_frame_size, void*);
 
 int nghttp2_session_callbacks_new(nghttp2_session_callbacks** callbacks_ptr);
 void nghttp2_session_callbacks_del(nghttp2_session_callbacks* callbacks);
@@ -69,12 +76,17 @@ void nghttp2_session_callbacks_set_on_frame_recv_callback(nghttp2_session_callba
 void nghttp2_session_callbacks_set_on_data_chunk_recv_callback(nghttp2_session_callbacks*,
                                                                nghttp2_on_data_chunk_recv_callback);
 void nghttp2_session_callbacks_set_on_stream_close_callback(nghttp2_session_callbacks*, nghttp2_on_stream_close_callback);
+void nghttp2_session_callbacks_set_send_callback(nghttp2_session_callbacks*, nghttp2_send_callback);
+void nghttp2_session_callbacks_set_send_data_callback(nghttp2_session_callbacks*, nghttp2_send_data_callback);
+void nghttp2_session_callbacks_set_data_source_read_length_callback(nghttp2_session_callbacks*,
+                                                                    nghttp2_data_source_read_length_callback);
 
 int nghttp2_session_server_new(nghttp2_session** session_ptr, const nghttp2_session_callbacks* callbacks, void* user_data);
 int nghttp2_session_client_new(nghttp2_session** session_ptr, const nghttp2_session_callbacks* callbacks, void* user_data);
 void nghttp2_session_del(nghttp2_session* session);
 ssize_t nghttp2_session_mem_recv(nghttp2_session* session, const uint8_t* in, size_t inlen);
 ssize_t nghttp2_session_mem_send(nghttp2_session* session, const uint8_t** data_ptr);
+int nghttp2_session_send(nghttp2_session* session);
 int nghttp2_session_want_read(nghttp2_session* session);
 int nghttp2_session_want_write(nghttp2_session* session);
 int nghttp2_session_set_local_window_size(nghttp2_session* session, uint8_t flags, int32_t stream_id,
@@ -106,8 +118,9 @@ enum : int32_t {
   NGHTTP2_SETTINGS_MAX_CONCURRENT_STREAMS = 3, NGHTTP2_SETTINGS_INITIAL_WINDOW_SIZE = 4,
   NGHTTP2_SETTINGS_MAX_FRAME_SIZE = 5, NGHTTP2_SETTINGS_MAX_HEADER_LIST_SIZE = 6,
 };
-enum : uint32_t { NGHTTP2_DATA_FLAG_EOF = 0x01, NGHTTP2_DATA_FLAG_NO_END_STREAM = 0x02 };
+enum : uint32_t { NGHTTP2_DATA_FLAG_EOF = 0x01, NGHTTP2_DATA_FLAG_NO_END_STREAM = 0x02,
+                  NGHTTP2_DATA_FLAG_NO_COPY = 0x04 };
 enum : uint8_t { NGHTTP2_NV_FLAG_NONE = 0, NGHTTP2_NV_FLAG_NO_COPY_NAME = 0x02, NGHTTP2_NV_FLAG_NO_COPY_VALUE = 0x04 };
-enum : int { NGHTTP2_ERR_DEFERRED = -508, NGHTTP2_ERR_CALLBACK_FAILURE = -902,
+enum : int { NGHTTP2_ERR_WOULDBLOCK = -504, NGHTTP2_ERR_DEFERRED = -508, NGHTTP2_ERR_CALLBACK_FAILURE = -902,
              NGHTTP2_ERR_TEMPORAL_CALLBACK_FAILURE = -521 };
 enum : uint32_t { NGHTTP2_NO_ERROR = 0, NGHTTP2_INTERNAL_ERROR = 2, NGHTTP2_CANCEL = 8 };

@@ -46,7 +46,9 @@ std::vector<TensorSpecC> specs_from(const py::list& l) {
 void register_server(py::module_& m) {
   py::class_<PyCall>(m, "Call")
       .def_property_readonly("method", [](const PyCall& c) { return c.call->method; })
-      .def_property_readonly("body", [](const PyCall& c) { return py::bytes(c.call->body); })
+      .def_property_readonly("body", [](const PyCall& c) {
+        return py::bytes(reinterpret_cast<const char*>(c.call->data()), c.call->size());
+      })
       .def_property_readonly("timeout_us", [](const PyCall& c) { return c.call->timeout_us; });
 
   py::class_<PyServer>(m, "Http2Server")

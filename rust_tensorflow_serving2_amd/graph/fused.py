@@ -181,7 +181,9 @@ class FusedConv:
         out = torch.empty((n, ho, wo, self.cout), device=x.device, dtype=BF16)
         key = ("conv", tuple(x.shape), x.dtype, self.cout, self.kh, self.kw, self.sh, res is not None)
         K = self.kh * 32 if self.c4 else self.kh * self.kw * self.cin
-        cfg, splits = tuned_config(key, M, self.cout, lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s), K)
+        dma = not self.c4 and self.cin % 8 == 0      # bf16 dense/im2col operands -> DMA-ring configs apply
+        cfg, splits = tuned_config(key, M, self.cout, lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s), K,
+                                   dma)
         return [H.conv2d(*args, cfg=cfg, out=out, splits=splits)]
 
 

@@ -31,13 +31,20 @@ constexpr int BK = 64;
 constexpr int kThreads = 256;
 constexpr int kGroupM = 8;
 
-template <int BM, int BN, int AMODE>
+template <int BM, int BN, int AMODE, int NSTAGE>
 struct IGemm {
   static constexpr int WM = BM / 2, WN = BN / 2;
   static constexpr int TM = WM / 16, TN = WN / 16;
   static constexpr int A_CHUNKS = BM * BK / 8 / kThreads;
   static constexpr int B_CHUNKS = BN * BK / 8 / kThreads;
-  static constexpr int LDS_MAIN = 2 * (BM + BN) * BK * 2;
+  // direct-to-LDS operand modes run a STAGES-deep DMA ring (S-1 k-tiles in
+  // flight while one is consumed): per k-tile a 64x64 tile does only ~128
+  // MFMA cycles per SIMD, far below one memory round trip, so two buffers
+  // leave the loop latency-bound.  Register-staged modes keep 2 buffers.
+  static constexpr bool GL = (AMODE == kADense || AMODE == kAIm2col);
+  static constexpr int STAGES = GL ? NSTAGE : 2;
+  static constexpr int PER_STAGE = A_CHUNKS + B_CHUNKS;   // DMA instructions per stage per wave
+  static constexpr int LDS_MAIN = STAGES * (BM + BN) * BK * 2;
   static constexpr int CS_LD = BN + 4;
   static constexpr int LDS_EPI = BM * CS_LD * 4;
   static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
@@ -45,12 +52,27 @@ struct IGemm {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
 
-template <int BM, int BN, int AMODE>
+// s_waitcnt vmcnt(N) only (expcnt/lgkmcnt left at their maxima; gfx9 encoding:
+// vmcnt[3:0] + vmcnt[5:4] at bits 15:14, expcnt 6:4, lgkmcnt 11:8).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// Workgroup barrier WITHOUT the vmcnt(0) drain that __syncthreads' fence
+// implies (that drain would empty the DMA ring every k-tile).  The "memory"
+// clobber keeps the compiler from moving LDS accesses across it; LDS reads
+// feeding MFMAs have already been waited on by then.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int BM, int BN, int AMODE, int NSTAGE>
 __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
-  using G = IGemm<BM, BN, AMODE>;
+  using G = IGemm<BM, BN, AMODE, NSTAGE>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int S = G::STAGES;
   uint16_t* As = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* Bs = As + 2 * BM * BK;
+  uint16_t* Bs = As + S * BM * BK;
 
   const int M = p.M, N = p.N, K = p.K;
   const int nbm = (M + BM - 1) / BM, nbn = (N + BN - 1) / BN;
@@ -72,7 +94,7 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   // DMAs 64 lanes x 16 B = 8 rows x 128 B into a lane-linear LDS image, so
   // lane l fills row (l>>3) at 16-B slot (l&7); the XOR swizzle is applied to
   // the *source* chunk instead (logical chunk = slot ^ (row & 7)).
-  constexpr bool GL = (AMODE == kADense || AMODE == kAIm2col);
+  constexpr bool GL = G::GL;
   const int gl_chunk = (lane & 7) ^ ((lane >> 3) & 7);
 
   // ---- per-thread A row descriptors
@@ -207,8 +229,8 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
       const_cast<uint16_t*>(p.b), 0, int(p.b_bytes), 0x00020000);
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-  auto gstage = [&](int buf, int kt) {
-    const int kc = kt * BK + gl_chunk * 8;
+  auto gstage = [&](int buf, int kt, bool live) {
+    const int kc = live ? kt * BK + gl_chunk * 8 : K + p.ldb;   // !live: every offset out of range
     uint16_t* as = As + buf * BM * BK;
     uint16_t* bs = Bs + buf * BN * BK;
     if (AMODE == kADense) {
@@ -265,26 +287,9 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   const int nk_all = (K + BK - 1) / BK;
   const int kt0 = p.splits > 1 ? blockIdx.y * p.kt_per_split : 0;
   const int nk = p.splits > 1 ? min(nk_all, kt0 + p.kt_per_split) - kt0 : nk_all;
-  if (GL) {
-    gstage(0, kt0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    gload(kt0);
-    sstore(0);
-  }
-  __syncthreads();
-
   const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (GL) {
-      // DMA of tile kt+1 into the other buffer runs under this tile's MFMAs
-      if (kt + 1 < nk) gstage(cur ^ 1, kt0 + kt + 1);
-    } else if (kt + 1 < nk) {
-      gload(kt0 + kt + 1);
-    }
-    const uint16_t* as = As + cur * BM * BK;
-    const uint16_t* bs = Bs + cur * BN * BK;
+
+  auto mfma_tile = [&](const uint16_t* as, const uint16_t* bs) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ch = kk * 4 + fq;
@@ -305,13 +310,36 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
         for (int j = 0; j < G::TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (GL) {
-      // retire this wave's DMA, then the barrier makes every wave's DMA visible
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (kt + 1 < nk) {
-      sstore(cur ^ 1);
+  };
+
+  if (GL) {
+    // prologue: S-1 k-tiles in flight
+#pragma unroll
+    for (int st = 0; st < S - 1; ++st) gstage(st, kt0 + st, st < nk);
+    for (int kt = 0; kt < nk; ++kt) {
+      // this wave's DMA of tile kt has landed once <= S-2 stages remain
+      // outstanding; the barrier publishes every wave's DMA and guarantees all
+      // waves are done reading tile kt-1, whose buffer the next DMA reuses
+      wait_vmcnt<(S - 2) * G::PER_STAGE>();
+      lds_barrier();
+      const int nxt = kt + S - 1;
+      gstage(nxt % S, kt0 + nxt, nxt < nk);
+      const int cur = kt % S;
+      mfma_tile(As + cur * BM * BK, Bs + cur * BN * BK);
     }
+    wait_vmcnt<0>();
     __syncthreads();
+  } else {
+    gload(kt0);
+    sstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) gload(kt0 + kt + 1);
+      mfma_tile(As + cur * BM * BK, Bs + cur * BN * BK);
+      if (kt + 1 < nk) sstore(cur ^ 1);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: stage fp32 tile in LDS, then coalesced 8-wide row chunks
@@ -409,20 +437,20 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   }
 }
 
-template <int BM, int BN, int AMODE>
+template <int BM, int BN, int AMODE, int NSTAGE>
 hipError_t launch_cfg(const IGemmArgs& a, hipStream_t s) {
-  using G = IGemm<BM, BN, AMODE>;
+  using G = IGemm<BM, BN, AMODE, NSTAGE>;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<BM, BN, AMODE>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<BM, BN, AMODE, NSTAGE>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int splits = a.splits > 1 ? a.splits : 1;
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE>), dim3(tiles, splits), dim3(kThreads), G::LDS, s, a);
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE, NSTAGE>), dim3(tiles, splits), dim3(kThreads), G::LDS, s, a);
   return hipGetLastError();
 }
 
@@ -457,21 +485,43 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(IGemmArgs p) {
   }
 }
 
+// Tile configs: (BM, BN, DMA ring depth).  Deeper rings hide more memory
+// latency per workgroup but cost LDS, i.e. resident workgroups per CU (160 KB
+// LDS): the tuner picks per layer (K=64 1x1 convs want occupancy, long-K
+// small-grid layers want depth).  Register-staged operand modes ignore the
+// depth (always 2).
+constexpr int kCfgBM[kNumIGemmConfigs] = {128, 128, 64, 64, 128, 64, 128, 64};
+constexpr int kCfgBN[kNumIGemmConfigs] = {128, 64, 128, 64, 128, 64, 64, 128};
+constexpr int kCfgST[kNumIGemmConfigs] = {2, 2, 2, 2, 3, 4, 3, 3};
+
 template <int AMODE>
 hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
+  constexpr bool GL = (AMODE == kADense || AMODE == kAIm2col);
+  if (!GL && cfg >= 4) cfg = (kCfgBM[cfg] == 128 ? (kCfgBN[cfg] == 128 ? 0 : 1) : (kCfgBN[cfg] == 128 ? 2 : 3));
   switch (cfg) {
-    case 0: return launch_cfg<128, 128, AMODE>(a, s);
-    case 1: return launch_cfg<128, 64, AMODE>(a, s);
-    case 2: return launch_cfg<64, 128, AMODE>(a, s);
-    case 3: return launch_cfg<64, 64, AMODE>(a, s);
-    default: return hipErrorInvalidValue;
+    case 0: return launch_cfg<128, 128, AMODE, 2>(a, s);
+    case 1: return launch_cfg<128, 64, AMODE, 2>(a, s);
+    case 2: return launch_cfg<64, 128, AMODE, 2>(a, s);
+    case 3: return launch_cfg<64, 64, AMODE, 2>(a, s);
+    default: break;
   }
+  if constexpr (GL) {
+    switch (cfg) {
+      case 4: return launch_cfg<128, 128, AMODE, 3>(a, s);
+      case 5: return launch_cfg<64, 64, AMODE, 4>(a, s);
+      case 6: return launch_cfg<128, 64, AMODE, 3>(a, s);
+      case 7: return launch_cfg<64, 128, AMODE, 3>(a, s);
+      default: break;
+    }
+  }
+  return hipErrorInvalidValue;
 }
 
 }  // namespace
 
-int igemm_config_bm(int cfg) { const int t[] = {128, 128, 64, 64}; return t[cfg]; }
-int igemm_config_bn(int cfg) { const int t[] = {128, 64, 128, 64}; return t[cfg]; }
+int igemm_config_bm(int cfg) { return kCfgBM[cfg]; }
+int igemm_config_bn(int cfg) { return kCfgBN[cfg]; }
+int igemm_config_stages(int cfg) { return kCfgST[cfg]; }
 
 hipError_t igemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) {
   switch (a_mode) {

@@ -49,10 +49,12 @@ hipError_t ingest_c4_launch(const float* x, uint16_t* y, int64_t pixels, int C, 
 // Sum split-K partial slabs and apply the epilogue (bias, residual, act, store).
 hipError_t splitk_reduce_launch(const IGemmArgs& args, hipStream_t stream);
 
-// Tile configs (BMxBN): 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64
-constexpr int kNumIGemmConfigs = 4;
+// Tile configs (BM x BN, DMA ring depth): 0..3 = 128x128, 128x64, 64x128,
+// 64x64 double-buffered; 4 = 128x128x3, 5 = 64x64x4, 6 = 128x64x3, 7 = 64x128x3
+constexpr int kNumIGemmConfigs = 8;
 int igemm_config_bm(int cfg);
 int igemm_config_bn(int cfg);
+int igemm_config_stages(int cfg);
 hipError_t igemm_launch(const IGemmArgs& args, int a_mode, int cfg, hipStream_t stream);
 
 // NHWC bf16 max-pool (TF SAME/VALID padding given explicitly).

@@ -59,6 +59,7 @@ class FastEndpoint:
             self.workers.append(th)
 
     def _work(self, lane_idx: int):
+        _C.set_thread_name(f"tfs-lane{lane_idx}")
         srv = self.t.srv
         while not self._stop.is_set():
             n = srv.acquire(self.id, lane_idx, 100)
@@ -103,6 +104,7 @@ class NativeTransport:
 
     # ------------------------------------------------------------ slow path
     def _serve(self):
+        _C.set_thread_name("tfs-py")
         srv, core = self.srv, self.core
         while not self._stop.is_set():
             call = srv.next_call(100)

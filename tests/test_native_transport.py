@@ -65,3 +65,14 @@ def test_native_loadgen(nserver):
     r = _C.run_loadgen("127.0.0.1", nserver.port, "/tensorflow.serving.PredictionService/Predict", [bad],
                        10, 4, 1, 1, 60.0)
     assert r["errors"] == 10 and "grpc-status 5" in r["first_error"]
+
+
+def test_native_loadgen_large_bodies(nserver):
+    """Multi-frame (zero-copy DATA) requests of different sizes on shared connections."""
+    bodies = [native.encode_predict_request(native.spec_tuple("hpt", None, None, ""),
+                                            {"x": np.full((n, 1), float(n), np.float32)})
+              for n in (50_000, 150_528, 7, 300_000)]
+    r = _C.run_loadgen("127.0.0.1", nserver.port, "/tensorflow.serving.PredictionService/Predict", bodies,
+                       64, 16, 3, 2, 120.0)
+    assert r["ok"] == 64 and r["errors"] == 0, r["first_error"]
+    assert r["bytes_sent"] >= 64 * min(len(b) for b in bodies)
