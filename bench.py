@@ -170,6 +170,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     cpu0 = thread_cpu() if args.cpu_report else None
+    io0 = server.transports[0].stats() if args.cpu_report and args.transport == "native" else None
     ru0 = os.times()
     t0 = time.perf_counter()
     r = drive(args.steps * per_step)
@@ -187,6 +188,12 @@ def main():
         cpu_report = {k: round(v / elapsed, 2) for k, v in sorted(groups.items(), key=lambda x: -x[1]) if v > 0.01}
         ru1 = os.times()
         cpu_report["process_total"] = round((ru1.user + ru1.system - ru0.user - ru0.system) / elapsed, 2)
+        cpu_report["loadgen_cores"] = round(r.get("cpu_s", 0.0) / elapsed, 2)
+        if io0 is not None:
+            io1 = server.transports[0].stats()
+            nreq = max(1, io1["requests"] - io0["requests"])
+            for k in ("io_s_recv", "io_s_h2", "io_s_dispatch", "io_s_send"):
+                cpu_report[k.replace("io_s_", "io_us_per_req_")] = round((io1[k] - io0[k]) / nreq * 1e6, 1)
     lat = np.asarray(r["latency_us"], dtype=np.float64)
     mine = torch.tensor([elapsed, float(r["ok"]), float(r["errors"]), np.percentile(lat, 50) if lat.size else 0,
                          np.percentile(lat, 99) if lat.size else 0], dtype=torch.float64, device=device)

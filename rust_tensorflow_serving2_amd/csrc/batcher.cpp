@@ -6,6 +6,8 @@
 namespace tfs {
 
 static const char* kPredictPath = "/tensorflow.serving.PredictionService/Predict";
+// how long a ready batch waits for a row whose payload is still arriving
+static constexpr std::chrono::milliseconds kStreamStall(200);
 
 Endpoint::Endpoint(int id_, std::string model_, int64_t version_, std::string signature_,
                    std::vector<TensorSpecC> inputs_, std::vector<TensorSpecC> outputs_, int max_rows_,
@@ -184,6 +186,81 @@ void Endpoint::drain_queue() {
   for (auto& j : jobs) copy_rows(j.slot, j.r0, j.n, j.src);
 }
 
+// ---------------------------------------------------------------- streaming rows
+void SlotStream::commit(std::unique_ptr<Call> call) { ep->commit_stream(*this, std::move(call)); }
+void SlotStream::abandon() { ep->abandon_stream(*this); }
+
+std::shared_ptr<StreamRes> Endpoint::reserve_stream(const std::shared_ptr<Endpoint>& self, const ProbeInfo& pi) {
+  // the same acceptance rules as offer(), on the header alone
+  if (inputs.size() != 1) return nullptr;
+  const TensorSpecC& in = inputs[0];
+  if (pi.alias != in.alias || pi.dtype != in.dtype || pi.shape.size() != in.row_shape.size() + 1) return nullptr;
+  for (size_t d = 0; d < in.row_shape.size(); ++d)
+    if (pi.shape[d + 1] != in.row_shape[d]) return nullptr;
+  const int64_t rows = pi.shape[0];
+  if (rows < 1 || rows > max_rows || pi.payload_len != size_t(rows) * in.row_bytes) return nullptr;
+  auto r = std::make_shared<SlotStream>();
+  std::lock_guard<std::mutex> lk(mu_);
+  if (closed_ || !queue_.empty()) return nullptr;   // keep FIFO order behind queued requests
+  const int n = int(rows);
+  const int slot = open_slot_locked(n);
+  if (slot < 0) return nullptr;
+  Slot& s = slots_[slot];
+  const int r0 = s.reserved;
+  s.reserved += n;
+  Pending p;
+  p.row0 = r0;
+  p.n = n;
+  p.sres = r;
+  s.reqs.push_back(std::move(p));
+  st_.requests++;
+  if (s.reserved == max_rows) {
+    s.state = kReady;
+    open_ = -1;
+  }
+  r->ep = self;
+  r->slot = slot;
+  r->idx = int(s.reqs.size()) - 1;
+  r->n = n;
+  r->dst = s.in_base[0] + size_t(r0) * in.row_bytes;
+  r->len = pi.payload_len;
+  return r;
+}
+
+void Endpoint::commit_stream(SlotStream& r, std::unique_ptr<Call> call) {
+  int expect = 0;
+  if (!r.state.compare_exchange_strong(expect, 1)) {
+    // the batcher gave the row up (payload stalled): the rows ran as padding
+    if (srv_) srv_->respond(*call, 14 /*UNAVAILABLE*/, "request payload arrived too slowly for its batch",
+                            std::string());
+    return;
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  Slot& s = slots_[r.slot];
+  s.reqs[r.idx].call = std::move(call);
+  s.copied += r.n;
+  if (s.copied == s.reserved) cv_ready_.notify_all();
+}
+
+void Endpoint::abandon_stream(SlotStream& r) {
+  int expect = 0;
+  if (!r.state.compare_exchange_strong(expect, 2)) return;
+  std::lock_guard<std::mutex> g(mu_);
+  Slot& s = slots_[r.slot];
+  s.copied += r.n;   // the row runs as padding; complete() skips it (no call)
+  if (s.copied == s.reserved) cv_ready_.notify_all();
+}
+
+void Endpoint::abandon_stalled_locked(Slot& s) {
+  for (auto& p : s.reqs) {
+    if (!p.sres) continue;
+    int expect = 0;
+    if (!p.sres->state.compare_exchange_strong(expect, 2)) continue;
+    s.copied += p.n;
+    while (p.sres->writers.load() != 0) {}   // an in-flight chunk copy finishes in microseconds
+  }
+}
+
 int Endpoint::acquire(int slot, int timeout_ms) {
   std::unique_lock<std::mutex> lk(mu_);
   if (slot < 0 || slot >= int(slots_.size())) return -1;
@@ -196,6 +273,17 @@ int Endpoint::acquire(int slot, int timeout_ms) {
       st_.batches++;
       st_.rows += s.reserved;
       return s.reserved;
+    }
+    if (s.state == kReady && s.reserved > 0) {
+      // rows still streaming in: give a stalled sender kStreamStall, then run without it
+      const auto stall = s.first + std::chrono::microseconds(timeout_us) + kStreamStall;
+      if (now >= stall) {
+        abandon_stalled_locked(s);
+        continue;
+      }
+      if (now >= deadline) return 0;
+      cv_ready_.wait_until(lk, std::min(stall, deadline));
+      continue;
     }
     if (s.state == kOpen && s.reserved > 0) {
       const auto due = s.first + std::chrono::microseconds(timeout_us);
@@ -223,6 +311,7 @@ void Endpoint::complete(int slot, Server& srv) {
   spec.signature_name = signature;
   std::vector<OutTensor> outs;
   for (auto& p : s.reqs) {
+    if (!p.call) continue;   // abandoned streaming row
     outs.clear();
     const size_t nout = p.outs.empty() ? outputs.size() : p.outs.size();
     for (size_t k = 0; k < nout; ++k) {
@@ -252,7 +341,8 @@ void Endpoint::complete(int slot, Server& srv) {
 
 void Endpoint::fail(int slot, Server& srv, int code, const std::string& msg) {
   Slot& s = slots_[slot];
-  for (auto& p : s.reqs) srv.respond(*p.call, code, msg, std::string());
+  for (auto& p : s.reqs)
+    if (p.call) srv.respond(*p.call, code, msg, std::string());
   {
     std::lock_guard<std::mutex> g(mu_);
     s.reqs.clear();
@@ -268,6 +358,7 @@ void Endpoint::close(Server* srv) {
   {
     std::lock_guard<std::mutex> g(mu_);
     closed_ = true;
+    for (auto& s : slots_) abandon_stalled_locked(s);
     left.swap(queue_);
     cv_ready_.notify_all();
     cv_free_.notify_all();
@@ -289,6 +380,21 @@ static std::string route_key(const std::string& m, const std::string& s, int64_t
   k.push_back('\0');
   k += v < 0 ? std::string("L") : std::to_string(v);
   return k;
+}
+
+std::shared_ptr<Endpoint> FastPath::route(const ModelSpecView& spec) {
+  if (spec.has_label) return nullptr;
+  const std::string sig = spec.signature_name.empty() ? "serving_default" : spec.signature_name;
+  std::shared_lock<std::shared_mutex> g(mu_);
+  auto it = routes_.find(route_key(spec.name, sig, spec.has_version ? spec.version : -1));
+  if (it == routes_.end()) return nullptr;
+  auto e = eps_.find(it->second);
+  return e == eps_.end() ? nullptr : e->second;
+}
+
+std::shared_ptr<StreamRes> FastPath::reserve_stream(const ProbeInfo& pi) {
+  auto ep = route(pi.spec);
+  return ep ? ep->reserve_stream(ep, pi) : nullptr;
 }
 
 bool FastPath::try_dispatch(std::unique_ptr<Call>& call) {
@@ -320,6 +426,7 @@ bool FastPath::try_dispatch(std::unique_ptr<Call>& call) {
 }
 
 int FastPath::add_endpoint(std::shared_ptr<Endpoint> ep) {
+  ep->set_server(srv_);
   std::unique_lock<std::shared_mutex> g(mu_);
   eps_[ep->id] = ep;
   return ep->id;

@@ -35,10 +35,22 @@ struct TensorSpecC {
   size_t row_bytes = 0;
 };
 
+class Endpoint;
+
+// A row reserved for a request whose payload is still streaming in (http2.h
+// StreamRes); committed by the IO thread when the message is complete.
+struct SlotStream final : StreamRes {
+  std::shared_ptr<Endpoint> ep;
+  int slot = -1, idx = -1, n = 0;
+  void commit(std::unique_ptr<Call> call) override;
+  void abandon() override;
+};
+
 struct Pending {
-  std::unique_ptr<Call> call;
+  std::unique_ptr<Call> call;   // null: abandoned streaming row (padding, no answer)
   int row0 = 0, n = 0;
   std::vector<int> outs;   // output indices to encode (empty = all)
+  std::shared_ptr<SlotStream> sres;
 };
 
 // A validated request waiting for a batch slot (every slot busy on the GPU).
@@ -76,6 +88,11 @@ class Endpoint {
   // IO thread, never blocks.  Returns 0 if accepted (batched or queued), 1 if
   // not applicable (slow path), 2 if rejected (queue full).
   int offer(std::unique_ptr<Call>& call, PredictRequestView& req);
+  // IO thread: reserve a row for a streaming request (nullptr = use the buffered path).
+  std::shared_ptr<StreamRes> reserve_stream(const std::shared_ptr<Endpoint>& self, const ProbeInfo& pi);
+  void commit_stream(SlotStream& r, std::unique_ptr<Call> call);
+  void abandon_stream(SlotStream& r);
+  void set_server(Server* srv) { srv_ = srv; }
   // GPU worker side.
   int acquire(int slot, int timeout_ms);
   void complete(int slot, Server& srv);
@@ -103,6 +120,9 @@ class Endpoint {
     size_t bytes;
   };
   void copy_rows(int slot, int r0, int n, const std::vector<const uint8_t*>& src);
+  // batcher-side abandonment of rows whose payload stalls (caller holds mu_)
+  void abandon_stalled_locked(Slot& s);
+  Server* srv_ = nullptr;
   std::mutex mu_;
   std::deque<Queued> queue_;
   size_t max_queue_ = 0;
@@ -118,6 +138,8 @@ class FastPath {
  public:
   explicit FastPath(Server* srv) : srv_(srv) {}
   bool try_dispatch(std::unique_ptr<Call>& call);
+  std::shared_ptr<Endpoint> route(const ModelSpecView& spec);
+  std::shared_ptr<StreamRes> reserve_stream(const ProbeInfo& pi);
   int add_endpoint(std::shared_ptr<Endpoint> ep);
   std::shared_ptr<Endpoint> endpoint(int id);
   void remove_endpoint(int id);

@@ -11,6 +11,7 @@
 // Responses from any thread are posted to the owning IO thread (eventfd).
 #pragma once
 #include <atomic>
+#include <cstring>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -21,6 +22,8 @@
 #include <thread>
 #include <unordered_map>
 #include <vector>
+
+#include "wire.h"
 
 namespace tfs {
 
@@ -48,9 +51,41 @@ class Server;
 // later through Server::respond).
 using FastDispatch = std::function<bool(std::unique_ptr<Call>&)>;
 
+// A batch-slot row reserved for a request that is still arriving: the IO
+// thread copies the tensor payload straight from its socket read buffer into
+// `dst` (pinned memory the GPU reads), so a 602 KB image is copied once in
+// user space instead of being assembled into a body first.
+struct StreamRes {
+  std::atomic<int> state{0};     // 0 streaming, 1 committed, 2 abandoned (by either side)
+  std::atomic<int> writers{0};   // IO thread inside write(); the batcher waits for 0 before reusing the row
+  uint8_t* dst = nullptr;
+  size_t len = 0, got = 0;
+  virtual ~StreamRes() = default;
+  // Every payload byte arrived and the message ended: hand over the call.
+  virtual void commit(std::unique_ptr<Call> call) = 0;
+  // The IO side gives up (stream reset, protocol error).
+  virtual void abandon() = 0;
+  // Copy the next chunk; false once the batcher has abandoned the row (too slow).
+  bool write(const uint8_t* p, size_t n) {
+    writers.fetch_add(1);
+    const bool live = state.load() == 0;
+    if (live) std::memcpy(dst + got, p, n);
+    writers.fetch_sub(1);
+    got += n;
+    return live;
+  }
+};
+
+// Reserve a row for a probed request header; nullptr = not streamable here.
+using StreamReserve = std::function<std::shared_ptr<StreamRes>(const ProbeInfo&)>;
+
 struct ServerStats {
   std::atomic<uint64_t> connections{0}, requests{0}, fast_path{0}, slow_path{0}, responses{0}, errors{0};
+  std::atomic<uint64_t> streamed{0};   // fast-path requests whose payload went socket -> slot directly
   std::atomic<uint64_t> bytes_in{0}, bytes_out{0};
+  // IO-thread time split (ns): recv() syscalls, nghttp2 frame processing incl.
+  // body assembly, fast-path dispatch (decode + batch-slot copy), send()
+  std::atomic<uint64_t> ns_recv{0}, ns_h2{0}, ns_dispatch{0}, ns_send{0};
 };
 
 class IoThread;
@@ -64,6 +99,8 @@ class Server {
   int port() const { return port_; }
 
   void set_fast_dispatch(FastDispatch fn) { fast_ = std::move(fn); }
+  void set_stream_reserve(StreamReserve fn) { reserve_ = std::move(fn); }
+  const StreamReserve& stream_reserve() const { return reserve_; }
   // Answer a call (thread-safe).  status = grpc code; body ignored unless OK.
   void respond(uint64_t conn_id, int io_index, int32_t stream_id, int status, std::string message,
                std::string body);
@@ -85,6 +122,7 @@ class Server {
   size_t max_message_;
   std::vector<std::unique_ptr<IoThread>> io_;
   FastDispatch fast_;
+  StreamReserve reserve_;
   std::mutex qmu_;
   std::condition_variable qcv_;
   std::deque<std::unique_ptr<Call>> queue_;
@@ -98,6 +136,7 @@ struct LoadGenResult {
   std::vector<double> latency_us;   // per successful request
   std::string first_error;
   uint64_t bytes_sent = 0, bytes_recv = 0;
+  double cpu_s = 0;                 // CPU time of the client threads
 };
 
 // Drive `total` unary calls of `method` against host:port with `concurrency`

@@ -6,6 +6,7 @@
 // `concurrency` unary calls in flight; per-call latency is recorded from
 // submit to end-of-stream (trailers) on the client clock.
 #include <pthread.h>
+#include <time.h>
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -384,6 +385,9 @@ LoadGenResult run_loadgen(const std::string& host, int port, const std::string& 
     ts.emplace_back([&, t, nconn] {
       pthread_setname_np(pthread_self(), "tfs-loadgen");
       client_thread(&sh, host, port, nconn, per_conn, &parts[t]);
+      timespec ts{};
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+      parts[t].cpu_s = double(ts.tv_sec) + 1e-9 * double(ts.tv_nsec);
     });
   }
   for (auto& t : ts) t.join();
@@ -394,6 +398,7 @@ LoadGenResult run_loadgen(const std::string& host, int port, const std::string& 
     res.errors += p.errors;
     res.bytes_sent += p.bytes_sent;
     res.bytes_recv += p.bytes_recv;
+    res.cpu_s += p.cpu_s;
     res.latency_us.insert(res.latency_us.end(), p.latency_us.begin(), p.latency_us.end());
     if (res.first_error.empty()) res.first_error = p.first_error;
   }

@@ -68,16 +68,29 @@ int64_t parse_grpc_timeout(const std::string& v) {
   }
 }
 
+enum StreamMode : int { kProbeMode = 0, kBufferMode = 1, kStreamMode = 2 };
+constexpr size_t kProbeMax = 4096;          // header bytes inspected before giving up on streaming
+constexpr size_t kStreamMin = 64 << 10;     // payloads smaller than this are simply buffered
+static const char* const kPredictMethod = "/tensorflow.serving.PredictionService/Predict";
+
 struct Stream {
   int32_t id = 0;
   std::string path;
-  std::string body;          // raw DATA (with gRPC prefix)
+  std::string body;          // raw DATA (with gRPC prefix); in stream mode only the header
   int64_t timeout_us = 0;
   bool bad_content_type = false;
+  // streaming decode (Predict payload copied straight into a batch slot)
+  int mode = kProbeMode;
+  std::shared_ptr<StreamRes> sres;
+  bool committed = false;
+  bool overflow = false;     // bytes beyond the gRPC message
   // response
   std::string resp;          // gRPC-framed message
   size_t resp_off = 0;
   bool responding = false;
+  ~Stream() {
+    if (sres && !committed) sres->abandon();   // reset / connection lost mid-payload
+  }
 };
 
 struct Outgoing {
@@ -227,8 +240,61 @@ class IoThread {
     Stream* st = static_cast<Stream*>(nghttp2_session_get_stream_user_data(s, sid));
     if (!st) return 0;
     IoThread* self = tls_self_;
-    if (st->body.empty() && len >= 5) {
-      const uint32_t msg = (uint32_t(data[1]) << 24) | (uint32_t(data[2]) << 16) | (uint32_t(data[3]) << 8) | data[4];
+    if (st->mode == kStreamMode) {
+      StreamRes* r = st->sres.get();
+      const size_t n = std::min(len, r->len - r->got);
+      if (n) r->write(data, n);
+      if (len > n) st->overflow = true;
+      return 0;
+    }
+    if (st->mode == kProbeMode) {
+      if (st->path != kPredictMethod || !self->srv_->stream_reserve()) {
+        st->mode = kBufferMode;
+      } else {
+        const size_t before = st->body.size();
+        const size_t take = std::min(len, kProbeMax - before);
+        st->body.append((const char*)data, take);
+        ProbeInfo pi;
+        Probe pr = probe_predict_header((const uint8_t*)st->body.data(), st->body.size(), kStreamMin, pi);
+        if (pr == Probe::kFound) {
+          std::shared_ptr<StreamRes> res = self->srv_->stream_reserve()(pi);
+          if (res) {
+            // payload = framed-message bytes [payload_off, payload_off + len): part may sit in
+            // the header buffer, the rest in this chunk (data[take..] is message offset before+take..)
+            size_t pos = pi.payload_off;
+            const size_t body_end = before + take;
+            if (pos < body_end) {
+              res->write((const uint8_t*)st->body.data() + pos, body_end - pos);
+              pos = body_end;
+            }
+            const size_t seen = before + len;
+            if (pos < seen) {
+              const size_t n = std::min(seen - pos, res->len - res->got);
+              res->write(data + (pos - before), n);
+              if (seen - pos > n) st->overflow = true;
+            }
+            st->body.resize(pi.payload_off);
+            st->sres = std::move(res);
+            st->mode = kStreamMode;
+            return 0;
+          }
+          pr = Probe::kNoStream;
+        }
+        if (pr == Probe::kNeedMore && take == len && st->body.size() < kProbeMax) return 0;
+        st->mode = kBufferMode;     // not streamable: buffer the rest as usual
+        data += take;
+        len -= take;
+      }
+    }
+    if (st->body.size() < 5 && st->body.size() + len >= 5) {
+      std::string hdr = st->body;
+      hdr.append((const char*)data, 5 - st->body.size());
+      const uint8_t* h = (const uint8_t*)hdr.data();
+      const uint32_t msg = (uint32_t(h[1]) << 24) | (uint32_t(h[2]) << 16) | (uint32_t(h[3]) << 8) | h[4];
+      if (msg <= self->srv_->max_message()) st->body.reserve(size_t(msg) + 5);
+    } else if (st->body.size() >= 5 && st->body.capacity() < 4096 + kProbeMax) {
+      const uint8_t* h = (const uint8_t*)st->body.data();
+      const uint32_t msg = (uint32_t(h[1]) << 24) | (uint32_t(h[2]) << 16) | (uint32_t(h[3]) << 8) | h[4];
       if (msg <= self->srv_->max_message()) st->body.reserve(size_t(msg) + 5);
     }
     if (st->body.size() + len > self->srv_->max_message() + 5) {
@@ -276,6 +342,33 @@ class IoThread {
 
   // ------------------------------------------------------------ request / response
   void request_done(Conn* c, Stream* st) {
+    if (st->mode == kStreamMode) {
+      StreamRes* r = st->sres.get();
+      if (st->bad_content_type || r->got != r->len || st->overflow) {
+        r->abandon();
+        st->committed = true;   // nothing left to abandon
+        answer(c, st, 13 /*INTERNAL*/,
+               st->bad_content_type ? "unsupported content-type (expected application/grpc)"
+                                    : "gRPC message length mismatch (streaming calls are not supported)",
+               std::string());
+        return;
+      }
+      auto call = std::make_unique<Call>();
+      call->conn_id = c->id;
+      call->io_index = index_;
+      call->stream_id = st->id;
+      call->method = st->path;
+      call->arrival = Clock::now();
+      call->timeout_us = st->timeout_us;
+      srv_->stats.requests++;
+      srv_->stats.fast_path++;
+      srv_->stats.streamed++;
+      srv_->stats.bytes_in += st->body.size() - 5 + r->len;
+      st->committed = true;
+      std::string().swap(st->body);
+      r->commit(std::move(call));
+      return;
+    }
     if (st->bad_content_type) {
       answer(c, st, 13 /*INTERNAL*/, "unsupported content-type (expected application/grpc)", std::string());
       return;
@@ -422,9 +515,14 @@ class IoThread {
 
   void on_readable(Conn* c) {
     for (;;) {
+      const auto t0 = Clock::now();
       ssize_t n = recv(c->fd, rbuf_.data(), rbuf_.size(), 0);
+      const auto t1 = Clock::now();
+      srv_->stats.ns_recv += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
       if (n > 0) {
         ssize_t r = nghttp2_session_mem_recv(c->sess, rbuf_.data(), size_t(n));
+        srv_->stats.ns_h2 +=
+            uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t1).count());
         if (r < 0) {
           c->dead = true;
           return;
@@ -482,9 +580,13 @@ class IoThread {
         if (it == conns_.end()) continue;
         Conn* c = it->second.get();
         if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) on_readable(c);
+        const auto tf = Clock::now();
         if (!c->dead && !flush(c)) c->dead = true;
+        srv_->stats.ns_send += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - tf).count());
       }
+      const auto td = Clock::now();
       drain_outbox();
+      srv_->stats.ns_send += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - td).count());
       for (auto it = conns_.begin(); it != conns_.end();) {
         if (it->second->dead) {
           Conn* c = it->second.get();
@@ -543,9 +645,14 @@ void Server::respond(uint64_t conn_id, int io_index, int32_t stream_id, int stat
 }
 
 void Server::dispatch(std::unique_ptr<Call> c) {
-  if (fast_ && fast_(c)) {
-    stats.fast_path++;
-    return;
+  if (fast_) {
+    const auto t0 = Clock::now();
+    const bool taken = fast_(c);
+    stats.ns_dispatch += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count());
+    if (taken) {
+      stats.fast_path++;
+      return;
+    }
   }
   stats.slow_path++;
   push_call(std::move(c));

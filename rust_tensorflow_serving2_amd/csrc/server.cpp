@@ -58,6 +58,7 @@ void register_server(py::module_& m) {
              p->fast = std::make_unique<FastPath>(p->srv.get());
              FastPath* fp = p->fast.get();
              p->srv->set_fast_dispatch([fp](std::unique_ptr<Call>& c) { return fp->try_dispatch(c); });
+             p->srv->set_stream_reserve([fp](const ProbeInfo& pi) { return fp->reserve_stream(pi); });
              return p;
            }),
            py::arg("host"), py::arg("port"), py::arg("io_threads") = 4, py::arg("max_message") = size_t(2147483647))
@@ -89,8 +90,11 @@ void register_server(py::module_& m) {
         py::dict d;
         d["connections"] = st.connections.load(); d["requests"] = st.requests.load();
         d["fast_path"] = st.fast_path.load(); d["slow_path"] = st.slow_path.load();
+        d["streamed"] = st.streamed.load();
         d["responses"] = st.responses.load(); d["errors"] = st.errors.load();
         d["bytes_in"] = st.bytes_in.load(); d["bytes_out"] = st.bytes_out.load();
+        d["io_s_recv"] = st.ns_recv.load() * 1e-9; d["io_s_h2"] = st.ns_h2.load() * 1e-9;
+        d["io_s_dispatch"] = st.ns_dispatch.load() * 1e-9; d["io_s_send"] = st.ns_send.load() * 1e-9;
         return d;
       })
       // ---- fast path endpoints
@@ -170,7 +174,7 @@ void register_server(py::module_& m) {
     py::dict d;
     d["ok"] = r.ok; d["errors"] = r.errors; d["elapsed_s"] = r.elapsed_s;
     d["latency_us"] = r.latency_us; d["first_error"] = r.first_error;
-    d["bytes_sent"] = r.bytes_sent; d["bytes_recv"] = r.bytes_recv;
+    d["bytes_sent"] = r.bytes_sent; d["bytes_recv"] = r.bytes_recv; d["cpu_s"] = r.cpu_s;
     return d;
   }, py::arg("host"), py::arg("port"), py::arg("method"), py::arg("bodies"), py::arg("total"),
      py::arg("concurrency") = 64, py::arg("connections") = 8, py::arg("threads") = 4, py::arg("timeout_s") = 120.0);

@@ -1,6 +1,8 @@
 // Protobuf wire codecs for the TF-Serving hot path (see wire.h).
 #include "wire.h"
 
+#include <algorithm>
+
 #if defined(__SSE4_2__)
 #include <nmmintrin.h>
 #endif
@@ -426,6 +428,97 @@ uint32_t crc32c_extend(uint32_t crc, const void* data, size_t n) {
   while (n--) c = T[0][(c ^ *p++) & 0xff] ^ (c >> 8);
 #endif
   return ~c;
+}
+
+// ---------------------------------------------------------------- streaming probe
+Probe probe_predict_header(const uint8_t* buf, size_t n, size_t min_payload, ProbeInfo& out) {
+  if (n < 5) return Probe::kNeedMore;
+  if (buf[0] != 0) return Probe::kNoStream;   // compressed
+  const size_t msglen = (size_t(buf[1]) << 24) | (size_t(buf[2]) << 16) | (size_t(buf[3]) << 8) | buf[4];
+  const uint8_t* base = buf + 5;
+  const size_t avail = std::min(n - 5, msglen);
+  bool have_spec = false;
+  try {
+    Reader r(base, avail);
+    while (true) {
+      if (r.done()) return avail == msglen ? Probe::kNoStream : Probe::kNeedMore;
+      const uint64_t key = r.varint();
+      const int field = int(key >> 3), wt = int(key & 7);
+      if (field == 1 && wt == 2) {
+        std::string_view sv = r.bytes();
+        parse_model_spec(sv, out.spec);
+        have_spec = true;
+        continue;
+      }
+      if (field != 2 || wt != 2 || !have_spec) return Probe::kNoStream;
+      // inputs map entry: must be the last field of the message
+      const uint64_t elen = r.varint();
+      const size_t estart = size_t(r.p - base);
+      if (estart + elen != msglen) return Probe::kNoStream;
+      Reader re(r.p, std::min<size_t>(elen, size_t(r.end - r.p)));
+      while (true) {
+        if (re.done()) return Probe::kNeedMore;
+        const uint64_t k2 = re.varint();
+        const int f2 = int(k2 >> 3), w2 = int(k2 & 7);
+        if (f2 == 1 && w2 == 2) {
+          std::string_view a = re.bytes();
+          out.alias.assign(a.data(), a.size());
+          continue;
+        }
+        if (f2 != 2 || w2 != 2 || out.alias.empty()) return Probe::kNoStream;
+        const uint64_t tlen = re.varint();
+        const size_t tstart = size_t(re.p - base);
+        if (tstart + tlen != msglen) return Probe::kNoStream;   // value ends the entry (and message)
+        Reader rt(re.p, std::min<size_t>(tlen, size_t(re.end - re.p)));
+        while (true) {
+          if (rt.done()) return Probe::kNeedMore;
+          const uint64_t k3 = rt.varint();
+          const int f3 = int(k3 >> 3), w3 = int(k3 & 7);
+          if (f3 == 1 && w3 == 0) {
+            out.dtype = int(rt.varint());
+          } else if (f3 == 2 && w3 == 2) {
+            std::string_view sh = rt.bytes();
+            Reader rs(reinterpret_cast<const uint8_t*>(sh.data()), sh.size());
+            out.shape.clear();
+            while (!rs.done()) {
+              const uint64_t k4 = rs.varint();
+              if ((k4 >> 3) == 2 && (k4 & 7) == 2) {
+                std::string_view dim = rs.bytes();
+                Reader rd(reinterpret_cast<const uint8_t*>(dim.data()), dim.size());
+                int64_t size = 0;
+                while (!rd.done()) {
+                  const uint64_t k5 = rd.varint();
+                  if ((k5 >> 3) == 1 && (k5 & 7) == 0) size = int64_t(rd.varint());
+                  else rd.skip(int(k5 & 7));
+                }
+                out.shape.push_back(size);
+              } else if ((k4 >> 3) == 3 && (k4 & 7) == 0) {
+                if (rs.varint() != 0) return Probe::kNoStream;   // unknown_rank
+              } else {
+                rs.skip(int(k4 & 7));
+              }
+            }
+          } else if (f3 == 3 && w3 == 0) {
+            rt.varint();   // version_number
+          } else if ((f3 == 4 || f3 == 5 || f3 == 6) && w3 == 2) {
+            const bool raw_ok = f3 == 4 ? (dtype_size(out.dtype) > 0 && out.dtype != DT_STRING)
+                                        : (f3 == 5 ? out.dtype == DT_FLOAT : out.dtype == DT_DOUBLE);
+            if (!raw_ok) return Probe::kNoStream;
+            const uint64_t plen = rt.varint();
+            const size_t poff = size_t(rt.p - base);
+            if (poff + plen != msglen || plen < min_payload) return Probe::kNoStream;
+            out.payload_off = 5 + poff;
+            out.payload_len = size_t(plen);
+            return Probe::kFound;
+          } else {
+            return Probe::kNoStream;
+          }
+        }
+      }
+    }
+  } catch (const WireError&) {
+    return Probe::kNeedMore;   // truncated so far (the caller bounds how long it waits)
+  }
 }
 
 }  // namespace tfs

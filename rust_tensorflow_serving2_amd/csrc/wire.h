@@ -137,6 +137,24 @@ struct PredictRequestView {
 };
 void parse_predict_request(const uint8_t* buf, size_t n, PredictRequestView& req);
 
+// ---------------------------------------------------------------- streaming probe
+// Header of a gRPC-framed PredictRequest whose LAST bytes are one large raw
+// tensor payload (the reference client's shape: ModelSpec, then one inputs
+// entry {alias, TensorProto{dtype, shape, float_val}} ending the message).
+// For such requests the payload can be copied from the socket buffer straight
+// into a batch slot as DATA frames arrive.
+struct ProbeInfo {
+  ModelSpecView spec;
+  std::string alias;
+  int dtype = 0;
+  std::vector<int64_t> shape;
+  size_t payload_off = 0;   // offset of the payload in the framed message (incl. the 5-byte prefix)
+  size_t payload_len = 0;
+};
+enum class Probe : int { kNeedMore = 0, kNoStream = 1, kFound = 2 };
+// `buf` = the first `n` bytes of the gRPC-framed message received so far.
+Probe probe_predict_header(const uint8_t* buf, size_t n, size_t min_payload, ProbeInfo& out);
+
 struct OutTensor {
   std::string alias;
   int dtype;

@@ -58,43 +58,75 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_kernel(const uint16_t* __res
 }
 
 // ---------------------------------------------------------------- global avg pool
+// Block = 4 waves on one (image, 512-channel chunk): lane owns 8 channels, the
+// 4 waves split the HW positions (loads unrolled so several are in flight),
+// partial sums meet in LDS.  N*C/512 blocks (e.g. 128 for ResNet-50 b32)
+// instead of one serial 49-load chain per thread.
 __global__ __launch_bounds__(256) void gap_nhwc_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                        int N, int HW, int C) {
+  __shared__ float part[3][64][8];
   const int C8 = C / 8;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N * C8) return;
-  const int n = i / C8, c8 = i - n * C8;
+  const int chunks = (C8 + 63) / 64;
+  const int n = blockIdx.x / chunks;
+  const int c8 = (blockIdx.x - n * chunks) * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const uint16_t* p = x + long(n) * HW * C + c8 * 8;
-  for (int h = 0; h < HW; ++h) {
-    float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(p + long(h) * C), f);
+  if (c8 < C8) {
+    const uint16_t* p = x + long(n) * HW * C + c8 * 8;
+#pragma unroll 4
+    for (int h = w; h < HW; h += 4) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(p + long(h) * C), f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) s[e] += f[e];
+      for (int e = 0; e < 8; ++e) s[e] += f[e];
+    }
   }
-  const float inv = 1.f / float(HW);
+  if (w > 0)
 #pragma unroll
-  for (int e = 0; e < 8; ++e) s[e] *= inv;
-  *reinterpret_cast<uint4*>(y + long(n) * C + c8 * 8) = pack8(s);
+    for (int e = 0; e < 8; ++e) part[w - 1][threadIdx.x & 63][e] = s[e];
+  __syncthreads();
+  if (w == 0 && c8 < C8) {
+    const float inv = 1.f / float(HW);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = (s[e] + part[0][threadIdx.x][e] + part[1][threadIdx.x][e] +
+                                        part[2][threadIdx.x][e]) * inv;
+    *reinterpret_cast<uint4*>(y + long(n) * C + c8 * 8) = pack8(s);
+  }
 }
 
 // ---------------------------------------------------------------- softmax + argmax
-// One wave per row.  ArgMax ties resolve to the smallest index (TF semantics).
+// One 256-thread block per row: every logit is loaded exactly once into
+// registers (up to 16 per thread, i.e. rows of <= 4096 classes stay in
+// registers), max/argmax and the exp-sum are block reductions (wave shuffles
+// + LDS).  ArgMax ties resolve to the smallest index (TF semantics).
+constexpr int kSmPer = 16;
 __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restrict__ logits, int in_bf16,
                                                              float* __restrict__ probs,
                                                              int64_t* __restrict__ classes, int rows, int cols) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+  __shared__ float smx[4];
+  __shared__ int sarg[4];
+  __shared__ float ssum[4];
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (row >= rows) return;
-  auto ld = [&](int c) -> float {
-    return in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * cols + c])
-                   : static_cast<const float*>(logits)[long(row) * cols + c];
-  };
+  float v[kSmPer];
   float mx = -INFINITY;
   int arg = 0x7fffffff;
-  for (int c = lane; c < cols; c += 64) {
-    const float v = ld(c);
-    if (v > mx || (v == mx && c < arg)) { mx = v; arg = c; }
+#pragma unroll
+  for (int k = 0; k < kSmPer; ++k) {
+    const int c = k * 256 + tid;
+    float x = -INFINITY;
+    if (c < cols)
+      x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * cols + c])
+                  : static_cast<const float*>(logits)[long(row) * cols + c];
+    v[k] = x;
+    if (c < cols && (x > mx || (x == mx && c < arg))) { mx = x; arg = c; }
+  }
+  // columns beyond the register tile (cols > 4096): strided tail, recomputed below
+  for (int c = kSmPer * 256 + tid; c < cols; c += 256) {
+    const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * cols + c])
+                            : static_cast<const float*>(logits)[long(row) * cols + c];
+    if (x > mx || (x == mx && c < arg)) { mx = x; arg = c; }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -102,13 +134,42 @@ __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restr
     const int oa = __shfl_xor(arg, o, 64);
     if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
   }
+  if (lane == 0) { smx[w] = mx; sarg[w] = arg; }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float om = smx[k];
+    const int oa = sarg[k];
+    if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+  }
   float s = 0.f;
-  for (int c = lane; c < cols; c += 64) s += __expf(ld(c) - mx);
+#pragma unroll
+  for (int k = 0; k < kSmPer; ++k) {
+    v[k] = (k * 256 + tid < cols) ? __expf(v[k] - mx) : 0.f;
+    s += v[k];
+  }
+  for (int c = kSmPer * 256 + tid; c < cols; c += 256) {
+    const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * cols + c])
+                            : static_cast<const float*>(logits)[long(row) * cols + c];
+    s += __expf(x - mx);
+  }
   s = wave_sum(s);
-  const float inv = 1.f / s;
-  if (probs)
-    for (int c = lane; c < cols; c += 64) probs[long(row) * cols + c] = __expf(ld(c) - mx) * inv;
-  if (classes && lane == 0) classes[row] = arg;
+  if (lane == 0) ssum[w] = s;
+  __syncthreads();
+  const float inv = 1.f / (ssum[0] + ssum[1] + ssum[2] + ssum[3]);
+  if (probs) {
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+      const int c = k * 256 + tid;
+      if (c < cols) probs[long(row) * cols + c] = v[k] * inv;
+    }
+    for (int c = kSmPer * 256 + tid; c < cols; c += 256) {
+      const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * cols + c])
+                              : static_cast<const float*>(logits)[long(row) * cols + c];
+      probs[long(row) * cols + c] = __expf(x - mx) * inv;
+    }
+  }
+  if (classes && tid == 0) classes[row] = arg;
 }
 
 // ---------------------------------------------------------------- casts
@@ -243,15 +304,16 @@ hipError_t maxpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int H, int
 }
 
 hipError_t global_avgpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s) {
-  const int work = N * (C / 8);
-  hipLaunchKernelGGL(gap_nhwc_kernel, dim3((work + 255) / 256), dim3(256), 0, s, x, y, N, HW, C);
+  const int chunks = (C / 8 + 63) / 64;
+  hipLaunchKernelGGL(gap_nhwc_kernel, dim3(N * chunks), dim3(256), 0, s, x, y, N, HW, C);
   return hipGetLastError();
 }
 
 hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, int64_t* classes, int rows,
                                  int cols, hipStream_t s) {
-  hipLaunchKernelGGL(softmax_argmax_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, logits, in_bf16, probs, classes,
-                     rows, cols);
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(softmax_argmax_kernel, dim3(rows), dim3(256), 0, s, logits, in_bf16, probs, classes, rows,
+                     cols);
   return hipGetLastError();
 }
 

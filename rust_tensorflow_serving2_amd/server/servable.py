@@ -35,6 +35,7 @@ class ServableOptions:
     fuse: Optional[bool] = None          # default: on for GPU devices
     compute_dtype: str = "bf16"          # bf16 on GPU (fp32 on CPU always)
     hip_graphs: bool = True
+    lanes: int = 4                       # GPU lanes = fast-path batch slots (stream + pinned staging + graphs)
     max_batch_size: int = 32
     allowed_batch_sizes: Tuple[int, ...] = ()
     warmup: bool = True
@@ -176,7 +177,7 @@ class Servable:
     def _make_runner(self, in_specs, out_specs) -> Runner:
         if self.options.is_gpu:
             from .gpu_runtime import GpuRunner
-            return GpuRunner(self, in_specs, out_specs)
+            return GpuRunner(self, in_specs, out_specs, lanes=self.options.lanes)
         return Runner(self, in_specs, out_specs)
 
     def input_specs(self, sig_name: str) -> Dict[str, TensorSpec]:

@@ -1,0 +1,124 @@
+"""The C++ Predict fast path without a GPU: a Python thread plays the GPU lane
+(acquire -> compute on the slot buffers -> complete) so the batcher, the
+streaming decode (payload copied socket -> slot row as DATA frames arrive),
+the buffered fallback and the FIFO queue are exercised on CPU."""
+import concurrent.futures as cf
+import threading
+
+import numpy as np
+import pytest
+
+from rust_tensorflow_serving2_amd import _C, native
+from rust_tensorflow_serving2_amd.schema import serving
+from rust_tensorflow_serving2_amd.utils import tensors as T
+
+import grpc
+
+ROW = 20000          # 80 KB of f32 per row: above the 64 KB streaming threshold
+PREDICT = "/tensorflow.serving.PredictionService/Predict"
+
+
+@pytest.fixture()
+def fast_server():
+    srv = _C.Http2Server("127.0.0.1", 0, 2)
+    ep = srv.add_endpoint("m", 1, "serving_default", [("x", T.DT_FLOAT, [ROW])], [("y", T.DT_FLOAT, [ROW])], 8, 3000)
+    slots = []
+    for k in range(2):
+        xin = np.zeros((8, ROW), np.float32)
+        yout = np.zeros((8, ROW), np.float32)
+        srv.set_slot_buffers(ep, k, [xin.ctypes.data], [yout.ctypes.data])
+        slots.append((xin, yout))
+    srv.set_route("m", "serving_default", -1, ep)
+    srv.set_route("m", "serving_default", 1, ep)
+    stop = threading.Event()
+    batches = []
+
+    def lane(k):
+        xin, yout = slots[k]
+        while not stop.is_set():
+            n = srv.acquire(ep, k, 50)
+            if n < 0:
+                return
+            if n == 0:
+                continue
+            batches.append(n)
+            yout[:n] = xin[:n] * 2 + 1
+            srv.complete(ep, k)
+
+    ts = [threading.Thread(target=lane, args=(k,), daemon=True) for k in range(2)]
+    srv.start()
+    for t in ts:
+        t.start()
+    yield srv, batches
+    stop.set()
+    srv.remove_endpoint(ep)
+    for t in ts:
+        t.join(timeout=5)
+    srv.stop()
+
+
+def _call(port, body):
+    with grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_send_message_length", 1 << 30),
+                                                            ("grpc.max_receive_message_length", 1 << 30)]) as ch:
+        return ch.unary_unary(PREDICT)(body, timeout=60)
+
+
+def _y(raw):
+    resp = serving.PredictResponse.FromString(raw)
+    return T.tensor_proto_to_numpy(resp.outputs["y"])
+
+
+def test_streamed_and_buffered_requests(fast_server):
+    srv, batches = fast_server
+    rng = np.random.default_rng(0)
+    reqs = []
+    for i in range(24):
+        n = 1 + i % 3
+        x = rng.standard_normal((n, ROW)).astype(np.float32)
+        filt = ["y"] if i % 4 == 3 else []        # an output_filter after the inputs -> buffered path
+        body = native.encode_predict_request(native.spec_tuple("m", None if i % 2 else 1, None, ""), {"x": x},
+                                             output_filter=filt)
+        reqs.append((x, body))
+    # one at a time: a slot is always open, so every request without an output_filter streams
+    for x, body in reqs[:8]:
+        np.testing.assert_allclose(_y(_call(srv.port, body)), x * 2 + 1, rtol=1e-6)
+    st = srv.stats()
+    assert st["fast_path"] == 8 and st["streamed"] == 6
+    # concurrently: requests that find every slot busy queue (buffered) behind the stream
+    with cf.ThreadPoolExecutor(12) as ex:
+        outs = list(ex.map(lambda r: _call(srv.port, r[1]), reqs[8:]))
+    for (x, _b), raw in zip(reqs[8:], outs):
+        np.testing.assert_allclose(_y(raw), x * 2 + 1, rtol=1e-6)
+    st = srv.stats()
+    assert st["fast_path"] == 24 and st["slow_path"] == 0 and st["streamed"] >= 6
+    assert sum(batches) >= 24
+
+
+def test_streamed_loadgen_mixed_sizes(fast_server):
+    """Many multiplexed streams per connection (frames of different streams interleave)."""
+    srv, _ = fast_server
+    bodies = [native.encode_predict_request(native.spec_tuple("m", None, None, ""),
+                                            {"x": np.full((n, ROW), n, np.float32)}) for n in (1, 2, 5, 8)]
+    r = _C.run_loadgen("127.0.0.1", srv.port, PREDICT, bodies, 200, 32, 4, 2, 120.0)
+    assert r["ok"] == 200 and r["errors"] == 0, r["first_error"]
+    assert srv.stats()["streamed"] > 0
+
+
+def test_wrong_shape_falls_back(fast_server):
+    """A header the endpoint does not accept is buffered and handed to the slow path."""
+    srv, _ = fast_server
+    body = native.encode_predict_request(native.spec_tuple("m", None, None, ""),
+                                         {"x": np.ones((1, ROW + 8), np.float32)})
+    got = []
+
+    def slow():
+        c = srv.next_call(5000)
+        got.append(c.body == body)
+        srv.respond(c, 3, "shape mismatch", b"")
+    th = threading.Thread(target=slow)
+    th.start()
+    with pytest.raises(grpc.RpcError) as ei:
+        _call(srv.port, body)
+    th.join()
+    assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT and got == [True]
+    assert srv.stats()["slow_path"] == 1

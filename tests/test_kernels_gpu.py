@@ -155,6 +155,21 @@ def test_pools_and_head():
     assert torch.equal(c.cpu(), torch.argmax(logits, -1)) and c[5].item() == 7
 
 
+@pytest.mark.parametrize("rows,cols", [(3, 5000), (2, 10), (1, 4096)])
+def test_softmax_argmax_shapes(rows, cols):
+    logits = rnd(rows, cols, scale=4, seed=rows + cols)
+    p, c = hip().softmax_argmax(logits.to(DEV))
+    assert torch.allclose(p.cpu(), torch.softmax(logits, -1), atol=1e-6)
+    assert torch.equal(c.cpu(), torch.argmax(logits, -1))
+
+
+@pytest.mark.parametrize("n,hw,c", [(3, 1, 72), (2, 9, 520), (1, 49, 4096)])
+def test_global_avgpool_shapes(n, hw, c):
+    g = rnd(n, hw, 1, c, seed=hw + c).to(BF)
+    gy = hip().global_avgpool(g.to(DEV))
+    assert (gy.float().cpu() - g.float().mean((1, 2))).abs().max() < 1e-2
+
+
 def test_layernorm_and_embedding():
     x = rnd(300, 768, seed=14).to(BF)
     r = rnd(300, 768, seed=15).to(BF)
