@@ -2,7 +2,13 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <dlfcn.h>
+#include <pthread.h>
+
 #include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <thread>
 
 #include "batcher.h"
 #include "http2.h"
@@ -12,9 +18,153 @@ using namespace tfs;
 
 namespace {
 
+// ---------------------------------------------------------------- native GPU lanes
+// The HIP runtime is resolved at run time (dlopen of the libamdhip64 that torch
+// already loaded), so this CPU extension builds without HIP and costs nothing
+// on machines without a GPU.
+struct HipRt {
+  using launch_t = int (*)(void*, void*);
+  using setdev_t = int (*)(int);
+  using errstr_t = const char* (*)(int);
+  using memcpy_t = int (*)(void*, const void*, size_t, int, void*);
+  using evcreate_t = int (*)(void**, unsigned);
+  using evrecord_t = int (*)(void*, void*);
+  using evsync_t = int (*)(void*);
+  using evdestroy_t = int (*)(void*);
+  launch_t launch = nullptr;
+  setdev_t set_device = nullptr;
+  errstr_t err = nullptr;
+  memcpy_t memcpy_async = nullptr;
+  evcreate_t event_create = nullptr;
+  evrecord_t event_record = nullptr;
+  evsync_t event_sync = nullptr;
+  evdestroy_t event_destroy = nullptr;
+  bool load() {
+    if (launch) return true;
+    void* h = dlopen("libamdhip64.so", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("libamdhip64.so", RTLD_NOW);
+    if (!h) return false;
+    auto sym = [&](const char* n) { return dlsym(h, n); };
+    set_device = reinterpret_cast<setdev_t>(sym("hipSetDevice"));
+    err = reinterpret_cast<errstr_t>(sym("hipGetErrorString"));
+    memcpy_async = reinterpret_cast<memcpy_t>(sym("hipMemcpyAsync"));
+    event_create = reinterpret_cast<evcreate_t>(sym("hipEventCreateWithFlags"));
+    event_record = reinterpret_cast<evrecord_t>(sym("hipEventRecord"));
+    event_sync = reinterpret_cast<evsync_t>(sym("hipEventSynchronize"));
+    event_destroy = reinterpret_cast<evdestroy_t>(sym("hipEventDestroy"));
+    launch = reinterpret_cast<launch_t>(sym("hipGraphLaunch"));
+    return launch && set_device && memcpy_async && event_create && event_record && event_sync && event_destroy;
+  }
+};
+constexpr int kHipMemcpyHostToDevice = 1, kHipMemcpyDeviceToHost = 2;
+constexpr unsigned kHipEventBlockingSync = 0x1, kHipEventDisableTiming = 0x2;
+
+HipRt& hip_rt() {
+  static HipRt rt;
+  return rt;
+}
+
+struct LaneCopy {
+  uintptr_t dst, src;
+  size_t row_bytes;
+};
+struct LaneBucket {
+  int rows = 0;
+  void* exec = nullptr;
+  std::vector<LaneCopy> in, out;   // per batch: n rows each way (live rows only)
+};
+
+// One GPU lane served entirely in C++: wait for the slot's batch, H2D the n
+// live rows (SDMA), launch the bucket's HIP graph, D2H the n result rows, and
+// block (interrupt-driven event, no spinning) until done; then encode and post
+// the responses.  No Python and no GIL per batch.
+class NativeLane {
+ public:
+  NativeLane(Server* srv, std::shared_ptr<Endpoint> ep, int slot, int device, void* stream,
+             std::vector<LaneBucket> buckets)
+      : srv_(srv), ep_(std::move(ep)), slot_(slot), device_(device), stream_(stream), buckets_(std::move(buckets)) {
+    std::sort(buckets_.begin(), buckets_.end(), [](auto& a, auto& b) { return a.rows < b.rows; });
+    th_ = std::thread([this] { run(); });
+  }
+  ~NativeLane() { join(); }
+  void join() {
+    if (th_.joinable()) th_.join();
+  }
+  int endpoint_id() const { return ep_->id; }
+  std::atomic<uint64_t> batches{0}, errors{0};
+
+ private:
+  int batch(HipRt& rt, void* done, int n) {
+    const LaneBucket* b = nullptr;
+    for (auto& x : buckets_)
+      if (x.rows >= n) {
+        b = &x;
+        break;
+      }
+    if (!b) return -1;
+    int e = 0;
+    for (auto& c : b->in)
+      if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
+                                  c.row_bytes * size_t(n), kHipMemcpyHostToDevice, stream_);
+    if (!e) e = rt.launch(b->exec, stream_);
+    for (auto& c : b->out)
+      if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
+                                  c.row_bytes * size_t(n), kHipMemcpyDeviceToHost, stream_);
+    if (!e) e = rt.event_record(done, stream_);
+    if (!e) e = rt.event_sync(done);
+    return e;
+  }
+  void run() {
+    pthread_setname_np(pthread_self(), "tfs-nlane");
+    HipRt& rt = hip_rt();
+    rt.set_device(device_);
+    void* done = nullptr;
+    if (rt.event_create(&done, kHipEventBlockingSync | kHipEventDisableTiming) != 0) done = nullptr;
+    for (;;) {
+      const int n = ep_->acquire(slot_, 100);
+      if (n < 0) break;   // endpoint closed
+      if (n == 0) continue;
+      const int e = done ? batch(rt, done, n) : -1;
+      if (e != 0) {
+        errors++;
+        std::string why = e > 0 && rt.err ? std::string(rt.err(e)) : std::string("no graph for this batch");
+        ep_->fail(slot_, *srv_, 13 /*INTERNAL*/, "GPU batch failed: " + why);
+        continue;
+      }
+      batches++;
+      ep_->complete(slot_, *srv_);
+    }
+    if (done) rt.event_destroy(done);
+  }
+  Server* srv_;
+  std::shared_ptr<Endpoint> ep_;
+  int slot_, device_;
+  void* stream_;
+  std::vector<LaneBucket> buckets_;
+  std::thread th_;
+};
+
 struct PyServer {
   std::unique_ptr<Server> srv;
   std::unique_ptr<FastPath> fast;
+  std::mutex lmu;
+  std::vector<std::unique_ptr<NativeLane>> lanes;
+  // join (and drop) the lanes of an endpoint that has been closed
+  void join_lanes(int ep_id) {
+    std::vector<std::unique_ptr<NativeLane>> done;
+    {
+      std::lock_guard<std::mutex> g(lmu);
+      for (auto it = lanes.begin(); it != lanes.end();) {
+        if (ep_id < 0 || (*it)->endpoint_id() == ep_id) {
+          done.push_back(std::move(*it));
+          it = lanes.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
+    for (auto& l : done) l->join();
+  }
 };
 
 // A slow-path call handed to Python.
@@ -133,7 +283,39 @@ void register_server(py::module_& m) {
       .def("clear_routes", [](PyServer& s, const std::string& model) { s.fast->clear_routes(model); })
       .def("remove_endpoint", [](PyServer& s, int id) {
         py::gil_scoped_release nogil;
-        s.fast->remove_endpoint(id);
+        s.fast->remove_endpoint(id);   // closes the endpoint: its native lanes see acquire() < 0
+        s.join_lanes(id);
+      })
+      .def("start_native_lane", [](PyServer& s, int id, int slot, int device, uintptr_t stream,
+                                   const py::list& buckets) {
+        auto ep = s.fast->endpoint(id);
+        if (!ep || buckets.empty() || !hip_rt().load()) return false;
+        std::vector<LaneBucket> bs;
+        for (auto item : buckets) {
+          auto t = item.cast<py::tuple>();
+          LaneBucket b;
+          b.rows = t[0].cast<int>();
+          b.exec = reinterpret_cast<void*>(t[1].cast<uintptr_t>());
+          for (auto c : t[2].cast<py::list>()) {
+            auto ct = c.cast<py::tuple>();
+            b.in.push_back({ct[0].cast<uintptr_t>(), ct[1].cast<uintptr_t>(), ct[2].cast<size_t>()});
+          }
+          for (auto c : t[3].cast<py::list>()) {
+            auto ct = c.cast<py::tuple>();
+            b.out.push_back({ct[0].cast<uintptr_t>(), ct[1].cast<uintptr_t>(), ct[2].cast<size_t>()});
+          }
+          bs.push_back(std::move(b));
+        }
+        std::lock_guard<std::mutex> g(s.lmu);
+        s.lanes.push_back(std::make_unique<NativeLane>(s.srv.get(), ep, slot, device,
+                                                       reinterpret_cast<void*>(stream), std::move(bs)));
+        return true;
+      }, py::arg("endpoint"), py::arg("slot"), py::arg("device"), py::arg("stream"), py::arg("buckets"))
+      .def("native_lane_stats", [](PyServer& s) {
+        std::lock_guard<std::mutex> g(s.lmu);
+        py::list out;
+        for (auto& l : s.lanes) out.append(py::make_tuple(l->endpoint_id(), l->batches.load(), l->errors.load()));
+        return out;
       })
       .def("acquire", [](PyServer& s, int id, int slot, int timeout_ms) {
         auto ep = s.fast->endpoint(id);

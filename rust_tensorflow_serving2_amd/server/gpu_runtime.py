@@ -80,9 +80,13 @@ class GpuRunner:
         self._rr = 0
         self._rr_lock = threading.Lock()
         self.lanes: List[_Lane] = []
+        # lanes handed to the native fast path are driven by C++ workers without
+        # the Python lane locks: the Python run() path then only uses the rest
+        # (one spare lane is always kept for it)
+        self.claimed: set = set()
         if self.batched:
             with torch.cuda.device(self.device):
-                self.lanes = [_Lane(self.device) for _ in range(max(1, lanes))]
+                self.lanes = [_Lane(self.device) for _ in range(max(1, lanes) + 1)]
                 for lane in self.lanes:
                     self._alloc_host(lane)
 
@@ -143,9 +147,18 @@ class GpuRunner:
                 return b
         return None
 
+    def fast_lanes(self) -> List[int]:
+        """Lanes the fast path may take (all but the spare kept for run())."""
+        return list(range(max(1, len(self.lanes) - 1)))
+
+    def claim(self, lane_idx: int) -> None:
+        with self._rr_lock:
+            self.claimed.add(lane_idx)
+
     def _pick_lane(self) -> _Lane:
         with self._rr_lock:
-            lane = self.lanes[self._rr % len(self.lanes)]
+            free = [i for i in range(len(self.lanes)) if i not in self.claimed] or [len(self.lanes) - 1]
+            lane = self.lanes[free[self._rr % len(free)]]
             self._rr += 1
         return lane
 
@@ -158,6 +171,10 @@ class GpuRunner:
             outs = self._finish(self.program.run(ins))
         lane.stream.synchronize()
         self._ensure_host_out(lane, outs)
+        # compute-only graph: the H2D/D2H copies stay separate hipMemcpyAsync calls
+        # so they run on the SDMA engines (copy nodes inside a graph can turn into
+        # blit kernels that read host memory over PCIe from the CUs) and move only
+        # the n live rows of a batch, not the whole bucket
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=lane.stream, capture_error_mode="thread_local"):
             outs = self._finish(self.program.run(ins))
@@ -174,13 +191,29 @@ class GpuRunner:
                 self._capture(lane, b)
         with torch.cuda.stream(lane.stream):
             for h, d in zip(lane.host_in, lane.static_in[b]):
-                d.copy_(h[:b], non_blocking=True)
+                d[:n].copy_(h[:n], non_blocking=True)
             lane.graphs[b].replay()
             for so, ho in zip(lane.static_out[b], lane.host_out):
-                ho[:b].copy_(so, non_blocking=True)
+                ho[:n].copy_(so[:n], non_blocking=True)
             lane.done.record(lane.stream)
         lane.done.synchronize()
         return b
+
+    def native_lane_spec(self, lane_idx: int):
+        """Everything a C++ lane worker needs to serve batches on this lane:
+        (device index, HIP stream handle, [(bucket, hipGraphExec handle,
+        [(device_in, pinned_in, row_bytes)], [(pinned_out, device_out, row_bytes)])])."""
+        lane = self.lanes[lane_idx]
+        buckets = []
+        for b in self.buckets:
+            ins = [(d.data_ptr(), h.data_ptr(), d[0].numel() * d.element_size())
+                   for d, h in zip(lane.static_in[b], lane.host_in)]
+            outs = [(h.data_ptr(), so.data_ptr(), so[0].numel() * so.element_size())
+                    for so, h in zip(lane.static_out[b], lane.host_out)]
+            if any(not isinstance(o, torch.Tensor) or not o.is_contiguous() for o in lane.static_out[b]):
+                return None
+            buckets.append((b, int(lane.graphs[b].raw_cuda_graph_exec()), ins, outs))
+        return self.device.index or 0, int(lane.stream.cuda_stream), buckets
 
     # ------------------------------------------------------------ run
     def run_lane(self, lane_idx: int, n: int) -> None:

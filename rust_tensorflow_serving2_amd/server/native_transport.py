@@ -13,6 +13,7 @@
 from __future__ import annotations
 
 import logging
+import os
 import threading
 from typing import Dict, List, Optional
 
@@ -23,6 +24,8 @@ from .. import _C
 from . import errors as E
 from .manager import AVAILABLE, END, UNLOADING
 from .servable import PREDICT_METHOD
+
+NATIVE_LANES = os.environ.get("TFSERVE_NATIVE_LANES", "1") != "0"
 
 log = logging.getLogger("tfserve.native")
 
@@ -49,10 +52,19 @@ class FastEndpoint:
         assert list(io_in) == in_aliases and list(io_out) == out_aliases
         self.workers: List[threading.Thread] = []
         self._stop = threading.Event()
-        for lane_idx in range(len(self.runner.lanes)):
+        lanes = self.runner.fast_lanes()
+        for lane_idx in lanes:
             in_ptrs, out_ptrs = self.runner.lane_host_pointers(lane_idx)
             srv.set_slot_buffers(self.id, lane_idx, in_ptrs, out_ptrs)
-        for lane_idx in range(len(self.runner.lanes)):
+        self.native_lanes = 0
+        for lane_idx in lanes:
+            self.runner.claim(lane_idx)
+            # C++ lane worker (graph launch without Python) when every bucket graph
+            # carries its own host copies; the Python worker otherwise
+            spec = self.runner.native_lane_spec(lane_idx) if NATIVE_LANES else None
+            if spec is not None and srv.start_native_lane(self.id, lane_idx, *spec):
+                self.native_lanes += 1
+                continue
             th = threading.Thread(target=self._work, args=(lane_idx,), daemon=True,
                                   name=f"tfs-gpu-{servable.name}-{lane_idx}")
             th.start()
