@@ -42,6 +42,25 @@ __device__ __forceinline__ float apply_act(float x, int act) {
   }
 }
 
+// Compile-time activation (epilogues dispatch on the runtime code once, then
+// run branch-free loops).
+template <int ACT>
+__device__ __forceinline__ float act_fn(float x) {
+  if constexpr (ACT == kActRelu) {
+    return x > 0.f ? x : 0.f;
+  } else if constexpr (ACT == kActGeluTanh) {
+    const float c = 0.7978845608028654f;
+    const float u = c * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.f + tanhf(u));
+  } else if constexpr (ACT == kActGeluErf) {
+    return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+  } else if constexpr (ACT == kActTanh) {
+    return tanhf(x);
+  } else {
+    return x;
+  }
+}
+
 // Bijective XCD-aware remap (MI355X: 8 XCDs, blocks dealt round-robin):
 // blocks that share an XCD get a contiguous range of logical tile ids, so
 // neighbouring tiles (which share A rows / B columns) hit the same L2.

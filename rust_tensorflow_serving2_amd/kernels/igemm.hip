@@ -31,9 +31,11 @@ constexpr int BK = 64;
 constexpr int kThreads = 256;
 constexpr int kGroupM = 8;
 
-template <int BM, int BN, int AMODE, int NSTAGE>
+template <int BM, int BN, int AMODE, int NSTAGE, int WAVES_M = 2>
 struct IGemm {
-  static constexpr int WM = BM / 2, WN = BN / 2;
+  // 4 waves in a WAVES_M x (4 / WAVES_M) grid, each owning a WM x WN sub-tile
+  static constexpr int WAVES_N = 4 / WAVES_M;
+  static constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   static constexpr int TM = WM / 16, TN = WN / 16;
   static constexpr int A_CHUNKS = BM * BK / 8 / kThreads;
   static constexpr int B_CHUNKS = BN * BK / 8 / kThreads;
@@ -66,9 +68,69 @@ __device__ __forceinline__ void wait_vmcnt() {
 // feeding MFMAs have already been waited on by then.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-template <int BM, int BN, int AMODE, int NSTAGE>
+// Epilogue over the fp32 tile staged in LDS: coalesced 8-column row chunks,
+// alpha * acc + bias (+ residual) -> activation -> bf16 / f32 store.
+template <int BM, int BN, int CS_LD, int ACT>
+__device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* Cs, int m0, int n0, int tid) {
+  const int M = p.M, N = p.N;
+  const float alpha = p.alpha;
+  constexpr int CPR = BN / 8;   // chunks per row
+  const bool vec_ok = (N % 8 == 0) && (p.ldc % 8 == 0) && (!p.residual || p.ldr % 8 == 0);
+  for (int c = tid; c < BM * CPR; c += kThreads) {
+    const int row = c / CPR, col = (c - row * CPR) * 8;
+    const int m = m0 + row, n = n0 + col;
+    if (m >= M || n >= N) continue;
+    const float4 lo = *reinterpret_cast<const float4*>(Cs + row * CS_LD + col);
+    const float4 hi = *reinterpret_cast<const float4*>(Cs + row * CS_LD + col + 4);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    if (vec_ok && n + 8 <= N) {
+      float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (p.bias) {
+        const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+        const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+        bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+        bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+      }
+      float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (p.residual) {
+        const uint4 rr = *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
+        const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          rv[2 * e] = bf16_to_f32(uint16_t(w[e] & 0xffff));
+          rv[2 * e + 1] = bf16_to_f32(uint16_t(w[e] >> 16));
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = act_fn<ACT>(v[e] * alpha + bv[e] + rv[e]);
+      if (p.out_f32) {
+        float* o = static_cast<float*>(p.out) + size_t(m) * p.ldc + n;
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        uint16_t b[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) b[e] = f32_to_bf16(v[e]);
+        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.out) + size_t(m) * p.ldc + n) =
+            make_uint4(b[0] | (uint32_t(b[1]) << 16), b[2] | (uint32_t(b[3]) << 16),
+                       b[4] | (uint32_t(b[5]) << 16), b[6] | (uint32_t(b[7]) << 16));
+      }
+    } else {
+      for (int e = 0; e < 8 && n + e < N; ++e) {
+        float x = v[e] * alpha;
+        if (p.bias) x += p.bias[n + e];
+        if (p.residual) x += bf16_to_f32(p.residual[size_t(m) * p.ldr + n + e]);
+        x = act_fn<ACT>(x);
+        if (p.out_f32) static_cast<float*>(p.out)[size_t(m) * p.ldc + n + e] = x;
+        else static_cast<uint16_t*>(p.out)[size_t(m) * p.ldc + n + e] = f32_to_bf16(x);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int AMODE, int NSTAGE, int WAVES_M>
 __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
-  using G = IGemm<BM, BN, AMODE, NSTAGE>;
+  using G = IGemm<BM, BN, AMODE, NSTAGE, WAVES_M>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int S = G::STAGES;
   uint16_t* As = reinterpret_cast<uint16_t*>(smem);
@@ -87,7 +149,7 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / G::WAVES_N, wn = wid % G::WAVES_N;
   const int chunk = tid & 7;
   const int row_base = tid >> 3;   // 0..31
   // Direct-to-LDS staging (dense / im2col operands): each wave instruction
@@ -378,79 +440,29 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
     }
     return;
   }
-  const bool vec_ok = (N % 8 == 0) && (p.ldc % 8 == 0) && (!p.residual || p.ldr % 8 == 0);
-  for (int c = tid; c < BM * CPR; c += kThreads) {
-    const int row = c / CPR, col = (c - row * CPR) * 8;
-    const int m = m0 + row, n = n0 + col;
-    if (m >= M || n >= N) continue;
-    const float4 lo = *reinterpret_cast<const float4*>(Cs + row * G::CS_LD + col);
-    const float4 hi = *reinterpret_cast<const float4*>(Cs + row * G::CS_LD + col + 4);
-    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    if (vec_ok && n + 8 <= N) {
-      float bv[8];
-      if (p.bias) {
-        const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
-        const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
-        bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
-        bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bv[e] = 0.f;
-      }
-      float rv[8];
-      if (p.residual) {
-        const uint4 rr = *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
-        const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          rv[2 * e] = bf16_to_f32(uint16_t(w[e] & 0xffff));
-          rv[2 * e + 1] = bf16_to_f32(uint16_t(w[e] >> 16));
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) rv[e] = 0.f;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e] * alpha + bv[e] + rv[e], p.act);
-      if (p.out_f32) {
-        float* o = static_cast<float*>(p.out) + size_t(m) * p.ldc + n;
-        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      } else {
-        uint16_t b[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) b[e] = f32_to_bf16(v[e]);
-        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.out) + size_t(m) * p.ldc + n) =
-            make_uint4(b[0] | (uint32_t(b[1]) << 16), b[2] | (uint32_t(b[3]) << 16),
-                       b[4] | (uint32_t(b[5]) << 16), b[6] | (uint32_t(b[7]) << 16));
-      }
-    } else {
-      for (int e = 0; e < 8 && n + e < N; ++e) {
-        float x = v[e] * alpha;
-        if (p.bias) x += p.bias[n + e];
-        if (p.residual) x += bf16_to_f32(p.residual[size_t(m) * p.ldr + n + e]);
-        x = apply_act(x, p.act);
-        if (p.out_f32) static_cast<float*>(p.out)[size_t(m) * p.ldc + n + e] = x;
-        else static_cast<uint16_t*>(p.out)[size_t(m) * p.ldc + n + e] = f32_to_bf16(x);
-      }
-    }
+  switch (p.act) {
+    case kActRelu: epilogue_rows<BM, BN, G::CS_LD, kActRelu>(p, Cs, m0, n0, tid); break;
+    case kActGeluTanh: epilogue_rows<BM, BN, G::CS_LD, kActGeluTanh>(p, Cs, m0, n0, tid); break;
+    case kActGeluErf: epilogue_rows<BM, BN, G::CS_LD, kActGeluErf>(p, Cs, m0, n0, tid); break;
+    case kActTanh: epilogue_rows<BM, BN, G::CS_LD, kActTanh>(p, Cs, m0, n0, tid); break;
+    default: epilogue_rows<BM, BN, G::CS_LD, 0>(p, Cs, m0, n0, tid); break;
   }
 }
 
-template <int BM, int BN, int AMODE, int NSTAGE>
+template <int BM, int BN, int AMODE, int NSTAGE, int WAVES_M = 2>
 hipError_t launch_cfg(const IGemmArgs& a, hipStream_t s) {
-  using G = IGemm<BM, BN, AMODE, NSTAGE>;
+  using G = IGemm<BM, BN, AMODE, NSTAGE, WAVES_M>;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<BM, BN, AMODE, NSTAGE>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<BM, BN, AMODE, NSTAGE, WAVES_M>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int splits = a.splits > 1 ? a.splits : 1;
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE, NSTAGE>), dim3(tiles, splits), dim3(kThreads), G::LDS, s, a);
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE, NSTAGE, WAVES_M>), dim3(tiles, splits), dim3(kThreads), G::LDS, s, a);
   return hipGetLastError();
 }
 
@@ -490,14 +502,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(IGemmArgs p) {
 // LDS): the tuner picks per layer (K=64 1x1 convs want occupancy, long-K
 // small-grid layers want depth).  Register-staged operand modes ignore the
 // depth (always 2).
-constexpr int kCfgBM[kNumIGemmConfigs] = {128, 128, 64, 64, 128, 64, 128, 64};
-constexpr int kCfgBN[kNumIGemmConfigs] = {128, 64, 128, 64, 128, 64, 64, 128};
-constexpr int kCfgST[kNumIGemmConfigs] = {2, 2, 2, 2, 3, 4, 3, 3};
+constexpr int kCfgBM[kNumIGemmConfigs] = {128, 128, 64, 64, 128, 64, 128, 64, 64, 256, 128, 256};
+constexpr int kCfgBN[kNumIGemmConfigs] = {128, 64, 128, 64, 128, 64, 64, 128, 256, 64, 256, 128};
+constexpr int kCfgST[kNumIGemmConfigs] = {2, 2, 2, 2, 3, 4, 3, 3, 2, 2, 2, 2};
+// register-staged operand modes only instantiate configs 0-3
+constexpr int kCfgBase[kNumIGemmConfigs] = {0, 1, 2, 3, 0, 3, 1, 2, 2, 1, 0, 0};
 
 template <int AMODE>
 hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
   constexpr bool GL = (AMODE == kADense || AMODE == kAIm2col);
-  if (!GL && cfg >= 4) cfg = (kCfgBM[cfg] == 128 ? (kCfgBN[cfg] == 128 ? 0 : 1) : (kCfgBN[cfg] == 128 ? 2 : 3));
+  if (!GL) cfg = kCfgBase[cfg];
   switch (cfg) {
     case 0: return launch_cfg<128, 128, AMODE, 2>(a, s);
     case 1: return launch_cfg<128, 64, AMODE, 2>(a, s);
@@ -511,6 +525,11 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
       case 5: return launch_cfg<64, 64, AMODE, 4>(a, s);
       case 6: return launch_cfg<128, 64, AMODE, 3>(a, s);
       case 7: return launch_cfg<64, 128, AMODE, 3>(a, s);
+      // wide tiles (one wave row / column): 4x the outputs per workgroup setup
+      case 8: return launch_cfg<64, 256, AMODE, 2, 1>(a, s);
+      case 9: return launch_cfg<256, 64, AMODE, 2, 4>(a, s);
+      case 10: return launch_cfg<128, 256, AMODE, 2, 2>(a, s);
+      case 11: return launch_cfg<256, 128, AMODE, 2, 4>(a, s);
       default: break;
     }
   }

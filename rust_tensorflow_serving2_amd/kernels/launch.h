@@ -50,8 +50,9 @@ hipError_t ingest_c4_launch(const float* x, uint16_t* y, int64_t pixels, int C, 
 hipError_t splitk_reduce_launch(const IGemmArgs& args, hipStream_t stream);
 
 // Tile configs (BM x BN, DMA ring depth): 0..3 = 128x128, 128x64, 64x128,
-// 64x64 double-buffered; 4 = 128x128x3, 5 = 64x64x4, 6 = 128x64x3, 7 = 64x128x3
-constexpr int kNumIGemmConfigs = 8;
+// 64x64 double-buffered; 4 = 128x128x3, 5 = 64x64x4, 6 = 128x64x3, 7 = 64x128x3;
+// wide: 8 = 64x256, 9 = 256x64, 10 = 128x256, 11 = 256x128 (dense / im2col only)
+constexpr int kNumIGemmConfigs = 12;
 int igemm_config_bm(int cfg);
 int igemm_config_bn(int cfg);
 int igemm_config_stages(int cfg);

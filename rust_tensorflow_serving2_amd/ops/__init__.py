@@ -69,8 +69,9 @@ def heuristic_config(M: int, N: int) -> int:
 # (BM, BN) per igemm config; configs 4.. add deeper direct-to-LDS DMA rings
 # (kernels/igemm.hip kCfgST) and only apply to dense / im2col operands.
 TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64),
-         4: (128, 128), 5: (64, 64), 6: (128, 64), 7: (64, 128)}
-DMA_ONLY = {4, 5, 6, 7}
+         4: (128, 128), 5: (64, 64), 6: (128, 64), 7: (64, 128),
+         8: (64, 256), 9: (256, 64), 10: (128, 256), 11: (256, 128)}
+DMA_ONLY = {4, 5, 6, 7, 8, 9, 10, 11}
 
 
 def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
@@ -90,8 +91,10 @@ def candidates(M: int, N: int, K: int, dma: bool = True):
     nk = -(-K // 64)
     out = []
     for cfg, (bm, bn) in TILES.items():
-        if cfg in DMA_ONLY and (not dma or nk < 3):
+        if cfg in DMA_ONLY and (not dma or (cfg in (4, 5, 6, 7) and nk < 3)):
             continue
+        if bn > 64 and N <= bn // 2 or bm > 64 and M <= bm // 2:
+            continue   # mostly-empty tiles
         tiles = -(-M // bm) * -(-N // bn)
         for s in (1, 2, 4, 8, 16):
             if s > 1 and (nk // s < 2 or tiles >= 1024 or tiles * s > 4096):
