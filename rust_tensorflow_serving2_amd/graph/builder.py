@@ -29,6 +29,8 @@ def attr_value(v) -> "tf.AttrValue":
     a = tf.AttrValue()
     if isinstance(v, tf.AttrValue):
         a.CopyFrom(v)
+    elif isinstance(v, tf.NameAttrList):
+        a.func.CopyFrom(v)
     elif isinstance(v, DType):
         a.type = int(v)
     elif isinstance(v, Shape):

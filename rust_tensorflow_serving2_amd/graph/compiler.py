@@ -62,10 +62,14 @@ def array_to_value(a: np.ndarray, dt: int):
 
 
 def bind_variables(g: Graph, bundle) -> None:
+    from .ir import restore_keys
+    keys = restore_keys(g) if bundle is not None else {}
     for node in list(g.nodes.values()):
         if node.op in ("VariableV2", "Variable", "VarHandleOp"):
             key = node.name
-            if node.op == "VarHandleOp":
+            if node.name in keys and keys[node.name] in bundle:
+                key = keys[node.name]          # saver graph (TF2 object-path keys)
+            elif node.op == "VarHandleOp":
                 sn = node.sattr("shared_name")
                 if sn and bundle is not None and sn in bundle:
                     key = sn

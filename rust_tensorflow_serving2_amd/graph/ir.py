@@ -162,4 +162,134 @@ def from_graph_def(gd) -> Graph:
         g.add(node)
     for fn in gd.library.function:
         g.functions[fn.signature.name] = fn
+    inline_functions(g)
     return g
+
+
+# ---------------------------------------------------------------- TF2 function inlining
+# Output-argument layout of builtin multi-output ops, for resolving function-body
+# tensor names "node:out_arg:idx" to flat output indices.
+_OUT_ARGS = {
+    "FusedBatchNorm": ["y", "batch_mean", "batch_variance", "reserve_space_1", "reserve_space_2"],
+    "FusedBatchNormV2": ["y", "batch_mean", "batch_variance", "reserve_space_1", "reserve_space_2"],
+    "FusedBatchNormV3": ["y", "batch_mean", "batch_variance", "reserve_space_1", "reserve_space_2",
+                         "reserve_space_3"],
+    "TopKV2": ["values", "indices"],
+    "Unique": ["y", "idx"],
+    "BroadcastGradientArgs": ["r0", "r1"],
+}
+CALL_OPS = ("PartitionedCall", "StatefulPartitionedCall")
+
+
+def _body_ref(ref: str, local: Dict[str, str], args: Dict[str, Tuple[str, int]],
+              out_base: Dict[str, Tuple[str, Dict[str, int]]]) -> Tuple[str, int]:
+    """Function-body tensor name -> (graph node, output index)."""
+    if ref in args:
+        return args[ref]
+    parts = ref.split(":")
+    node = parts[0]
+    if node not in local:
+        raise ValueError(f"function body references unknown tensor {ref!r}")
+    if len(parts) == 1:
+        return local[node], 0
+    if len(parts) == 2:                       # "node:idx" (GraphDef style, rare in bodies)
+        return local[node], int(parts[1])
+    out_arg, idx = parts[1], int(parts[2])
+    op, offsets = out_base[node]
+    if out_arg in offsets:
+        return local[node], offsets[out_arg] + idx
+    return local[node], idx                   # single (list) output argument
+
+
+def inline_functions(g: Graph, max_depth: int = 64) -> int:
+    """Inline every PartitionedCall / StatefulPartitionedCall (and direct calls of
+    library functions) so TF2 SavedModels become one flat graph the compiler
+    can fold and fuse.  The call node becomes an IdentityN of the function's
+    return tensors, so its consumers and control dependents are untouched.
+    Returns the number of calls inlined."""
+    if not g.functions:
+        return 0
+    done = 0
+    for _round in range(max_depth):
+        calls = [n for n in list(g.nodes.values())
+                 if (n.op in CALL_OPS and n.attrs.get("f")) or n.op in g.functions]
+        if not calls:
+            return done
+        for call in calls:
+            fname = call.attrs.get("f") if call.op in CALL_OPS else call.op
+            fdef = g.functions.get(fname)
+            if fdef is None:
+                raise ValueError(f"{call.name}: function {fname!r} not in the graph's library")
+            sig = fdef.signature
+            if len(sig.input_arg) != len(call.inputs):
+                raise ValueError(f"{call.name}: {len(call.inputs)} inputs for {fname} "
+                                 f"which takes {len(sig.input_arg)}")
+            args = {a.name: src for a, src in zip(sig.input_arg, call.inputs)}
+            local: Dict[str, str] = {}
+            out_base: Dict[str, Tuple[str, Dict[str, int]]] = {}
+            for nd in fdef.node_def:
+                local[nd.name] = g.unique_name(f"{call.name}/{nd.name}")
+                offsets: Dict[str, int] = {}
+                # (Stateful)PartitionedCall has ONE list output arg ("output"); a direct
+                # call of a library function exposes that function's output args
+                inner = g.functions.get(nd.op)
+                names = [a.name for a in inner.signature.output_arg] if inner is not None \
+                    else _OUT_ARGS.get(nd.op, [])
+                for k, a in enumerate(names):
+                    offsets[a] = k
+                out_base[nd.name] = (nd.op, offsets)
+            for nd in fdef.node_def:
+                node = Node(name=local[nd.name], op=nd.op, device=nd.device)
+                for ref in nd.input:
+                    if ref.startswith("^"):
+                        c = ref[1:]
+                        if c in local:
+                            node.ctrl.append(local[c])
+                        elif c in args:
+                            node.ctrl.append(args[c][0])
+                        continue
+                    node.inputs.append(_body_ref(ref, local, args, out_base))
+                for k, v in nd.attr.items():
+                    node.attrs[k] = attr_to_py(v)
+                node.ctrl.extend(call.ctrl)
+                g.add(node)
+            rets = [_body_ref(fdef.ret[a.name], local, args, out_base) for a in sig.output_arg]
+            call.op = "IdentityN"
+            call.inputs = rets
+            call.attrs = {"T": [0] * len(rets), "_inlined": fname}
+            # keep the call's control inputs only through the inlined nodes
+            call.ctrl = [local[n] for n in fdef.control_ret.values() if n in local]
+            done += 1
+    raise ValueError("function call nesting deeper than %d" % max_depth)
+
+
+def restore_keys(g: Graph) -> Dict[str, str]:
+    """Variable node -> checkpoint key, read off the saver's restore subgraph
+    (RestoreV2 tensor_names -> [Identity] -> Assign / AssignVariableOp).  TF2
+    SavedModels key variables by object path ("layer/kernel/.ATTRIBUTES/
+    VARIABLE_VALUE"), which neither the node name nor shared_name carries."""
+    def through_identity(name: str, idx: int) -> Tuple[str, int]:
+        seen = 0
+        while name in g.nodes and g.nodes[name].op in ("Identity", "IdentityN") and seen < 64:
+            n = g.nodes[name]
+            name, idx = n.inputs[idx if n.op == "IdentityN" else 0]
+            seen += 1
+        return name, idx
+
+    out: Dict[str, str] = {}
+    for n in g.nodes.values():
+        if n.op not in ("Assign", "AssignVariableOp") or len(n.inputs) < 2:
+            continue
+        var, _ = through_identity(*n.inputs[0])
+        src, idx = through_identity(*n.inputs[1])
+        r = g.nodes.get(src)
+        if r is None or r.op not in ("RestoreV2", "Restore", "RestoreSlice") or len(r.inputs) < 2:
+            continue
+        names_node = g.nodes.get(r.inputs[1][0])
+        if names_node is None or names_node.op != "Const":
+            continue
+        vals = np.asarray(names_node.attrs.get("value"), dtype=object).reshape(-1)
+        if idx < len(vals):
+            key = vals[idx]
+            out[var] = key.decode() if isinstance(key, bytes) else str(key)
+    return out

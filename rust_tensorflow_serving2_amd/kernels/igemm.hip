@@ -70,30 +70,75 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "me
 
 // Epilogue over the fp32 tile staged in LDS: coalesced 8-column row chunks,
 // alpha * acc + bias (+ residual) -> activation -> bf16 / f32 store.
+// Chunk `it` of this thread: row-major 8-column chunks, kThreads apart; since
+// kThreads is a multiple of the chunks per row, a thread's column never changes.
+template <int BM, int BN>
+struct EpiMap {
+  static constexpr int CPR = BN / 8;
+  static constexpr int ITERS = BM * CPR / kThreads;
+  static_assert(kThreads % CPR == 0 && (BM * CPR) % kThreads == 0, "epilogue chunk mapping");
+  static constexpr int PRE = ITERS <= 8 ? ITERS : 0;   // residual chunks prefetched into registers
+};
+
+template <int BM, int BN>
+__device__ __forceinline__ void epi_rowcol(int tid, int it, int& row, int& col) {
+  constexpr int CPR = BN / 8;
+  const int c = tid + it * kThreads;
+  row = c / CPR;
+  col = (c - row * CPR) * 8;
+}
+
+// Issue the residual loads of this thread's epilogue chunks early (before the
+// K loop) so their latency hides under the operand DMA and the MFMAs.
+template <int BM, int BN>
+__device__ __forceinline__ void prefetch_residual(const IGemmArgs& p, int m0, int n0, int tid,
+                                                  uint4 (&rpre)[EpiMap<BM, BN>::PRE > 0 ? EpiMap<BM, BN>::PRE : 1]) {
+  constexpr int PRE = EpiMap<BM, BN>::PRE;
+  if (PRE == 0 || !p.residual || p.splits > 1 || (p.N % 8) || (p.ldr % 8)) return;
+#pragma unroll
+  for (int it = 0; it < PRE; ++it) {
+    int row, col;
+    epi_rowcol<BM, BN>(tid, it, row, col);
+    const int m = m0 + row, n = n0 + col;
+    rpre[it] = (m < p.M && n + 8 <= p.N) ? *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n)
+                                          : make_uint4(0, 0, 0, 0);
+  }
+}
+
 template <int BM, int BN, int CS_LD, int ACT>
-__device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* Cs, int m0, int n0, int tid) {
+__device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* Cs, int m0, int n0, int tid,
+                                              const uint4 (&rpre)[EpiMap<BM, BN>::PRE > 0 ? EpiMap<BM, BN>::PRE : 1]) {
+  using EM = EpiMap<BM, BN>;
   const int M = p.M, N = p.N;
   const float alpha = p.alpha;
-  constexpr int CPR = BN / 8;   // chunks per row
   const bool vec_ok = (N % 8 == 0) && (p.ldc % 8 == 0) && (!p.residual || p.ldr % 8 == 0);
-  for (int c = tid; c < BM * CPR; c += kThreads) {
-    const int row = c / CPR, col = (c - row * CPR) * 8;
+  // bias: fixed column per thread -> loaded once
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  {
+    int row0, col0;
+    epi_rowcol<BM, BN>(tid, 0, row0, col0);
+    const int n = n0 + col0;
+    if (p.bias && vec_ok && n + 8 <= N) {
+      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+      const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+      bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+      bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < EM::ITERS; ++it) {
+    int row, col;
+    epi_rowcol<BM, BN>(tid, it, row, col);
     const int m = m0 + row, n = n0 + col;
     if (m >= M || n >= N) continue;
     const float4 lo = *reinterpret_cast<const float4*>(Cs + row * CS_LD + col);
     const float4 hi = *reinterpret_cast<const float4*>(Cs + row * CS_LD + col + 4);
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     if (vec_ok && n + 8 <= N) {
-      float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (p.bias) {
-        const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
-        const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
-        bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
-        bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
-      }
       float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (p.residual) {
-        const uint4 rr = *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
+        const uint4 rr = EM::PRE > 0 ? rpre[EM::PRE > 0 ? it : 0]
+                                     : *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
         const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -346,6 +391,9 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
 #pragma unroll
     for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  uint4 rpre[EpiMap<BM, BN>::PRE > 0 ? EpiMap<BM, BN>::PRE : 1];
+  prefetch_residual<BM, BN>(p, m0, n0, tid, rpre);
+
   const int nk_all = (K + BK - 1) / BK;
   const int kt0 = p.splits > 1 ? blockIdx.y * p.kt_per_split : 0;
   const int nk = p.splits > 1 ? min(nk_all, kt0 + p.kt_per_split) - kt0 : nk_all;
@@ -441,11 +489,11 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
     return;
   }
   switch (p.act) {
-    case kActRelu: epilogue_rows<BM, BN, G::CS_LD, kActRelu>(p, Cs, m0, n0, tid); break;
-    case kActGeluTanh: epilogue_rows<BM, BN, G::CS_LD, kActGeluTanh>(p, Cs, m0, n0, tid); break;
-    case kActGeluErf: epilogue_rows<BM, BN, G::CS_LD, kActGeluErf>(p, Cs, m0, n0, tid); break;
-    case kActTanh: epilogue_rows<BM, BN, G::CS_LD, kActTanh>(p, Cs, m0, n0, tid); break;
-    default: epilogue_rows<BM, BN, G::CS_LD, 0>(p, Cs, m0, n0, tid); break;
+    case kActRelu: epilogue_rows<BM, BN, G::CS_LD, kActRelu>(p, Cs, m0, n0, tid, rpre); break;
+    case kActGeluTanh: epilogue_rows<BM, BN, G::CS_LD, kActGeluTanh>(p, Cs, m0, n0, tid, rpre); break;
+    case kActGeluErf: epilogue_rows<BM, BN, G::CS_LD, kActGeluErf>(p, Cs, m0, n0, tid, rpre); break;
+    case kActTanh: epilogue_rows<BM, BN, G::CS_LD, kActTanh>(p, Cs, m0, n0, tid, rpre); break;
+    default: epilogue_rows<BM, BN, G::CS_LD, 0>(p, Cs, m0, n0, tid, rpre); break;
   }
 }
 

@@ -41,10 +41,18 @@ def write_bundle(prefix: str, tensors: Dict[str, np.ndarray],
     off = 0
     with open(data_file(prefix, 0, 1), "wb") as f:
         for name in names:
-            a = np.require(tensors[name], requirements="C")
+            a = np.asarray(tensors[name])
             dt = dtypes.get(name) or T.dt_of(a)
             if dt == T.DT_STRING:
                 raise ValueError("string variables are not supported in bundles")
+            if dt == T.DT_BFLOAT16:
+                if a.dtype.itemsize != 2:
+                    raise ValueError(f"{name}: DT_BFLOAT16 needs the raw 16-bit pattern (got {a.dtype})")
+            else:
+                want = np.dtype(T.np_dtype(dt))
+                if a.dtype != want:
+                    a = a.astype(want)      # the entry's bytes must match its declared dtype
+            a = np.require(a, requirements="C")
             raw = memoryview(a.reshape(-1)).cast("B") if a.size else b""
             f.write(raw)
             e = tf.BundleEntryProto(dtype=dt, shard_id=0, offset=off, size=len(raw),
