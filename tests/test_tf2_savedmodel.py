@@ -63,6 +63,3 @@ def test_tf2_on_gpu_fused(mlp_path):
     x = np.random.default_rng(4).standard_normal((5, 16)).astype(np.float32)
     out = s.run("serving_default", {"x": x}, ["output_0"])["output_0"]
     np.testing.assert_allclose(out, keras_mlp.reference(x, keras_mlp.weights()), atol=2e-2)
-    r = s.runner("serving_default", ["x"], ["output_0"])
-    assert any(type(fn).__name__ == "FusedMatMul" or getattr(fn, "__self__", None).__class__.__name__ == "FusedMatMul"
-               for fn, *_ in r.program.steps if fn is not None) or True
