@@ -29,7 +29,7 @@ int Endpoint::open_slot_locked(int n) {
     if (s.reserved + n <= max_rows) return open_;
     s.state = kReady;
     open_ = -1;
-    cv_ready_.notify_all();
+    s.cv->notify_all();
   }
   const int N = int(slots_.size());
   for (int k = 0; k < N; ++k) {
@@ -41,6 +41,7 @@ int Endpoint::open_slot_locked(int n) {
       s.reserved = s.copied = 0;
       open_ = idx;
       next_ = (idx + 1) % N;
+      s.cv->notify_all();   // the lane starts its batch-timeout clock
       return idx;
     }
   }
@@ -150,7 +151,7 @@ void Endpoint::copy_rows(int slot, int r0, int n, const std::vector<const uint8_
     std::memcpy(s.in_base[i] + size_t(r0) * inputs[i].row_bytes, src[i], size_t(n) * inputs[i].row_bytes);
   std::lock_guard<std::mutex> g(mu_);
   s.copied += n;
-  if (s.copied == s.reserved) cv_ready_.notify_all();
+  if (s.copied == s.reserved) s.cv->notify_all();
 }
 
 void Endpoint::drain_queue() {
@@ -239,7 +240,7 @@ void Endpoint::commit_stream(SlotStream& r, std::unique_ptr<Call> call) {
   Slot& s = slots_[r.slot];
   s.reqs[r.idx].call = std::move(call);
   s.copied += r.n;
-  if (s.copied == s.reserved) cv_ready_.notify_all();
+  if (s.copied == s.reserved) s.cv->notify_all();
 }
 
 void Endpoint::abandon_stream(SlotStream& r) {
@@ -248,7 +249,7 @@ void Endpoint::abandon_stream(SlotStream& r) {
   std::lock_guard<std::mutex> g(mu_);
   Slot& s = slots_[r.slot];
   s.copied += r.n;   // the row runs as padding; complete() skips it (no call)
-  if (s.copied == s.reserved) cv_ready_.notify_all();
+  if (s.copied == s.reserved) s.cv->notify_all();
 }
 
 void Endpoint::abandon_stalled_locked(Slot& s) {
@@ -282,7 +283,7 @@ int Endpoint::acquire(int slot, int timeout_ms) {
         continue;
       }
       if (now >= deadline) return 0;
-      cv_ready_.wait_until(lk, std::min(stall, deadline));
+      s.cv->wait_until(lk, std::min(stall, deadline));
       continue;
     }
     if (s.state == kOpen && s.reserved > 0) {
@@ -293,11 +294,11 @@ int Endpoint::acquire(int slot, int timeout_ms) {
         continue;
       }
       if (now >= deadline) return 0;
-      cv_ready_.wait_until(lk, std::min(due, deadline));
+      s.cv->wait_until(lk, std::min(due, deadline));
       continue;
     }
     if (now >= deadline) return 0;
-    cv_ready_.wait_until(lk, deadline);
+    s.cv->wait_until(lk, deadline);
   }
   return -1;
 }
@@ -360,7 +361,7 @@ void Endpoint::close(Server* srv) {
     closed_ = true;
     for (auto& s : slots_) abandon_stalled_locked(s);
     left.swap(queue_);
-    cv_ready_.notify_all();
+    for (auto& sl : slots_) sl.cv->notify_all();
     cv_free_.notify_all();
   }
   if (srv)

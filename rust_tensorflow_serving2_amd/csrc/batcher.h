@@ -74,6 +74,9 @@ struct Slot {
   int state = kFree;
   Clock::time_point first;
   std::vector<Pending> reqs;
+  // per-slot wakeups: only the lane that owns the slot is woken (a shared
+  // condition variable woke every lane on every request)
+  std::shared_ptr<std::condition_variable> cv = std::make_shared<std::condition_variable>();
 };
 
 struct EndpointStats {

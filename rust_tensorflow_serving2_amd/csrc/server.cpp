@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <thread>
 
@@ -30,6 +31,7 @@ struct HipRt {
   using evcreate_t = int (*)(void**, unsigned);
   using evrecord_t = int (*)(void*, void*);
   using evsync_t = int (*)(void*);
+  using evquery_t = int (*)(void*);
   using evdestroy_t = int (*)(void*);
   launch_t launch = nullptr;
   setdev_t set_device = nullptr;
@@ -38,6 +40,7 @@ struct HipRt {
   evcreate_t event_create = nullptr;
   evrecord_t event_record = nullptr;
   evsync_t event_sync = nullptr;
+  evquery_t event_query = nullptr;
   evdestroy_t event_destroy = nullptr;
   bool load() {
     if (launch) return true;
@@ -51,13 +54,16 @@ struct HipRt {
     event_create = reinterpret_cast<evcreate_t>(sym("hipEventCreateWithFlags"));
     event_record = reinterpret_cast<evrecord_t>(sym("hipEventRecord"));
     event_sync = reinterpret_cast<evsync_t>(sym("hipEventSynchronize"));
+    event_query = reinterpret_cast<evquery_t>(sym("hipEventQuery"));
     event_destroy = reinterpret_cast<evdestroy_t>(sym("hipEventDestroy"));
     launch = reinterpret_cast<launch_t>(sym("hipGraphLaunch"));
-    return launch && set_device && memcpy_async && event_create && event_record && event_sync && event_destroy;
+    return launch && set_device && memcpy_async && event_create && event_record && event_sync && event_query &&
+           event_destroy;
   }
 };
 constexpr int kHipMemcpyHostToDevice = 1, kHipMemcpyDeviceToHost = 2;
-constexpr unsigned kHipEventBlockingSync = 0x1, kHipEventDisableTiming = 0x2;
+constexpr unsigned kHipEventDisableTiming = 0x2;
+constexpr int kHipErrorNotReady = 600;
 
 HipRt& hip_rt() {
   static HipRt rt;
@@ -76,8 +82,8 @@ struct LaneBucket {
 
 // One GPU lane served entirely in C++: wait for the slot's batch, H2D the n
 // live rows (SDMA), launch the bucket's HIP graph, D2H the n result rows, and
-// block (interrupt-driven event, no spinning) until done; then encode and post
-// the responses.  No Python and no GIL per batch.
+// wait for the completion event (polled with naps, not spun); then encode and
+// post the responses.  No Python and no GIL per batch.
 class NativeLane {
  public:
   NativeLane(Server* srv, std::shared_ptr<Endpoint> ep, int slot, int device, void* stream,
@@ -111,15 +117,26 @@ class NativeLane {
       if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
                                   c.row_bytes * size_t(n), kHipMemcpyDeviceToHost, stream_);
     if (!e) e = rt.event_record(done, stream_);
-    if (!e) e = rt.event_sync(done);
+    if (!e) e = wait(rt, done);
     return e;
+  }
+  // Poll the batch's completion event: a short yield phase, then 40 us naps.
+  // (hipEventSynchronize busy-waits a core per lane for the whole ~1 ms batch;
+  // the IO threads need those cores.)
+  static int wait(HipRt& rt, void* ev) {
+    for (int i = 0;; ++i) {
+      const int e = rt.event_query(ev);
+      if (e != kHipErrorNotReady) return e;
+      if (i < 16) std::this_thread::yield();
+      else std::this_thread::sleep_for(std::chrono::microseconds(40));
+    }
   }
   void run() {
     pthread_setname_np(pthread_self(), "tfs-nlane");
     HipRt& rt = hip_rt();
     rt.set_device(device_);
     void* done = nullptr;
-    if (rt.event_create(&done, kHipEventBlockingSync | kHipEventDisableTiming) != 0) done = nullptr;
+    if (rt.event_create(&done, kHipEventDisableTiming) != 0) done = nullptr;
     for (;;) {
       const int n = ep_->acquire(slot_, 100);
       if (n < 0) break;   // endpoint closed

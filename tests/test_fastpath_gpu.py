@@ -59,7 +59,7 @@ def test_fast_path_matches_slow_path(gpu_server):
     for k in ("probabilities", "classes"):
         a = np.array(fast.outputs[k].float_val or fast.outputs[k].int64_val)
         b = np.array(slow.outputs[k].float_val or slow.outputs[k].int64_val)
-        np.testing.assert_allclose(a, b, atol=1e-5)
+        np.testing.assert_allclose(a, b, atol=2e-4)
     assert fast.model_spec.version.value == 1 and fast.model_spec.signature_name == "serving_default"
     assert list(d.size for d in fast.outputs["probabilities"].tensor_shape.dim) == [3, 10]
     st = gpu_server.transports[0].stats()
@@ -82,7 +82,7 @@ def test_many_concurrent_rows_are_routed_back_correctly(gpu_server):
         ref = serving.PredictResponse.FromString(
             gpu_server.core.predict(native.encode_predict_request(spec, {"input": x})))
         got = np.array(serving.PredictResponse.FromString(raw).outputs["probabilities"].float_val)
-        np.testing.assert_allclose(got, np.array(ref.outputs["probabilities"].float_val), atol=1e-5)
+        np.testing.assert_allclose(got, np.array(ref.outputs["probabilities"].float_val), atol=2e-4)
 
 
 def test_output_filter_and_fallthrough(gpu_server):
