@@ -50,6 +50,13 @@ int Endpoint::open_slot_locked(int n) {
 
 int Endpoint::offer(std::unique_ptr<Call>& call, PredictRequestView& req) {
   if (req.inputs.size() != inputs.size()) return 1;
+  if (call->expired()) {
+    if (srv_) {
+      srv_->stats.expired++;
+      srv_->respond(*call, 4 /*DEADLINE_EXCEEDED*/, "Deadline Exceeded", std::string());
+      return 0;
+    }
+  }
   // match aliases (inputs sorted by alias on registration)
   std::vector<TensorView*> tv(inputs.size(), nullptr);
   for (auto& kv : req.inputs) {
@@ -311,8 +318,14 @@ void Endpoint::complete(int slot, Server& srv) {
   spec.version = version;
   spec.signature_name = signature;
   std::vector<OutTensor> outs;
+  const auto now = Clock::now();
   for (auto& p : s.reqs) {
     if (!p.call) continue;   // abandoned streaming row
+    if (p.call->expired(now)) {
+      srv.stats.expired++;
+      srv.respond(*p.call, 4 /*DEADLINE_EXCEEDED*/, "Deadline Exceeded", std::string());
+      continue;
+    }
     outs.clear();
     const size_t nout = p.outs.empty() ? outputs.size() : p.outs.size();
     for (size_t k = 0; k < nout; ++k) {

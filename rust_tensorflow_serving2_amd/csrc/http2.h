@@ -43,6 +43,10 @@ struct Call {
   size_t size() const { return body.size() - off; }
   Clock::time_point arrival;
   int64_t timeout_us = 0;  // grpc-timeout, 0 = none
+  // the client's deadline (grpc-timeout) has passed: answer DEADLINE_EXCEEDED, skip the work
+  bool expired(Clock::time_point now = Clock::now()) const {
+    return timeout_us > 0 && now - arrival > std::chrono::microseconds(timeout_us);
+  }
 };
 
 class Server;
@@ -82,6 +86,7 @@ using StreamReserve = std::function<std::shared_ptr<StreamRes>(const ProbeInfo&)
 struct ServerStats {
   std::atomic<uint64_t> connections{0}, requests{0}, fast_path{0}, slow_path{0}, responses{0}, errors{0};
   std::atomic<uint64_t> streamed{0};   // fast-path requests whose payload went socket -> slot directly
+  std::atomic<uint64_t> expired{0};    // answered DEADLINE_EXCEEDED (client grpc-timeout passed)
   std::atomic<uint64_t> bytes_in{0}, bytes_out{0};
   // IO-thread time split (ns): recv() syscalls, nghttp2 frame processing incl.
   // body assembly, fast-path dispatch (decode + batch-slot copy), send()

@@ -3,6 +3,7 @@
 #include <pybind11/stl.h>
 
 #include <dlfcn.h>
+#include <cstdlib>
 #include <pthread.h>
 
 #include <algorithm>
@@ -89,6 +90,12 @@ class NativeLane {
   NativeLane(Server* srv, std::shared_ptr<Endpoint> ep, int slot, int device, void* stream,
              std::vector<LaneBucket> buckets)
       : srv_(srv), ep_(std::move(ep)), slot_(slot), device_(device), stream_(stream), buckets_(std::move(buckets)) {
+    // fault injection for tests: TFSERVE_FAULT=lane_every=N fails every Nth batch
+    if (const char* f = getenv("TFSERVE_FAULT")) {
+      const std::string spec(f);
+      const auto k = spec.find("lane_every=");
+      if (k != std::string::npos) fault_every_ = std::atoi(spec.c_str() + k + 11);
+    }
     std::sort(buckets_.begin(), buckets_.end(), [](auto& a, auto& b) { return a.rows < b.rows; });
     th_ = std::thread([this] { run(); });
   }
@@ -141,6 +148,11 @@ class NativeLane {
       const int n = ep_->acquire(slot_, 100);
       if (n < 0) break;   // endpoint closed
       if (n == 0) continue;
+      if (fault_every_ > 0 && ++seen_ % uint64_t(fault_every_) == 0) {
+        errors++;
+        ep_->fail(slot_, *srv_, 13 /*INTERNAL*/, "injected fault (TFSERVE_FAULT)");
+        continue;
+      }
       const int e = done ? batch(rt, done, n) : -1;
       if (e != 0) {
         errors++;
@@ -158,6 +170,8 @@ class NativeLane {
   int slot_, device_;
   void* stream_;
   std::vector<LaneBucket> buckets_;
+  int fault_every_ = 0;
+  uint64_t seen_ = 0;
   std::thread th_;
 };
 
@@ -216,7 +230,8 @@ void register_server(py::module_& m) {
       .def_property_readonly("body", [](const PyCall& c) {
         return py::bytes(reinterpret_cast<const char*>(c.call->data()), c.call->size());
       })
-      .def_property_readonly("timeout_us", [](const PyCall& c) { return c.call->timeout_us; });
+      .def_property_readonly("timeout_us", [](const PyCall& c) { return c.call->timeout_us; })
+      .def_property_readonly("expired", [](const PyCall& c) { return c.call->expired(); });
 
   py::class_<PyServer>(m, "Http2Server")
       .def(py::init([](const std::string& host, int port, int io_threads, size_t max_message) {
@@ -249,6 +264,7 @@ void register_server(py::module_& m) {
       .def("respond", [](PyServer& s, PyCall& c, int status, const std::string& message, const py::bytes& body) {
         if (!c.call) throw std::runtime_error("call already answered");
         std::string b = body;
+        if (status == 4 && c.call->expired()) s.srv->stats.expired++;
         s.srv->respond(*c.call, status, message, std::move(b));
         c.call.reset();
       }, py::arg("call"), py::arg("status"), py::arg("message"), py::arg("body"))
@@ -257,7 +273,7 @@ void register_server(py::module_& m) {
         py::dict d;
         d["connections"] = st.connections.load(); d["requests"] = st.requests.load();
         d["fast_path"] = st.fast_path.load(); d["slow_path"] = st.slow_path.load();
-        d["streamed"] = st.streamed.load();
+        d["streamed"] = st.streamed.load(); d["expired"] = st.expired.load();
         d["responses"] = st.responses.load(); d["errors"] = st.errors.load();
         d["bytes_in"] = st.bytes_in.load(); d["bytes_out"] = st.bytes_out.load();
         d["io_s_recv"] = st.ns_recv.load() * 1e-9; d["io_s_h2"] = st.ns_h2.load() * 1e-9;

@@ -122,8 +122,14 @@ class NativeTransport:
             call = srv.next_call(100)
             if call is None:
                 continue
+            if call.expired:                      # the client's grpc-timeout already passed
+                srv.respond(call, E.DEADLINE_EXCEEDED, "Deadline Exceeded", b"")
+                continue
             try:
                 body = core.handle(call.method, call.body)
+                if call.expired:
+                    srv.respond(call, E.DEADLINE_EXCEEDED, "Deadline Exceeded", b"")
+                    continue
                 srv.respond(call, 0, "", body)
             except E.ServingError as e:
                 srv.respond(call, e.code, e.message, b"")

@@ -4,6 +4,7 @@ streaming decode (payload copied socket -> slot row as DATA frames arrive),
 the buffered fallback and the FIFO queue are exercised on CPU."""
 import concurrent.futures as cf
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -122,3 +123,43 @@ def test_wrong_shape_falls_back(fast_server):
     th.join()
     assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT and got == [True]
     assert srv.stats()["slow_path"] == 1
+
+
+def test_deadline_exceeded_is_not_computed_twice():
+    """A request whose grpc-timeout passes while its batch waits is answered
+    DEADLINE_EXCEEDED by the batcher instead of being encoded."""
+    srv = _C.Http2Server("127.0.0.1", 0, 1)
+    ep = srv.add_endpoint("m", 1, "serving_default", [("x", T.DT_FLOAT, [ROW])], [("y", T.DT_FLOAT, [ROW])], 8, 1000)
+    xin = np.zeros((8, ROW), np.float32)
+    yout = np.zeros((8, ROW), np.float32)
+    srv.set_slot_buffers(ep, 0, [xin.ctypes.data], [yout.ctypes.data])
+    srv.set_route("m", "serving_default", -1, ep)
+    stop = threading.Event()
+
+    def slow_lane():
+        while not stop.is_set():
+            n = srv.acquire(ep, 0, 50)
+            if n < 0:
+                return
+            if n > 0:
+                stop.wait(0.4)               # the GPU is "busy" past the client deadline
+                srv.complete(ep, 0)
+
+    th = threading.Thread(target=slow_lane, daemon=True)
+    srv.start()
+    th.start()
+    try:
+        body = native.encode_predict_request(native.spec_tuple("m", None, None, ""), {"x": np.ones((1, ROW), np.float32)})
+        with grpc.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+            with pytest.raises(grpc.RpcError) as ei:
+                ch.unary_unary(PREDICT)(body, timeout=0.15)
+        assert ei.value.code() == grpc.StatusCode.DEADLINE_EXCEEDED
+        deadline = time.time() + 5
+        while srv.stats()["expired"] < 1 and time.time() < deadline:
+            time.sleep(0.05)
+        assert srv.stats()["expired"] == 1
+    finally:
+        stop.set()
+        srv.remove_endpoint(ep)
+        th.join(timeout=5)
+        srv.stop()

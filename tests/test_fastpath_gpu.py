@@ -106,3 +106,42 @@ def test_loadgen_against_fast_path(gpu_server):
               for i in range(8)]
     r = _C.run_loadgen("127.0.0.1", gpu_server.port, PREDICT, bodies, 400, 32, 4, 2, 120.0)
     assert r["ok"] == 400 and r["errors"] == 0, r["first_error"]
+
+
+def test_native_lanes_and_injected_faults(tmp_path, monkeypatch):
+    """Native C++ lanes serve the batches; an injected lane fault fails only the
+    requests of that batch (INTERNAL) and the server keeps serving."""
+    from rust_tensorflow_serving2_amd.models import resnet
+    import time
+    monkeypatch.setenv("TFSERVE_FAULT", "lane_every=3")
+    base = str(tmp_path / "resnet")
+    resnet.export(os.path.join(base, "1"), blocks=(1, 1, 1, 1), width=16, num_classes=10, image_size=32, seed=6)
+    so = ServableOptions(device="cuda:0", max_batch_size=4, allowed_batch_sizes=(1, 2, 4), lanes=1)
+    srv = ModelServer(ServerOptions(port=0, host="127.0.0.1", model_name="resnet", model_base_path=base,
+                                    device="cuda:0", transport="native", servable=so,
+                                    file_system_poll_wait_seconds=0, batch_timeout_us=200)).start()
+    try:
+        tr = srv.transports[0]
+        for _ in range(300):
+            if tr.stats().get("endpoints"):
+                break
+            time.sleep(0.05)
+        eps = list(tr._eps.values())
+        assert eps and eps[0].native_lanes == 1
+        x = np.random.default_rng(7).random((1, 32, 32, 3), dtype=np.float32)
+        body = native.encode_predict_request(native.spec_tuple("resnet", None, None, ""), {"input": x})
+        codes = []
+        with grpc.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+            stub = ch.unary_unary(PREDICT)
+            for _ in range(9):                       # sequential: one request per batch
+                try:
+                    stub(body, timeout=30)
+                    codes.append("OK")
+                except grpc.RpcError as e:
+                    assert "injected fault" in e.details()
+                    codes.append(e.code().name)
+        assert codes.count("INTERNAL") == 3 and codes.count("OK") == 6, codes
+        stats = srv.transports[0].srv.native_lane_stats()
+        assert stats and stats[0][2] == 3
+    finally:
+        srv.stop()
