@@ -40,8 +40,10 @@ def build_parser() -> argparse.ArgumentParser:
     a("--port", type=int, default=8500, help="gRPC port (PredictionService + ModelService)")
     a("--rest_api_port", type=int, default=0, help="REST/HTTP port (0 = disabled)")
     a("--host", "--grpc_host", default="0.0.0.0", dest="host")
-    a("--model_name", default="default")
-    a("--model_base_path", default="")
+    # MODEL_NAME / MODEL_BASE_PATH env: the tensorflow/serving container convention
+    # (serving/rundocker.sh:15 passes -e MODEL_NAME=resnet)
+    a("--model_name", default=os.environ.get("MODEL_NAME", "default"))
+    a("--model_base_path", default=os.environ.get("MODEL_BASE_PATH", ""))
     a("--model_config_file", default="", help="text-format ModelServerConfig (supersedes --model_name/base_path)")
     a("--model_config_file_poll_wait_seconds", type=float, default=0.0)
     a("--file_system_poll_wait_seconds", type=float, default=1.0)
@@ -59,6 +61,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--batch_timeout_us", type=int, default=2000, help="fast-path batch window when batching params unset")
     a("--max_batch_size", type=int, default=32, help="fast-path GPU batch (HIP-graph bucket) limit")
     a("--hip_graphs", type=_bool, nargs="?", const=True, default=True)
+    a("--dtype", default="bf16", choices=["bf16", "fp32"],
+      help="GPU compute dtype: bf16 = fused MFMA kernels; fp32 = unfused fp32 reference path")
     a("--log_level", default="INFO")
     return ap
 
@@ -107,7 +111,8 @@ def make_server(args, rank: int = 0, world: int = 1):
         weight_source = ReplicatedWeightSource(store, device=dev)
         replicas = ReplicaControl(store, rank, world)
     sopts = ServableOptions(device=device, hip_graphs=args.hip_graphs, warmup=args.enable_model_warmup,
-                            max_batch_size=args.max_batch_size)
+                            max_batch_size=args.max_batch_size, compute_dtype=args.dtype,
+                            fuse=False if args.dtype == "fp32" else None)
     opts = ServerOptions(port=args.port, rest_api_port=args.rest_api_port, host=args.host,
                          model_name=args.model_name, model_base_path=args.model_base_path,
                          model_config_file=args.model_config_file,

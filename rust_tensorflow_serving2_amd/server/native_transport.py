@@ -104,6 +104,8 @@ class NativeTransport:
         self.srv = _C.Http2Server(host, port, io_threads, max_message)
         self.port = self.srv.port
         self.metrics = metrics if metrics is not None else getattr(core, "metrics", None)
+        if self.metrics is not None:
+            self.metrics.collectors.append(self.prometheus_lines)
         self.fast_path = fast_path
         self.batch_timeout_us = batch_timeout_us
         if batcher is not None:
@@ -225,6 +227,29 @@ class NativeTransport:
             self.core.manager.listeners.remove(self._on_state)
         except ValueError:
             pass
+
+    def prometheus_lines(self):
+        """C++ front-end and fast-path counters in Prometheus text form."""
+        st = self.srv.stats()
+        out = ["# TYPE tfserve_native_requests_total counter"]
+        for k in ("requests", "fast_path", "slow_path", "streamed", "expired", "responses", "errors"):
+            out.append(f'tfserve_native_requests_total{{kind="{k}"}} {st.get(k, 0)}')
+        out.append("# TYPE tfserve_native_bytes_total counter")
+        out.append(f'tfserve_native_bytes_total{{dir="in"}} {st.get("bytes_in", 0)}')
+        out.append(f'tfserve_native_bytes_total{{dir="out"}} {st.get("bytes_out", 0)}')
+        out.append("# TYPE tfserve_native_io_seconds_total counter")
+        for k in ("recv", "h2", "dispatch", "send"):
+            out.append(f'tfserve_native_io_seconds_total{{phase="{k}"}} {st.get("io_s_" + k, 0.0):.6f}')
+        out.append("# TYPE tfserve_fastpath_batches_total counter")
+        with self._eps_lock:
+            eps = list(self._eps.items())
+        for (name, ver, sig), ep in eps:
+            es = self.srv.endpoint_stats(ep.id)
+            lab = f'model="{name}",version="{ver}",signature="{sig}"'
+            out.append(f"tfserve_fastpath_batches_total{{{lab}}} {es.get('batches', 0)}")
+            out.append(f"tfserve_fastpath_rows_total{{{lab}}} {es.get('rows', 0)}")
+            out.append(f"tfserve_fastpath_rejected_total{{{lab}}} {es.get('rejected', 0)}")
+        return out
 
     def stats(self) -> dict:
         d = dict(self.srv.stats())

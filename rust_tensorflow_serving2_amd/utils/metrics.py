@@ -50,6 +50,8 @@ class Metrics:
         self.queue_depth: Dict[str, int] = defaultdict(int)
         self.device_busy_s: Dict[str, float] = defaultdict(float)
         self.started = time.time()
+        # extra exporters (e.g. the native transport's C++ counters): () -> [lines]
+        self.collectors: List = []
 
     def observe_rpc(self, method: str, code: int, seconds: float):
         with self._lock:
@@ -90,6 +92,12 @@ class Metrics:
             for k, v in sorted(self.device_busy_s.items()):
                 out.append(f'tfserve_device_busy_seconds{{device="{k}"}} {v:.6f}')
             out.append(f"tfserve_uptime_seconds {time.time() - self.started:.3f}")
+            collectors = list(self.collectors)
+        for c in collectors:
+            try:
+                out.extend(c())
+            except Exception:       # a broken exporter must not break /metrics
+                pass
         return "\n".join(out) + "\n"
 
 

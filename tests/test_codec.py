@@ -119,3 +119,47 @@ def test_crc32c_vectors():
     assert native.crc32c_unmask(m) == 0x12345678
     # incremental == one-shot
     assert native.crc32c(b"6789", native.crc32c(b"12345")) == native.crc32c(b"123456789")
+
+
+_TYPED = {  # dtype -> (numpy dtype, TensorProto repeated field)
+    T.DT_FLOAT: (np.float32, "float_val"), T.DT_DOUBLE: (np.float64, "double_val"),
+    T.DT_INT32: (np.int32, "int_val"), T.DT_INT64: (np.int64, "int64_val"),
+    T.DT_BOOL: (np.bool_, "bool_val"), T.DT_UINT8: (np.uint8, "int_val"), T.DT_INT16: (np.int16, "int_val"),
+}
+
+
+@settings(max_examples=80, deadline=None)
+@given(st.sampled_from(sorted(_TYPED)), st.lists(st.integers(1, 5), min_size=0, max_size=3),
+       st.sampled_from(["typed", "content", "fill"]), st.integers(0, 10_000))
+def test_upb_built_tensors_decode_natively(dt, shape, form, seed):
+    """TensorProtos assembled by upb setters (independent of the native encoder)
+    decode to the same array with the C++ codec, including TF's fill rule."""
+    npdt, field = _TYPED[dt]
+    rng = np.random.default_rng(seed)
+    n = int(np.prod(shape)) if shape else 1
+    if np.dtype(npdt).kind == "f":
+        vals = rng.standard_normal(n).astype(npdt)
+    elif npdt == np.bool_:
+        vals = rng.integers(0, 2, n).astype(npdt)
+    else:
+        info = np.iinfo(npdt)
+        vals = rng.integers(max(info.min, -2**31), min(info.max, 2**31 - 1), n, dtype=np.int64).astype(npdt)
+    t = tf.TensorProto(dtype=dt)
+    for d in shape:
+        t.tensor_shape.dim.add(size=d)
+    if form == "content":
+        t.tensor_content = vals.tobytes()
+        want = vals.reshape(shape)
+    elif form == "fill" and n > 1:
+        getattr(t, field).append(vals[0].item())      # one value repeats to fill the shape
+        want = np.full(shape, vals[0], dtype=npdt)
+    else:
+        getattr(t, field).extend(v.item() for v in vals)
+        want = vals.reshape(shape)
+    req = serving.PredictRequest()
+    req.model_spec.name = "m"
+    req.inputs["x"].CopyFrom(t)
+    _spec, arrays, _f, dts = native.decode_predict_request(req.SerializeToString())
+    got = arrays["x"]
+    assert dts["x"] == dt and got.dtype == np.dtype(npdt) and got.shape == tuple(shape)
+    np.testing.assert_array_equal(got, want)

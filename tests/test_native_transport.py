@@ -76,3 +76,23 @@ def test_native_loadgen_large_bodies(nserver):
                        64, 16, 3, 2, 120.0)
     assert r["ok"] == 64 and r["errors"] == 0, r["first_error"]
     assert r["bytes_sent"] >= 64 * min(len(b) for b in bodies)
+
+
+def test_native_counters_in_prometheus_metrics(hpt_path):
+    import json
+    import urllib.request
+    srv = ModelServer(ServerOptions(port=0, rest_api_port=-1, host="127.0.0.1", model_name="hpt",
+                                    model_base_path=hpt_path, transport="native",
+                                    file_system_poll_wait_seconds=0)).start()
+    try:
+        body = native.encode_predict_request(native.spec_tuple("hpt", None, None, ""),
+                                             {"x": np.ones((1, 1), np.float32)})
+        r = _C.run_loadgen("127.0.0.1", srv.port, "/tensorflow.serving.PredictionService/Predict", [body],
+                           20, 4, 1, 1, 60.0)
+        assert r["ok"] == 20
+        with urllib.request.urlopen(f"http://127.0.0.1:{srv.rest_port}/monitoring/prometheus/metrics") as f:
+            text = f.read().decode()
+        assert 'tfserve_native_requests_total{kind="requests"} 20' in text
+        assert 'tfserve_native_io_seconds_total{phase="recv"}' in text
+    finally:
+        srv.stop()
