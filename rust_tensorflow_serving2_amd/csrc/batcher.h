@@ -98,6 +98,11 @@ class Endpoint {
   void set_server(Server* srv) { srv_ = srv; }
   // GPU worker side.
   int acquire(int slot, int timeout_ms);
+  // when the slot's current batch opened (first row reserved); for tracing
+  Clock::time_point slot_opened(int slot) {
+    std::lock_guard<std::mutex> g(mu_);
+    return slots_[slot].first;
+  }
   void complete(int slot, Server& srv);
   void fail(int slot, Server& srv, int code, const std::string& msg);
   // Responds UNAVAILABLE to requests still queued when `srv` is given.

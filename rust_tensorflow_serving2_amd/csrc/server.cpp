@@ -71,6 +71,37 @@ HipRt& hip_rt() {
   return rt;
 }
 
+// ---------------------------------------------------------------- batch trace
+// One record per GPU batch served by a native lane (--trace_dir): times are
+// microseconds on the steady clock: batch opened (first row reserved),
+// acquired by the lane (batch closed), H2D+graph+D2H issued, GPU done, responses posted.
+struct BatchTrace {
+  int endpoint, slot, rows;
+  double opened_us, acquired_us, issued_us, done_us, posted_us;
+};
+struct TraceBuf {
+  std::mutex mu;
+  std::vector<BatchTrace> recs;
+  std::atomic<bool> on{false};
+  void add(const BatchTrace& t) {
+    std::lock_guard<std::mutex> g(mu);
+    if (recs.size() < 1000000) recs.push_back(t);
+  }
+  std::vector<BatchTrace> drain() {
+    std::lock_guard<std::mutex> g(mu);
+    std::vector<BatchTrace> out;
+    out.swap(recs);
+    return out;
+  }
+};
+TraceBuf& trace_buf() {
+  static TraceBuf t;
+  return t;
+}
+double us_of(Clock::time_point t) {
+  return std::chrono::duration<double, std::micro>(t.time_since_epoch()).count();
+}
+
 struct LaneCopy {
   uintptr_t dst, src;
   size_t row_bytes;
@@ -153,6 +184,8 @@ class NativeLane {
         ep_->fail(slot_, *srv_, 13 /*INTERNAL*/, "injected fault (TFSERVE_FAULT)");
         continue;
       }
+      const bool tracing = trace_buf().on.load(std::memory_order_relaxed);
+      const auto t_acq = Clock::now();
       const int e = done ? batch(rt, done, n) : -1;
       if (e != 0) {
         errors++;
@@ -161,7 +194,12 @@ class NativeLane {
         continue;
       }
       batches++;
+      const auto t_done = Clock::now();
+      const auto t_open = tracing ? ep_->slot_opened(slot_) : t_done;
       ep_->complete(slot_, *srv_);
+      if (tracing)
+        trace_buf().add({ep_->id, slot_, n, us_of(t_open), us_of(t_acq), us_of(t_acq), us_of(t_done),
+                         us_of(Clock::now())});
     }
     if (done) rt.event_destroy(done);
   }
@@ -344,6 +382,15 @@ void register_server(py::module_& m) {
                                                        reinterpret_cast<void*>(stream), std::move(bs)));
         return true;
       }, py::arg("endpoint"), py::arg("slot"), py::arg("device"), py::arg("stream"), py::arg("buckets"))
+      .def("set_tracing", [](PyServer&, bool on) { trace_buf().on = on; })
+      .def("drain_trace", [](PyServer&) {
+        py::list out;
+        for (auto& t : trace_buf().drain())
+          out.append(py::make_tuple(t.endpoint, t.slot, t.rows, t.opened_us, t.acquired_us, t.issued_us,
+                                    t.done_us, t.posted_us));
+        return out;
+      })
+      .def_static("now_us", []() { return us_of(Clock::now()); })
       .def("native_lane_stats", [](PyServer& s) {
         std::lock_guard<std::mutex> g(s.lmu);
         py::list out;

@@ -63,6 +63,7 @@ def build_parser() -> argparse.ArgumentParser:
     a("--hip_graphs", type=_bool, nargs="?", const=True, default=True)
     a("--dtype", default="bf16", choices=["bf16", "fp32"],
       help="GPU compute dtype: bf16 = fused MFMA kernels; fp32 = unfused fp32 reference path")
+    a("--trace_dir", default="", help="write request/batch timelines (JSON lines) here")
     a("--log_level", default="INFO")
     return ap
 
@@ -120,7 +121,8 @@ def make_server(args, rank: int = 0, world: int = 1):
                          device=device, enable_batching=args.enable_batching, batching_parameters=batching,
                          transport=args.transport, file_system_poll_wait_seconds=args.file_system_poll_wait_seconds,
                          io_threads=args.io_threads, batch_timeout_us=args.batch_timeout_us, servable=sopts,
-                         monitoring=args.monitoring, weight_source=weight_source, replicas=replicas)
+                         monitoring=args.monitoring, weight_source=weight_source, replicas=replicas,
+                         trace_dir=args.trace_dir)
     return ModelServer(opts)
 
 

@@ -57,6 +57,7 @@ class ServingCore:
         self.request_logger = request_logger
         self.metrics = metrics
         self.replicas = None          # parallel.replicas.ReplicaControl when serving N GPU replicas
+        self.tracer = None            # utils.tracing.Tracer (--trace_dir)
         self.handlers = {
             METHOD_PREFIX_P + "Predict": self.predict,
             METHOD_PREFIX_P + "Classify": self.classify,
@@ -83,8 +84,12 @@ class ServingCore:
             log.exception("internal error in %s", method)
             raise E.internal(f"{type(e).__name__}: {e}") from None
         finally:
+            t1 = time.perf_counter()
             if self.metrics is not None:
-                self.metrics.observe_rpc(method, code, time.perf_counter() - t0)
+                self.metrics.observe_rpc(method, code, t1 - t0)
+            if self.tracer is not None:
+                end = time.monotonic() * 1e6
+                self.tracer.rpc(method, end - (t1 - t0) * 1e6, end, code)
 
     # ------------------------------------------------------------------ helpers
     def _resolve(self, name, version, label):

@@ -45,6 +45,7 @@ class ServerOptions:
     replicas: Optional[object] = None              # parallel.replicas.ReplicaControl (N replicas)
     model_config_file: str = ""                    # text-format ModelServerConfig
     model_config_file_poll_wait_seconds: float = 0.0
+    trace_dir: str = ""                            # request/batch timeline (utils/tracing.py)
 
 
 class ModelServer:
@@ -64,6 +65,11 @@ class ModelServer:
         self.manager = ModelManager(self._load, poll_wait_seconds=opts.file_system_poll_wait_seconds)
         self.core = ServingCore(self.manager, self.batcher, self.request_logs, self.metrics)
         self.core.replicas = opts.replicas
+        self.tracer = None
+        if opts.trace_dir:
+            from ..utils.tracing import Tracer
+            self.tracer = Tracer(opts.trace_dir)
+            self.core.tracer = self.tracer
         self.transports = []
         self._cfg_thread = None
         self._cfg_stop = threading.Event()
@@ -144,6 +150,8 @@ class ModelServer:
             t = GrpcTransport(self.core, self.opts.port, self.opts.host, self.opts.grpc_workers)
         self.transports.append(t.start())
         self.port = t.port
+        if self.tracer is not None and self.opts.transport == "native":
+            self.tracer.attach_native(t.srv)
         if self.opts.rest_api_port:
             from .rest import RestTransport
             # 0 = disabled (TF Serving convention); -1 = any free port (tests)
@@ -166,3 +174,5 @@ class ModelServer:
             self.batcher.stop()
         self.manager.stop()
         self.request_logs.close()
+        if self.tracer is not None:
+            self.tracer.close()

@@ -96,3 +96,22 @@ def test_native_counters_in_prometheus_metrics(hpt_path):
         assert 'tfserve_native_io_seconds_total{phase="recv"}' in text
     finally:
         srv.stop()
+
+
+def test_trace_dir_records_rpcs(hpt_path, tmp_path):
+    from rust_tensorflow_serving2_amd.utils import tracing
+    srv = ModelServer(ServerOptions(port=0, host="127.0.0.1", model_name="hpt", model_base_path=hpt_path,
+                                    transport="native", file_system_poll_wait_seconds=0,
+                                    trace_dir=str(tmp_path / "tr"))).start()
+    try:
+        body = native.encode_predict_request(native.spec_tuple("hpt", None, None, ""),
+                                             {"x": np.ones((1, 1), np.float32)})
+        assert _C.run_loadgen("127.0.0.1", srv.port, "/tensorflow.serving.PredictionService/Predict", [body],
+                              10, 2, 1, 1, 60.0)["ok"] == 10
+    finally:
+        srv.stop()
+    recs = tracing.load(srv.tracer.path)
+    rpcs = [r for r in recs if r["type"] == "rpc"]
+    assert len(rpcs) == 10 and all(r["end_us"] >= r["start_us"] for r in rpcs)
+    chrome = tracing.to_chrome(recs)
+    assert len(chrome["traceEvents"]) == 10
