@@ -31,12 +31,19 @@ constexpr int BK = 64;
 constexpr int kThreads = 256;
 constexpr int kGroupM = 8;
 
-template <int BM, int BN, int AMODE, int NSTAGE, int WAVES_M = 2>
+template <int BM, int BN, int AMODE, int NSTAGE, int WAVES_M = 2, int BKT = 64>
 struct IGemm {
   // 4 waves in a WAVES_M x (4 / WAVES_M) grid, each owning a WM x WN sub-tile
   static constexpr int WAVES_N = 4 / WAVES_M;
   static constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   static constexpr int TM = WM / 16, TN = WN / 16;
+  // direct-to-LDS modes may use deeper k-tiles (BK = 128 / 256): fewer barriers
+  // and DMA round trips per MFMA; register-staged modes keep BK = 64
+  static constexpr bool GL_ = (AMODE == kADense || AMODE == kAIm2col);
+  static constexpr int BK = GL_ ? BKT : 64;
+  static constexpr int CPR = BK / 8;                    // 16-B chunks per LDS row
+  static constexpr int RPI = 64 / CPR;                  // rows per wave DMA instruction (1 KB)
+  static constexpr int SWZ = CPR >= 16 ? 15 : 7;        // XOR swizzle mask (conflict-free b128 reads)
   static constexpr int A_CHUNKS = BM * BK / 8 / kThreads;
   static constexpr int B_CHUNKS = BN * BK / 8 / kThreads;
   // direct-to-LDS operand modes run a STAGES-deep DMA ring (S-1 k-tiles in
@@ -52,7 +59,6 @@ struct IGemm {
   static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
 };
 
-__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
 
 // s_waitcnt vmcnt(N) only (expcnt/lgkmcnt left at their maxima; gfx9 encoding:
 // vmcnt[3:0] + vmcnt[5:4] at bits 15:14, expcnt 6:4, lgkmcnt 11:8).
@@ -173,9 +179,11 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
   }
 }
 
-template <int BM, int BN, int AMODE, int NSTAGE, int WAVES_M>
+template <int BM, int BN, int AMODE, int NSTAGE, int WAVES_M, int BKT>
 __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
-  using G = IGemm<BM, BN, AMODE, NSTAGE, WAVES_M>;
+  using G = IGemm<BM, BN, AMODE, NSTAGE, WAVES_M, BKT>;
+  constexpr int BK = G::BK;
+  auto swz = [](int row, int ch) { return ch ^ (row & G::SWZ); };
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int S = G::STAGES;
   uint16_t* As = reinterpret_cast<uint16_t*>(smem);
@@ -202,7 +210,10 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   // lane l fills row (l>>3) at 16-B slot (l&7); the XOR swizzle is applied to
   // the *source* chunk instead (logical chunk = slot ^ (row & 7)).
   constexpr bool GL = G::GL;
-  const int gl_chunk = (lane & 7) ^ ((lane >> 3) & 7);
+  // DMA lane -> (row within the 1-KB instruction block, 16-B slot); the slot
+  // holds logical chunk slot ^ (row & SWZ) (the swizzle applied at the source)
+  const int gl_row = lane / G::CPR, gl_slot = lane % G::CPR;
+  auto gl_chunk_of = [&](int i) { return gl_slot ^ ((i * G::RPI + gl_row) & G::SWZ); };
 
   // ---- per-thread A row descriptors
   int a_off[G::A_CHUNKS];     // element offset of the row's base (dense: m*lda; im2col: image base)
@@ -210,7 +221,7 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   bool a_ok[G::A_CHUNKS];
 #pragma unroll
   for (int i = 0; i < G::A_CHUNKS; ++i) {
-    const int rloc = GL ? wid * (BM / 4) + i * 8 + (lane >> 3) : row_base + 32 * i;
+    const int rloc = GL ? wid * (BM / 4) + i * G::RPI + gl_row : row_base + 32 * i;
     const int m = m0 + rloc;
     a_ok[i] = m < M;
     const int mm = a_ok[i] ? m : 0;
@@ -336,36 +347,94 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
       const_cast<uint16_t*>(p.b), 0, int(p.b_bytes), 0x00020000);
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+  // Per-lane byte offsets precomputed once: every k-tile then costs one add per
+  // 16-B chunk (out-of-range rows keep a kOOB base, which stays out of range
+  // after adding k offsets).  K tails are checked only in the last k-tile.
+  uint32_t b_base[G::B_CHUNKS];
+  int b_kofs[G::B_CHUNKS];        // this lane's k offset within a k-tile (elements)
+#pragma unroll
+  for (int i = 0; i < G::B_CHUNKS; ++i) {
+    const int n = n0 + wid * (BN / 4) + i * G::RPI + gl_row;
+    b_kofs[i] = gl_chunk_of(i) * 8;
+    b_base[i] = n < N ? (uint32_t(n) * uint32_t(p.ldb) + uint32_t(b_kofs[i])) * 2u : kOOB;
+  }
+  uint32_t a_base[G::A_CHUNKS];   // dense: row base; im2col: pixel base (tap 0, channel chunk)
+  int a_kofs[G::A_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < G::A_CHUNKS; ++i) {
+    a_kofs[i] = gl_chunk_of(i) * 8;
+    if (AMODE == kADense)
+      a_base[i] = a_ok[i] ? uint32_t(a_off[i] + a_kofs[i]) * 2u : kOOB;
+    else if (AMODE == kAIm2col)
+      a_base[i] = uint32_t(a_off[i] + (a_hi[i] * p.W + a_wi[i]) * p.C + a_kofs[i]) * 2u;
+    else
+      a_base[i] = 0;
+  }
+  // im2col with C % 64 == 0: one k-tile = one tap's 64-channel slice.  The
+  // tap walk (channel offset, kw, kh) advances incrementally in scalar regs.
+  const bool c_tiles = (AMODE == kAIm2col) && (p.C % BK == 0);
+  int t_ci = 0, t_kw = 0, t_kh = 0;
+  auto tap_seek = [&](int kt) {       // (only for the first stage / split-K start)
+    const int kc0 = kt * BK;
+    const int tap = kc0 / p.C;
+    t_ci = kc0 - tap * p.C;
+    t_kh = tap / p.KW;
+    t_kw = tap - t_kh * p.KW;
+  };
+
   auto gstage = [&](int buf, int kt, bool live) {
-    const int kc = live ? kt * BK + gl_chunk * 8 : K + p.ldb;   // !live: every offset out of range
+    const int kc0 = kt * BK;                 // wave-uniform
     uint16_t* as = As + buf * BM * BK;
     uint16_t* bs = Bs + buf * BN * BK;
     if (AMODE == kADense) {
+      const bool tail = kc0 + BK > K;
 #pragma unroll
       for (int i = 0; i < G::A_CHUNKS; ++i) {
-        const uint32_t off = (a_ok[i] && kc < K) ? uint32_t(a_off[i] + kc) * 2u : kOOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(as + (wid * (BM / 4) + i * 8) * BK), 16, off,
-                                                 0, 0, 0);
+        uint32_t off = a_base[i] + uint32_t(kc0) * 2u;
+        if (!live || (tail && kc0 + a_kofs[i] >= K)) off = kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(as + (wid * (BM / 4) + i * G::RPI) * BK), 16,
+                                                 off, 0, 0, 0);
+      }
+    } else if (c_tiles) {
+      const int tap_off = (t_kh * p.W + t_kw) * p.C + t_ci;
+      const bool kok = live && kc0 < K;
+#pragma unroll
+      for (int i = 0; i < G::A_CHUNKS; ++i) {
+        const bool ok = kok && a_ok[i] && (unsigned)(a_hi[i] + t_kh) < (unsigned)p.H &&
+                        (unsigned)(a_wi[i] + t_kw) < (unsigned)p.W;
+        const uint32_t off = ok ? a_base[i] + uint32_t(tap_off) * 2u : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(as + (wid * (BM / 4) + i * G::RPI) * BK), 16,
+                                                 off, 0, 0, 0);
+      }
+      // advance to the next k-tile's tap slice
+      t_ci += BK;
+      if (t_ci == p.C) {
+        t_ci = 0;
+        if (++t_kw == p.KW) {
+          t_kw = 0;
+          ++t_kh;
+        }
       }
     } else {
-      const int tap = kc / p.C;
-      const int ci = kc - tap * p.C;
-      const int kh = tap / p.KW, kw = tap - kh * p.KW;
-      const bool kok = kc < K;
 #pragma unroll
       for (int i = 0; i < G::A_CHUNKS; ++i) {
+        const int kc = kc0 + a_kofs[i];
+        const int tap = kc / p.C;
+        const int ci = kc - tap * p.C;
+        const int kh = tap / p.KW, kw = tap - kh * p.KW;
         const int hi = a_hi[i] + kh, wi = a_wi[i] + kw;
-        const bool ok = kok && a_ok[i] && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+        const bool ok = live && kc < K && a_ok[i] && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
         const uint32_t off = ok ? uint32_t(a_off[i] + (hi * p.W + wi) * p.C + ci) * 2u : kOOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(as + (wid * (BM / 4) + i * 8) * BK), 16, off,
-                                                 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(as + (wid * (BM / 4) + i * G::RPI) * BK), 16,
+                                                 off, 0, 0, 0);
       }
     }
+    const bool btail = kc0 + BK > p.ldb;
 #pragma unroll
     for (int i = 0; i < G::B_CHUNKS; ++i) {
-      const int n = n0 + wid * (BN / 4) + i * 8 + (lane >> 3);
-      const uint32_t off = (n < N && kc < p.ldb) ? (uint32_t(n) * uint32_t(p.ldb) + uint32_t(kc)) * 2u : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_ptr_t)(bs + (wid * (BN / 4) + i * 8) * BK), 16, off,
+      uint32_t off = b_base[i] + uint32_t(kc0) * 2u;
+      if (!live || (btail && kc0 + b_kofs[i] >= p.ldb)) off = kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_ptr_t)(bs + (wid * (BN / 4) + i * G::RPI) * BK), 16, off,
                                                0, 0, 0);
     }
   };
@@ -401,7 +470,7 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
 
   auto mfma_tile = [&](const uint16_t* as, const uint16_t* bs) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < BK / 32; ++kk) {
       const int ch = kk * 4 + fq;
       bf16x8 af[G::TM], bfr[G::TN];
 #pragma unroll
@@ -423,6 +492,7 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   };
 
   if (GL) {
+    if (c_tiles) tap_seek(kt0);
     // prologue: S-1 k-tiles in flight
 #pragma unroll
     for (int st = 0; st < S - 1; ++st) gstage(st, kt0 + st, st < nk);
@@ -497,20 +567,25 @@ __global__ __launch_bounds__(kThreads, 2) void igemm_kernel(IGemmArgs p) {
   }
 }
 
-template <int BM, int BN, int AMODE, int NSTAGE, int WAVES_M = 2>
-hipError_t launch_cfg(const IGemmArgs& a, hipStream_t s) {
-  using G = IGemm<BM, BN, AMODE, NSTAGE, WAVES_M>;
+template <int BM, int BN, int AMODE, int NSTAGE, int WAVES_M = 2, int BKT = 64>
+hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
+  using G = IGemm<BM, BN, AMODE, NSTAGE, WAVES_M, BKT>;
+  IGemmArgs a = a0;
+  if (a.splits > 1) {   // split ranges in units of this config's k-tile
+    const int nk = (a.K + G::BK - 1) / G::BK;
+    a.kt_per_split = (nk + a.splits - 1) / a.splits;
+  }
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<BM, BN, AMODE, NSTAGE, WAVES_M>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<BM, BN, AMODE, NSTAGE, WAVES_M, BKT>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int splits = a.splits > 1 ? a.splits : 1;
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE, NSTAGE, WAVES_M>), dim3(tiles, splits), dim3(kThreads), G::LDS, s, a);
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE, NSTAGE, WAVES_M, BKT>), dim3(tiles, splits), dim3(kThreads), G::LDS, s, a);
   return hipGetLastError();
 }
 
@@ -550,11 +625,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(IGemmArgs p) {
 // LDS): the tuner picks per layer (K=64 1x1 convs want occupancy, long-K
 // small-grid layers want depth).  Register-staged operand modes ignore the
 // depth (always 2).
-constexpr int kCfgBM[kNumIGemmConfigs] = {128, 128, 64, 64, 128, 64, 128, 64, 64, 256, 128, 256};
-constexpr int kCfgBN[kNumIGemmConfigs] = {128, 64, 128, 64, 128, 64, 64, 128, 256, 64, 256, 128};
-constexpr int kCfgST[kNumIGemmConfigs] = {2, 2, 2, 2, 3, 4, 3, 3, 2, 2, 2, 2};
+constexpr int kCfgBM[kNumIGemmConfigs] = {128, 128, 64, 64, 128, 64, 128, 64, 64, 256, 128, 256, 64, 64, 64, 128, 128};
+constexpr int kCfgBN[kNumIGemmConfigs] = {128, 64, 128, 64, 128, 64, 64, 128, 256, 64, 256, 128, 64, 64, 128, 64, 128};
+constexpr int kCfgST[kNumIGemmConfigs] = {2, 2, 2, 2, 3, 4, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+constexpr int kCfgBK[kNumIGemmConfigs] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 128, 256, 128, 128, 128};
 // register-staged operand modes only instantiate configs 0-3
-constexpr int kCfgBase[kNumIGemmConfigs] = {0, 1, 2, 3, 0, 3, 1, 2, 2, 1, 0, 0};
+constexpr int kCfgBase[kNumIGemmConfigs] = {0, 1, 2, 3, 0, 3, 1, 2, 2, 1, 0, 0, 3, 3, 2, 1, 0};
 
 template <int AMODE>
 hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
@@ -578,6 +654,12 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
       case 9: return launch_cfg<256, 64, AMODE, 2, 4>(a, s);
       case 10: return launch_cfg<128, 256, AMODE, 2, 2>(a, s);
       case 11: return launch_cfg<256, 128, AMODE, 2, 4>(a, s);
+      // deep k-tiles: 2-4x the MFMA work per barrier / DMA round trip
+      case 12: return launch_cfg<64, 64, AMODE, 2, 2, 128>(a, s);
+      case 13: return launch_cfg<64, 64, AMODE, 2, 2, 256>(a, s);
+      case 14: return launch_cfg<64, 128, AMODE, 2, 2, 128>(a, s);
+      case 15: return launch_cfg<128, 64, AMODE, 2, 2, 128>(a, s);
+      case 16: return launch_cfg<128, 128, AMODE, 2, 2, 128>(a, s);
       default: break;
     }
   }
@@ -589,6 +671,7 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
 int igemm_config_bm(int cfg) { return kCfgBM[cfg]; }
 int igemm_config_bn(int cfg) { return kCfgBN[cfg]; }
 int igemm_config_stages(int cfg) { return kCfgST[cfg]; }
+int igemm_config_bk(int cfg) { return kCfgBK[cfg]; }
 
 hipError_t igemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) {
   switch (a_mode) {

@@ -52,10 +52,12 @@ hipError_t splitk_reduce_launch(const IGemmArgs& args, hipStream_t stream);
 // Tile configs (BM x BN, DMA ring depth): 0..3 = 128x128, 128x64, 64x128,
 // 64x64 double-buffered; 4 = 128x128x3, 5 = 64x64x4, 6 = 128x64x3, 7 = 64x128x3;
 // wide: 8 = 64x256, 9 = 256x64, 10 = 128x256, 11 = 256x128 (dense / im2col only)
-constexpr int kNumIGemmConfigs = 12;
+// deep k-tiles (BK): 12 = 64x64/128, 13 = 64x64/256, 14 = 64x128/128, 15 = 128x64/128, 16 = 128x128/128
+constexpr int kNumIGemmConfigs = 17;
 int igemm_config_bm(int cfg);
 int igemm_config_bn(int cfg);
 int igemm_config_stages(int cfg);
+int igemm_config_bk(int cfg);
 hipError_t igemm_launch(const IGemmArgs& args, int a_mode, int cfg, hipStream_t stream);
 
 // NHWC bf16 max-pool (TF SAME/VALID padding given explicitly).

@@ -70,8 +70,10 @@ def heuristic_config(M: int, N: int) -> int:
 # (kernels/igemm.hip kCfgST) and only apply to dense / im2col operands.
 TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64),
          4: (128, 128), 5: (64, 64), 6: (128, 64), 7: (64, 128),
-         8: (64, 256), 9: (256, 64), 10: (128, 256), 11: (256, 128)}
-DMA_ONLY = {4, 5, 6, 7, 8, 9, 10, 11}
+         8: (64, 256), 9: (256, 64), 10: (128, 256), 11: (256, 128),
+         12: (64, 64), 13: (64, 64), 14: (64, 128), 15: (128, 64), 16: (128, 128)}
+DMA_ONLY = {4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16}
+TILE_BK = {12: 128, 13: 256, 14: 128, 15: 128, 16: 128}     # k-tile depth (default 64)
 
 
 def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
@@ -93,6 +95,8 @@ def candidates(M: int, N: int, K: int, dma: bool = True):
     for cfg, (bm, bn) in TILES.items():
         if cfg in DMA_ONLY and (not dma or (cfg in (4, 5, 6, 7) and nk < 3)):
             continue
+        if K < 2 * TILE_BK.get(cfg, 64) and cfg in TILE_BK:
+            continue   # deep k-tiles only pay off with several of them
         if bn > 64 and N <= bn // 2 or bm > 64 and M <= bm // 2:
             continue   # mostly-empty tiles
         tiles = -(-M // bm) * -(-N // bn)

@@ -57,7 +57,7 @@ CONV_SHAPES = [
 
 
 @pytest.mark.parametrize("shape", CONV_SHAPES)
-@pytest.mark.parametrize("cfg,splits", [(0, 1), (1, 1), (2, 1), (3, 1), (3, 3), (1, 4), (4, 1), (5, 2), (6, 1),
+@pytest.mark.parametrize("cfg,splits", [(0, 1), (1, 1), (2, 1), (3, 1), (3, 3), (1, 4), (4, 1), (5, 2), (6, 1), (12, 1), (13, 1), (14, 2), (15, 1), (16, 1),
                                         (7, 1), (8, 1), (9, 1), (10, 1), (11, 2)])
 def test_conv_matches_fp32(shape, cfg, splits):
     n, h, w, cin, cout, k, s, pads = shape
@@ -123,7 +123,7 @@ def test_asymmetric_identity_gemm():
 @pytest.mark.parametrize("m,n,k,act", [(32, 1001, 2048, "none"), (256, 2304, 768, "none"),
                                        (256, 3072, 768, "gelu_tanh"), (256, 768, 3072, "none"),
                                        (8, 768, 768, "tanh"), (100, 72, 40, "gelu_erf")])
-@pytest.mark.parametrize("cfg,splits", [(0, 1), (3, 1), (3, 8), (1, 3), (5, 1), (8, 1), (9, 2), (10, 1), (11, 1)])
+@pytest.mark.parametrize("cfg,splits", [(0, 1), (3, 1), (3, 8), (1, 3), (5, 1), (8, 1), (9, 2), (10, 1), (11, 1), (12, 1), (13, 3), (16, 1)])
 def test_linear_matches_fp32(m, n, k, act, cfg, splits):
     x = rnd(m, k, seed=7).to(BF)
     w = rnd(n, k, scale=1 / math.sqrt(k), seed=8).to(BF)
