@@ -89,11 +89,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # TFSERVE_BENCH_BACKEND=gloo rehearses the multi-rank flow with fewer GPUs than
+    # ranks (ranks share devices round-robin); the real run uses nccl (= RCCL)
+    backend = os.environ.get("TFSERVE_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     logging.basicConfig(level=logging.WARNING)
 
     from rust_tensorflow_serving2_amd import _C, native
@@ -119,7 +127,8 @@ def main():
     weight_source = None
     if world > 1:
         from rust_tensorflow_serving2_amd.parallel.weights import ReplicatedWeightSource
-        weight_source = ReplicatedWeightSource(dist.distributed_c10d._get_default_store(), device=device)
+        weight_source = ReplicatedWeightSource(dist.distributed_c10d._get_default_store(),
+                                               device=device if backend == "nccl" else torch.device("cpu"))
     sopts = ServableOptions(device=str(device), max_batch_size=args.batch,
                             allowed_batch_sizes=tuple(sorted({1, 2, 4, 8, 16, args.batch})))
     port = (args.port + local) if args.port else 0
@@ -196,7 +205,8 @@ def main():
                 cpu_report[k.replace("io_s_", "io_us_per_req_")] = round((io1[k] - io0[k]) / nreq * 1e6, 1)
     lat = np.asarray(r["latency_us"], dtype=np.float64)
     mine = torch.tensor([elapsed, float(r["ok"]), float(r["errors"]), np.percentile(lat, 50) if lat.size else 0,
-                         np.percentile(lat, 99) if lat.size else 0], dtype=torch.float64, device=device)
+                         np.percentile(lat, 99) if lat.size else 0], dtype=torch.float64,
+                        device=device if backend == "nccl" else "cpu")
     if world > 1:
         allv = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allv, mine)
