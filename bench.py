@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--transport", default="native", choices=["native", "grpc"])
     ap.add_argument("--batch-timeout-us", type=int, default=2000)
+    ap.add_argument("--distinct-requests", type=int, default=64, help="distinct pre-encoded request bodies")
+    ap.add_argument("--lanes", type=int, default=4, help="GPU lanes (batch slots in flight) per rank")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "tiny", "bert-base"],
                     help="resnet50 = headline config; bert-base = BASELINE config 3 (seq 128); "
                          "tiny = same 224x224x3 payload, negligible compute (transport ceiling probe)")
@@ -129,7 +131,7 @@ def main():
         from rust_tensorflow_serving2_amd.parallel.weights import ReplicatedWeightSource
         weight_source = ReplicatedWeightSource(dist.distributed_c10d._get_default_store(),
                                                device=device if backend == "nccl" else torch.device("cpu"))
-    sopts = ServableOptions(device=str(device), max_batch_size=args.batch,
+    sopts = ServableOptions(device=str(device), max_batch_size=args.batch, lanes=args.lanes,
                             allowed_batch_sizes=tuple(sorted({1, 2, 4, 8, 16, args.batch})))
     port = (args.port + local) if args.port else 0
     server = ModelServer(ServerOptions(port=port, host="127.0.0.1", model_name=model_name, model_base_path=base,
@@ -152,7 +154,7 @@ def main():
     rng = np.random.default_rng(1234 + rank)
     bodies = []
     spec = native.spec_tuple(model_name, None, None, "serving_default")
-    for _ in range(64):
+    for _ in range(args.distinct_requests):
         rb = args.request_batch
         if args.model == "bert-base":
             S = args.seq_len

@@ -73,7 +73,8 @@ struct StreamRes {
   bool write(const uint8_t* p, size_t n) {
     writers.fetch_add(1);
     const bool live = state.load() == 0;
-    if (live) std::memcpy(dst + got, p, n);
+    // p == dst + got: the IO thread already recv()'d these bytes into the row
+    if (live && p != dst + got) std::memcpy(dst + got, p, n);
     writers.fetch_sub(1);
     got += n;
     return live;
@@ -88,6 +89,7 @@ struct ServerStats {
   std::atomic<uint64_t> streamed{0};   // fast-path requests whose payload went socket -> slot directly
   std::atomic<uint64_t> expired{0};    // answered DEADLINE_EXCEEDED (client grpc-timeout passed)
   std::atomic<uint64_t> bytes_in{0}, bytes_out{0};
+  std::atomic<uint64_t> direct_bytes{0};   // payload bytes recv()'d straight into batch rows
   // IO-thread time split (ns): recv() syscalls, nghttp2 frame processing incl.
   // body assembly, fast-path dispatch (decode + batch-slot copy), send()
   std::atomic<uint64_t> ns_recv{0}, ns_h2{0}, ns_dispatch{0}, ns_send{0};

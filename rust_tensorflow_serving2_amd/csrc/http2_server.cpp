@@ -103,7 +103,56 @@ struct Outgoing {
 
 }  // namespace
 
+// Frame boundaries of the inbound byte stream, tracked alongside nghttp2 so a
+// recv() can stop exactly where a DATA payload starts: the payload of a
+// streaming Predict then goes from the socket straight into its pinned batch
+// row (one kernel->user copy, no pass through the read buffer).
+struct FrameTrack {
+  size_t preface = 24;      // client connection preface still to pass
+  uint8_t hdr[9];
+  int hlen = 0;             // bytes of a partial frame header seen
+  bool in_payload = false;
+  size_t remain = 0;        // payload bytes left in the current frame
+  uint8_t type = 0, flags = 0;
+  int32_t sid = 0;
+  void advance(const uint8_t* p, size_t n) {
+    while (n) {
+      size_t k;
+      if (preface) {
+        k = std::min(preface, n);
+        preface -= k;
+      } else if (in_payload) {
+        k = std::min(remain, n);
+        remain -= k;
+        in_payload = remain != 0;
+      } else {
+        k = std::min<size_t>(size_t(9 - hlen), n);
+        memcpy(hdr + hlen, p, k);
+        hlen += int(k);
+        if (hlen == 9) {
+          hlen = 0;
+          remain = (size_t(hdr[0]) << 16) | (size_t(hdr[1]) << 8) | hdr[2];
+          type = hdr[3];
+          flags = hdr[4];
+          sid = int32_t(((uint32_t(hdr[5]) << 24) | (uint32_t(hdr[6]) << 16) | (uint32_t(hdr[7]) << 8) | hdr[8]) &
+                        0x7fffffffu);
+          in_payload = remain != 0;
+        }
+      }
+      p += k;
+      n -= k;
+    }
+  }
+  // bytes up to the end of the next frame header
+  size_t to_next_payload() const {
+    if (preface) return preface + 9;
+    if (in_payload) return remain + 9;
+    return size_t(9 - hlen);
+  }
+};
+
 struct Conn {
+  FrameTrack ft;
   int fd = -1;
   uint64_t id = 0;
   nghttp2_session* sess = nullptr;
@@ -513,21 +562,60 @@ class IoThread {
     return true;
   }
 
+  // Where the next recv() lands: normally the read buffer, but only up to the
+  // end of the next frame header; inside the DATA payload of a streaming
+  // Predict, straight into the request's batch row (the row's `writers` count
+  // is held across the syscall so the batcher cannot hand the row to another
+  // request meanwhile).
+  uint8_t* recv_target(Conn* c, size_t& want, StreamRes*& held) {
+    FrameTrack& ft = c->ft;
+    held = nullptr;
+    if (ft.in_payload && ft.type == 0 /*DATA*/ && !(ft.flags & 0x8 /*PADDED*/)) {
+      auto it = c->streams.find(ft.sid);
+      Stream* st = it == c->streams.end() ? nullptr : it->second.get();
+      if (st && st->mode == kStreamMode && !st->overflow && st->sres) {
+        StreamRes* r = st->sres.get();
+        const size_t room = r->len - r->got;
+        if (room) {
+          r->writers.fetch_add(1);
+          if (r->state.load() == 0) {
+            held = r;
+            want = std::min(ft.remain, room);
+            srv_->stats.direct_bytes += want;
+            return r->dst + r->got;
+          }
+          r->writers.fetch_sub(1);
+        }
+      }
+      if (st && st->mode == kProbeMode) {   // the Predict header: probe, then stream the rest
+        want = std::min(ft.remain, kProbeMax);
+        return rbuf_.data();
+      }
+    }
+    want = std::min(rbuf_.size(), ft.to_next_payload());
+    return rbuf_.data();
+  }
+
   void on_readable(Conn* c) {
     for (;;) {
       const auto t0 = Clock::now();
-      ssize_t n = recv(c->fd, rbuf_.data(), rbuf_.size(), 0);
+      size_t want = 0;
+      StreamRes* held = nullptr;
+      uint8_t* buf = recv_target(c, want, held);
+      ssize_t n = recv(c->fd, buf, want, 0);
+      if (held) held->writers.fetch_sub(1);
       const auto t1 = Clock::now();
       srv_->stats.ns_recv += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
       if (n > 0) {
-        ssize_t r = nghttp2_session_mem_recv(c->sess, rbuf_.data(), size_t(n));
+        c->ft.advance(buf, size_t(n));
+        ssize_t r = nghttp2_session_mem_recv(c->sess, buf, size_t(n));
         srv_->stats.ns_h2 +=
             uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t1).count());
         if (r < 0) {
           c->dead = true;
           return;
         }
-        if (size_t(n) < rbuf_.size()) break;
+        if (size_t(n) < want) break;   // socket drained
         continue;
       }
       if (n == 0) {

@@ -311,7 +311,7 @@ void register_server(py::module_& m) {
         py::dict d;
         d["connections"] = st.connections.load(); d["requests"] = st.requests.load();
         d["fast_path"] = st.fast_path.load(); d["slow_path"] = st.slow_path.load();
-        d["streamed"] = st.streamed.load(); d["expired"] = st.expired.load();
+        d["streamed"] = st.streamed.load(); d["expired"] = st.expired.load(); d["direct_bytes"] = st.direct_bytes.load();
         d["responses"] = st.responses.load(); d["errors"] = st.errors.load();
         d["bytes_in"] = st.bytes_in.load(); d["bytes_out"] = st.bytes_out.load();
         d["io_s_recv"] = st.ns_recv.load() * 1e-9; d["io_s_h2"] = st.ns_h2.load() * 1e-9;

@@ -85,6 +85,7 @@ def test_streamed_and_buffered_requests(fast_server):
         np.testing.assert_allclose(_y(_call(srv.port, body)), x * 2 + 1, rtol=1e-6)
     st = srv.stats()
     assert st["fast_path"] == 8 and st["streamed"] == 6
+    assert st["direct_bytes"] > 0     # payload bytes recv()'d straight into batch rows
     # concurrently: requests that find every slot busy queue (buffered) behind the stream
     with cf.ThreadPoolExecutor(12) as ex:
         outs = list(ex.map(lambda r: _call(srv.port, r[1]), reqs[8:]))
@@ -102,7 +103,7 @@ def test_streamed_loadgen_mixed_sizes(fast_server):
                                             {"x": np.full((n, ROW), n, np.float32)}) for n in (1, 2, 5, 8)]
     r = _C.run_loadgen("127.0.0.1", srv.port, PREDICT, bodies, 200, 32, 4, 2, 120.0)
     assert r["ok"] == 200 and r["errors"] == 0, r["first_error"]
-    assert srv.stats()["streamed"] > 0
+    assert srv.stats()["streamed"] > 0 and srv.stats()["direct_bytes"] > 0
 
 
 def test_wrong_shape_falls_back(fast_server):
