@@ -45,6 +45,22 @@ def _digest(paths, flags) -> str:
     return h.hexdigest()
 
 
+def _local_includes(src, headers):
+    """Headers of ``headers`` that ``src`` includes (transitively, via #include "...")."""
+    by_name = {os.path.basename(h): h for h in headers}
+    seen, todo = set(), [src]
+    while todo:
+        with open(todo.pop()) as f:
+            for line in f:
+                line = line.strip()
+                if line.startswith("#include \""):
+                    h = by_name.get(line.split('"')[1])
+                    if h and h not in seen:
+                        seen.add(h)
+                        todo.append(h)
+    return sorted(seen)
+
+
 def _compile_all(compiler, sources, headers, flags, tag, jobs):
     os.makedirs(BUILD, exist_ok=True)
     objs, todo = [], []
@@ -52,7 +68,7 @@ def _compile_all(compiler, sources, headers, flags, tag, jobs):
         base = os.path.splitext(os.path.basename(src))[0]
         obj = os.path.join(BUILD, f"{tag}_{base}.o")
         stamp = obj + ".sha1"
-        d = _digest([src] + headers, flags + [compiler])
+        d = _digest([src] + _local_includes(src, headers), flags + [compiler])
         if not (os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == d):
             todo.append((src, obj, stamp, d))
         objs.append(obj)

@@ -182,8 +182,9 @@ class FusedConv:
         key = ("conv", tuple(x.shape), x.dtype, self.cout, self.kh, self.kw, self.sh, res is not None)
         K = self.kh * 32 if self.c4 else self.kh * self.kw * self.cin
         dma = not self.c4 and self.cin % 8 == 0      # bf16 dense/im2col operands -> DMA-ring configs apply
+        aligned = dma and self.cin % 64 == 0     # pipelined cgemm kernel applies
         cfg, splits = tuned_config(key, M, self.cout, lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s), K,
-                                   dma)
+                                   dma, aligned)
         return [H.conv2d(*args, cfg=cfg, out=out, splits=splits)]
 
 
@@ -222,7 +223,7 @@ class FusedMatMul:
         out = torch.empty(shape, device=x.device, dtype=torch.float32 if self.out_f32 else BF16)
         key = ("mm", M, self.n, self.k, res is not None, self.out_f32)
         run = lambda c, s: H.linear(x, self.w, self.b, res, ACT[self.act], c, self.out_f32, 1.0, out, s)  # noqa
-        cfg, splits = tuned_config(key, M, self.n, run, self.k)
+        cfg, splits = tuned_config(key, M, self.n, run, self.k, True, self.k % 64 == 0)
         return [run(cfg, splits)]
 
 

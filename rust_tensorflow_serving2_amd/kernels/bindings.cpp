@@ -9,6 +9,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include "launch.h"
+#include "cgemm.h"
 
 namespace {
 
@@ -23,15 +24,27 @@ void check(hipError_t e, const char* what) {
 }
 
 // Launch with optional split-K: raw fp32 slabs in a workspace + reduce/epilogue kernel.
+// cfg < kNumIGemmConfigs: igemm.hip (any operand mode); cfg in [kCGemmCfgBase,
+// kCGemmCfgBase + kNumCGemmConfigs): the pipelined cgemm.hip kernel (64-aligned operands).
+bool is_cgemm_cfg(int64_t cfg) {
+  return cfg >= tfsk::kCGemmCfgBase && cfg < tfsk::kCGemmCfgBase + tfsk::kNumCGemmConfigs;
+}
+
+hipError_t launch_any(const tfsk::IGemmArgs& a, int a_mode, int64_t cfg, hipStream_t st) {
+  return is_cgemm_cfg(cfg) ? tfsk::cgemm_launch(a, a_mode, int(cfg), st) : tfsk::igemm_launch(a, a_mode, int(cfg), st);
+}
+
 void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, const Tensor& like, hipStream_t st) {
-  TORCH_CHECK(cfg >= 0 && cfg < tfsk::kNumIGemmConfigs, "bad tile config");
+  TORCH_CHECK((cfg >= 0 && cfg < tfsk::kNumIGemmConfigs) || is_cgemm_cfg(cfg), "bad tile config ", cfg);
+  TORCH_CHECK(!is_cgemm_cfg(cfg) || tfsk::cgemm_supported(a, a_mode),
+              "tile config ", cfg, " needs 64-aligned operands (K % 64, C % 64)");
   const int nk = (a.K + 63) / 64;
   if (splits > nk) splits = nk;
   if (splits <= 1) {
     a.splits = 1;
     a.kt_per_split = nk;
     a.ws = nullptr;
-    TORCH_CHECK(tfsk::igemm_launch(a, a_mode, cfg, st) == hipSuccess, "igemm launch failed");
+    TORCH_CHECK(launch_any(a, a_mode, cfg, st) == hipSuccess, "conv/GEMM launch failed");
     return;
   }
   const int per = (nk + splits - 1) / splits;
@@ -40,7 +53,7 @@ void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, cons
   a.splits = int(splits);
   a.kt_per_split = per;
   a.ws = ws.data_ptr<float>();
-  TORCH_CHECK(tfsk::igemm_launch(a, a_mode, cfg, st) == hipSuccess, "igemm(split-K) launch failed");
+  TORCH_CHECK(launch_any(a, a_mode, cfg, st) == hipSuccess, "conv/GEMM (split-K) launch failed");
   TORCH_CHECK(tfsk::splitk_reduce_launch(a, st) == hipSuccess, "split-K reduce launch failed");
 }
 
@@ -318,5 +331,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention", &attention, py::arg("qkv"), py::arg("mask_bias"), py::arg("heads"), py::arg("scale"),
         py::arg("out") = py::none(), py::arg("mask_bstride") = 0, py::arg("mask_qstride") = 0);
   m.def("num_configs", []() { return tfsk::kNumIGemmConfigs; });
-  m.def("config_tile", [](int cfg) { return std::make_pair(tfsk::igemm_config_bm(cfg), tfsk::igemm_config_bn(cfg)); });
+  m.def("cgemm_configs", []() {
+    std::vector<int> v;
+    for (int c = 0; c < tfsk::kNumCGemmConfigs; ++c) v.push_back(tfsk::kCGemmCfgBase + c);
+    return v;
+  });
+  m.def("config_tile", [](int cfg) {
+    if (is_cgemm_cfg(cfg)) return std::make_pair(tfsk::cgemm_config_bm(cfg), tfsk::cgemm_config_bn(cfg));
+    return std::make_pair(tfsk::igemm_config_bm(cfg), tfsk::igemm_config_bn(cfg));
+  });
 }

@@ -1,0 +1,461 @@
+// Pipelined MFMA conv / GEMM for MI355X (gfx950): bf16 operands, fp32 accumulate.
+//
+// C[M][N] = epilogue( A[M][K] * B[N][K]^T ), the same contract as igemm.hip, for
+// the 64-aligned cases that make up almost all of ResNet-50 / BERT:
+//   A dense row-major (K % 64 == 0), or the implicit im2col of an NHWC tensor
+//   with C % 64 == 0, so one 64-deep k-tile is exactly one filter tap x 64
+//   channels;  B = weights [Cout][ldb].
+//
+// Why a second kernel: rocprofv3 PMC of igemm on the ResNet 3x3 layers showed
+// ~90 SALU+VALU instructions per 16 MFMAs and a vmcnt(0) drain every k-tile
+// (SQ_ACTIVE_INST_ANY 44 %, SQ_WAIT_ANY 41 %, MFMA busy 11-16 % of wave
+// cycles).  This kernel is built so the steady-state k-tile costs little more
+// than its MFMAs:
+//   * S-deep ring of direct-to-LDS DMAs (buffer_load ... lds): the wait before
+//     tile t is a counted vmcnt((S-2) * pieces) — never a drain — followed by a
+//     bare s_barrier;
+//   * every per-lane DMA offset is precomputed once (voffset) and the k-tile
+//     advance is a wave-uniform scalar (soffset): no VALU address math per tile;
+//   * im2col padding = one precomputed tap-validity bit mask per DMA row
+//     (3 VALU per piece), the tap walk runs in SGPRs, and the buffer
+//     descriptor is rebased by the top/left padding so every in-image offset is
+//     non-negative; invalid taps read through an out-of-range voffset (zeros);
+//   * the loop is unrolled by S, so ring slots and all LDS fragment offsets
+//     are compile-time immediates;
+//   * LDS rows are 128 B with 16-B chunks XOR-swizzled by (row & 7): the DMA
+//     lane writes slot l&7 of row l>>3 from source chunk (l&7)^(l>>3), the
+//     ds_read_b128 fragment reads undo it (conflict-free);
+//   * 4 or 8 waves per workgroup, each owning a WM x WN sub-tile of
+//     v_mfma_f32_16x16x32_bf16 accumulators; bijective XCD-aware tile remap +
+//     GROUP_M ordering; epilogue staged through LDS as fp32 for coalesced
+//     16-B bias/residual/activation/store row chunks (residual prefetched into
+//     registers before the K loop).
+#include "common.h"
+#include "cgemm.h"
+
+namespace tfsk {
+
+namespace {
+
+constexpr int KT = 64;                    // k-tile depth (bf16) = 128 B per LDS row
+constexpr uint32_t kOOB = 0x80000000u;    // voffset beyond any buffer: the DMA returns zeros
+constexpr int kGroupM = 8;
+
+template <int BM, int BN, int WGM, int WGN, int S>
+struct CG {
+  static constexpr int NW = WGM * WGN, NT = 64 * NW;
+  static constexpr int WM = BM / WGM, WN = BN / WGN;
+  static constexpr int TM = WM / 16, TN = WN / 16;
+  static constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW);   // 1-KB DMA pieces per wave per stage
+  static constexpr int PPW = APW + BPW;
+  static constexpr int A_ST = BM * KT, B_ST = BN * KT;            // elements per ring slot
+  static constexpr int LDS_MAIN = S * (A_ST + B_ST) * 2;
+  static constexpr int CS_LD = BN + 4;
+  static constexpr int LDS_EPI = BM * CS_LD * 4;
+  static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+  static_assert(APW >= 1 && BPW >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "DMA piece split");
+  static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
+  static_assert(S >= 2 && (S - 2) * PPW < 64, "ring depth / vmcnt range");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt at their maxima; gfx9 encoding).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// Barrier without the vmcnt(0) drain __syncthreads' fence would add.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// ---- epilogue over the fp32 tile staged in LDS (8-column row chunks, NT threads)
+template <int BM, int BN, int NT>
+struct Epi {
+  static constexpr int CPR = BN / 8;
+  static constexpr int ITERS = BM * CPR / NT;
+  static constexpr int PRE = ITERS <= 8 ? ITERS : 0;
+  static_assert(NT % CPR == 0 && (BM * CPR) % NT == 0, "epilogue chunk mapping");
+};
+
+// chunk `it` of thread `tid`: row-major 8-column chunks, NT apart (a thread's column is fixed)
+template <int BN, int NT>
+__device__ __forceinline__ void epi_rowcol(int tid, int it, int& row, int& col) {
+  constexpr int CPR = BN / 8;
+  const int c = tid + it * NT;
+  row = c / CPR;
+  col = (c - row * CPR) * 8;
+}
+
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void prefetch_residual(const IGemmArgs& p, int m0, int n0, int tid,
+                                                  uint4 (&rpre)[Epi<BM, BN, NT>::PRE > 0 ? Epi<BM, BN, NT>::PRE : 1]) {
+  using E = Epi<BM, BN, NT>;
+  if (E::PRE == 0 || !p.residual || p.splits > 1 || (p.N % 8) || (p.ldr % 8)) return;
+#pragma unroll
+  for (int it = 0; it < E::PRE; ++it) {
+    int row, col;
+    epi_rowcol<BN, NT>(tid, it, row, col);
+    const int m = m0 + row, n = n0 + col;
+    rpre[it] = (m < p.M && n + 8 <= p.N) ? *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n)
+                                          : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int BM, int BN, int NT, int CS_LD, int ACT>
+__device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* Cs, int m0, int n0, int tid,
+                                              const uint4 (&rpre)[Epi<BM, BN, NT>::PRE > 0 ? Epi<BM, BN, NT>::PRE : 1]) {
+  using E = Epi<BM, BN, NT>;
+  const int M = p.M, N = p.N;
+  const float alpha = p.alpha;
+  const bool vec_ok = (N % 8 == 0) && (p.ldc % 8 == 0) && (!p.residual || p.ldr % 8 == 0);
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  {
+    int row0, col0;
+    epi_rowcol<BN, NT>(tid, 0, row0, col0);
+    const int n = n0 + col0;
+    if (p.bias && vec_ok && n + 8 <= N) {
+      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+      const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+      bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+      bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < E::ITERS; ++it) {
+    int row, col;
+    epi_rowcol<BN, NT>(tid, it, row, col);
+    const int m = m0 + row, n = n0 + col;
+    if (m >= M || n >= N) continue;
+    const float4 lo = *reinterpret_cast<const float4*>(Cs + row * CS_LD + col);
+    const float4 hi = *reinterpret_cast<const float4*>(Cs + row * CS_LD + col + 4);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    if (vec_ok && n + 8 <= N) {
+      float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (p.residual) {
+        const uint4 rr = E::PRE > 0 ? rpre[E::PRE > 0 ? it : 0]
+                                    : *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
+        const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          rv[2 * e] = bf16_to_f32(uint16_t(w[e] & 0xffff));
+          rv[2 * e + 1] = bf16_to_f32(uint16_t(w[e] >> 16));
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = act_fn<ACT>(v[e] * alpha + bv[e] + rv[e]);
+      if (p.out_f32) {
+        float* o = static_cast<float*>(p.out) + size_t(m) * p.ldc + n;
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        uint16_t b[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) b[e] = f32_to_bf16(v[e]);
+        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.out) + size_t(m) * p.ldc + n) =
+            make_uint4(b[0] | (uint32_t(b[1]) << 16), b[2] | (uint32_t(b[3]) << 16),
+                       b[4] | (uint32_t(b[5]) << 16), b[6] | (uint32_t(b[7]) << 16));
+      }
+    } else {
+      for (int e = 0; e < 8 && n + e < N; ++e) {
+        float x = v[e] * alpha;
+        if (p.bias) x += p.bias[n + e];
+        if (p.residual) x += bf16_to_f32(p.residual[size_t(m) * p.ldr + n + e]);
+        x = act_fn<ACT>(x);
+        if (p.out_f32) static_cast<float*>(p.out)[size_t(m) * p.ldc + n + e] = x;
+        else static_cast<uint16_t*>(p.out)[size_t(m) * p.ldc + n + e] = f32_to_bf16(x);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int S, bool IM2COL>
+__global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
+  using G = CG<BM, BN, WGM, WGN, S>;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  char* const smem = reinterpret_cast<char*>(smem_raw);
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+  // ---- tile of this workgroup (XCD remap + GROUP_M ordering)
+  const int M = p.M, N = p.N;
+  const int nbm = (M + BM - 1) / BM, nbn = (N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = kGroupM * nbn;
+  const int first_m = (wg / per_group) * kGroupM;
+  const int gsz = min(nbm - first_m, kGroupM);
+  const int bm = first_m + (wg % per_group) % gsz;
+  const int bn = (wg % per_group) / gsz;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WGN, wn = wid % WGN;
+  // DMA lane -> row (lane >> 3) of its 8-row piece, LDS slot (lane & 7) holding
+  // logical chunk (lane & 7) ^ (row & 7)
+  const int prow = lane >> 3;
+  const uint32_t kc = uint32_t(((lane & 7) ^ prow) * 8);
+
+  // ---- buffer descriptors (wave-uniform: kernel args only)
+  const char* abase = static_cast<const char*>(p.a);
+  uint32_t arec = uint32_t(p.a_bytes);
+  if (IM2COL) {
+    const uint32_t shift = uint32_t((p.PT * p.W + p.PL) * p.C) * 2u;
+    abase -= shift;
+    arec += shift;
+  }
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(abase), 0, int(arec), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.b), 0, int(p.b_bytes), 0x00020000);
+
+  // ---- per-lane DMA offsets (computed once)
+  uint32_t a_off[G::APW], a_msk[G::APW];
+#pragma unroll
+  for (int j = 0; j < G::APW; ++j) {
+    const int m = m0 + (wid * G::APW + j) * 8 + prow;
+    const bool ok = m < M;
+    a_msk[j] = 0;
+    if (!IM2COL) {
+      a_off[j] = ok ? (uint32_t(m) * uint32_t(p.lda) + kc) * 2u : kOOB;
+    } else {
+      const int mm = ok ? m : 0;
+      const int hw = p.Ho * p.Wo;
+      const int n = mm / hw, r = mm - n * hw;
+      const int ho = r / p.Wo, wo = r - ho * p.Wo;
+      const int hb = ho * p.SH, wb = wo * p.SW;          // tap (0,0) in padded coordinates
+      a_off[j] = (uint32_t((n * p.H + hb) * p.W + wb) * uint32_t(p.C) + kc) * 2u;
+      uint32_t msk = 0;
+      const int hi0 = hb - p.PT, wi0 = wb - p.PL;
+      int t = 0;
+      for (int kh = 0; kh < p.KH; ++kh)
+        for (int kw = 0; kw < p.KW; ++kw, ++t)
+          if (ok && (unsigned)(hi0 + kh) < (unsigned)p.H && (unsigned)(wi0 + kw) < (unsigned)p.W) msk |= 1u << t;
+      a_msk[j] = msk;
+    }
+  }
+  uint32_t b_off[G::BPW];
+#pragma unroll
+  for (int j = 0; j < G::BPW; ++j) {
+    const int n = n0 + (wid * G::BPW + j) * 8 + prow;
+    b_off[j] = n < N ? (uint32_t(n) * uint32_t(p.ldb) + kc) * 2u : kOOB;
+  }
+
+  // ---- k range of this workgroup (split-K: blockIdx.y selects a slice)
+  const int nk_all = p.K / KT;
+  int kt0 = 0, nk = nk_all;
+  if (p.splits > 1) {
+    kt0 = blockIdx.y * p.kt_per_split;
+    nk = min(nk_all - kt0, p.kt_per_split);
+  }
+
+  // ---- scalar producer walk: k element offset; im2col tap (kh, kw) + channel offset
+  int w_k = kt0 * KT;
+  int w_ci = 0, w_kh = 0, w_kw = 0, w_tap = 0;
+  if (IM2COL) {
+    w_tap = w_k / p.C;
+    w_ci = w_k - w_tap * p.C;
+    w_kh = w_tap / p.KW;
+    w_kw = w_tap - w_kh * p.KW;
+  }
+
+  auto issue = [&](int slot) {
+    const uint32_t a_soff = IM2COL ? uint32_t((w_kh * p.W + w_kw) * p.C + w_ci) * 2u : uint32_t(w_k) * 2u;
+    const uint32_t b_soff = uint32_t(w_k) * 2u;
+#pragma unroll
+    for (int j = 0; j < G::APW; ++j) {
+      uint32_t v = a_off[j];
+      if (IM2COL) v = ((a_msk[j] >> w_tap) & 1u) ? v : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsA, (lds_ptr_t)(smem + (slot * G::A_ST + (wid * G::APW + j) * 512) * 2), 16, v, a_soff, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < G::BPW; ++j) {
+      // (a named local, not b_off[j] in the call: with the array element as a
+      // builtin argument hipcc's host pass silently drops the kernel stub)
+      const uint32_t v = b_off[j];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsB, (lds_ptr_t)(smem + (S * G::A_ST + slot * G::B_ST + (wid * G::BPW + j) * 512) * 2), 16, v, b_soff,
+          0, 0);
+    }
+    w_k += KT;
+    if (IM2COL) {
+      w_ci += KT;
+      if (w_ci == p.C) {
+        w_ci = 0;
+        ++w_tap;
+        if (++w_kw == p.KW) {
+          w_kw = 0;
+          ++w_kh;
+        }
+      }
+    }
+  };
+
+  // ---- consumer: per-lane fragment byte offsets within a ring slot (k-subtile 0 / 1)
+  const int fr = lane & 15, fq = lane >> 4;
+  const uint32_t ra0 = uint32_t(((wm * G::WM + fr) * KT + ((fq ^ (fr & 7)) * 8)) * 2);
+  const uint32_t ra1 = uint32_t(((wm * G::WM + fr) * KT + (((4 + fq) ^ (fr & 7)) * 8)) * 2);
+  const uint32_t rb0 = uint32_t(((wn * G::WN + fr) * KT + ((fq ^ (fr & 7)) * 8)) * 2);
+  const uint32_t rb1 = uint32_t(((wn * G::WN + fr) * KT + (((4 + fq) ^ (fr & 7)) * 8)) * 2);
+
+  f32x4 acc[G::TM][G::TN];
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int slot) {
+    const char* sa = smem + slot * G::A_ST * 2;
+    const char* sb = smem + (S * G::A_ST + slot * G::B_ST) * 2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[G::TM], bfr[G::TN];
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(sa + (kk ? ra1 : ra0) + i * 16 * KT * 2);
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sb + (kk ? rb1 : rb0) + j * 16 * KT * 2);
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  uint4 rpre[Epi<BM, BN, G::NT>::PRE > 0 ? Epi<BM, BN, G::NT>::PRE : 1];
+  prefetch_residual<BM, BN, G::NT>(p, m0, n0, tid, rpre);
+
+  // ---- prologue: S-1 k-tiles in flight
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s);
+
+  // ---- main loop, unrolled by the ring depth (slot indices are immediates)
+  for (int kt = 0; kt < nk; kt += S) {
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      const int t = kt + u;
+      if (t < nk) {
+        // tile t landed (this wave's DMAs) once only the younger groups remain
+        if (t + S - 2 < nk) wait_vmcnt<(S - 2) * G::PPW>();
+        else wait_vmcnt<0>();
+        // ... and every wave's (and every wave is done reading slot (t-1) % S)
+        lds_barrier();
+        if (t + S - 1 < nk) issue((u + S - 1) % S);
+        compute(u);
+      }
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  // ---- epilogue: stage the fp32 tile in LDS, then coalesced row chunks
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * G::WM + i * 16 + fq * 4 + r) * G::CS_LD + wn * G::WN + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+
+  if (p.splits > 1) {
+    // raw (alpha-scaled) partial slab of this K slice; splitk_reduce applies the epilogue
+    const float alpha = p.alpha;
+    float* ws = p.ws + size_t(blockIdx.y) * M * N;
+    constexpr int CPR = BN / 8;
+    const bool v4 = (N % 4 == 0);
+    for (int c = tid; c < BM * CPR; c += G::NT) {
+      const int row = c / CPR, col = (c - row * CPR) * 8;
+      const int m = m0 + row, n = n0 + col;
+      if (m >= M || n >= N) continue;
+      const float* src = Cs + row * G::CS_LD + col;
+      float* dst = ws + size_t(m) * N + n;
+      if (v4 && n + 8 <= N) {
+        float4 a = *reinterpret_cast<const float4*>(src);
+        float4 b = *reinterpret_cast<const float4*>(src + 4);
+        a.x *= alpha; a.y *= alpha; a.z *= alpha; a.w *= alpha;
+        b.x *= alpha; b.y *= alpha; b.z *= alpha; b.w *= alpha;
+        *reinterpret_cast<float4*>(dst) = a;
+        *reinterpret_cast<float4*>(dst + 4) = b;
+      } else {
+        for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = src[e] * alpha;
+      }
+    }
+    return;
+  }
+  switch (p.act) {
+    case kActRelu: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActRelu>(p, Cs, m0, n0, tid, rpre); break;
+    case kActGeluTanh: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActGeluTanh>(p, Cs, m0, n0, tid, rpre); break;
+    case kActGeluErf: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActGeluErf>(p, Cs, m0, n0, tid, rpre); break;
+    case kActTanh: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActTanh>(p, Cs, m0, n0, tid, rpre); break;
+    default: epilogue_rows<BM, BN, G::NT, G::CS_LD, 0>(p, Cs, m0, n0, tid, rpre); break;
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int S, bool IM2COL>
+hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
+  using G = CG<BM, BN, WGM, WGN, S>;
+  IGemmArgs a = a0;
+  const int nk = a.K / KT;
+  const int splits = a.splits > 1 ? a.splits : 1;
+  if (splits > 1) a.kt_per_split = (nk + splits - 1) / splits;
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  if (tiles == 0) return hipSuccess;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, IM2COL>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((cgemm_kernel<BM, BN, WGM, WGN, S, IM2COL>), dim3(tiles, splits), dim3(G::NT), G::LDS, s, a);
+  return hipGetLastError();
+}
+
+// Config table (tile BM x BN, wave grid, ring depth).  LDS per workgroup =
+// S * (BM + BN) * 128 B (or the fp32 epilogue tile if larger).
+constexpr int kBM[kNumCGemmConfigs] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256};
+constexpr int kBN[kNumCGemmConfigs] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64};
+
+template <bool IM2COL>
+hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
+  switch (cfg) {
+    case 0: return launch_cfg<128, 128, 2, 2, 3, IM2COL>(a, s);   // 96 KB, wave 64x64
+    case 1: return launch_cfg<128, 128, 2, 2, 2, IM2COL>(a, s);   // 64 KB (2 WG/CU)
+    case 2: return launch_cfg<64, 128, 2, 2, 4, IM2COL>(a, s);    // 96 KB, wave 32x64
+    case 3: return launch_cfg<128, 64, 2, 2, 4, IM2COL>(a, s);    // 96 KB, wave 64x32
+    case 4: return launch_cfg<64, 64, 2, 2, 4, IM2COL>(a, s);     // 64 KB, wave 32x32
+    case 5: return launch_cfg<256, 128, 4, 2, 3, IM2COL>(a, s);   // 144 KB, 8 waves of 64x64
+    case 6: return launch_cfg<128, 256, 2, 4, 3, IM2COL>(a, s);   // 144 KB, 8 waves of 64x64
+    case 7: return launch_cfg<128, 128, 2, 4, 4, IM2COL>(a, s);   // 128 KB, 8 waves of 64x32
+    case 8: return launch_cfg<64, 256, 1, 4, 3, IM2COL>(a, s);    // 120 KB, wave 64x64
+    case 9: return launch_cfg<256, 64, 4, 1, 3, IM2COL>(a, s);    // 120 KB, wave 64x64
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+bool cgemm_supported(const IGemmArgs& a, int a_mode) {
+  if (a.K <= 0 || a.K % KT || a.ldb % 8 || a.ldb < a.K) return false;
+  if (a_mode == kADense) return a.lda % 8 == 0 && a.lda >= a.K;
+  if (a_mode == kAIm2col)
+    return a.C % KT == 0 && a.KH * a.KW <= 32 && a.K == a.KH * a.KW * a.C &&
+           a.a_bytes + int64_t(a.PT * a.W + a.PL) * a.C * 2 < 0x7ffffff0LL;
+  return false;
+}
+
+int cgemm_config_bm(int cfg) { return kBM[cfg - kCGemmCfgBase]; }
+int cgemm_config_bn(int cfg) { return kBN[cfg - kCGemmCfgBase]; }
+
+hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) {
+  if (cfg < kCGemmCfgBase || cfg >= kCGemmCfgBase + kNumCGemmConfigs || !cgemm_supported(a, a_mode))
+    return hipErrorInvalidValue;
+  cfg -= kCGemmCfgBase;
+  return a_mode == kAIm2col ? launch_mode<true>(a, cfg, s) : launch_mode<false>(a, cfg, s);
+}
+
+}  // namespace tfsk

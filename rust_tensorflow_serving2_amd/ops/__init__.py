@@ -74,6 +74,10 @@ TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64),
          12: (64, 64), 13: (64, 64), 14: (64, 128), 15: (128, 64), 16: (128, 128)}
 DMA_ONLY = {4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16}
 TILE_BK = {12: 128, 13: 256, 14: 128, 15: 128, 16: 128}     # k-tile depth (default 64)
+# pipelined cgemm kernel (kernels/cgemm.hip; 64-aligned operands only): config id -> (BM, BN)
+CGEMM = {32: (128, 128), 33: (128, 128), 34: (64, 128), 35: (128, 64), 36: (64, 64),
+         37: (256, 128), 38: (128, 256), 39: (128, 128), 40: (64, 256), 41: (256, 64)}
+TILES.update(CGEMM)
 
 
 def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
@@ -86,14 +90,17 @@ def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
     return s
 
 
-def candidates(M: int, N: int, K: int, dma: bool = True):
+def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False):
     """(tile config, split-K) pairs worth timing for an M x N x K problem
     (``dma``: the operand mode uses the direct-to-LDS path, so the deeper
-    DMA-ring configs apply)."""
+    DMA-ring configs apply; ``aligned64``: K and the conv channels are
+    multiples of 64, so the pipelined cgemm configs apply)."""
     nk = -(-K // 64)
     out = []
     for cfg, (bm, bn) in TILES.items():
         if cfg in DMA_ONLY and (not dma or (cfg in (4, 5, 6, 7) and nk < 3)):
+            continue
+        if cfg in CGEMM and not (aligned64 and dma and K % 64 == 0):
             continue
         if K < 2 * TILE_BK.get(cfg, 64) and cfg in TILE_BK:
             continue   # deep k-tiles only pay off with several of them
@@ -108,7 +115,7 @@ def candidates(M: int, N: int, K: int, dma: bool = True):
 
 
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
-                 dma: bool = True) -> Tuple[int, int]:
+                 dma: bool = True, aligned64: bool = False) -> Tuple[int, int]:
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
     heuristic is used)."""
@@ -124,7 +131,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
             return hit
         best, best_t = None, float("inf")
         flush = _flush_buffer()
-        for c, s in candidates(M, N, K, dma):
+        for c, s in candidates(M, N, K, dma, aligned64):
             launch(c, s)   # warm (also sets the kernel's LDS attribute)
             t = 0.0
             for _rep in range(3):

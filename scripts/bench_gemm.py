@@ -38,7 +38,7 @@ def conv_case(n, h, w, cin, cout, k, s, pad):
     flop = 2 * M * N * K
     res = {"shape": f"conv {n}x{h}x{w}x{cin} k{k}s{s} -> {cout}", "M": M, "N": N, "K": K}
     best = (1e9, None)
-    for cfg, sp in candidates(M, N, K):
+    for cfg, sp in candidates(M, N, K, True, cin % 64 == 0):
         t = timeit(lambda: hip().conv2d(x, wt, b, None, k, k, s, s, pad, pad, pad, pad, ACT["relu"], cfg,
                                         None, False, sp))
         res[f"c{cfg}s{sp}"] = round(t, 1)
@@ -59,7 +59,7 @@ def gemm_case(m, n, k):
     flop = 2 * m * n * k
     res = {"shape": f"gemm {m}x{n}x{k}", "M": m, "N": n, "K": k}
     best = (1e9, None)
-    for cfg, sp in candidates(m, n, k):
+    for cfg, sp in candidates(m, n, k, True, k % 64 == 0):
         t = timeit(lambda: hip().linear(x, w, b, None, 0, cfg, n % 8 != 0, 1.0, None, sp))
         res[f"c{cfg}s{sp}"] = round(t, 1)
         best = min(best, (t, (cfg, sp)))

@@ -76,6 +76,68 @@ def test_conv_matches_fp32(shape, cfg, splits):
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
 
 
+CGEMM_CFGS = list(range(32, 42))
+CGEMM_CONV_SHAPES = [s for s in CONV_SHAPES if s[3] % 64 == 0] + [
+    (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)),   # tiny image: most taps hit padding at the border rows
+    (1, 15, 13, 64, 192, 3, 2, (0, 1, 1, 1)),  # odd sizes, asymmetric pads, N tail
+]
+
+
+@pytest.mark.parametrize("shape", CGEMM_CONV_SHAPES)
+@pytest.mark.parametrize("cfg", CGEMM_CFGS)
+def test_cgemm_conv_matches_fp32(shape, cfg):
+    """Pipelined cgemm kernel (im2col with C % 64 == 0 and 1x1 dense) vs fp32 conv."""
+    n, h, w, cin, cout, k, s, pads = shape
+    x = rnd(n, h, w, cin, seed=1).to(BF)
+    wt = rnd(k, k, cin, cout, scale=1 / math.sqrt(k * k * cin), seed=2).to(BF).float()
+    b = rnd(cout, scale=0.1, seed=3)
+    ho = (h + pads[0] + pads[1] - k) // s + 1
+    wo = (w + pads[2] + pads[3] - k) // s + 1
+    res = rnd(n, ho, wo, cout, seed=4).to(BF)
+    ref = ref_conv(x, wt, b, s, pads, res, "relu")
+    for splits in (1, 3):
+        y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), k, k, s, s, *pads, act=ACT["relu"],
+                         cfg=cfg, splits=splits)
+        torch.cuda.synchronize()
+        err = (y.float().cpu() - ref).abs().max().item()
+        assert y.shape == (n, ho, wo, cout)
+        assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
+
+
+@pytest.mark.parametrize("m,n,k", [(32, 1001, 2048), (256, 2304, 768), (1000, 768, 3072), (8, 72, 64)])
+@pytest.mark.parametrize("cfg", CGEMM_CFGS)
+def test_cgemm_linear_matches_fp32(m, n, k, cfg):
+    x = rnd(m, k, seed=7).to(BF)
+    w = rnd(n, k, scale=1 / math.sqrt(k), seed=8).to(BF)
+    b = rnd(n, scale=0.1, seed=9)
+    res = rnd(m, n, seed=10).to(BF)
+    out_f32 = n % 8 != 0
+    ref = x.float() @ w.float().t() + b + res.float()
+    for act, fn in (("none", lambda t: t), ("gelu_tanh", lambda t: F.gelu(t, approximate="tanh"))):
+        y = hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), res.to(DEV), ACT[act], cfg, out_f32)
+        err = (y.float().cpu() - fn(ref)).abs().max().item()
+        assert err < 3e-2 * max(1.0, ref.abs().max().item()), (act, err)
+
+
+@pytest.mark.parametrize("cfg", CGEMM_CFGS)
+def test_cgemm_asymmetric_identity(cfg):
+    """A = I, asymmetric B (exact in bf16 / fp32): catches a transposed or
+    swizzle-permuted C tile in every cgemm config."""
+    m, n, k = 256, 256, 128
+    a = torch.eye(m, k).to(BF)
+    bmat = (torch.arange(n * k, dtype=torch.float32).reshape(n, k) % 17 - 8)
+    y = hip().linear(a.to(DEV), bmat.to(BF).to(DEV), None, None, 0, cfg, True)
+    assert torch.equal(y.cpu(), a.float() @ bmat.t())
+
+
+def test_cgemm_rejects_unaligned():
+    """cgemm configs refuse (loudly) operands that are not 64-aligned."""
+    x = torch.zeros(4, 40, device=DEV, dtype=BF)
+    w = torch.zeros(8, 40, device=DEV, dtype=BF)
+    with pytest.raises(RuntimeError, match="64-aligned"):
+        hip().linear(x, w, None, None, 0, 32, False)
+
+
 @pytest.mark.parametrize("k,c,cfg", [(7, 3, 1), (7, 3, 0), (3, 3, 3), (5, 4, 1)])
 def test_stem_conv_fp32_input(k, c, cfg):
     """fp32 request tensor with few channels: the ingest cast is fused into the
