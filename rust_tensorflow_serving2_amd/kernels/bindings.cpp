@@ -223,6 +223,34 @@ Tensor ingest_c4(const Tensor& x, const c10::optional<Tensor>& out) {
   return y;
 }
 
+// Zero-copy ingest: the kernel reads fp32 rows straight out of a *pinned host*
+// tensor (device-accessible; e.g. a lane's request staging buffer) over PCIe,
+// instead of an SDMA copy followed by a device pass.
+void need_pinned_f32(const Tensor& x, const char* name) {
+  TORCH_CHECK(x.device().is_cpu() && x.is_pinned(), name, " must be a pinned host tensor");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous(), name, " must be contiguous float32");
+}
+
+void ingest_c4_from_host(const Tensor& x, const Tensor& out) {
+  need_pinned_f32(x, "x");
+  need(out, at::kBFloat16, "out");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) >= 1 && x.size(3) <= 4, "ingest_c4_from_host: x must be NHWC with C <= 4");
+  const int64_t pixels = x.numel() / x.size(3);
+  TORCH_CHECK(out.numel() == pixels * 4, "ingest_c4_from_host: out must hold pixels x 4 channels");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
+  check(tfsk::ingest_c4_launch(x.data_ptr<float>(), bf16p_mut(out), pixels, int(x.size(3)), cur_stream(out)),
+        "ingest_c4_from_host");
+}
+
+void cast_bf16_from_host(const Tensor& x, const Tensor& out) {
+  need_pinned_f32(x, "x");
+  need(out, at::kBFloat16, "out");
+  TORCH_CHECK(out.numel() == x.numel(), "cast_bf16_from_host: size mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
+  check(tfsk::cast_f32_bf16_launch(x.data_ptr<float>(), bf16p_mut(out), x.numel(), cur_stream(out)),
+        "cast_bf16_from_host");
+}
+
 Tensor cast_bf16(const Tensor& x, const c10::optional<Tensor>& out) {
   need(x, at::kFloat, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -324,6 +352,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("want_classes") = true, py::arg("probs_out") = py::none(), py::arg("classes_out") = py::none());
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("out") = py::none());
   m.def("ingest_c4", &ingest_c4, "fp32 NHWC (C<=4) -> bf16 NHWC C=4", py::arg("x"), py::arg("out") = py::none());
+  m.def("ingest_c4_from_host", &ingest_c4_from_host, "ingest_c4 reading a pinned host tensor (zero-copy)",
+        py::arg("x"), py::arg("out"));
+  m.def("cast_bf16_from_host", &cast_bf16_from_host, "fp32 pinned host tensor -> bf16 device tensor",
+        py::arg("x"), py::arg("out"));
   m.def("layernorm", &layernorm, py::arg("x"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("out") = py::none());
   m.def("embed_ln", &embed_ln, py::arg("ids"), py::arg("type_ids"), py::arg("word"), py::arg("pos"),

@@ -7,12 +7,12 @@ namespace tfsk {
 // Config ids continue after the igemm ones so one `cfg` integer selects either
 // kernel family: cgemm configs are kCGemmCfgBase .. kCGemmCfgBase + kNumCGemmConfigs - 1.
 constexpr int kCGemmCfgBase = 32;
-constexpr int kNumCGemmConfigs = 10;
+constexpr int kNumCGemmConfigs = 13;
 
 // Operand requirements (else cgemm_launch returns hipErrorInvalidValue):
 //   dense (a_mode kADense): K % 64 == 0, lda % 8 == 0;
 //   im2col (kAIm2col): C % 64 == 0 (a k-tile is one filter tap x 64 channels), KH*KW <= 32;
-//   weights: ldb % 8 == 0, ldb >= K.
+//   weights: ldb % 8 == 0, ldb >= K;  epilogue: N, ldc (and ldr) % 8 == 0.
 bool cgemm_supported(const IGemmArgs& a, int a_mode);
 int cgemm_config_bm(int cfg);
 int cgemm_config_bn(int cfg);

@@ -101,69 +101,90 @@ __device__ __forceinline__ void prefetch_residual(const IGemmArgs& p, int m0, in
   }
 }
 
+// This thread's 8 bias values (its epilogue column is fixed), loaded before the
+// K loop so the latency of the load hides under it instead of stalling the
+// epilogue of every workgroup.
+template <int BN, int NT>
+__device__ __forceinline__ void prefetch_bias(const IGemmArgs& p, int n0, int tid, float4& b0, float4& b1) {
+  int row0, col0;
+  epi_rowcol<BN, NT>(tid, 0, row0, col0);
+  const int n = n0 + col0;
+  b0 = b1 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.bias && p.splits <= 1 && p.N % 8 == 0 && n + 8 <= p.N) {
+    b0 = *reinterpret_cast<const float4*>(p.bias + n);
+    b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+  }
+}
+
+// Two floats -> packed bf16 pair (round-to-nearest-even; a plain __bf16 cast
+// compiles to one v_cvt_pk_bf16_f32 on gfx950 and keeps NaNs NaN).
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const __bf16 lo = static_cast<__bf16>(a), hi = static_cast<__bf16>(b);
+  return uint32_t(__builtin_bit_cast(uint16_t, lo)) | (uint32_t(__builtin_bit_cast(uint16_t, hi)) << 16);
+}
+
+// One 8-column chunk: alpha * acc + bias (+ residual) -> act -> 16-B bf16 (or
+// 2 x 16-B f32) store.  cgemm_supported() guarantees N, ldc, ldr % 8 == 0, so
+// there is no scalar tail path (it used to dominate the kernel's code size).
+template <int ACT>
+__device__ __forceinline__ void epi_chunk(const IGemmArgs& p, const float* src, int m, int n, const float (&bv)[8],
+                                          const uint4 rr) {
+  const float4 lo = *reinterpret_cast<const float4*>(src);
+  const float4 hi = *reinterpret_cast<const float4*>(src + 4);
+  float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+  const float alpha = p.alpha;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = act_fn<ACT>(v[2 * e] * alpha + bv[2 * e] + __uint_as_float(w[e] << 16));
+    v[2 * e + 1] = act_fn<ACT>(v[2 * e + 1] * alpha + bv[2 * e + 1] + __uint_as_float(w[e] & 0xffff0000u));
+  }
+  if (p.out_f32) {
+    float* o = static_cast<float*>(p.out) + size_t(m) * p.ldc + n;
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.out) + size_t(m) * p.ldc + n) =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                   pack_bf16x2(v[6], v[7]));
+  }
+}
+
+// Cheap activations (none / ReLU): fully unrolled over the thread's chunks,
+// residual from the registers prefetched before the K loop.  Transcendental
+// ones (GELU / tanh; BERT FFN and pooler, no residual): a rolled loop, so the
+// erf/tanh expansion is emitted once instead of ITERS x 8 times.
 template <int BM, int BN, int NT, int CS_LD, int ACT>
 __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* Cs, int m0, int n0, int tid,
-                                              const uint4 (&rpre)[Epi<BM, BN, NT>::PRE > 0 ? Epi<BM, BN, NT>::PRE : 1]) {
+                                              const uint4 (&rpre)[Epi<BM, BN, NT>::PRE > 0 ? Epi<BM, BN, NT>::PRE : 1],
+                                              const float4 b0, const float4 b1) {
   using E = Epi<BM, BN, NT>;
   const int M = p.M, N = p.N;
-  const float alpha = p.alpha;
-  const bool vec_ok = (N % 8 == 0) && (p.ldc % 8 == 0) && (!p.residual || p.ldr % 8 == 0);
-  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  {
-    int row0, col0;
-    epi_rowcol<BN, NT>(tid, 0, row0, col0);
-    const int n = n0 + col0;
-    if (p.bias && vec_ok && n + 8 <= N) {
-      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
-      const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
-      bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
-      bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+  const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  constexpr bool cheap = (ACT == kActNone || ACT == kActRelu);
+  if constexpr (cheap) {
+#pragma unroll
+    for (int it = 0; it < E::ITERS; ++it) {
+      int row, col;
+      epi_rowcol<BN, NT>(tid, it, row, col);
+      const int m = m0 + row, n = n0 + col;
+      if (m >= M || n >= N) continue;
+      uint4 rr = make_uint4(0, 0, 0, 0);
+      if (p.residual)
+        rr = E::PRE > 0 ? rpre[E::PRE > 0 ? it : 0]
+                        : *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
+      epi_chunk<ACT>(p, Cs + row * CS_LD + col, m, n, bv, rr);
     }
-  }
-#pragma unroll
-  for (int it = 0; it < E::ITERS; ++it) {
-    int row, col;
-    epi_rowcol<BN, NT>(tid, it, row, col);
-    const int m = m0 + row, n = n0 + col;
-    if (m >= M || n >= N) continue;
-    const float4 lo = *reinterpret_cast<const float4*>(Cs + row * CS_LD + col);
-    const float4 hi = *reinterpret_cast<const float4*>(Cs + row * CS_LD + col + 4);
-    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    if (vec_ok && n + 8 <= N) {
-      float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (p.residual) {
-        const uint4 rr = E::PRE > 0 ? rpre[E::PRE > 0 ? it : 0]
-                                    : *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
-        const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          rv[2 * e] = bf16_to_f32(uint16_t(w[e] & 0xffff));
-          rv[2 * e + 1] = bf16_to_f32(uint16_t(w[e] >> 16));
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = act_fn<ACT>(v[e] * alpha + bv[e] + rv[e]);
-      if (p.out_f32) {
-        float* o = static_cast<float*>(p.out) + size_t(m) * p.ldc + n;
-        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      } else {
-        uint16_t b[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) b[e] = f32_to_bf16(v[e]);
-        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.out) + size_t(m) * p.ldc + n) =
-            make_uint4(b[0] | (uint32_t(b[1]) << 16), b[2] | (uint32_t(b[3]) << 16),
-                       b[4] | (uint32_t(b[5]) << 16), b[6] | (uint32_t(b[7]) << 16));
-      }
-    } else {
-      for (int e = 0; e < 8 && n + e < N; ++e) {
-        float x = v[e] * alpha;
-        if (p.bias) x += p.bias[n + e];
-        if (p.residual) x += bf16_to_f32(p.residual[size_t(m) * p.ldr + n + e]);
-        x = act_fn<ACT>(x);
-        if (p.out_f32) static_cast<float*>(p.out)[size_t(m) * p.ldc + n + e] = x;
-        else static_cast<uint16_t*>(p.out)[size_t(m) * p.ldc + n + e] = f32_to_bf16(x);
-      }
+  } else {
+#pragma unroll 1
+    for (int it = 0; it < E::ITERS; ++it) {
+      int row, col;
+      epi_rowcol<BN, NT>(tid, it, row, col);
+      const int m = m0 + row, n = n0 + col;
+      if (m >= M || n >= N) continue;
+      const uint4 rr = p.residual ? *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n)
+                                  : make_uint4(0, 0, 0, 0);
+      epi_chunk<ACT>(p, Cs + row * CS_LD + col, m, n, bv, rr);
     }
   }
 }
@@ -185,6 +206,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   const int bm = first_m + (wg % per_group) % gsz;
   const int bn = (wg % per_group) / gsz;
   const int m0 = bm * BM, n0 = bn * BN;
+
+  // profiling ablations (act >= 100): bit 0 skips the operand DMAs, bit 1 the
+  // LDS reads + MFMAs, bit 2 exits right away, bit 3 skips the epilogue
+  // (timing only; results are garbage)
+  const int dbg = p.act >= 100 ? p.act - 100 : 0;
+  if (dbg & 4) return;
+  const bool do_dma = !(dbg & 1), do_mma = !(dbg & 2);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -223,13 +251,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
       const int ho = r / p.Wo, wo = r - ho * p.Wo;
       const int hb = ho * p.SH, wb = wo * p.SW;          // tap (0,0) in padded coordinates
       a_off[j] = (uint32_t((n * p.H + hb) * p.W + wb) * uint32_t(p.C) + kc) * 2u;
-      uint32_t msk = 0;
+      // tap t = kh*KW + kw is valid iff row hi0+kh and column wi0+kw are inside
       const int hi0 = hb - p.PT, wi0 = wb - p.PL;
-      int t = 0;
+      uint32_t wbits = 0;
+      for (int kw = 0; kw < p.KW; ++kw) wbits |= uint32_t((unsigned)(wi0 + kw) < (unsigned)p.W) << kw;
+      uint32_t msk = 0;
       for (int kh = 0; kh < p.KH; ++kh)
-        for (int kw = 0; kw < p.KW; ++kw, ++t)
-          if (ok && (unsigned)(hi0 + kh) < (unsigned)p.H && (unsigned)(wi0 + kw) < (unsigned)p.W) msk |= 1u << t;
-      a_msk[j] = msk;
+        if ((unsigned)(hi0 + kh) < (unsigned)p.H) msk |= wbits << (kh * p.KW);
+      a_msk[j] = ok ? msk : 0u;
     }
   }
   uint32_t b_off[G::BPW];
@@ -325,11 +354,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
 
   uint4 rpre[Epi<BM, BN, G::NT>::PRE > 0 ? Epi<BM, BN, G::NT>::PRE : 1];
   prefetch_residual<BM, BN, G::NT>(p, m0, n0, tid, rpre);
+  float4 bias0, bias1;
+  prefetch_bias<BN, G::NT>(p, n0, tid, bias0, bias1);
 
   // ---- prologue: S-1 k-tiles in flight
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
-    if (s < nk) issue(s);
+    if (s < nk && do_dma) issue(s);
 
   // ---- main loop, unrolled by the ring depth (slot indices are immediates)
   for (int kt = 0; kt < nk; kt += S) {
@@ -342,13 +373,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
         else wait_vmcnt<0>();
         // ... and every wave's (and every wave is done reading slot (t-1) % S)
         lds_barrier();
-        if (t + S - 1 < nk) issue((u + S - 1) % S);
-        compute(u);
+        if (t + S - 1 < nk && do_dma) issue((u + S - 1) % S);
+        if (do_mma) compute(u);
       }
     }
   }
   wait_vmcnt<0>();
   __syncthreads();
+  if (dbg & 8) return;
 
   // ---- epilogue: stage the fp32 tile in LDS, then coalesced row chunks
   float* Cs = reinterpret_cast<float*>(smem);
@@ -387,11 +419,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
     return;
   }
   switch (p.act) {
-    case kActRelu: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActRelu>(p, Cs, m0, n0, tid, rpre); break;
-    case kActGeluTanh: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActGeluTanh>(p, Cs, m0, n0, tid, rpre); break;
-    case kActGeluErf: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActGeluErf>(p, Cs, m0, n0, tid, rpre); break;
-    case kActTanh: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActTanh>(p, Cs, m0, n0, tid, rpre); break;
-    default: epilogue_rows<BM, BN, G::NT, G::CS_LD, 0>(p, Cs, m0, n0, tid, rpre); break;
+    case kActRelu: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActRelu>(p, Cs, m0, n0, tid, rpre, bias0, bias1); break;
+    case kActGeluTanh: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActGeluTanh>(p, Cs, m0, n0, tid, rpre, bias0, bias1); break;
+    case kActGeluErf: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActGeluErf>(p, Cs, m0, n0, tid, rpre, bias0, bias1); break;
+    case kActTanh: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActTanh>(p, Cs, m0, n0, tid, rpre, bias0, bias1); break;
+    default: epilogue_rows<BM, BN, G::NT, G::CS_LD, 0>(p, Cs, m0, n0, tid, rpre, bias0, bias1); break;
   }
 }
 
@@ -417,8 +449,8 @@ hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
 
 // Config table (tile BM x BN, wave grid, ring depth).  LDS per workgroup =
 // S * (BM + BN) * 128 B (or the fp32 epilogue tile if larger).
-constexpr int kBM[kNumCGemmConfigs] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256};
-constexpr int kBN[kNumCGemmConfigs] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64};
+constexpr int kBM[kNumCGemmConfigs] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256, 64, 64, 128};
+constexpr int kBN[kNumCGemmConfigs] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64, 64, 128, 64};
 
 template <bool IM2COL>
 hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
@@ -433,6 +465,11 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
     case 7: return launch_cfg<128, 128, 2, 4, 4, IM2COL>(a, s);   // 128 KB, 8 waves of 64x32
     case 8: return launch_cfg<64, 256, 1, 4, 3, IM2COL>(a, s);    // 120 KB, wave 64x64
     case 9: return launch_cfg<256, 64, 4, 1, 3, IM2COL>(a, s);    // 120 KB, wave 64x64
+    // double-buffered, small LDS: several workgroups per CU overlap each
+    // other's prologue / barrier / epilogue latency
+    case 10: return launch_cfg<64, 64, 2, 2, 2, IM2COL>(a, s);    // 32 KB (5 WG/CU)
+    case 11: return launch_cfg<64, 128, 2, 2, 2, IM2COL>(a, s);   // 48 KB (3 WG/CU)
+    case 12: return launch_cfg<128, 64, 2, 2, 2, IM2COL>(a, s);   // 48 KB (3 WG/CU)
     default: return hipErrorInvalidValue;
   }
 }
@@ -441,6 +478,7 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
 
 bool cgemm_supported(const IGemmArgs& a, int a_mode) {
   if (a.K <= 0 || a.K % KT || a.ldb % 8 || a.ldb < a.K) return false;
+  if (a.N % 8 || a.ldc % 8 || (a.residual && a.ldr % 8)) return false;   // 16-B epilogue chunks only
   if (a_mode == kADense) return a.lda % 8 == 0 && a.lda >= a.K;
   if (a_mode == kAIm2col)
     return a.C % KT == 0 && a.KH * a.KW <= 32 && a.K == a.KH * a.KW * a.C &&

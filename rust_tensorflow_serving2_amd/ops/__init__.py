@@ -76,7 +76,8 @@ DMA_ONLY = {4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16}
 TILE_BK = {12: 128, 13: 256, 14: 128, 15: 128, 16: 128}     # k-tile depth (default 64)
 # pipelined cgemm kernel (kernels/cgemm.hip; 64-aligned operands only): config id -> (BM, BN)
 CGEMM = {32: (128, 128), 33: (128, 128), 34: (64, 128), 35: (128, 64), 36: (64, 64),
-         37: (256, 128), 38: (128, 256), 39: (128, 128), 40: (64, 256), 41: (256, 64)}
+         37: (256, 128), 38: (128, 256), 39: (128, 128), 40: (64, 256), 41: (256, 64),
+         42: (64, 64), 43: (64, 128), 44: (128, 64)}
 TILES.update(CGEMM)
 
 
@@ -100,7 +101,7 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
     for cfg, (bm, bn) in TILES.items():
         if cfg in DMA_ONLY and (not dma or (cfg in (4, 5, 6, 7) and nk < 3)):
             continue
-        if cfg in CGEMM and not (aligned64 and dma and K % 64 == 0):
+        if cfg in CGEMM and not (aligned64 and dma and K % 64 == 0 and N % 8 == 0):
             continue
         if K < 2 * TILE_BK.get(cfg, 64) and cfg in TILE_BK:
             continue   # deep k-tiles only pay off with several of them

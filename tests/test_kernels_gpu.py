@@ -76,7 +76,7 @@ def test_conv_matches_fp32(shape, cfg, splits):
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
 
 
-CGEMM_CFGS = list(range(32, 42))
+CGEMM_CFGS = list(range(32, 45))
 CGEMM_CONV_SHAPES = [s for s in CONV_SHAPES if s[3] % 64 == 0] + [
     (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)),   # tiny image: most taps hit padding at the border rows
     (1, 15, 13, 64, 192, 3, 2, (0, 1, 1, 1)),  # odd sizes, asymmetric pads, N tail
@@ -104,16 +104,17 @@ def test_cgemm_conv_matches_fp32(shape, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
 
 
-@pytest.mark.parametrize("m,n,k", [(32, 1001, 2048), (256, 2304, 768), (1000, 768, 3072), (8, 72, 64)])
+@pytest.mark.parametrize("m,n,k", [(32, 1000, 2048), (256, 2304, 768), (1000, 768, 3072), (8, 72, 64)])
 @pytest.mark.parametrize("cfg", CGEMM_CFGS)
 def test_cgemm_linear_matches_fp32(m, n, k, cfg):
     x = rnd(m, k, seed=7).to(BF)
     w = rnd(n, k, scale=1 / math.sqrt(k), seed=8).to(BF)
     b = rnd(n, scale=0.1, seed=9)
     res = rnd(m, n, seed=10).to(BF)
-    out_f32 = n % 8 != 0
     ref = x.float() @ w.float().t() + b + res.float()
-    for act, fn in (("none", lambda t: t), ("gelu_tanh", lambda t: F.gelu(t, approximate="tanh"))):
+    for act, fn, out_f32 in (("none", lambda t: t, False), ("relu", torch.relu, True),
+                             ("gelu_tanh", lambda t: F.gelu(t, approximate="tanh"), False),
+                             ("gelu_erf", F.gelu, True), ("tanh", torch.tanh, False)):
         y = hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), res.to(DEV), ACT[act], cfg, out_f32)
         err = (y.float().cpu() - fn(ref)).abs().max().item()
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (act, err)
@@ -131,11 +132,16 @@ def test_cgemm_asymmetric_identity(cfg):
 
 
 def test_cgemm_rejects_unaligned():
-    """cgemm configs refuse (loudly) operands that are not 64-aligned."""
+    """cgemm configs refuse (loudly) operands that are not 64-aligned (K) or
+    whose output rows are not 16-B chunks (N % 8)."""
     x = torch.zeros(4, 40, device=DEV, dtype=BF)
     w = torch.zeros(8, 40, device=DEV, dtype=BF)
     with pytest.raises(RuntimeError, match="64-aligned"):
         hip().linear(x, w, None, None, 0, 32, False)
+    x = torch.zeros(4, 64, device=DEV, dtype=BF)
+    w = torch.zeros(12, 64, device=DEV, dtype=BF)
+    with pytest.raises(RuntimeError, match="64-aligned"):
+        hip().linear(x, w, None, None, 0, 32, True)
 
 
 @pytest.mark.parametrize("k,c,cfg", [(7, 3, 1), (7, 3, 0), (3, 3, 3), (5, 4, 1)])
