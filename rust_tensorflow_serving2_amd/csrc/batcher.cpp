@@ -158,7 +158,8 @@ void Endpoint::copy_rows(int slot, int r0, int n, const std::vector<const uint8_
     std::memcpy(s.in_base[i] + size_t(r0) * inputs[i].row_bytes, src[i], size_t(n) * inputs[i].row_bytes);
   std::lock_guard<std::mutex> g(mu_);
   s.copied += n;
-  if (s.copied == s.reserved) s.cv->notify_all();
+  s.ready.emplace_back(r0, n);
+  s.cv->notify_all();
 }
 
 void Endpoint::drain_queue() {
@@ -247,7 +248,8 @@ void Endpoint::commit_stream(SlotStream& r, std::unique_ptr<Call> call) {
   Slot& s = slots_[r.slot];
   s.reqs[r.idx].call = std::move(call);
   s.copied += r.n;
-  if (s.copied == s.reserved) s.cv->notify_all();
+  s.ready.emplace_back(s.reqs[r.idx].row0, r.n);
+  s.cv->notify_all();
 }
 
 void Endpoint::abandon_stream(SlotStream& r) {
@@ -269,13 +271,19 @@ void Endpoint::abandon_stalled_locked(Slot& s) {
   }
 }
 
-int Endpoint::acquire(int slot, int timeout_ms) {
+int Endpoint::acquire(int slot, int timeout_ms, std::vector<std::pair<int, int>>* ranges) {
   std::unique_lock<std::mutex> lk(mu_);
   if (slot < 0 || slot >= int(slots_.size())) return -1;
   const auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
   while (!closed_) {
     Slot& s = slots_[slot];
     const auto now = Clock::now();
+    if (ranges && !s.ready.empty()) {
+      ranges->insert(ranges->end(), s.ready.begin(), s.ready.end());
+      s.ready.clear();
+      // hand the rows over now unless this already completes the batch
+      if (!(s.state == kReady && s.reserved > 0 && s.copied == s.reserved)) return 0;
+    }
     if (s.state == kReady && s.reserved > 0 && s.copied == s.reserved) {
       s.state = kRunning;
       st_.batches++;
@@ -346,6 +354,7 @@ void Endpoint::complete(int slot, Server& srv) {
   {
     std::lock_guard<std::mutex> g(mu_);
     s.reqs.clear();
+    s.ready.clear();
     s.reserved = s.copied = 0;
     s.state = kFree;
     cv_free_.notify_all();
@@ -360,6 +369,7 @@ void Endpoint::fail(int slot, Server& srv, int code, const std::string& msg) {
   {
     std::lock_guard<std::mutex> g(mu_);
     s.reqs.clear();
+    s.ready.clear();
     s.reserved = s.copied = 0;
     s.state = kFree;
     cv_free_.notify_all();

@@ -74,6 +74,10 @@ struct Slot {
   int state = kFree;
   Clock::time_point first;
   std::vector<Pending> reqs;
+  // row ranges (row0, n) whose bytes are complete in the pinned buffer and not
+  // yet handed to the lane (eager H2D: the lane copies rows to the device
+  // while the batch is still filling, off the batch's critical path)
+  std::vector<std::pair<int, int>> ready;
   // per-slot wakeups: only the lane that owns the slot is woken (a shared
   // condition variable woke every lane on every request)
   std::shared_ptr<std::condition_variable> cv = std::make_shared<std::condition_variable>();
@@ -96,8 +100,10 @@ class Endpoint {
   void commit_stream(SlotStream& r, std::unique_ptr<Call> call);
   void abandon_stream(SlotStream& r);
   void set_server(Server* srv) { srv_ = srv; }
-  // GPU worker side.
-  int acquire(int slot, int timeout_ms);
+  // GPU worker side.  With `ranges`, rows that completed since the last call
+  // are appended to it (the worker copies them to the device right away) and
+  // the call also returns 0 early whenever new rows are available.
+  int acquire(int slot, int timeout_ms, std::vector<std::pair<int, int>>* ranges = nullptr);
   // when the slot's current batch opened (first row reserved); for tracing
   Clock::time_point slot_opened(int slot) {
     std::lock_guard<std::mutex> g(mu_);

@@ -34,6 +34,9 @@ struct HipRt {
   using evsync_t = int (*)(void*);
   using evquery_t = int (*)(void*);
   using evdestroy_t = int (*)(void*);
+  using screate_t = int (*)(void**, unsigned);
+  using sdestroy_t = int (*)(void*);
+  using swait_t = int (*)(void*, void*, unsigned);
   launch_t launch = nullptr;
   setdev_t set_device = nullptr;
   errstr_t err = nullptr;
@@ -43,6 +46,9 @@ struct HipRt {
   evsync_t event_sync = nullptr;
   evquery_t event_query = nullptr;
   evdestroy_t event_destroy = nullptr;
+  screate_t stream_create = nullptr;
+  sdestroy_t stream_destroy = nullptr;
+  swait_t stream_wait_event = nullptr;
   bool load() {
     if (launch) return true;
     void* h = dlopen("libamdhip64.so", RTLD_NOW | RTLD_NOLOAD);
@@ -58,12 +64,16 @@ struct HipRt {
     event_query = reinterpret_cast<evquery_t>(sym("hipEventQuery"));
     event_destroy = reinterpret_cast<evdestroy_t>(sym("hipEventDestroy"));
     launch = reinterpret_cast<launch_t>(sym("hipGraphLaunch"));
+    stream_create = reinterpret_cast<screate_t>(sym("hipStreamCreateWithFlags"));
+    stream_destroy = reinterpret_cast<sdestroy_t>(sym("hipStreamDestroy"));
+    stream_wait_event = reinterpret_cast<swait_t>(sym("hipStreamWaitEvent"));
     return launch && set_device && memcpy_async && event_create && event_record && event_sync && event_query &&
            event_destroy;
   }
 };
 constexpr int kHipMemcpyHostToDevice = 1, kHipMemcpyDeviceToHost = 2;
 constexpr unsigned kHipEventDisableTiming = 0x2;
+constexpr unsigned kHipStreamNonBlocking = 0x1;
 constexpr int kHipErrorNotReady = 600;
 
 HipRt& hip_rt() {
@@ -128,6 +138,20 @@ class NativeLane {
       if (k != std::string::npos) fault_every_ = std::atoi(spec.c_str() + k + 11);
     }
     std::sort(buckets_.begin(), buckets_.end(), [](auto& a, auto& b) { return a.rows < b.rows; });
+    // eager H2D (rows copied to the device while the batch fills) needs every
+    // bucket graph to read the same device input rows (GpuRunner shares one
+    // max-bucket buffer per lane).  Opt-in (TFSERVE_EAGER_H2D=1): measured on
+    // ResNet-50 b32 it LOSES (29-33k vs 39-41k RPC/s) — one hipMemcpyAsync per
+    // 602 KB row costs more lane-thread time and SDMA setup than the single
+    // batched copy it takes off the critical path.
+    eager_ = !buckets_.empty();
+    for (auto& b : buckets_) {
+      if (b.in.size() != buckets_.back().in.size()) eager_ = false;
+      for (size_t i = 0; eager_ && i < b.in.size(); ++i)
+        if (b.in[i].dst != buckets_.back().in[i].dst || b.in[i].src != buckets_.back().in[i].src) eager_ = false;
+    }
+    const char* eager_env = getenv("TFSERVE_EAGER_H2D");
+    eager_ = eager_ && eager_env && std::atoi(eager_env) != 0;
     th_ = std::thread([this] { run(); });
   }
   ~NativeLane() { join(); }
@@ -147,9 +171,15 @@ class NativeLane {
       }
     if (!b) return -1;
     int e = 0;
-    for (auto& c : b->in)
-      if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
-                                  c.row_bytes * size_t(n), kHipMemcpyHostToDevice, stream_);
+    if (eager_) {
+      // every row was already queued on the copy stream as it arrived
+      e = rt.event_record(copied_, copy_stream_);
+      if (!e) e = rt.stream_wait_event(stream_, copied_, 0);
+    } else {
+      for (auto& c : b->in)
+        if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
+                                    c.row_bytes * size_t(n), kHipMemcpyHostToDevice, stream_);
+    }
     if (!e) e = rt.launch(b->exec, stream_);
     for (auto& c : b->out)
       if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
@@ -169,16 +199,41 @@ class NativeLane {
       else std::this_thread::sleep_for(std::chrono::microseconds(40));
     }
   }
+  // H2D of rows that just completed in the pinned slot (row ranges from acquire)
+  int copy_rows(HipRt& rt, const std::vector<std::pair<int, int>>& ranges) {
+    const LaneBucket& b = buckets_.back();
+    int e = 0;
+    for (auto& r : ranges)
+      for (auto& c : b.in)
+        if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst + size_t(r.first) * c.row_bytes),
+                                    reinterpret_cast<const void*>(c.src + size_t(r.first) * c.row_bytes),
+                                    c.row_bytes * size_t(r.second), kHipMemcpyHostToDevice, copy_stream_);
+    return e;
+  }
   void run() {
     pthread_setname_np(pthread_self(), "tfs-nlane");
     HipRt& rt = hip_rt();
     rt.set_device(device_);
     void* done = nullptr;
     if (rt.event_create(&done, kHipEventDisableTiming) != 0) done = nullptr;
+    if (eager_ && (!rt.stream_create || !rt.stream_wait_event ||
+                   rt.stream_create(&copy_stream_, kHipStreamNonBlocking) != 0 ||
+                   rt.event_create(&copied_, kHipEventDisableTiming) != 0))
+      eager_ = false;
+    std::vector<std::pair<int, int>> ranges;
+    int copy_err = 0;
     for (;;) {
-      const int n = ep_->acquire(slot_, 100);
+      ranges.clear();
+      const int n = ep_->acquire(slot_, 100, eager_ ? &ranges : nullptr);
+      if (!ranges.empty() && !copy_err) copy_err = copy_rows(rt, ranges);
       if (n < 0) break;   // endpoint closed
       if (n == 0) continue;
+      if (copy_err) {
+        errors++;
+        ep_->fail(slot_, *srv_, 13 /*INTERNAL*/, std::string("GPU row copy failed: ") + (rt.err ? rt.err(copy_err) : ""));
+        copy_err = 0;
+        continue;
+      }
       if (fault_every_ > 0 && ++seen_ % uint64_t(fault_every_) == 0) {
         errors++;
         ep_->fail(slot_, *srv_, 13 /*INTERNAL*/, "injected fault (TFSERVE_FAULT)");
@@ -202,12 +257,17 @@ class NativeLane {
                          us_of(Clock::now())});
     }
     if (done) rt.event_destroy(done);
+    if (copied_) rt.event_destroy(copied_);
+    if (copy_stream_ && rt.stream_destroy) rt.stream_destroy(copy_stream_);
   }
   Server* srv_;
   std::shared_ptr<Endpoint> ep_;
   int slot_, device_;
   void* stream_;
   std::vector<LaneBucket> buckets_;
+  bool eager_ = false;
+  void* copy_stream_ = nullptr;
+  void* copied_ = nullptr;
   int fault_every_ = 0;
   uint64_t seen_ = 0;
   std::thread th_;

@@ -208,7 +208,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   const int m0 = bm * BM, n0 = bn * BN;
 
   // profiling ablations (act >= 100): bit 0 skips the operand DMAs, bit 1 the
-  // LDS reads + MFMAs, bit 2 exits right away, bit 3 skips the epilogue
+  // LDS reads + MFMAs, bit 2 exits right away, bit 3 skips the epilogue, bit 4
+  // exits after the per-lane setup
   // (timing only; results are garbage)
   const int dbg = p.act >= 100 ? p.act - 100 : 0;
   if (dbg & 4) return;
@@ -356,6 +357,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   prefetch_residual<BM, BN, G::NT>(p, m0, n0, tid, rpre);
   float4 bias0, bias1;
   prefetch_bias<BN, G::NT>(p, n0, tid, bias0, bias1);
+
+  if (dbg & 16) {   // ablation: setup only (keep the per-lane state live)
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < G::APW; ++j) keep ^= a_off[j] ^ a_msk[j];
+#pragma unroll
+    for (int j = 0; j < G::BPW; ++j) keep ^= b_off[j];
+    asm volatile("" ::"v"(keep), "v"(ra0), "v"(rb1), "s"(w_tap), "s"(w_ci));
+    return;
+  }
 
   // ---- prologue: S-1 k-tiles in flight
 #pragma unroll

@@ -131,19 +131,22 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
       bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
     }
   }
-#pragma unroll
-  for (int it = 0; it < EM::ITERS; ++it) {
+  // cheap activations: fully unrolled, residual from prefetched registers;
+  // GELU / tanh: rolled (the transcendental expansion is emitted once, not
+  // ITERS x 8 times — it used to make this kernel tens of thousands of
+  // instructions, far beyond the instruction cache)
+  auto chunk = [&](int it, bool use_pre) {
     int row, col;
     epi_rowcol<BM, BN>(tid, it, row, col);
     const int m = m0 + row, n = n0 + col;
-    if (m >= M || n >= N) continue;
+    if (m >= M || n >= N) return;
     const float4 lo = *reinterpret_cast<const float4*>(Cs + row * CS_LD + col);
     const float4 hi = *reinterpret_cast<const float4*>(Cs + row * CS_LD + col + 4);
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     if (vec_ok && n + 8 <= N) {
       float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (p.residual) {
-        const uint4 rr = EM::PRE > 0 ? rpre[EM::PRE > 0 ? it : 0]
+        const uint4 rr = (EM::PRE > 0 && use_pre) ? rpre[EM::PRE > 0 ? it : 0]
                                      : *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
         const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
@@ -176,6 +179,13 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
         else static_cast<uint16_t*>(p.out)[size_t(m) * p.ldc + n + e] = f32_to_bf16(x);
       }
     }
+  };
+  if constexpr (ACT == 0 || ACT == kActRelu) {
+#pragma unroll
+    for (int it = 0; it < EM::ITERS; ++it) chunk(it, true);
+  } else {
+#pragma unroll 1
+    for (int it = 0; it < EM::ITERS; ++it) chunk(it, false);
   }
 }
 

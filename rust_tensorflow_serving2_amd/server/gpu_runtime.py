@@ -58,6 +58,10 @@ class _Lane:
         self.static_out: Dict[int, List[torch.Tensor]] = {}
         self.host_in: List[torch.Tensor] = []      # pinned [max_bucket, ...]
         self.host_out: List[torch.Tensor] = []     # pinned [max_bucket, ...]
+        # device inputs [max_bucket, ...]: every bucket graph reads a leading-row
+        # view of the same buffer, so rows can be copied to the device as they
+        # arrive (native lanes' eager H2D), before the batch size is known
+        self.dev_in: List[torch.Tensor] = []
         self.done = torch.cuda.Event()
 
 
@@ -164,7 +168,11 @@ class GpuRunner:
 
     def _capture(self, lane: _Lane, b: int) -> None:
         dev = self.device
-        ins = [torch.zeros([b] + list(s.shape[1:]), dtype=_torch_dtype(s.dtype), device=dev) for s in self.in_specs]
+        if not lane.dev_in:
+            bmax = self.buckets[-1]
+            lane.dev_in = [torch.zeros([bmax] + list(s.shape[1:]), dtype=_torch_dtype(s.dtype), device=dev)
+                           for s in self.in_specs]
+        ins = [t[:b] for t in lane.dev_in]
         # eager warm-up on the lane's stream (autotunes kernel tiles for this shape)
         with torch.cuda.stream(lane.stream):
             self._finish(self.program.run(ins))

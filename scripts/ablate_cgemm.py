@@ -53,7 +53,7 @@ def main():
         for cfg in cfgs:
             row = {"layer": f"{h}x{h}x{cin} k{k}->{cout}", "cfg": cfg}
             for mode, name in ((0, "full"), (101, "no_dma"), (102, "no_mma"), (103, "neither"),
-                               (111, "neither_no_epi"), (104, "empty")):
+                               (111, "neither_no_epi"), (116, "setup_only"), (104, "empty")):
                 t = timeit(lambda: hip().conv2d(x, w, b, None, k, k, s, s, pad, pad, pad, pad, mode, cfg))
                 row[name] = round(t, 1)
             row["tflops_full"] = round(flop / row["full"] / 1e6)
