@@ -188,6 +188,45 @@ class FusedConv:
         return [H.conv2d(*args, cfg=cfg, out=out, splits=splits)]
 
 
+class FusedDualConv:
+    """``act(conv1x1(h) + conv1x1_stride(x) + b)`` as ONE GEMM over the
+    K-concatenated operands [h | x(strided)] and weights [W_h ; W_x] (cgemm
+    dual-source A mode): a ResNet bottleneck's expand conv and its projection
+    shortcut, without writing / re-reading the projection's output."""
+
+    def __init__(self, conv_h: FusedConv, conv_x: FusedConv, act: str, device, use_hip: bool, name: str):
+        self.c1, self.c2 = conv_h.cin, conv_x.cin
+        self.cout = conv_h.cout
+        self.sh, self.sw = conv_x.sh, conv_x.sw
+        self.act = act
+        self.use_hip = use_hip
+        self.name = name
+        if use_hip:
+            w = torch.cat([conv_h.w[:, :self.c1], conv_x.w[:, :self.c2]], dim=1)   # [Cout][C1 + C2] bf16
+            self.w = _pad_k(w.cpu(), 8).contiguous().to(device)
+            self.b = (conv_h.b + conv_x.b).contiguous()
+        else:
+            self.w1, self.w2 = conv_h.w_ref, conv_x.w_ref
+            self.b_ref = conv_h.b_ref + conv_x.b_ref
+
+    def __call__(self, ctx, node, ins):
+        h, x = O.to_torch(ins[0]), O.to_torch(ins[1])
+        if not self.use_hip:
+            y = h.float() @ self.w1.reshape(self.c1, self.cout)
+            xs = x.float()[:, ::self.sh, ::self.sw, :]
+            y = y + xs @ self.w2.reshape(self.c2, self.cout) + self.b_ref
+            return [_ref_act(y, self.act).contiguous()]
+        from ..ops import ACT, hip, tuned_config
+        H = hip()
+        h, x = _to_bf16(h).contiguous(), _to_bf16(x).contiguous()
+        n, ho, wo, _ = h.shape
+        out = torch.empty((n, ho, wo, self.cout), device=h.device, dtype=BF16)
+        key = ("dual", tuple(h.shape), tuple(x.shape), self.cout, self.sh)
+        run = lambda c, s: H.conv2d_dual(h, x, self.w, self.b, self.sh, self.sw, ACT[self.act], c, out, s)  # noqa
+        cfg, splits = tuned_config(key, n * ho * wo, self.cout, run, self.c1 + self.c2, True, True, cgemm_only=True)
+        return [run(cfg, splits)]
+
+
 class FusedMatMul:
     def __init__(self, w_kn: torch.Tensor, bias: Optional[torch.Tensor], act: str, out_f32: bool,
                  device, use_hip: bool, name: str):
@@ -243,7 +282,7 @@ def _impl_op(ctx, node, ins):
     return node.attrs["_impl"](ctx, node, ins)
 
 
-for _op in ("_FusedConv2D", "_FusedMatMul", "_GlobalAvgPool", "_MaxPool", "_SoftmaxArgMax", "_LayerNorm",
+for _op in ("_FusedConv2D", "_FusedDualConv", "_FusedMatMul", "_GlobalAvgPool", "_MaxPool", "_SoftmaxArgMax", "_LayerNorm",
             "_FusedQKV", "_Attention", "_EmbedLN"):
     O.OPS[_op] = _impl_op
 
@@ -493,6 +532,49 @@ def fuse_softmax_argmax(g, order, fed, fetch_refs, device, opts):
             am.attrs = {}
 
 
+def _is_1x1(impl) -> bool:
+    """A 1x1 conv without padding (SAME never pads a 1x1 filter)."""
+    return isinstance(impl, FusedConv) and impl.kh == impl.kw == 1 and impl.use_hip and not impl.c4 and \
+        (impl.padding != "EXPLICIT" or not any(impl.pads))
+
+
+def fuse_dual_conv(g, order, fed, fetch_refs, device, opts):
+    """Merge ``_FusedConv2D(a, residual=_FusedConv2D(b))`` where both are 1x1
+    convs, the residual producer has no activation and no other consumer, and
+    one of them has stride 1, into ``_FusedDualConv(h=stride-1 input, x=other
+    input)`` (GPU only; both channel counts multiples of 64)."""
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    if not c.use_hip:
+        return
+    for name in order:
+        n = g.nodes.get(name)
+        if n is None or n.op != "_FusedConv2D" or len(n.inputs) != 2:
+            continue
+        a = n.attrs["_impl"]
+        r = g.nodes.get(n.inputs[1][0])
+        if r is None or r.op != "_FusedConv2D" or len(r.inputs) != 1 or n.inputs[1][1] != 0:
+            continue
+        b = r.attrs["_impl"]
+        if not (_is_1x1(a) and _is_1x1(b)) or b.act != "none" or c.only_consumer(r.name) is not n:
+            continue
+        if a.cin % 64 or b.cin % 64 or a.cout != b.cout or a.cout % 8:
+            continue
+        # the stride-1 conv's input is the dense source (its rows are the output pixels)
+        if a.sh == a.sw == 1:
+            conv_h, h_ref, conv_x, x_ref = a, n.inputs[0], b, r.inputs[0]
+        elif b.sh == b.sw == 1:
+            conv_h, h_ref, conv_x, x_ref = b, r.inputs[0], a, n.inputs[0]
+        else:
+            continue
+        impl = FusedDualConv(conv_h, conv_x, a.act, device, c.use_hip, n.name)
+        n.op = "_FusedDualConv"
+        n.inputs = [h_ref, x_ref]
+        n.ctrl = _merge_ctrl([r, n])
+        n.attrs = {"_impl": impl}
+        del g.nodes[r.name]
+        c.refresh()
+
+
 def default_passes(options=None):
     from .patterns import bert_passes
-    return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_matmul]
+    return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_dual_conv, fuse_matmul]

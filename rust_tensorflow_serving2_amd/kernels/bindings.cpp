@@ -122,6 +122,45 @@ Tensor conv2d(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   return y;
 }
 
+// ResNet bottleneck tail in one GEMM: act(conv1x1(h) + conv1x1_stride(x) + bias)
+// with w = [Cout][C_h + C_x] (expand weights | projection weights).
+// h: NHWC [N][Ho][Wo][C_h] bf16 (dense rows), x: NHWC [N][H][W][C_x] bf16
+// sampled at (ho*SH, wo*SW).  cgemm configs only (C_h, C_x % 64 == 0).
+Tensor conv2d_dual(const Tensor& h, const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
+                   int64_t SH, int64_t SW, int64_t act, int64_t cfg, const c10::optional<Tensor>& out, int64_t splits) {
+  need(h, at::kBFloat16, "h");
+  need(x, at::kBFloat16, "x");
+  need(w, at::kBFloat16, "w");
+  TORCH_CHECK(h.dim() == 4 && x.dim() == 4 && h.size(0) == x.size(0), "conv2d_dual: NHWC h and x, same batch");
+  TORCH_CHECK(is_cgemm_cfg(cfg), "conv2d_dual needs a cgemm tile config");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(h.device());
+  const int N = h.size(0), Ho = h.size(1), Wo = h.size(2), C1 = h.size(3);
+  const int H = x.size(1), W = x.size(2), C2 = x.size(3);
+  TORCH_CHECK(SH >= 1 && SW >= 1 && (H - 1) / SH + 1 == Ho && (W - 1) / SW + 1 == Wo,
+              "conv2d_dual: x sampled at stride (SH, SW) must give h's spatial size");
+  const int Cout = w.size(0), ldb = w.size(1);
+  TORCH_CHECK(ldb >= C1 + C2 && ldb % 8 == 0, "conv2d_dual: weights must hold K = C_h + C_x");
+  Tensor y = out.has_value() ? *out : torch::empty({N, Ho, Wo, Cout}, h.options());
+  need(y, at::kBFloat16, "out");
+  TORCH_CHECK(y.numel() == int64_t(N) * Ho * Wo * Cout, "out has the wrong size");
+  tfsk::IGemmArgs a{};
+  a.a = h.data_ptr(); a.a_bytes = h.numel() * 2;
+  a.a2 = x.data_ptr(); a.a2_bytes = x.numel() * 2;
+  a.b = bf16p(w); a.b_bytes = w.numel() * 2;
+  TORCH_CHECK(a.a_bytes < 0x7ffffff0LL && a.a2_bytes < 0x7ffffff0LL && a.b_bytes < 0x7ffffff0LL,
+              "conv2d_dual operands must be < 2 GiB");
+  a.M = N * Ho * Wo; a.N = Cout; a.K = C1 + C2; a.K1 = C1; a.lda = C1; a.ldb = ldb;
+  a.H = H; a.W = W; a.C = C2; a.KH = 1; a.KW = 1; a.SH = SH; a.SW = SW; a.PT = 0; a.PL = 0; a.Ho = Ho; a.Wo = Wo;
+  if (bias.has_value()) {
+    need(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == Cout, "bias size");
+    a.bias = bias->data_ptr<float>();
+  }
+  a.act = act; a.out = y.data_ptr(); a.ldc = Cout; a.out_f32 = 0; a.alpha = 1.f;
+  run_igemm(a, tfsk::kADual, cfg, splits, h, cur_stream(h));
+  return y;
+}
+
 // x: [M][K] bf16 (any leading dims), w: [N][ldb] bf16 -> [.., N]
 Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
               const c10::optional<Tensor>& residual, int64_t act, int64_t cfg, bool out_f32, double alpha,
@@ -342,7 +381,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias"), py::arg("residual"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
         py::arg("pt"), py::arg("pb"), py::arg("pl"), py::arg("pr"), py::arg("act") = 0, py::arg("cfg") = 0,
         py::arg("out") = py::none(), py::arg("out_f32") = false, py::arg("splits") = 1);
-  m.def("linear", &linear, "x @ w^T (+bias +residual +act)", py::arg("x"), py::arg("w"), py::arg("bias"),
+  m.def("conv2d_dual", &conv2d_dual, "act(conv1x1(h) + conv1x1_stride(x) + bias) as one K-concatenated GEMM",
+        py::arg("h"), py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"), py::arg("sw"), py::arg("act") = 0,
+        py::arg("cfg") = 36, py::arg("out") = py::none(), py::arg("splits") = 1);
+  m.def("linear", &linear,"x @ w^T (+bias +residual +act)", py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("residual") = py::none(), py::arg("act") = 0, py::arg("cfg") = 0, py::arg("out_f32") = false,
         py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("splits") = 1);
   m.def("maxpool", &maxpool, py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),

@@ -189,9 +189,10 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int S, bool IM2COL>
+template <int BM, int BN, int WGM, int WGN, int S, int AM>
 __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   using G = CG<BM, BN, WGM, WGN, S>;
+  constexpr bool IM2COL = (AM == 1), DUAL = (AM == 2);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   char* const smem = reinterpret_cast<char*>(smem_raw);
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -235,9 +236,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
       __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(abase), 0, int(arec), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.b), 0, int(p.b_bytes), 0x00020000);
+  // dual mode: second A source (1x1 / strided samples of an NHWC tensor)
+  const __amdgpu_buffer_rsrc_t rsA2 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(DUAL ? p.a2 : p.a), 0, int(DUAL ? p.a2_bytes : p.a_bytes), 0x00020000);
 
   // ---- per-lane DMA offsets (computed once)
-  uint32_t a_off[G::APW], a_msk[G::APW];
+  uint32_t a_off[G::APW], a_msk[G::APW], a_off2[DUAL ? G::APW : 1];
 #pragma unroll
   for (int j = 0; j < G::APW; ++j) {
     const int m = m0 + (wid * G::APW + j) * 8 + prow;
@@ -245,6 +249,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
     a_msk[j] = 0;
     if (!IM2COL) {
       a_off[j] = ok ? (uint32_t(m) * uint32_t(p.lda) + kc) * 2u : kOOB;
+      if constexpr (DUAL) {
+        const int mm = ok ? m : 0;
+        const int hw = p.Ho * p.Wo;
+        const int n = mm / hw, r = mm - n * hw;
+        const int ho = r / p.Wo, wo = r - ho * p.Wo;
+        a_off2[j] = ok ? (uint32_t((n * p.H + ho * p.SH) * p.W + wo * p.SW) * uint32_t(p.C) + kc) * 2u : kOOB;
+      }
     } else {
       const int mm = ok ? m : 0;
       const int hw = p.Ho * p.Wo;
@@ -290,12 +301,22 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   auto issue = [&](int slot) {
     const uint32_t a_soff = IM2COL ? uint32_t((w_kh * p.W + w_kw) * p.C + w_ci) * 2u : uint32_t(w_k) * 2u;
     const uint32_t b_soff = uint32_t(w_k) * 2u;
+    if (DUAL && w_k >= p.K1) {   // wave-uniform: the k-tile lies in the second source
+      const uint32_t soff2 = uint32_t(w_k - p.K1) * 2u;
 #pragma unroll
-    for (int j = 0; j < G::APW; ++j) {
-      uint32_t v = a_off[j];
-      if (IM2COL) v = ((a_msk[j] >> w_tap) & 1u) ? v : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsA, (lds_ptr_t)(smem + (slot * G::A_ST + (wid * G::APW + j) * 512) * 2), 16, v, a_soff, 0, 0);
+      for (int j = 0; j < G::APW; ++j) {
+        const uint32_t v = a_off2[DUAL ? j : 0];
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsA2, (lds_ptr_t)(smem + (slot * G::A_ST + (wid * G::APW + j) * 512) * 2), 16, v, soff2, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < G::APW; ++j) {
+        uint32_t v = a_off[j];
+        if (IM2COL) v = ((a_msk[j] >> w_tap) & 1u) ? v : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsA, (lds_ptr_t)(smem + (slot * G::A_ST + (wid * G::APW + j) * 512) * 2), 16, v, a_soff, 0, 0);
+      }
     }
 #pragma unroll
     for (int j = 0; j < G::BPW; ++j) {
@@ -438,7 +459,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int S, bool IM2COL>
+template <int BM, int BN, int WGM, int WGN, int S, int AM>
 hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
   using G = CG<BM, BN, WGM, WGN, S>;
   IGemmArgs a = a0;
@@ -449,12 +470,12 @@ hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
   if (tiles == 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, IM2COL>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, AM>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((cgemm_kernel<BM, BN, WGM, WGN, S, IM2COL>), dim3(tiles, splits), dim3(G::NT), G::LDS, s, a);
+  hipLaunchKernelGGL((cgemm_kernel<BM, BN, WGM, WGN, S, AM>), dim3(tiles, splits), dim3(G::NT), G::LDS, s, a);
   return hipGetLastError();
 }
 
@@ -463,24 +484,24 @@ hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
 constexpr int kBM[kNumCGemmConfigs] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256, 64, 64, 128};
 constexpr int kBN[kNumCGemmConfigs] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64, 64, 128, 64};
 
-template <bool IM2COL>
+template <int AM>
 hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
   switch (cfg) {
-    case 0: return launch_cfg<128, 128, 2, 2, 3, IM2COL>(a, s);   // 96 KB, wave 64x64
-    case 1: return launch_cfg<128, 128, 2, 2, 2, IM2COL>(a, s);   // 64 KB (2 WG/CU)
-    case 2: return launch_cfg<64, 128, 2, 2, 4, IM2COL>(a, s);    // 96 KB, wave 32x64
-    case 3: return launch_cfg<128, 64, 2, 2, 4, IM2COL>(a, s);    // 96 KB, wave 64x32
-    case 4: return launch_cfg<64, 64, 2, 2, 4, IM2COL>(a, s);     // 64 KB, wave 32x32
-    case 5: return launch_cfg<256, 128, 4, 2, 3, IM2COL>(a, s);   // 144 KB, 8 waves of 64x64
-    case 6: return launch_cfg<128, 256, 2, 4, 3, IM2COL>(a, s);   // 144 KB, 8 waves of 64x64
-    case 7: return launch_cfg<128, 128, 2, 4, 4, IM2COL>(a, s);   // 128 KB, 8 waves of 64x32
-    case 8: return launch_cfg<64, 256, 1, 4, 3, IM2COL>(a, s);    // 120 KB, wave 64x64
-    case 9: return launch_cfg<256, 64, 4, 1, 3, IM2COL>(a, s);    // 120 KB, wave 64x64
+    case 0: return launch_cfg<128, 128, 2, 2, 3, AM>(a, s);   // 96 KB, wave 64x64
+    case 1: return launch_cfg<128, 128, 2, 2, 2, AM>(a, s);   // 64 KB (2 WG/CU)
+    case 2: return launch_cfg<64, 128, 2, 2, 4, AM>(a, s);    // 96 KB, wave 32x64
+    case 3: return launch_cfg<128, 64, 2, 2, 4, AM>(a, s);    // 96 KB, wave 64x32
+    case 4: return launch_cfg<64, 64, 2, 2, 4, AM>(a, s);     // 64 KB, wave 32x32
+    case 5: return launch_cfg<256, 128, 4, 2, 3, AM>(a, s);   // 144 KB, 8 waves of 64x64
+    case 6: return launch_cfg<128, 256, 2, 4, 3, AM>(a, s);   // 144 KB, 8 waves of 64x64
+    case 7: return launch_cfg<128, 128, 2, 4, 4, AM>(a, s);   // 128 KB, 8 waves of 64x32
+    case 8: return launch_cfg<64, 256, 1, 4, 3, AM>(a, s);    // 120 KB, wave 64x64
+    case 9: return launch_cfg<256, 64, 4, 1, 3, AM>(a, s);    // 120 KB, wave 64x64
     // double-buffered, small LDS: several workgroups per CU overlap each
     // other's prologue / barrier / epilogue latency
-    case 10: return launch_cfg<64, 64, 2, 2, 2, IM2COL>(a, s);    // 32 KB (5 WG/CU)
-    case 11: return launch_cfg<64, 128, 2, 2, 2, IM2COL>(a, s);   // 48 KB (3 WG/CU)
-    case 12: return launch_cfg<128, 64, 2, 2, 2, IM2COL>(a, s);   // 48 KB (3 WG/CU)
+    case 10: return launch_cfg<64, 64, 2, 2, 2, AM>(a, s);    // 32 KB (5 WG/CU)
+    case 11: return launch_cfg<64, 128, 2, 2, 2, AM>(a, s);   // 48 KB (3 WG/CU)
+    case 12: return launch_cfg<128, 64, 2, 2, 2, AM>(a, s);   // 48 KB (3 WG/CU)
     default: return hipErrorInvalidValue;
   }
 }
@@ -494,6 +515,9 @@ bool cgemm_supported(const IGemmArgs& a, int a_mode) {
   if (a_mode == kAIm2col)
     return a.C % KT == 0 && a.KH * a.KW <= 32 && a.K == a.KH * a.KW * a.C &&
            a.a_bytes + int64_t(a.PT * a.W + a.PL) * a.C * 2 < 0x7ffffff0LL;
+  if (a_mode == kADual)
+    return a.a2 && a.K1 > 0 && a.K1 % KT == 0 && a.lda % 8 == 0 && a.lda >= a.K1 && a.C % KT == 0 &&
+           a.K == a.K1 + a.C && a.KH == 1 && a.KW == 1 && a.PT == 0 && a.PL == 0 && a.a2_bytes < 0x7ffffff0LL;
   return false;
 }
 
@@ -504,7 +528,11 @@ hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) 
   if (cfg < kCGemmCfgBase || cfg >= kCGemmCfgBase + kNumCGemmConfigs || !cgemm_supported(a, a_mode))
     return hipErrorInvalidValue;
   cfg -= kCGemmCfgBase;
-  return a_mode == kAIm2col ? launch_mode<true>(a, cfg, s) : launch_mode<false>(a, cfg, s);
+  switch (a_mode) {
+    case kAIm2col: return launch_mode<1>(a, cfg, s);
+    case kADual: return launch_mode<2>(a, cfg, s);
+    default: return launch_mode<0>(a, cfg, s);
+  }
 }
 
 }  // namespace tfsk

@@ -34,6 +34,14 @@ struct IGemmArgs {
   // loads; must be < 2^31)
   int64_t a_bytes;
   int64_t b_bytes;
+  // dual-source A (cgemm only): k < K1 reads the dense `a` [M][lda], k >= K1
+  // reads `a2`, an NHWC tensor sampled by a 1x1 / stride (SH, SW) conv with the
+  // geometry fields above (C = its channels).  One GEMM then computes
+  // conv1x1(a) + conv1x1_strided(a2) — a ResNet bottleneck's expand conv and
+  // its projection shortcut (K-concatenated weights, summed bias).
+  const void* a2;
+  int64_t a2_bytes;
+  int K1;
 };
 
 // kAStem7x7x3: fp32 NHWC input with C == 3 and a 7-wide filter (the ResNet
@@ -41,7 +49,7 @@ struct IGemmArgs {
 // kAC4: bf16 NHWC with exactly 4 channels (RGB + zero pad, written by
 // ingest_c4) and KW <= 8; k = kh*32 + kw*4 + c, so one 16-B operand chunk is
 // two 8-B filter taps and kh = k >> 5 (no division in the gather).
-enum AMode : int { kADense = 0, kAIm2col = 1, kAStemF32 = 2, kAStem7x7x3 = 3, kAC4 = 4 };
+enum AMode : int { kADense = 0, kAIm2col = 1, kAStemF32 = 2, kAStem7x7x3 = 3, kAC4 = 4, kADual = 5 };
 
 // fp32 NHWC with C <= 4 channels -> bf16 NHWC with 4 channels (zero padded).
 hipError_t ingest_c4_launch(const float* x, uint16_t* y, int64_t pixels, int C, hipStream_t stream);

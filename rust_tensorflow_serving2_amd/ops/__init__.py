@@ -91,7 +91,7 @@ def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
     return s
 
 
-def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False):
+def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False, cgemm_only: bool = False):
     """(tile config, split-K) pairs worth timing for an M x N x K problem
     (``dma``: the operand mode uses the direct-to-LDS path, so the deeper
     DMA-ring configs apply; ``aligned64``: K and the conv channels are
@@ -102,6 +102,8 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
         if cfg in DMA_ONLY and (not dma or (cfg in (4, 5, 6, 7) and nk < 3)):
             continue
         if cfg in CGEMM and not (aligned64 and dma and K % 64 == 0 and N % 8 == 0):
+            continue
+        if cgemm_only and cfg not in CGEMM:
             continue
         if K < 2 * TILE_BK.get(cfg, 64) and cfg in TILE_BK:
             continue   # deep k-tiles only pay off with several of them
@@ -116,7 +118,7 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
 
 
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
-                 dma: bool = True, aligned64: bool = False) -> Tuple[int, int]:
+                 dma: bool = True, aligned64: bool = False, cgemm_only: bool = False) -> Tuple[int, int]:
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
     heuristic is used)."""
@@ -124,7 +126,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
     if hit is not None:
         return hit
     if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
-        c = heuristic_config(M, N)
+        c = 42 if cgemm_only else heuristic_config(M, N)
         return c, heuristic_splits(M, N, K, c)
     with _TUNE_LOCK:
         hit = _TUNED.get(key)
@@ -132,7 +134,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
             return hit
         best, best_t = None, float("inf")
         flush = _flush_buffer()
-        for c, s in candidates(M, N, K, dma, aligned64):
+        for c, s in candidates(M, N, K, dma, aligned64, cgemm_only):
             launch(c, s)   # warm (also sets the kernel's LDS attribute)
             t = 0.0
             for _rep in range(3):

@@ -131,6 +131,25 @@ def test_cgemm_asymmetric_identity(cfg):
     assert torch.equal(y.cpu(), a.float() @ bmat.t())
 
 
+@pytest.mark.parametrize("n,ho,c1,h,c2,s,cout", [(2, 56, 64, 56, 64, 1, 256), (2, 28, 128, 56, 256, 2, 512),
+                                                 (1, 7, 512, 14, 1024, 2, 2048), (1, 5, 64, 9, 128, 2, 72)])
+@pytest.mark.parametrize("cfg", [32, 36, 42, 43, 44])
+def test_conv2d_dual_matches_fp32(n, ho, c1, h, c2, s, cout, cfg):
+    """One GEMM for a bottleneck tail: relu(conv1x1(h) + conv1x1_stride(x) + b)."""
+    hh = rnd(n, ho, ho, c1, seed=21).to(BF)
+    x = rnd(n, h, h, c2, seed=22).to(BF)
+    w1 = rnd(cout, c1, scale=1 / math.sqrt(c1), seed=23).to(BF)
+    w2 = rnd(cout, c2, scale=1 / math.sqrt(c2), seed=24).to(BF)
+    b = rnd(cout, scale=0.1, seed=25)
+    w = torch.cat([w1, w2], 1).contiguous()
+    ref = torch.relu(hh.float() @ w1.float().t() + x.float()[:, ::s, ::s, :] @ w2.float().t() + b)
+    for splits in (1, 2):
+        y = hip().conv2d_dual(hh.to(DEV), x.to(DEV), w.to(DEV), b.to(DEV), s, s, ACT["relu"], cfg, None, splits)
+        err = (y.float().cpu() - ref).abs().max().item()
+        assert y.shape == (n, ho, ho, cout)
+        assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
+
+
 def test_cgemm_rejects_unaligned():
     """cgemm configs refuse (loudly) operands that are not 64-aligned (K) or
     whose output rows are not 16-B chunks (N % 8)."""

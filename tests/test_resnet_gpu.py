@@ -37,7 +37,10 @@ def test_resnet50_gpu_matches_cpu(resnet50):
     np.testing.assert_allclose(g2["probabilities"], g["probabilities"][:3], atol=2e-4)
     runner = next(iter(gpu._runners.values()))
     hist = runner.program.op_histogram()
-    assert hist.get("_FusedConv2D") == 53 and "Conv2D" not in hist
+    # 53 convs: 4 stage-entry (expand conv + projection shortcut) pairs run as
+    # one K-concatenated dual-source GEMM each
+    assert hist.get("_FusedDualConv") == 4 and "Conv2D" not in hist
+    assert hist.get("_FusedConv2D") + 2 * hist["_FusedDualConv"] == 53
 
 
 def test_smoke():
