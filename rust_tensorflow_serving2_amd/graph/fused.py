@@ -128,14 +128,17 @@ class FusedConv:
         self.use_hip = use_hip
         self.name = name
         self.device = device
-        # RGB(A) stems: input re-laid out as bf16 RGBA by ingest_c4, weights as
-        # [Cout][kh][8 taps][4 ch] so the kernel's operand gather is 8-B vector loads
+        # RGB(A) stems: the fp32 request is re-laid out as zero-bordered bf16 RGBA
+        # (ingest_c4_padded), weights as [Cout][kh (padded to even)][8 taps][4 ch]:
+        # a 64-deep k-tile is then 2 filter rows x 8 taps x 4 channels = two
+        # contiguous 64-B runs of the padded image, DMA'd with no bounds checks
         self.c4 = use_hip and self.cin <= 4 and self.kw <= 8
+        self.khp = self.kh + (self.kh % 2) if self.c4 else self.kh
         if use_hip:
             if self.c4:
-                w4 = torch.zeros(self.kh, 8, 4, self.cout)
-                w4[:, :self.kw, :self.cin, :] = w_hwio.float()
-                w_nk = w4.permute(3, 0, 1, 2).reshape(self.cout, self.kh * 32)
+                w4 = torch.zeros(self.khp, 8, 4, self.cout)
+                w4[:self.kh, :self.kw, :self.cin, :] = w_hwio.float()
+                w_nk = w4.permute(3, 0, 1, 2).reshape(self.cout, self.khp * 32)
             else:
                 k = self.kh * self.kw * self.cin
                 w_nk = w_hwio.permute(3, 0, 1, 2).reshape(self.cout, k)
@@ -165,7 +168,14 @@ class FusedConv:
             return [_ref_act(y, self.act).contiguous()]
         from ..ops import ACT, hip, tuned_config
         if self.c4:
-            x = hip().ingest_c4(x.float().contiguous())   # fp32 RGB request -> bf16 RGBA
+            # fp32 RGB request -> zero-bordered bf16 RGBA sized for the padded
+            # (khp x 8) filter; the conv itself then has no padding
+            h, w = x.shape[1], x.shape[2]
+            ho = (h + pt + pb - self.kh) // self.sh + 1
+            wo = (w + pl + pr - self.kw) // self.sw + 1
+            hp, wp = (ho - 1) * self.sh + self.khp, (wo - 1) * self.sw + 8
+            x = hip().ingest_c4_padded(x.float().contiguous(), hp, wp, pt, pl)
+            pt = pb = pl = pr = 0
         elif self.cin % 8 != 0:
             x = x.float().contiguous()            # generic: fp32 operand gather + cast in-kernel
         else:
@@ -174,15 +184,17 @@ class FusedConv:
             res = _to_bf16(res).contiguous()
         H = hip()
         n, h, w, _ = x.shape
-        ho = (h + pt + pb - self.kh) // self.sh + 1
-        wo = (w + pl + pr - self.kw) // self.sw + 1
+        kh, kw = (self.khp, 8) if self.c4 else (self.kh, self.kw)
+        ho = (h + pt + pb - kh) // self.sh + 1
+        wo = (w + pl + pr - kw) // self.sw + 1
         M = n * ho * wo
-        args = (x, self.w, self.b, res, self.kh, self.kw, self.sh, self.sw, pt, pb, pl, pr, ACT[self.act])
+        args = (x, self.w, self.b, res, kh, kw, self.sh, self.sw, pt, pb, pl, pr, ACT[self.act])
         out = torch.empty((n, ho, wo, self.cout), device=x.device, dtype=BF16)
-        key = ("conv", tuple(x.shape), x.dtype, self.cout, self.kh, self.kw, self.sh, res is not None)
-        K = self.kh * 32 if self.c4 else self.kh * self.kw * self.cin
+        key = ("conv", tuple(x.shape), x.dtype, self.cout, kh, kw, self.sh, res is not None)
+        K = kh * 32 if self.c4 else kh * kw * self.cin
         dma = not self.c4 and self.cin % 8 == 0      # bf16 dense/im2col operands -> DMA-ring configs apply
-        aligned = dma and self.cin % 64 == 0     # pipelined cgemm kernel applies
+        # pipelined cgemm kernel applies (im2col / dense with C % 64, or the padded RGBA stem)
+        aligned = (dma and self.cin % 64 == 0) or self.c4
         cfg, splits = tuned_config(key, M, self.cout, lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s), K,
                                    dma, aligned)
         return [H.conv2d(*args, cfg=cfg, out=out, splits=splits)]

@@ -281,6 +281,18 @@ void ingest_c4_from_host(const Tensor& x, const Tensor& out) {
         "ingest_c4_from_host");
 }
 
+Tensor ingest_c4_padded(const Tensor& x, int64_t Hp, int64_t Wp, int64_t pt, int64_t pl) {
+  need(x, at::kFloat, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) >= 1 && x.size(3) <= 4, "ingest_c4_padded: NHWC with C <= 4");
+  TORCH_CHECK(pt >= 0 && pl >= 0 && Hp >= pt + x.size(1) && Wp >= pl + x.size(2), "ingest_c4_padded: padding");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = torch::empty({x.size(0), Hp, Wp, 4}, x.options().dtype(at::kBFloat16));
+  check(tfsk::ingest_c4_pad_launch(x.data_ptr<float>(), bf16p_mut(y), x.size(0), x.size(1), x.size(2), x.size(3),
+                                   Hp, Wp, pt, pl, cur_stream(x)),
+        "ingest_c4_padded");
+  return y;
+}
+
 void cast_bf16_from_host(const Tensor& x, const Tensor& out) {
   need_pinned_f32(x, "x");
   need(out, at::kBFloat16, "out");
@@ -394,6 +406,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("want_classes") = true, py::arg("probs_out") = py::none(), py::arg("classes_out") = py::none());
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("out") = py::none());
   m.def("ingest_c4", &ingest_c4, "fp32 NHWC (C<=4) -> bf16 NHWC C=4", py::arg("x"), py::arg("out") = py::none());
+  m.def("ingest_c4_padded", &ingest_c4_padded, "fp32 NHWC (C<=4) -> zero-bordered bf16 RGBA [N][Hp][Wp][4]",
+        py::arg("x"), py::arg("hp"), py::arg("wp"), py::arg("pt"), py::arg("pl"));
   m.def("ingest_c4_from_host", &ingest_c4_from_host, "ingest_c4 reading a pinned host tensor (zero-copy)",
         py::arg("x"), py::arg("out"));
   m.def("cast_bf16_from_host", &cast_bf16_from_host, "fp32 pinned host tensor -> bf16 device tensor",

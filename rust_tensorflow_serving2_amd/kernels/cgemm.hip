@@ -192,7 +192,7 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
 template <int BM, int BN, int WGM, int WGN, int S, int AM>
 __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   using G = CG<BM, BN, WGM, WGN, S>;
-  constexpr bool IM2COL = (AM == 1), DUAL = (AM == 2);
+  constexpr bool IM2COL = (AM == 1), DUAL = (AM == 2), STEM = (AM == 3);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   char* const smem = reinterpret_cast<char*>(smem_raw);
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -247,7 +247,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
     const int m = m0 + (wid * G::APW + j) * 8 + prow;
     const bool ok = m < M;
     a_msk[j] = 0;
-    if (!IM2COL) {
+    if (STEM) {
+      // pre-padded bf16 RGBA, k = kh*32 + kw*4 + c: a k-tile is filter rows
+      // (2t, 2t+1) x 8 taps x 4 channels = 2 runs of 64 contiguous bytes; this
+      // lane's logical chunk lc holds row lc>>2, pixels 2*(lc&3) .. +1
+      const int lc = (lane & 7) ^ prow;
+      const int mm = ok ? m : 0;
+      const int hw = p.Ho * p.Wo;
+      const int n = mm / hw, r = mm - n * hw;
+      const int ho = r / p.Wo, wo = r - ho * p.Wo;
+      a_off[j] = ok ? uint32_t(((n * p.H + ho * p.SH + (lc >> 2)) * p.W + wo * p.SW + (lc & 3) * 2) * 4) * 2u : kOOB;
+    } else if (!IM2COL) {
       a_off[j] = ok ? (uint32_t(m) * uint32_t(p.lda) + kc) * 2u : kOOB;
       if constexpr (DUAL) {
         const int mm = ok ? m : 0;
@@ -299,7 +309,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   }
 
   auto issue = [&](int slot) {
-    const uint32_t a_soff = IM2COL ? uint32_t((w_kh * p.W + w_kw) * p.C + w_ci) * 2u : uint32_t(w_k) * 2u;
+    const uint32_t a_soff = IM2COL ? uint32_t((w_kh * p.W + w_kw) * p.C + w_ci) * 2u
+                            : STEM ? uint32_t(w_k >> 6) * uint32_t(p.W) * 16u   // 2 filter rows per k-tile
+                                   : uint32_t(w_k) * 2u;
     const uint32_t b_soff = uint32_t(w_k) * 2u;
     if (DUAL && w_k >= p.K1) {   // wave-uniform: the k-tile lies in the second source
       const uint32_t soff2 = uint32_t(w_k - p.K1) * 2u;
@@ -515,6 +527,9 @@ bool cgemm_supported(const IGemmArgs& a, int a_mode) {
   if (a_mode == kAIm2col)
     return a.C % KT == 0 && a.KH * a.KW <= 32 && a.K == a.KH * a.KW * a.C &&
            a.a_bytes + int64_t(a.PT * a.W + a.PL) * a.C * 2 < 0x7ffffff0LL;
+  if (a_mode == kAC4)
+    return a.C == 4 && a.KW == 8 && a.KH % 2 == 0 && a.K == a.KH * 32 && a.PT == 0 && a.PL == 0 &&
+           a.H >= (a.Ho - 1) * a.SH + a.KH && a.W >= (a.Wo - 1) * a.SW + a.KW;
   if (a_mode == kADual)
     return a.a2 && a.K1 > 0 && a.K1 % KT == 0 && a.lda % 8 == 0 && a.lda >= a.K1 && a.C % KT == 0 &&
            a.K == a.K1 + a.C && a.KH == 1 && a.KW == 1 && a.PT == 0 && a.PL == 0 && a.a2_bytes < 0x7ffffff0LL;
@@ -531,6 +546,7 @@ hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) 
   switch (a_mode) {
     case kAIm2col: return launch_mode<1>(a, cfg, s);
     case kADual: return launch_mode<2>(a, cfg, s);
+    case kAC4: return launch_mode<3>(a, cfg, s);
     default: return launch_mode<0>(a, cfg, s);
   }
 }

@@ -54,6 +54,10 @@ enum AMode : int { kADense = 0, kAIm2col = 1, kAStemF32 = 2, kAStem7x7x3 = 3, kA
 // fp32 NHWC with C <= 4 channels -> bf16 NHWC with 4 channels (zero padded).
 hipError_t ingest_c4_launch(const float* x, uint16_t* y, int64_t pixels, int C, hipStream_t stream);
 
+// Same into a zero-bordered [N][Hp][Wp][4] buffer (image placed at row pt, column pl).
+hipError_t ingest_c4_pad_launch(const float* x, uint16_t* y, int N, int H, int W, int C, int Hp, int Wp, int pt,
+                               int pl, hipStream_t stream);
+
 // Sum split-K partial slabs and apply the epilogue (bias, residual, act, store).
 hipError_t splitk_reduce_launch(const IGemmArgs& args, hipStream_t stream);
 

@@ -305,6 +305,26 @@ __global__ void ingest_rgb4_kernel(const float4* __restrict__ x, uint4* __restri
   }
 }
 
+// fp32 NHWC (C <= 4) -> bf16 RGBA into a zero-bordered [N][Hp][Wp][4] buffer
+// (image at row pt, column pl): the stem conv then runs without padding, so
+// every 16-B operand chunk it DMAs (2 pixels x 4 channels) is in bounds.
+__global__ void ingest_c4_pad_kernel(const float* __restrict__ x, uint2* __restrict__ y, int N, int H, int W, int C,
+                                     int Hp, int Wp, int pt, int pl) {
+  const long total = long(N) * Hp * Wp;
+  for (long i = blockIdx.x * long(blockDim.x) + threadIdx.x; i < total; i += long(gridDim.x) * blockDim.x) {
+    const int xo = int(i % Wp);
+    const long r = i / Wp;
+    const int yo = int(r % Hp), n = int(r / Hp);
+    const int yi = yo - pt, xi = xo - pl;
+    uint16_t v[4] = {0, 0, 0, 0};
+    if ((unsigned)yi < (unsigned)H && (unsigned)xi < (unsigned)W) {
+      const float* src = x + ((long(n) * H + yi) * W + xi) * C;
+      for (int c = 0; c < C; ++c) v[c] = f32_to_bf16(src[c]);
+    }
+    y[i] = make_uint2(v[0] | (uint32_t(v[1]) << 16), v[2] | (uint32_t(v[3]) << 16));
+  }
+}
+
 int grid_for(long work, int block) {
   long g = (work + block - 1) / block;
   if (g > 256 * 16) g = 256 * 16;
@@ -349,6 +369,14 @@ hipError_t ingest_c4_launch(const float* x, uint16_t* y, int64_t pixels, int C, 
     return hipGetLastError();
   }
   hipLaunchKernelGGL(ingest_c4_kernel, dim3(grid_for(pixels, 256)), dim3(256), 0, s, x, y, long(pixels), C);
+  return hipGetLastError();
+}
+
+hipError_t ingest_c4_pad_launch(const float* x, uint16_t* y, int N, int H, int W, int C, int Hp, int Wp, int pt,
+                               int pl, hipStream_t s) {
+  const long total = long(N) * Hp * Wp;
+  hipLaunchKernelGGL(ingest_c4_pad_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, x,
+                     reinterpret_cast<uint2*>(y), N, H, W, C, Hp, Wp, pt, pl);
   return hipGetLastError();
 }
 

@@ -101,7 +101,7 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
     for cfg, (bm, bn) in TILES.items():
         if cfg in DMA_ONLY and (not dma or (cfg in (4, 5, 6, 7) and nk < 3)):
             continue
-        if cfg in CGEMM and not (aligned64 and dma and K % 64 == 0 and N % 8 == 0):
+        if cfg in CGEMM and not (aligned64 and K % 64 == 0 and N % 8 == 0):
             continue
         if cgemm_only and cfg not in CGEMM:
             continue

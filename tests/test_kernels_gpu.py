@@ -197,6 +197,28 @@ def test_rgba_stem_path(k, c):
         assert (y.float().cpu() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("k,c,s", [(7, 3, 2), (3, 3, 1), (5, 4, 2), (1, 3, 1)])
+@pytest.mark.parametrize("cfg", [36, 42, 43, 44, 32])
+def test_cgemm_padded_rgba_stem(k, c, s, cfg):
+    """ingest_c4_padded (zero-bordered bf16 RGBA) + cgemm stem mode (even kh,
+    8 taps: every operand chunk is two in-bounds pixels) vs the fp32 conv."""
+    n, h, w = 3, 37, 29
+    x = torch.rand(n, h, w, c)
+    wt = rnd(k, k, c, 64, scale=0.1, seed=17).to(BF).float()
+    b = rnd(64, scale=0.1, seed=18)
+    pt, pb, pl, pr = k // 2, (k - 1) // 2, k // 2, (k - 1) // 2
+    ho, wo = (h + pt + pb - k) // s + 1, (w + pl + pr - k) // s + 1
+    khp = k + k % 2
+    w4 = torch.zeros(khp, 8, 4, 64)
+    w4[:k, :k, :c, :] = wt
+    wp = w4.permute(3, 0, 1, 2).reshape(64, khp * 32).to(BF).contiguous().to(DEV)
+    xp = hip().ingest_c4_padded(x.to(DEV), (ho - 1) * s + khp, (wo - 1) * s + 8, pt, pl)
+    y = hip().conv2d(xp, wp, b.to(DEV), None, khp, 8, s, s, 0, 0, 0, 0, act=ACT["relu"], cfg=cfg)
+    ref = ref_conv(x.to(BF).float(), wt, b, s, (pt, pb, pl, pr), None, "relu")
+    assert y.shape == ref.shape
+    assert (y.float().cpu() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+
 def test_asymmetric_identity_gemm():
     """A = I, asymmetric B: catches a transposed C write (guide §3)."""
     m = n = 64
