@@ -154,6 +154,54 @@ def _fold(g: Graph, order: List[str], fed: Set[str]) -> None:
         node.ctrl = []
 
 
+# Pure ops that are safe to merge when they have identical inputs and attrs.
+_CSE_OPS = {"Add", "AddV2", "Sub", "Mul", "RealDiv", "Maximum", "Minimum", "Neg", "ExpandDims", "Reshape",
+            "Squeeze", "Cast", "Transpose", "StridedSlice", "Identity", "Exp", "Rsqrt", "Sqrt", "Tanh", "Relu",
+            "Pow", "SquaredDifference", "Mean", "Sum", "ConcatV2", "Pack", "Shape", "Fill", "Tile", "GatherV2",
+            "OneHot", "BiasAdd", "Softmax", "Erf"}
+
+
+def _attrs_key(attrs) -> Optional[str]:
+    try:
+        return repr(sorted((k, v) for k, v in attrs.items() if not isinstance(v, torch.Tensor)))
+    except TypeError:
+        return None
+
+
+def cse(graph: Graph, order: Sequence[str], fed_nodes: Set[str], fetch_refs) -> int:
+    """Common-subexpression elimination: small constants with equal values and
+    pure ops with identical (op, inputs, attrs) collapse onto one node.  BERT's
+    TF graph, for one, recomputes the attention-mask adder ``(1 - mask) *
+    -10000`` in every layer: 12 copies of three elementwise kernels per batch
+    become one.  Returns the number of nodes merged."""
+    fetch_nodes = {n for n, _ in fetch_refs}
+    rep: Dict[str, str] = {}
+    seen: Dict[tuple, str] = {}
+    for name in order:
+        n = graph.nodes[name]
+        if rep:
+            n.inputs = [(rep.get(s, s), i) for s, i in n.inputs]
+            n.ctrl = [rep.get(c, c) for c in n.ctrl]
+        if name in fetch_nodes or name in fed_nodes or n.ctrl:
+            continue
+        key = None
+        if n.op == "Const":
+            v = n.value[0] if n.value else const_value(n)
+            if isinstance(v, torch.Tensor) and v.numel() <= 64 and (not n.value or len(n.value) == 1):
+                key = ("Const", str(v.dtype), tuple(v.shape), v.detach().cpu().numpy().tobytes())
+        elif n.op in _CSE_OPS:
+            ak = _attrs_key(n.attrs)
+            if ak is not None:
+                key = (n.op, tuple(n.inputs), ak)
+        if key is None:
+            continue
+        if key in seen:
+            rep[name] = seen[key]
+        else:
+            seen[key] = name
+    return len(rep)
+
+
 def compile_program(graph: Graph, feeds: Sequence[str], fetches: Sequence[str],
                     device: torch.device = torch.device("cpu"), passes: Sequence = (),
                     pass_options: Optional[dict] = None) -> Program:
@@ -167,6 +215,8 @@ def compile_program(graph: Graph, feeds: Sequence[str], fetches: Sequence[str],
     order = graph.topo([n for n, _ in fetch_refs], stop=fed_nodes)
     _fold(graph, order, fed_nodes)
     order = graph.topo([n for n, _ in fetch_refs], stop=fed_nodes)
+    if cse(graph, order, fed_nodes, fetch_refs):
+        order = graph.topo([n for n, _ in fetch_refs], stop=fed_nodes)
     for p in passes:
         p(graph, order, fed_nodes, fetch_refs, device, pass_options or {})
         order = graph.topo([n for n, _ in fetch_refs], stop=fed_nodes)

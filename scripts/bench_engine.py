@@ -19,17 +19,31 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[1, 32])
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--baseline", action="store_true")
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert-base"])
     args = ap.parse_args()
-    from rust_tensorflow_serving2_amd.models import resnet
+    from rust_tensorflow_serving2_amd.models import bert, resnet
     from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
     path = os.path.join(tempfile.mkdtemp(), "1")
-    resnet.export(path)
-    s = Servable("resnet", 1, path, ServableOptions(device="cuda:0", max_batch_size=max(args.batch)))
-    r = s.runner("serving_default", ["input"], ["classes", "probabilities"])
+    opts = ServableOptions(device="cuda:0", max_batch_size=max(args.batch))
+    if args.model == "bert-base":
+        bert.export(path, seed=0)
+        s = Servable("bert", 1, path, opts)
+        r = s.runner("serving_default", ["input_ids", "input_mask", "segment_ids"], ["pooled_output", "probabilities"])
+        flop_per_item = 2 * 85e6 * 128 + 4 * 12 * 128 * 128 * 768   # encoder GEMMs + attention, seq 128
+    else:
+        resnet.export(path)
+        s = Servable("resnet", 1, path, opts)
+        r = s.runner("serving_default", ["input"], ["classes", "probabilities"])
+        flop_per_item = 2 * 4.1e9
     res = {}
     for b in args.batch:
-        x = np.random.default_rng(0).random((b, 224, 224, 3), dtype=np.float32)
-        r.run([x])  # capture
+        rng = np.random.default_rng(0)
+        if args.model == "bert-base":
+            x = [rng.integers(0, 30522, (b, 128)).astype(np.int32), np.ones((b, 128), np.int32),
+                 np.zeros((b, 128), np.int32)]
+        else:
+            x = [rng.random((b, 224, 224, 3), dtype=np.float32)]
+        r.run(x)  # capture
         bucket = r._bucket(b)
         g = next(l.graphs[bucket] for l in r.lanes if bucket in l.graphs)
         torch.cuda.synchronize()
@@ -44,12 +58,12 @@ def main():
         # full runner path: H2D + replay + D2H
         t = time.perf_counter()
         for _ in range(args.iters // 2):
-            r.run([x])
+            r.run(x)
         dt_full = (time.perf_counter() - t) / (args.iters // 2)
         res[b] = {"graph_ms": dt * 1e3, "img_per_s": b / dt, "run_ms": dt_full * 1e3,
-                  "tflops": 2 * 4.1e9 * b / dt / 1e12}
-        print(json.dumps({"batch": b, **res[b]}), flush=True)
-    if args.baseline:
+                  "tflops": flop_per_item * b / dt / 1e12}
+        print(json.dumps({"model": args.model, "batch": b, **res[b]}), flush=True)
+    if args.baseline and args.model == "resnet50":
         baseline(args)
 
 
