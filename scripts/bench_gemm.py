@@ -73,6 +73,11 @@ def gemm_case(m, n, k):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--gemm-only":
+        for c in (gemm_case(4096, 4096, 4096), gemm_case(4096, 3072, 768), gemm_case(4096, 2304, 768),
+                  gemm_case(4096, 768, 3072), gemm_case(4096, 768, 768)):
+            print(json.dumps(c), flush=True)
+        return
     cases = [
         conv_case(32, 56, 56, 64, 64, 3, 1, 1),
         conv_case(32, 56, 56, 64, 256, 1, 1, 0),
@@ -82,7 +87,10 @@ def main():
         conv_case(32, 7, 7, 512, 2048, 1, 1, 0),
         gemm_case(32, 1001, 2048),
         gemm_case(4096, 4096, 4096),
-        gemm_case(4096, 3072, 768),
+        gemm_case(4096, 3072, 768),      # BERT-base b32 FFN1
+        gemm_case(4096, 2304, 768),      # fused QKV
+        gemm_case(4096, 768, 3072),      # FFN2
+        gemm_case(4096, 768, 768),       # attention output projection
     ]
     for c in cases:
         print(json.dumps(c), flush=True)
