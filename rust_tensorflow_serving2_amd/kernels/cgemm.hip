@@ -59,6 +59,16 @@ struct CG {
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
+// a / d for 0 <= a < 2^24, d >= 1 via the float reciprocal `inv` = 1/d (one
+// multiply + a +-1 fix-up, ~8 VALU instead of the ~35 of an integer division):
+// the per-lane im2col setup divides every DMA row's pixel index twice.
+__device__ __forceinline__ int fdiv(int a, int d, float inv) {
+  int q = int(float(a) * inv);
+  const int r = a - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
 // s_waitcnt vmcnt(N) only (expcnt / lgkmcnt at their maxima; gfx9 encoding).
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -241,6 +251,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
       const_cast<void*>(DUAL ? p.a2 : p.a), 0, int(DUAL ? p.a2_bytes : p.a_bytes), 0x00020000);
 
   // ---- per-lane DMA offsets (computed once)
+  const float inv_hw = 1.f / float(p.Ho * p.Wo), inv_wo = 1.f / float(p.Wo);
   uint32_t a_off[G::APW], a_msk[G::APW], a_off2[DUAL ? G::APW : 1];
 #pragma unroll
   for (int j = 0; j < G::APW; ++j) {
@@ -254,23 +265,23 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
       const int lc = (lane & 7) ^ prow;
       const int mm = ok ? m : 0;
       const int hw = p.Ho * p.Wo;
-      const int n = mm / hw, r = mm - n * hw;
-      const int ho = r / p.Wo, wo = r - ho * p.Wo;
+      const int n = fdiv(mm, hw, inv_hw), r = mm - n * hw;
+      const int ho = fdiv(r, p.Wo, inv_wo), wo = r - ho * p.Wo;
       a_off[j] = ok ? uint32_t(((n * p.H + ho * p.SH + (lc >> 2)) * p.W + wo * p.SW + (lc & 3) * 2) * 4) * 2u : kOOB;
     } else if (!IM2COL) {
       a_off[j] = ok ? (uint32_t(m) * uint32_t(p.lda) + kc) * 2u : kOOB;
       if constexpr (DUAL) {
         const int mm = ok ? m : 0;
         const int hw = p.Ho * p.Wo;
-        const int n = mm / hw, r = mm - n * hw;
-        const int ho = r / p.Wo, wo = r - ho * p.Wo;
+        const int n = fdiv(mm, hw, inv_hw), r = mm - n * hw;
+        const int ho = fdiv(r, p.Wo, inv_wo), wo = r - ho * p.Wo;
         a_off2[j] = ok ? (uint32_t((n * p.H + ho * p.SH) * p.W + wo * p.SW) * uint32_t(p.C) + kc) * 2u : kOOB;
       }
     } else {
       const int mm = ok ? m : 0;
       const int hw = p.Ho * p.Wo;
-      const int n = mm / hw, r = mm - n * hw;
-      const int ho = r / p.Wo, wo = r - ho * p.Wo;
+      const int n = fdiv(mm, hw, inv_hw), r = mm - n * hw;
+      const int ho = fdiv(r, p.Wo, inv_wo), wo = r - ho * p.Wo;
       const int hb = ho * p.SH, wb = wo * p.SW;          // tap (0,0) in padded coordinates
       a_off[j] = (uint32_t((n * p.H + hb) * p.W + wb) * uint32_t(p.C) + kc) * 2u;
       // tap t = kh*KW + kw is valid iff row hi0+kh and column wi0+kw are inside
@@ -523,6 +534,7 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
 bool cgemm_supported(const IGemmArgs& a, int a_mode) {
   if (a.K <= 0 || a.K % KT || a.ldb % 8 || a.ldb < a.K) return false;
   if (a.N % 8 || a.ldc % 8 || (a.residual && a.ldr % 8)) return false;   // 16-B epilogue chunks only
+  if (a.M >= (1 << 23)) return false;   // fdiv() row-index decomposition is exact below 2^23
   if (a_mode == kADense) return a.lda % 8 == 0 && a.lda >= a.K;
   if (a_mode == kAIm2col)
     return a.C % KT == 0 && a.KH * a.KW <= 32 && a.K == a.KH * a.KW * a.C &&
