@@ -170,9 +170,13 @@ def main():
     conc = args.concurrency or 4 * args.batch
     per_step = max(1, args.batch // args.request_batch)
 
+    # one persistent client: connections (TCP + HTTP/2 handshakes, window
+    # ramp-up) are set up before warmup and reused by the timed run, as a
+    # serving client keeps its channel open
+    loadgen = _C.LoadGen("127.0.0.1", server.port, PREDICT, bodies, conc, args.connections, args.client_threads)
+
     def drive(n):
-        return _C.run_loadgen("127.0.0.1", server.port, PREDICT, bodies, n, conc, args.connections,
-                              args.client_threads, 600.0)
+        return loadgen.run(n, 600.0)
 
     w = drive(max(per_step, args.warmup * per_step))
     if w["errors"]:

@@ -146,6 +146,24 @@ struct LoadGenResult {
   double cpu_s = 0;                 // CPU time of the client threads
 };
 
+// Persistent load generator: `threads` client threads each own a share of
+// `connections` HTTP/2 connections, opened once in the constructor (like a
+// real client's channel) and reused by every run(); `concurrency` unary calls
+// of `method` stay in flight, bodies used round-robin (pre-serialised).
+class LoadGen {
+ public:
+  LoadGen(const std::string& host, int port, const std::string& method, const std::vector<std::string>& bodies,
+          int concurrency, int connections, int threads);
+  ~LoadGen();
+  LoadGenResult run(uint64_t total, double timeout_s);
+  struct Worker;
+
+ private:
+  std::shared_ptr<void> sh_;       // shared request state (type private to the .cpp)
+  void* cbs_ = nullptr;            // nghttp2_session_callbacks*
+  std::vector<std::unique_ptr<Worker>> workers_;
+};
+
 // Drive `total` unary calls of `method` against host:port with `concurrency`
 // streams in flight spread over `connections` HTTP/2 connections served by
 // `threads` client threads.  Bodies are used round-robin (pre-serialised).

@@ -272,7 +272,7 @@ bool cflush(ClientConn* c, int ep, uint64_t tag) {
   return true;
 }
 
-void client_thread(Shared* sh, const std::string& host, int port, int nconn, int per_conn, LoadGenResult* out) {
+nghttp2_session_callbacks* make_callbacks() {
   nghttp2_session_callbacks* cbs;
   nghttp2_session_callbacks_new(&cbs);
   nghttp2_session_callbacks_set_on_header_callback(cbs, on_header);
@@ -281,40 +281,101 @@ void client_thread(Shared* sh, const std::string& host, int port, int nconn, int
   nghttp2_session_callbacks_set_data_source_read_length_callback(cbs, read_length);
   nghttp2_session_callbacks_set_send_callback(cbs, on_send);
   nghttp2_session_callbacks_set_send_data_callback(cbs, on_send_data);
-  int ep = epoll_create1(0);
+  return cbs;
+}
+
+}  // namespace
+
+// One client thread's connections (HTTP/2 sessions + epoll set); they persist
+// across LoadGen::run() calls like a real client's channel does.
+struct LoadGen::Worker {
+  int ep = -1;
   std::vector<std::unique_ptr<ClientConn>> conns;
-  for (int i = 0; i < nconn; ++i) {
-    auto c = std::make_unique<ClientConn>();
-    try {
-      c->fd = connect_to(host, port);
-    } catch (const std::exception& e) {
-      if (out->first_error.empty()) out->first_error = e.what();
-      out->errors++;
-      continue;
+  LoadGenResult part;
+  std::string connect_error;
+  ~Worker() {
+    for (auto& c : conns) {
+      if (c->sess) nghttp2_session_del(c->sess);
+      if (c->fd >= 0) ::close(c->fd);
     }
-    c->sh = sh;
-    c->target = per_conn;
+    if (ep >= 0) ::close(ep);
+  }
+};
+
+LoadGen::LoadGen(const std::string& host, int port, const std::string& method,
+                 const std::vector<std::string>& bodies, int concurrency, int connections, int threads) {
+  if (bodies.empty()) throw std::invalid_argument("no request bodies");
+  auto shp = std::make_shared<Shared>();
+  sh_ = shp;
+  Shared* sh = shp.get();
+  sh->path = method;
+  sh->authority = host + ":" + std::to_string(port);
+  for (auto& b : bodies) {
+    std::string f(5 + b.size(), '\0');
+    grpc_frame_header(reinterpret_cast<uint8_t*>(&f[0]), uint32_t(b.size()));
+    memcpy(&f[5], b.data(), b.size());
+    sh->framed.push_back(std::move(f));
+  }
+  cbs_ = make_callbacks();
+  threads = std::max(1, std::min(threads, connections));
+  connections = std::max(connections, threads);
+  const int per_conn = std::max(1, concurrency / connections);
+  for (int t = 0; t < threads; ++t) {
+    auto w = std::make_unique<Worker>();
+    w->ep = epoll_create1(0);
+    const int nconn = connections / threads + (t < connections % threads ? 1 : 0);
+    for (int i = 0; i < nconn; ++i) {
+      auto c = std::make_unique<ClientConn>();
+      try {
+        c->fd = connect_to(host, port);
+      } catch (const std::exception& e) {
+        if (w->connect_error.empty()) w->connect_error = e.what();
+        continue;
+      }
+      c->sh = sh;
+      c->target = per_conn;
+      c->next_body = uint64_t(t * 131 + i) * 7919;
+      nghttp2_session_client_new(&c->sess, static_cast<nghttp2_session_callbacks*>(cbs_), c.get());
+      nghttp2_settings_entry iv[] = {{NGHTTP2_SETTINGS_MAX_CONCURRENT_STREAMS, 4096},
+                                     {NGHTTP2_SETTINGS_INITIAL_WINDOW_SIZE, 16u << 20}};
+      nghttp2_submit_settings(c->sess, NGHTTP2_FLAG_NONE, iv, 2);
+      nghttp2_session_set_local_window_size(c->sess, NGHTTP2_FLAG_NONE, 0, 1 << 30);
+      epoll_event ev{};
+      ev.events = EPOLLIN;
+      ev.data.u64 = w->conns.size();
+      epoll_ctl(w->ep, EPOLL_CTL_ADD, c->fd, &ev);
+      w->conns.push_back(std::move(c));
+    }
+    workers_.push_back(std::move(w));
+  }
+}
+
+LoadGen::~LoadGen() {
+  workers_.clear();
+  if (cbs_) nghttp2_session_callbacks_del(static_cast<nghttp2_session_callbacks*>(cbs_));
+}
+
+namespace {
+
+void worker_loop(LoadGen::Worker* w, Shared* sh) {
+  LoadGenResult* out = &w->part;
+  if (!w->connect_error.empty()) {
+    out->first_error = w->connect_error;
+    out->errors++;
+  }
+  auto& conns = w->conns;
+  for (auto& c : conns) {
     c->lat = &out->latency_us;
     c->ok = &out->ok;
     c->err = &out->errors;
     c->first_error = &out->first_error;
     c->bytes_sent = &out->bytes_sent;
     c->bytes_recv = &out->bytes_recv;
-    c->next_body = uint64_t(i) * 7919;
-    nghttp2_session_client_new(&c->sess, cbs, c.get());
-    nghttp2_settings_entry iv[] = {{NGHTTP2_SETTINGS_MAX_CONCURRENT_STREAMS, 4096},
-                                   {NGHTTP2_SETTINGS_INITIAL_WINDOW_SIZE, 16u << 20}};
-    nghttp2_submit_settings(c->sess, NGHTTP2_FLAG_NONE, iv, 2);
-    nghttp2_session_set_local_window_size(c->sess, NGHTTP2_FLAG_NONE, 0, 1 << 30);
-    epoll_event ev{};
-    ev.events = EPOLLIN;
-    ev.data.u64 = conns.size();
-    epoll_ctl(ep, EPOLL_CTL_ADD, c->fd, &ev);
-    conns.push_back(std::move(c));
   }
   for (size_t i = 0; i < conns.size(); ++i) {
+    if (conns[i]->dead) continue;
     while (submit_one(conns[i].get())) {}
-    if (!cflush(conns[i].get(), ep, i)) conns[i]->dead = true;
+    if (!cflush(conns[i].get(), w->ep, i)) conns[i]->dead = true;
   }
   std::vector<uint8_t> rbuf(1 << 20);
   std::vector<epoll_event> evs(64);
@@ -327,7 +388,7 @@ void client_thread(Shared* sh, const std::string& host, int port, int nconn, int
       if (out->first_error.empty()) out->first_error = "load generator timed out";
       break;
     }
-    int n = epoll_wait(ep, evs.data(), int(evs.size()), 100);
+    int n = epoll_wait(w->ep, evs.data(), int(evs.size()), 100);
     for (int i = 0; i < n; ++i) {
       const uint64_t idx = evs[i].data.u64;
       ClientConn* c = conns[idx].get();
@@ -344,56 +405,45 @@ void client_thread(Shared* sh, const std::string& host, int port, int nconn, int
           break;
         }
       }
-      if (!c->dead && !cflush(c, ep, idx)) c->dead = true;
+      if (!c->dead && !cflush(c, w->ep, idx)) c->dead = true;
       if (c->dead && out->first_error.empty()) out->first_error = "connection lost";
     }
   }
   for (auto& c : conns) {
-    out->errors += uint64_t(std::max(0, c->inflight));
-    if (c->sess) nghttp2_session_del(c->sess);
-    if (c->fd >= 0) ::close(c->fd);
+    if (c->dead && c->inflight > 0) {   // requests lost with a dead connection
+      out->errors += uint64_t(c->inflight);
+      c->inflight = 0;
+    }
   }
-  ::close(ep);
-  nghttp2_session_callbacks_del(cbs);
 }
 
 }  // namespace
 
-LoadGenResult run_loadgen(const std::string& host, int port, const std::string& method,
-                          const std::vector<std::string>& bodies, uint64_t total, int concurrency, int connections,
-                          int threads, double timeout_s) {
-  if (bodies.empty()) throw std::invalid_argument("no request bodies");
-  Shared sh;
-  sh.path = method;
-  sh.authority = host + ":" + std::to_string(port);
-  sh.total = total;
-  sh.deadline = Clock::now() + std::chrono::microseconds(int64_t(timeout_s * 1e6));
-  for (auto& b : bodies) {
-    std::string f(5 + b.size(), '\0');
-    grpc_frame_header(reinterpret_cast<uint8_t*>(&f[0]), uint32_t(b.size()));
-    memcpy(&f[5], b.data(), b.size());
-    sh.framed.push_back(std::move(f));
-  }
-  threads = std::max(1, std::min(threads, connections));
-  connections = std::max(connections, threads);
-  const int per_conn = std::max(1, concurrency / connections);
-  std::vector<LoadGenResult> parts(threads);
+LoadGenResult LoadGen::run(uint64_t total, double timeout_s) {
+  Shared* sh = static_cast<Shared*>(sh_.get());
+  sh->total = total;
+  sh->issued = 0;
+  sh->finished = 0;
+  sh->deadline = Clock::now() + std::chrono::microseconds(int64_t(timeout_s * 1e6));
   std::vector<std::thread> ts;
   const auto t0 = Clock::now();
-  for (int t = 0; t < threads; ++t) {
-    const int nconn = connections / threads + (t < connections % threads ? 1 : 0);
-    ts.emplace_back([&, t, nconn] {
+  for (auto& wp : workers_) {
+    wp->part = LoadGenResult();
+    LoadGen::Worker* w = wp.get();
+    ts.emplace_back([w, sh] {
       pthread_setname_np(pthread_self(), "tfs-loadgen");
-      client_thread(&sh, host, port, nconn, per_conn, &parts[t]);
-      timespec ts{};
-      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
-      parts[t].cpu_s = double(ts.tv_sec) + 1e-9 * double(ts.tv_nsec);
+      timespec a{}, b{};
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &a);
+      worker_loop(w, sh);
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &b);
+      w->part.cpu_s = double(b.tv_sec - a.tv_sec) + 1e-9 * double(b.tv_nsec - a.tv_nsec);
     });
   }
   for (auto& t : ts) t.join();
   LoadGenResult res;
   res.elapsed_s = std::chrono::duration<double>(Clock::now() - t0).count();
-  for (auto& p : parts) {
+  for (auto& w : workers_) {
+    const LoadGenResult& p = w->part;
     res.ok += p.ok;
     res.errors += p.errors;
     res.bytes_sent += p.bytes_sent;
@@ -403,6 +453,13 @@ LoadGenResult run_loadgen(const std::string& host, int port, const std::string& 
     if (res.first_error.empty()) res.first_error = p.first_error;
   }
   return res;
+}
+
+LoadGenResult run_loadgen(const std::string& host, int port, const std::string& method,
+                          const std::vector<std::string>& bodies, uint64_t total, int concurrency, int connections,
+                          int threads, double timeout_s) {
+  LoadGen lg(host, port, method, bodies, concurrency, connections, threads);
+  return lg.run(total, timeout_s);
 }
 
 }  // namespace tfs

@@ -484,6 +484,29 @@ void register_server(py::module_& m) {
         return d;
       });
 
+  py::class_<LoadGen>(m, "LoadGen")
+      .def(py::init([](const std::string& host, int port, const std::string& method, const py::list& bodies,
+                       int concurrency, int connections, int threads) {
+             std::vector<std::string> b;
+             for (auto x : bodies) b.push_back(x.cast<std::string>());
+             py::gil_scoped_release nogil;
+             return std::make_unique<LoadGen>(host, port, method, b, concurrency, connections, threads);
+           }),
+           py::arg("host"), py::arg("port"), py::arg("method"), py::arg("bodies"), py::arg("concurrency") = 64,
+           py::arg("connections") = 8, py::arg("threads") = 4)
+      .def("run", [](LoadGen& lg, uint64_t total, double timeout_s) {
+        LoadGenResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = lg.run(total, timeout_s);
+        }
+        py::dict d;
+        d["ok"] = r.ok; d["errors"] = r.errors; d["elapsed_s"] = r.elapsed_s;
+        d["latency_us"] = r.latency_us; d["first_error"] = r.first_error;
+        d["bytes_sent"] = r.bytes_sent; d["bytes_recv"] = r.bytes_recv; d["cpu_s"] = r.cpu_s;
+        return d;
+      }, py::arg("total"), py::arg("timeout_s") = 120.0);
+
   m.def("run_loadgen", [](const std::string& host, int port, const std::string& method, const py::list& bodies,
                           uint64_t total, int concurrency, int connections, int threads, double timeout_s) {
     std::vector<std::string> b;

@@ -67,6 +67,21 @@ def test_native_loadgen(nserver):
     assert r["errors"] == 10 and "grpc-status 5" in r["first_error"]
 
 
+def test_persistent_loadgen_reuses_connections(nserver):
+    """LoadGen opens its HTTP/2 connections once; repeated runs (warmup, then
+    the timed window in bench.py) reuse them and count only their own calls."""
+    body = native.encode_predict_request(native.spec_tuple("hpt", None, None, ""), {"x": np.ones((3, 1), np.float32)})
+    lg = _C.LoadGen("127.0.0.1", nserver.port, "/tensorflow.serving.PredictionService/Predict", [body], 16, 4, 2)
+    assert lg.run(1, 60.0)["ok"] == 1     # every connection accepted by now
+    before = nserver.transports[0].stats()["connections"]
+    for n in (50, 200, 7):
+        r = lg.run(n, 60.0)
+        assert r["ok"] == n and r["errors"] == 0, r["first_error"]
+        assert len(r["latency_us"]) == n
+    assert nserver.transports[0].stats()["connections"] == before   # no new connections per run
+    del lg
+
+
 def test_native_loadgen_large_bodies(nserver):
     """Multi-frame (zero-copy DATA) requests of different sizes on shared connections."""
     bodies = [native.encode_predict_request(native.spec_tuple("hpt", None, None, ""),
