@@ -10,7 +10,9 @@
 //                           x S/16 columns; row max/sum via 16-lane xor shuffles
 //   ctx = P V               P re-laid out through a per-wave LDS strip into the
 //                           A-operand layout; V stored transposed (Vt[d][key],
-//                           rows padded by 16 B) so B fragments are 16-B reads
+//                           rows padded by 16 B) so B fragments are 16-B reads;
+//                           the transpose is done in registers on 8x8 blocks
+//                           so staging is 16-B loads and 16-B LDS stores
 // S <= 256, S % 32 == 0, D == 64.  The S x S matrix never touches HBM.
 #include "common.h"
 #include "launch.h"
@@ -20,20 +22,25 @@ namespace tfsk {
 namespace {
 
 constexpr int D = 64;
-constexpr int QB = 64;       // query rows per workgroup (4 waves x 16)
 
-template <int S>
-__global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restrict__ qkv,
-                                                        const float* __restrict__ mask_bias,
-                                                        uint16_t* __restrict__ ctx, int H, float scale,
-                                                        long mask_bstride, long mask_qstride) {
+// query rows per workgroup (16 per wave).  64 measured faster than one
+// workgroup per (batch, head) with QB = S at BERT-base b32 S=128 (161 vs 182 us
+// per 12 layers): twice the workgroups outweigh staging K/V twice.
+constexpr int qb_for(int) { return 64; }
+
+template <int S, int QB>
+__global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __restrict__ qkv,
+                                                           const float* __restrict__ mask_bias,
+                                                           uint16_t* __restrict__ ctx, int H, float scale,
+                                                           long mask_bstride, long mask_qstride) {
+  constexpr int NTH = QB * 4;            // QB / 16 waves
   constexpr int VT_LD = S + 8;           // Vt row stride (elements): +16 B pad
   constexpr int P_LD = S + 8;
   constexpr int NT = S / 16;             // key tiles
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);          // [S][64] swizzled
   uint16_t* Vt = Ks + S * D;                                  // [64][VT_LD]
-  uint16_t* Ps = Vt + D * VT_LD;                              // [4][16][P_LD]
+  uint16_t* Ps = Vt + D * VT_LD;                              // [QB/16][16][P_LD]
 
   const int qblocks = S / QB;
   const int bid = blockIdx.x;
@@ -45,17 +52,33 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
   const long row_stride = 3L * H * D;
   const uint16_t* base = qkv + long(b) * S * row_stride;
 
-  // ---- stage K (row-major, swizzled) and V (transposed) for this (b, h)
-  for (int c = tid; c < S * 8; c += 256) {
+  // ---- stage K (row-major, XOR-swizzled 16-B chunks)
+  for (int c = tid; c < S * 8; c += NTH) {
     const int key = c >> 3, ch = c & 7;
     const uint4 kv = *reinterpret_cast<const uint4*>(base + long(key) * row_stride + H * D + h * D + ch * 8);
     *reinterpret_cast<uint4*>(Ks + key * D + ((ch ^ (key & 7)) * 8)) = kv;
-    const uint4 vv = *reinterpret_cast<const uint4*>(base + long(key) * row_stride + 2 * H * D + h * D + ch * 8);
-    const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+  }
+  // ---- stage V transposed: an 8-key x 8-dim block per step, transposed in
+  // registers (8 x 16-B loads in, 8 x 16-B LDS stores out)
+  for (int blk = tid; blk < (S / 8) * 8; blk += NTH) {
+    const int kg = blk >> 3, ch = blk & 7;
+    uint32_t w[8][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      Vt[(ch * 8 + 2 * e) * VT_LD + key] = uint16_t(w[e] & 0xffff);
-      Vt[(ch * 8 + 2 * e + 1) * VT_LD + key] = uint16_t(w[e] >> 16);
+    for (int k = 0; k < 8; ++k) {
+      const uint4 v = *reinterpret_cast<const uint4*>(base + long(kg * 8 + k) * row_stride + 2 * H * D + h * D +
+                                                      ch * 8);
+      w[k][0] = v.x; w[k][1] = v.y; w[k][2] = v.z; w[k][3] = v.w;
+    }
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = (d & 1) ? (w[2 * j][d >> 1] >> 16) : (w[2 * j][d >> 1] & 0xffffu);
+        const uint32_t hi = (d & 1) ? (w[2 * j + 1][d >> 1] & 0xffff0000u) : (w[2 * j + 1][d >> 1] << 16);
+        o[j] = lo | hi;
+      }
+      *reinterpret_cast<uint4*>(Vt + (ch * 8 + d) * VT_LD + kg * 8) = make_uint4(o[0], o[1], o[2], o[3]);
     }
   }
   // ---- Q fragments straight from global (A operand: row = fr, k = 8*fq + j)
@@ -139,16 +162,18 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
 template <int S>
 hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, int H, float scale, long bs, long qs,
                     hipStream_t st) {
-  constexpr int lds = (S * D + D * (S + 8) + 4 * 16 * (S + 8)) * 2;
+  constexpr int QB = qb_for(S);
+  constexpr int lds = (S * D + D * (S + 8) + (QB / 16) * 16 * (S + 8)) * 2;
+  static_assert(S % QB == 0 && lds <= 160 * 1024, "attention tile");
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<S>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<S, QB>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int grid = B * H * (S / QB);
-  hipLaunchKernelGGL((attention_kernel<S>), dim3(grid), dim3(256), lds, st, qkv, mb, ctx, H, scale, bs, qs);
+  hipLaunchKernelGGL((attention_kernel<S, QB>), dim3(grid), dim3(QB * 4), lds, st, qkv, mb, ctx, H, scale, bs, qs);
   return hipGetLastError();
 }
 

@@ -28,6 +28,11 @@ from . import errors as E
 
 log = logging.getLogger("tfserve.gpu")
 
+# Serialises HIP-graph capture (and the eager warm-up around it) with
+# torch.cuda.empty_cache() on unload: emptying the caching allocator while
+# another thread is capturing or warming up a servable can deadlock the two.
+CAPTURE_LOCK = threading.RLock()
+
 
 def buckets_for(max_batch: int, allowed: Sequence[int] = ()) -> List[int]:
     if allowed:
@@ -167,6 +172,10 @@ class GpuRunner:
         return lane
 
     def _capture(self, lane: _Lane, b: int) -> None:
+        with CAPTURE_LOCK:
+            self._capture_locked(lane, b)
+
+    def _capture_locked(self, lane: _Lane, b: int) -> None:
         dev = self.device
         if not lane.dev_in:
             bmax = self.buckets[-1]

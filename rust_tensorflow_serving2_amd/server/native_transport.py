@@ -115,6 +115,11 @@ class NativeTransport:
         self._stop = threading.Event()
         self._eps: Dict[tuple, FastEndpoint] = {}
         self._eps_lock = threading.Lock()
+        # fast-path registrations run in background threads (graph capture takes
+        # a while); a version that starts unloading meanwhile is cancelled, and
+        # stop() waits for them so no capture outlives the transport
+        self._reg_threads: List[threading.Thread] = []
+        self._cancelled: set = set()
 
     # ------------------------------------------------------------ slow path
     def _serve(self):
@@ -143,9 +148,20 @@ class NativeTransport:
         if not self.fast_path:
             return
         if state == AVAILABLE:
-            threading.Thread(target=self._register, args=(name, version), daemon=True).start()
+            with self._eps_lock:
+                self._cancelled.discard((name, version))
+                self._reg_threads = [t for t in self._reg_threads if t.is_alive()]
+                th = threading.Thread(target=self._register, args=(name, version), daemon=True,
+                                      name=f"tfs-fastreg-{name}-{version}")
+                self._reg_threads.append(th)
+            th.start()
         elif state in (UNLOADING, END):
+            with self._eps_lock:
+                self._cancelled.add((name, version))
             self._unregister(name, version)
+
+    def _reg_cancelled(self, name: str, version: int) -> bool:
+        return self._stop.is_set() or (name, version) in self._cancelled
 
     def _register(self, name: str, version: int):
         mgr = self.core.manager
@@ -157,7 +173,7 @@ class NativeTransport:
             if not servable.options.is_gpu:
                 return
             for sig_name, sig in servable.signatures.items():
-                if sig.method_name != PREDICT_METHOD:
+                if sig.method_name != PREDICT_METHOD or self._reg_cancelled(name, version):
                     continue
                 ins = servable.input_specs(sig_name)
                 if not all(s.shape and s.shape[0] == -1 and all(d >= 0 for d in s.shape[1:]) for s in ins.values()):
@@ -171,7 +187,12 @@ class NativeTransport:
                     log.exception("fast path unavailable for %s/%s", name, sig_name)
                     continue
                 with self._eps_lock:
-                    self._eps[(name, version, sig_name)] = ep
+                    cancelled = self._reg_cancelled(name, version)
+                    if not cancelled:
+                        self._eps[(name, version, sig_name)] = ep
+                if cancelled:   # the version began unloading while its graphs were captured
+                    ep.close()
+                    continue
                 self.srv.set_route(name, sig_name, version, ep.id)
                 log.info("fast path: %s v%d %s -> endpoint %d", name, version, sig_name, ep.id)
             self._refresh_latest(name)
@@ -215,6 +236,10 @@ class NativeTransport:
 
     def stop(self, grace: Optional[float] = 1.0):
         self._stop.set()
+        with self._eps_lock:
+            regs = list(self._reg_threads)
+        for th in regs:   # in-flight registrations see _stop and close what they built
+            th.join(timeout=120)
         with self._eps_lock:
             eps = list(self._eps.values())
             self._eps.clear()

@@ -250,4 +250,6 @@ class Servable:
         self._runners.clear()
         self.bundle = None
         if self.options.is_gpu:
-            torch.cuda.empty_cache()
+            from .gpu_runtime import CAPTURE_LOCK
+            with CAPTURE_LOCK:   # never while another servable captures its graphs
+                torch.cuda.empty_cache()
