@@ -199,6 +199,13 @@ def cse(graph: Graph, order: Sequence[str], fed_nodes: Set[str], fetch_refs) -> 
             rep[name] = seen[key]
         else:
             seen[key] = name
+    if rep:
+        # drop the merged duplicates so later passes see the true consumer sets
+        for n in graph.nodes.values():
+            n.inputs = [(rep.get(s, s), i) for s, i in n.inputs]
+            n.ctrl = [rep.get(c, c) for c in n.ctrl]
+        for name in rep:
+            del graph.nodes[name]
     return len(rep)
 
 

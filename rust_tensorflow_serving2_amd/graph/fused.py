@@ -295,7 +295,7 @@ def _impl_op(ctx, node, ins):
 
 
 for _op in ("_FusedConv2D", "_FusedDualConv", "_FusedMatMul", "_GlobalAvgPool", "_MaxPool", "_SoftmaxArgMax", "_LayerNorm",
-            "_FusedQKV", "_Attention", "_EmbedLN"):
+            "_FusedQKV", "_Attention", "_EmbeddingLN", "_KeyMaskAdder"):
     O.OPS[_op] = _impl_op
 
 

@@ -431,5 +431,191 @@ def fuse_attention(g, order, fed, fetch_refs, device, opts):
         c.refresh()
 
 
+# ------------------------------------------------------------------ embeddings
+class EmbeddingLNOp:
+    """LN(sum of row gathers + position rows), the BERT embedding block
+    (modeling.py ``embedding_lookup`` / ``embedding_postprocessor``) as one
+    ``embed_ln`` launch: one wave per token, tables held in bf16."""
+
+    def __init__(self, tables, pos, seq, gamma, beta, eps, device, use_hip):
+        self.seq, self.eps, self.use_hip = int(seq), float(eps), use_hip
+        self.tables_f = [t.float().contiguous() for t in tables]
+        self.pos_f = None if pos is None else pos.float().reshape(-1, tables[0].shape[1]).contiguous()
+        self.g = gamma.float().reshape(-1).contiguous().to(device)
+        self.b = beta.float().reshape(-1).contiguous().to(device)
+        self.hip_ok = use_hip and device.type == "cuda" and len(tables) <= 2
+        if self.hip_ok:
+            self.tables = [t.to(device=device, dtype=BF16).contiguous() for t in tables]
+            self.pos = None if pos is None else self.pos_f.to(device=device, dtype=BF16).contiguous()
+            self.tables_f = self.pos_f = None     # only the bf16 copies stay resident
+        else:
+            self.tables_f = [t.to(device) for t in self.tables_f]
+            self.pos_f = None if self.pos_f is None else self.pos_f.to(device)
+
+    def __call__(self, ctx, node, ins):
+        idx = [O.to_torch(v) for v in ins]
+        S = self.seq
+        n = idx[0].numel()
+        for i in idx[1:]:
+            if i.numel() != n:
+                raise O.OpError(f"{node.name}: embedding index counts differ")
+        if n % S:
+            raise O.OpError(f"{node.name}: {n} ids do not reshape to [-1, {S}]")
+        if self.hip_ok:
+            from ..ops import hip
+            dev = self.g.device
+            ii = [i.to(dev, torch.int32).reshape(-1).contiguous() for i in idx]
+            y = hip().embed_ln(ii[0], ii[1] if len(ii) > 1 else None, self.tables[0], self.pos,
+                               self.tables[1] if len(ii) > 1 else None, self.g, self.b, self.eps, S)
+            return [y.reshape(-1, S, y.shape[-1])]
+        acc = None
+        for i, t in zip(idx, self.tables_f):
+            i = i.reshape(-1).to(t.device).long()
+            if t.device.type == "cpu":
+                if n and (int(i.min()) < 0 or int(i.max()) >= t.shape[0]):
+                    raise O.OpError(f"{node.name}: indices out of range [0, {t.shape[0]})")
+                r = t.index_select(0, i)
+            else:
+                ok = (i >= 0) & (i < t.shape[0])
+                r = t.index_select(0, i.clamp(0, t.shape[0] - 1)) * ok[:, None].float()
+            acc = r if acc is None else acc + r
+        y = acc.reshape(-1, S, acc.shape[-1])
+        if self.pos_f is not None:
+            y = y + self.pos_f[:S]
+        return [F.layer_norm(y, (y.shape[-1],), self.g, self.b, self.eps)]
+
+
+def _gather_term(g, c, ref):
+    """Reshape(GatherV2(table, idx, 0), [-1, S, Hd]) -> (table, idx_ref, S, nodes)."""
+    rs = _node(g, ref)
+    if rs is None or rs.op != "Reshape":
+        return None
+    shp = _const_t(g, rs.inputs[1])
+    ga = _node(g, rs.inputs[0])
+    if shp is None or ga is None or ga.op != "GatherV2" or int(ga.attr("batch_dims", 0)) != 0:
+        return None
+    shp = shp.reshape(-1).tolist()
+    table, ax = _const_t(g, ga.inputs[0]), _scalar(g, ga.inputs[2])
+    if table is None or table.dim() != 2 or ax != 0 or len(shp) != 3 or shp[0] != -1 or shp[2] != table.shape[1]:
+        return None
+    return table, ga.inputs[1], int(shp[1]), [rs, ga]
+
+
+def fuse_embedding(g, order, fed, fetch_refs, device, opts):
+    """_LayerNorm(word gather + [type gather] + [position rows]) -> _EmbeddingLN."""
+    from .fused import _Ctx
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    for name in order:
+        ln = g.nodes.get(name)
+        if ln is None or ln.op != "_LayerNorm":
+            continue
+        leaves, interior, stack = [], [], [ln.inputs[0]]
+        while stack and len(leaves) <= 3:
+            ref = stack.pop()
+            n = _node(g, ref)
+            if n is not None and n.op in ("Add", "AddV2") and len(n.inputs) == 2:
+                interior.append(n)
+                stack += n.inputs
+            else:
+                leaves.append(ref)
+        if not interior or len(leaves) > 3:
+            continue
+        gathers, pos = [], []
+        for ref in leaves:
+            gt = _gather_term(g, c, ref)
+            if gt is not None:
+                gathers.append(gt)
+                continue
+            v = _const_t(g, ref)
+            if v is None:
+                break
+            pos.append(v)
+        else:
+            if not gathers or len(pos) > 1:
+                continue
+            S, Hd = gathers[0][2], gathers[0][0].shape[1]
+            if any(gt[2] != S or gt[0].shape[1] != Hd for gt in gathers):
+                continue
+            p = pos[0] if pos else None
+            if p is not None and tuple(p.shape) not in ((1, S, Hd), (S, Hd)):
+                continue
+            impl = ln.attrs["_impl"]
+            nodes = interior + [n for gt in gathers for n in gt[3]]
+            if not _interior_ok(c, nodes, ln):
+                continue
+            gathers.sort(key=lambda gt: -gt[0].shape[0])    # largest (word) table first
+            _remove(g, nodes)
+            ln.op = "_EmbeddingLN"
+            ln.inputs = [gt[1] for gt in gathers]
+            ln.ctrl = []
+            ln.attrs = {"_impl": EmbeddingLNOp([gt[0] for gt in gathers], p, S, impl.g.cpu(), impl.b.cpu(), impl.eps,
+                                               device, c.use_hip)}
+            c.refresh()
+
+
+# ------------------------------------------------------------------ attention mask
+class KeyMaskAdderOp:
+    """(one - X) * scale for a key mask X [B, 1, S], shaped [B, 1, 1, S]: the
+    BERT attention adder (modeling.py ``create_attention_mask_from_input_mask``
+    + ``(1 - mask) * -10000``) without materialising the [B, S, S] broadcast.
+    Only _Attention consumes it, and it broadcasts over the query axis."""
+
+    def __init__(self, one, scale):
+        self.one, self.scale = float(one), float(scale)
+
+    def __call__(self, ctx, node, ins):
+        x = O.to_torch(ins[0])
+        if x.dim() != 3 or x.shape[1] != 1:
+            raise O.Unsupported("key mask must be [B, 1, S]")
+        return [(x.float() * -self.scale).add_(self.one * self.scale).unsqueeze(1)]
+
+
+def fuse_key_mask(g, order, fed, fetch_refs, device, opts):
+    """Mul(Sub(1, ExpandDims(Mul(ones[1,S,1], X), 1)), c) feeding only _Attention
+    nodes -> _KeyMaskAdder(X)."""
+    from .fused import _Ctx
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    for name in order:
+        mul = g.nodes.get(name)
+        if mul is None or mul.op != "Mul" or len(mul.inputs) != 2 or name in c.fetch_nodes:
+            continue
+        cons = c.cons.get(name, [])
+        if not cons or any(g.nodes[cn].op != "_Attention" or pos != 1 or oi != 0 for cn, pos, oi in cons):
+            continue
+        for k in (0, 1):
+            sub, scale = _node(g, mul.inputs[k]), _scalar(g, mul.inputs[1 - k])
+            if sub is not None and sub.op == "Sub" and scale is not None:
+                break
+        else:
+            continue
+        one, ex = _scalar(g, sub.inputs[0]), _node(g, sub.inputs[1])
+        if one is None or ex is None or ex.op != "ExpandDims" or _scalar(g, ex.inputs[1]) != 1:
+            continue
+        bm = _node(g, ex.inputs[0])
+        if bm is None or bm.op != "Mul" or len(bm.inputs) != 2:
+            continue
+        x_ref = None
+        for k in (0, 1):
+            ones = _const_t(g, bm.inputs[k])
+            if ones is not None and ones.dim() == 3 and ones.shape[0] == 1 and ones.shape[2] == 1 and \
+                    bool((ones == 1).all()):
+                x_ref = bm.inputs[1 - k]
+                S = ones.shape[1]
+        if x_ref is None or not _interior_ok(c, [sub, ex, bm], mul):
+            continue
+        interior = [sub, ex, bm]
+        cast = _node(g, x_ref)
+        if cast is not None and cast.op == "Cast" and not cast.ctrl and \
+                O.dt_attr(cast, "DstT") == torch.float32 and _interior_ok(c, interior + [cast], mul):
+            interior.append(cast)        # the op casts to f32 itself
+            x_ref = cast.inputs[0]
+        _remove(g, interior)
+        mul.op = "_KeyMaskAdder"
+        mul.inputs = [x_ref]
+        mul.ctrl = []
+        mul.attrs = {"_impl": KeyMaskAdderOp(one, scale), "_seq": S}
+        c.refresh()
+
+
 def bert_passes():
-    return [fuse_layernorm, fuse_attention]
+    return [fuse_layernorm, fuse_embedding, fuse_attention, fuse_key_mask]

@@ -333,28 +333,44 @@ Tensor layernorm(const Tensor& x, const c10::optional<Tensor>& residual, const T
   return y;
 }
 
-Tensor embed_ln(const Tensor& ids, const c10::optional<Tensor>& type_ids, const Tensor& word, const Tensor& pos,
-                const Tensor& type, const Tensor& gamma, const Tensor& beta, double eps) {
-  need(ids, at::kLong, "ids");
+// ids / type_ids: int32, any shape, flattened to tokens; pos: [>= seq, Hd] rows
+// indexed by token % seq. Returns ids.shape + [Hd].
+Tensor embed_ln(const Tensor& ids, const c10::optional<Tensor>& type_ids, const Tensor& word,
+                const c10::optional<Tensor>& pos, const c10::optional<Tensor>& type, const Tensor& gamma,
+                const Tensor& beta, double eps, int64_t seq) {
+  need(ids, at::kInt, "ids");
   need(word, at::kBFloat16, "word");
-  need(pos, at::kBFloat16, "pos");
-  need(type, at::kBFloat16, "type");
   need(gamma, at::kFloat, "gamma");
   need(beta, at::kFloat, "beta");
-  TORCH_CHECK(ids.dim() == 2, "ids must be [batch, seq]");
+  TORCH_CHECK(word.dim() == 2, "word table must be 2-D");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(ids.device());
-  const int B = ids.size(0), S = ids.size(1), Hd = word.size(1);
-  TORCH_CHECK(Hd % 8 == 0 && pos.size(1) == Hd && type.size(1) == Hd && pos.size(0) >= S, "embedding shapes");
-  const int64_t* tt = nullptr;
+  const int64_t tokens = ids.numel(), Hd = word.size(1);
+  TORCH_CHECK(Hd % 8 == 0 && Hd <= 2048, "embed_ln: hidden must be a multiple of 8 and <= 2048");
+  TORCH_CHECK(gamma.numel() == Hd && beta.numel() == Hd, "embed_ln: LN params shape");
+  TORCH_CHECK(seq > 0 && tokens % seq == 0 && tokens < (int64_t(1) << 31), "embed_ln: tokens must be batch * seq");
+  const int* tt = nullptr;
+  const uint16_t *pp = nullptr, *tp = nullptr;
+  int ntypes = 0;
   if (type_ids.has_value()) {
-    need(*type_ids, at::kLong, "type_ids");
-    TORCH_CHECK(type_ids->numel() == ids.numel(), "type_ids shape");
-    tt = type_ids->data_ptr<int64_t>();
+    TORCH_CHECK(type.has_value(), "embed_ln: type_ids without a type table");
+    need(*type_ids, at::kInt, "type_ids");
+    need(*type, at::kBFloat16, "type");
+    TORCH_CHECK(type_ids->numel() == tokens && type->dim() == 2 && type->size(1) == Hd, "embed_ln: type shapes");
+    tt = type_ids->data_ptr<int>();
+    tp = bf16p(*type);
+    ntypes = type->size(0);
   }
-  Tensor y = torch::empty({B, S, Hd}, word.options());
-  check(tfsk::embed_ln_launch(ids.data_ptr<int64_t>(), tt, bf16p(word), bf16p(pos), bf16p(type),
-                              gamma.data_ptr<float>(), beta.data_ptr<float>(), bf16p_mut(y), B * S, S, Hd,
-                              word.size(0), type.size(0), float(eps), cur_stream(ids)), "embed_ln");
+  if (pos.has_value()) {
+    need(*pos, at::kBFloat16, "pos");
+    TORCH_CHECK(pos->dim() == 2 && pos->size(1) == Hd && pos->size(0) >= seq, "embed_ln: pos shape");
+    pp = bf16p(*pos);
+  }
+  auto shape = ids.sizes().vec();
+  shape.push_back(Hd);
+  Tensor y = torch::empty(shape, word.options());
+  check(tfsk::embed_ln_launch(ids.data_ptr<int>(), tt, bf16p(word), pp, tp, gamma.data_ptr<float>(),
+                              beta.data_ptr<float>(), bf16p_mut(y), tokens, seq, Hd, word.size(0), ntypes,
+                              float(eps), cur_stream(ids)), "embed_ln");
   return y;
 }
 
@@ -415,7 +431,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm", &layernorm, py::arg("x"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("out") = py::none());
   m.def("embed_ln", &embed_ln, py::arg("ids"), py::arg("type_ids"), py::arg("word"), py::arg("pos"),
-        py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("eps"));
+        py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("seq"));
   m.def("attention", &attention, py::arg("qkv"), py::arg("mask_bias"), py::arg("heads"), py::arg("scale"),
         py::arg("out") = py::none(), py::arg("mask_bstride") = 0, py::arg("mask_qstride") = 0);
   m.def("num_configs", []() { return tfsk::kNumIGemmConfigs; });

@@ -90,8 +90,9 @@ hipError_t cast_bf16_f32_launch(const uint16_t* x, float* y, int64_t n, hipStrea
 // y = LN(x + r) ; if `sum_out` != nullptr the pre-norm sum is also written.
 hipError_t layernorm_launch(const uint16_t* x, const uint16_t* r, const float* gamma, const float* beta,
                             uint16_t* y, int rows, int cols, float eps, hipStream_t stream);
-// Embedding: y[t] = LN(word[ids[t]] + pos[t % S] + type[tt[t]]) (bf16 tables, f32 LN params)
-hipError_t embed_ln_launch(const int64_t* ids, const int64_t* type_ids, const uint16_t* word,
+// Embedding: y[t] = LN(word[ids[t]] + pos[t % S] + type[tt[t]]) (bf16 tables, f32 LN params;
+// int32 ids, out-of-range ids add a zero row; type_ids / pos may be null; hidden % 8 == 0, <= 2048)
+hipError_t embed_ln_launch(const int* ids, const int* type_ids, const uint16_t* word,
                            const uint16_t* pos, const uint16_t* type, const float* gamma,
                            const float* beta, uint16_t* y, int tokens, int seq, int hidden,
                            int vocab, int ntypes, float eps, hipStream_t stream);

@@ -236,8 +236,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
 }
 
 // ---------------------------------------------------------------- embedding + LN
-__global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* __restrict__ ids,
-                                                       const int64_t* __restrict__ tids,
+// One wave per token: y[t] = LN(word[ids[t]] + type[tids[t]] + pos[t % seq]).
+// An id outside its table contributes a zero row (TF's GPU GatherV2 reads zeros
+// there and never faults); `tids` / `pos` may be null. The row sum stays in
+// registers (hidden <= 64 * 8 * kEmbChunks) so the variance is two-pass.
+constexpr int kEmbChunks = 4;
+
+__global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ ids, const int* __restrict__ tids,
                                                        const uint16_t* __restrict__ word,
                                                        const uint16_t* __restrict__ pos,
                                                        const uint16_t* __restrict__ type,
@@ -248,32 +253,61 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* __restrict
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (t >= tokens) return;
-  long id = ids[t];
-  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
-  long tt = tids ? tids[t] : 0;
-  tt = tt < 0 ? 0 : (tt >= ntypes ? ntypes - 1 : tt);
+  const int id = ids[t];
+  const bool wok = id >= 0 && id < vocab;
+  const int tt = tids ? tids[t] : -1;
+  const bool tok = tt >= 0 && tt < ntypes;
   const int p = t % seq;
-  float s = 0.f, ss = 0.f;
-  for (int c = lane * 8; c < hidden; c += 512) {
-    float a[8], b[8], d[8];
-    unpack8(*reinterpret_cast<const uint4*>(word + id * hidden + c), a);
-    unpack8(*reinterpret_cast<const uint4*>(pos + long(p) * hidden + c), b);
-    unpack8(*reinterpret_cast<const uint4*>(type + tt * hidden + c), d);
+  float v[kEmbChunks][8];
+  float s = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { const float v = a[e] + b[e] + d[e]; s += v; ss += v * v; }
+  for (int k = 0; k < kEmbChunks; ++k) {
+    const int c = (k * 64 + lane) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[k][e] = 0.f;
+    if (c < hidden) {
+      float a[8];
+      if (wok) {
+        unpack8(*reinterpret_cast<const uint4*>(word + long(id) * hidden + c), a);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[k][e] += a[e];
+      }
+      if (tok) {
+        unpack8(*reinterpret_cast<const uint4*>(type + long(tt) * hidden + c), a);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[k][e] += a[e];
+      }
+      if (pos) {
+        unpack8(*reinterpret_cast<const uint4*>(pos + long(p) * hidden + c), a);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[k][e] += a[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[k][e];
+    }
   }
-  s = wave_sum(s);
-  ss = wave_sum(ss);
-  const float mean = s / hidden;
-  const float inv = rsqrtf(fmaxf(ss / hidden - mean * mean, 0.f) + eps);
-  for (int c = lane * 8; c < hidden; c += 512) {
-    float a[8], b[8], d[8];
-    unpack8(*reinterpret_cast<const uint4*>(word + id * hidden + c), a);
-    unpack8(*reinterpret_cast<const uint4*>(pos + long(p) * hidden + c), b);
-    unpack8(*reinterpret_cast<const uint4*>(type + tt * hidden + c), d);
+  const float mean = wave_sum(s) / hidden;
+  float ss = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) a[e] = (a[e] + b[e] + d[e] - mean) * inv * gamma[c + e] + beta[c + e];
-    *reinterpret_cast<uint4*>(y + long(t) * hidden + c) = pack8(a);
+  for (int k = 0; k < kEmbChunks; ++k)
+    if ((k * 64 + lane) * 8 < hidden) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = v[k][e] - mean; ss += d * d; }
+    }
+  const float inv = rsqrtf(wave_sum(ss) / hidden + eps);
+#pragma unroll
+  for (int k = 0; k < kEmbChunks; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < hidden) {
+      const float4 g0 = *reinterpret_cast<const float4*>(gamma + c), g1 = *reinterpret_cast<const float4*>(gamma + c + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(beta + c), b1 = *reinterpret_cast<const float4*>(beta + c + 4);
+      const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[k][e] - mean) * inv * g[e] + bb[e];
+      *reinterpret_cast<uint4*>(y + long(t) * hidden + c) = pack8(o);
+    }
   }
 }
 
@@ -392,9 +426,10 @@ hipError_t layernorm_launch(const uint16_t* x, const uint16_t* r, const float* g
   return hipGetLastError();
 }
 
-hipError_t embed_ln_launch(const int64_t* ids, const int64_t* type_ids, const uint16_t* word, const uint16_t* pos,
+hipError_t embed_ln_launch(const int* ids, const int* type_ids, const uint16_t* word, const uint16_t* pos,
                            const uint16_t* type, const float* gamma, const float* beta, uint16_t* y, int tokens,
                            int seq, int hidden, int vocab, int ntypes, float eps, hipStream_t s) {
+  if (hidden % 8 || hidden > 64 * 8 * kEmbChunks || seq <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(embed_ln_kernel, dim3((tokens + 3) / 4), dim3(256), 0, s, ids, type_ids, word, pos, type,
                      gamma, beta, y, tokens, seq, hidden, vocab, ntypes, eps);
   return hipGetLastError();

@@ -15,6 +15,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="bert-base", choices=["bert-base", "resnet50"])
     ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--fuse", action="store_true", help="run the fusion passes on a CPU device too")
     a = ap.parse_args()
     from rust_tensorflow_serving2_amd.models import bert, resnet
     from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
@@ -25,7 +26,8 @@ def main():
     else:
         resnet.export(path, seed=0)
         ins, outs = ["input"], ["classes", "probabilities"]
-    s = Servable(a.model, 1, path, ServableOptions(device=a.device, max_batch_size=4))
+    s = Servable(a.model, 1, path, ServableOptions(device=a.device, max_batch_size=4,
+                                                       fuse=True if a.fuse else None))
     r = s.runner("serving_default", ins, outs)
     prog = r.program
     print(sorted(prog.op_histogram().items(), key=lambda x: -x[1]))

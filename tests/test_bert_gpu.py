@@ -39,4 +39,5 @@ def test_bert_base_gpu_matches_cpu(bert_base):
     assert np.abs(g["probabilities"] - c["probabilities"]).max() < 1e-2
     runner = next(iter(gpu._runners.values()))
     hist = runner.program.op_histogram()
-    assert hist["_Attention"] == 12 and hist["_FusedQKV"] == 12 and hist["_LayerNorm"] == 25
+    assert hist["_Attention"] == 12 and hist["_FusedQKV"] == 12 and hist["_LayerNorm"] == 24
+    assert hist["_EmbeddingLN"] == 1 and hist["_KeyMaskAdder"] == 1 and "GatherV2" not in hist

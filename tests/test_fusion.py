@@ -49,9 +49,24 @@ def test_bert_fusion_exact(tiny_bert):
     for k in outs:
         np.testing.assert_allclose(a[k], b[k], atol=1e-5)
     hist = fused.runner("serving_default", sorted(feeds), outs).program.op_histogram()
-    assert hist["_LayerNorm"] == 5 and hist["_Attention"] == 2 and hist["_FusedQKV"] == 2
+    assert hist["_LayerNorm"] == 4 and hist["_Attention"] == 2 and hist["_FusedQKV"] == 2
+    # embedding gathers + adds + LN -> one op; the [B,S,S] mask adder chain -> one [B,1,1,S] op
+    assert hist["_EmbeddingLN"] == 1 and hist["_KeyMaskAdder"] == 1
+    assert "GatherV2" not in hist and "ExpandDims" not in hist and "Cast" not in hist
     assert hist["_FusedMatMul"] == 8 and "MatMul" not in hist and "BatchMatMulV2" not in hist
     assert "Rsqrt" not in hist and "Pow" not in hist and "Tanh" not in hist
+
+
+def test_bert_fused_embedding_rejects_out_of_range_ids_on_cpu(tiny_bert):
+    """The fused embedding keeps GatherV2's CPU contract: an id outside the
+    vocabulary is an error, as in the unfused graph."""
+    from rust_tensorflow_serving2_amd.server.errors import ServingError
+    _ref, fused = _pair(tiny_bert)
+    ids = np.full((1, 32), 5, np.int32)
+    ids[0, 3] = 100                                 # vocab_size == 100
+    feeds = {"input_ids": ids, "input_mask": np.ones((1, 32), np.int32), "segment_ids": np.zeros((1, 32), np.int32)}
+    with pytest.raises(ServingError, match="out of range"):
+        fused.run("serving_default", feeds, ["pooled_output"])
 
 
 def test_gelu_erf_form_matches():

@@ -287,13 +287,39 @@ def test_layernorm_and_embedding():
     y = hip().layernorm(x.to(DEV), r.to(DEV), gm.to(DEV), bt.to(DEV), 1e-12)
     ref = F.layer_norm(x.float() + r.float(), (768,), gm, bt, 1e-12)
     assert (y.float().cpu() - ref).abs().max() < 5e-2
-    ids = torch.randint(0, 1000, (3, 128))
-    tt = torch.randint(0, 2, (3, 128))
+    ids = torch.randint(0, 1000, (3, 128), dtype=torch.int32)
+    tt = torch.randint(0, 2, (3, 128), dtype=torch.int32)
     word, pos, typ = rnd(1000, 768, seed=18).to(BF), rnd(512, 768, seed=19).to(BF), rnd(2, 768, seed=20).to(BF)
     e = hip().embed_ln(ids.to(DEV), tt.to(DEV), word.to(DEV), pos.to(DEV), typ.to(DEV), gm.to(DEV), bt.to(DEV),
-                       1e-12)
-    ref = F.layer_norm(word.float()[ids] + pos.float()[:128] + typ.float()[tt], (768,), gm, bt, 1e-12)
+                       1e-12, 128)
+    ref = F.layer_norm(word.float()[ids.long()] + pos.float()[:128] + typ.float()[tt.long()], (768,), gm, bt, 1e-12)
+    assert e.shape == (3, 128, 768)
     assert (e.float().cpu() - ref).abs().max() < 5e-2
+
+
+@pytest.mark.parametrize("hd", [64, 520, 1024, 2048])
+def test_embedding_out_of_range_rows_are_zero(hd):
+    """Ids outside a table add a zero row (TF's GPU GatherV2); type ids and
+    positions are optional; hidden sizes up to 2048 in 8-wide chunks."""
+    S = 16
+    ids = torch.randint(0, 50, (2 * S,), dtype=torch.int32)
+    ids[3], ids[7] = -1, 50
+    tt = torch.randint(0, 3, (2 * S,), dtype=torch.int32)
+    tt[5] = 9
+    word, typ, pos = rnd(50, hd, seed=31).to(BF), rnd(3, hd, seed=32).to(BF), rnd(S, hd, seed=33).to(BF)
+    gm, bt = rnd(hd, seed=34), rnd(hd, seed=35)
+    wz = torch.cat([word.float(), torch.zeros(1, hd)])
+    tz = torch.cat([typ.float(), torch.zeros(1, hd)])
+    wi = torch.where((ids >= 0) & (ids < 50), ids, 50).long()
+    ti = torch.where((tt >= 0) & (tt < 3), tt, 3).long()
+    full = wz[wi] + tz[ti] + pos.float().repeat(2, 1)
+    e = hip().embed_ln(ids.to(DEV), tt.to(DEV), word.to(DEV), pos.to(DEV), typ.to(DEV), gm.to(DEV), bt.to(DEV),
+                       1e-6, S)
+    assert (e.float().cpu() - F.layer_norm(full, (hd,), gm, bt, 1e-6)).abs().max() < 5e-2
+    e2 = hip().embed_ln(ids.to(DEV), None, word.to(DEV), None, None, gm.to(DEV), bt.to(DEV), 1e-6, S)
+    assert (e2.float().cpu() - F.layer_norm(wz[wi], (hd,), gm, bt, 1e-6)).abs().max() < 5e-2
+    with pytest.raises(RuntimeError):
+        hip().embed_ln(ids.to(DEV), None, word.to(DEV), None, None, gm.to(DEV), bt.to(DEV), 1e-6, 5)   # 32 % 5
 
 
 @pytest.mark.parametrize("s", [64, 128, 256])
