@@ -190,7 +190,7 @@ class FusedConv:
         M = n * ho * wo
         args = (x, self.w, self.b, res, kh, kw, self.sh, self.sw, pt, pb, pl, pr, ACT[self.act])
         out = torch.empty((n, ho, wo, self.cout), device=x.device, dtype=BF16)
-        key = ("conv", tuple(x.shape), x.dtype, self.cout, kh, kw, self.sh, res is not None)
+        key = ("conv", tuple(x.shape), x.dtype, self.cout, kh, kw, self.sh, res is not None, self.act)
         K = kh * 32 if self.c4 else kh * kw * self.cin
         dma = not self.c4 and self.cin % 8 == 0      # bf16 dense/im2col operands -> DMA-ring configs apply
         # pipelined cgemm kernel applies (im2col / dense with C % 64, or the padded RGBA stem)
@@ -233,7 +233,7 @@ class FusedDualConv:
         h, x = _to_bf16(h).contiguous(), _to_bf16(x).contiguous()
         n, ho, wo, _ = h.shape
         out = torch.empty((n, ho, wo, self.cout), device=h.device, dtype=BF16)
-        key = ("dual", tuple(h.shape), tuple(x.shape), self.cout, self.sh)
+        key = ("dual", tuple(h.shape), tuple(x.shape), self.cout, self.sh, self.act)
         run = lambda c, s: H.conv2d_dual(h, x, self.w, self.b, self.sh, self.sw, ACT[self.act], c, out, s)  # noqa
         cfg, splits = tuned_config(key, n * ho * wo, self.cout, run, self.c1 + self.c2, True, True, cgemm_only=True)
         return [run(cfg, splits)]
@@ -272,7 +272,7 @@ class FusedMatMul:
         M = x.numel() // self.k
         shape = list(x.shape[:-1]) + [self.n]
         out = torch.empty(shape, device=x.device, dtype=torch.float32 if self.out_f32 else BF16)
-        key = ("mm", M, self.n, self.k, res is not None, self.out_f32)
+        key = ("mm", M, self.n, self.k, res is not None, self.out_f32, self.act)
         run = lambda c, s: H.linear(x, self.w, self.b, res, ACT[self.act], c, self.out_f32, 1.0, out, s)  # noqa
         cfg, splits = tuned_config(key, M, self.n, run, self.k, True, self.k % 64 == 0)
         return [run(cfg, splits)]

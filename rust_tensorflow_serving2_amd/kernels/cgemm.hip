@@ -160,10 +160,10 @@ __device__ __forceinline__ void epi_chunk(const IGemmArgs& p, const float* src, 
   }
 }
 
-// Cheap activations (none / ReLU): fully unrolled over the thread's chunks,
-// residual from the registers prefetched before the K loop.  Transcendental
-// ones (GELU / tanh; BERT FFN and pooler, no residual): a rolled loop, so the
-// erf/tanh expansion is emitted once instead of ITERS x 8 times.
+// Cheap activations (none / ReLU / GELU-tanh / tanh -- the last two are an exp
+// and a rcp, common.h sigm2): fully unrolled over the thread's chunks, residual
+// from the registers prefetched before the K loop.  erf GELU (Keras FFNs): a
+// rolled loop, so the erf expansion is emitted once instead of ITERS x 8 times.
 template <int BM, int BN, int NT, int CS_LD, int ACT>
 __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* Cs, int m0, int n0, int tid,
                                               const uint4 (&rpre)[Epi<BM, BN, NT>::PRE > 0 ? Epi<BM, BN, NT>::PRE : 1],
@@ -171,7 +171,7 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
   using E = Epi<BM, BN, NT>;
   const int M = p.M, N = p.N;
   const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-  constexpr bool cheap = (ACT == kActNone || ACT == kActRelu);
+  constexpr bool cheap = (ACT != kActGeluErf);   // GELU-tanh / tanh are exp + rcp (common.h sigm2)
   if constexpr (cheap) {
 #pragma unroll
     for (int it = 0; it < E::ITERS; ++it) {

@@ -28,16 +28,19 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
   return bf16_t(u >> 16);
 }
 
+// 1 / (1 + exp(-2u)): one v_exp_f32 + one v_rcp_f32 (both ~1 ulp; the
+// epilogues round to bf16). 0.5 x (1 + tanh u) == x * sigm2(u) and
+// tanh x == 2 sigm2(x) - 1, so GELU-tanh / tanh cost two transcendental ops
+// instead of ocml tanhf's branchy expansion (which made BERT's FFN1 epilogue
+// a visible share of the GEMM). exp overflow -> rcp(inf) = 0: correct limits.
+__device__ __forceinline__ float sigm2(float u) { return __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u)); }
+
 __device__ __forceinline__ float apply_act(float x, int act) {
   switch (act) {
     case kActRelu: return x > 0.f ? x : 0.f;
-    case kActGeluTanh: {
-      const float c = 0.7978845608028654f;
-      float u = c * (x + 0.044715f * x * x * x);
-      return 0.5f * x * (1.f + tanhf(u));
-    }
+    case kActGeluTanh: return x * sigm2(0.7978845608028654f * (x + 0.044715f * x * x * x));
     case kActGeluErf: return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
-    case kActTanh: return tanhf(x);
+    case kActTanh: return 2.f * sigm2(x) - 1.f;
     default: return x;
   }
 }
@@ -49,13 +52,11 @@ __device__ __forceinline__ float act_fn(float x) {
   if constexpr (ACT == kActRelu) {
     return x > 0.f ? x : 0.f;
   } else if constexpr (ACT == kActGeluTanh) {
-    const float c = 0.7978845608028654f;
-    const float u = c * (x + 0.044715f * x * x * x);
-    return 0.5f * x * (1.f + tanhf(u));
+    return x * sigm2(0.7978845608028654f * (x + 0.044715f * x * x * x));
   } else if constexpr (ACT == kActGeluErf) {
     return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
   } else if constexpr (ACT == kActTanh) {
-    return tanhf(x);
+    return 2.f * sigm2(x) - 1.f;
   } else {
     return x;
   }

@@ -7,9 +7,10 @@ back to PyTorch, so a GPU test that passes has run the native kernels.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
-from typing import Callable, Dict, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 
@@ -51,6 +52,10 @@ ACT = {"none": 0, "relu": 1, "gelu_tanh": 2, "gelu_erf": 3, "tanh": 4}
 _TUNED: Dict[Tuple, int] = {}
 _TUNE_LOCK = threading.Lock()
 AUTOTUNE = os.environ.get("TFSERVE_AUTOTUNE", "1") != "0"
+# per key: [(median cold launch ms, (config, splits))] ascending, from tuned_config
+_TUNE_TIMES: Dict[Tuple, List[Tuple[float, Tuple[int, int]]]] = {}
+_GRAPH_TUNED: set = set()
+_REC = threading.local()
 
 
 def heuristic_config(M: int, N: int) -> int:
@@ -122,6 +127,9 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
     heuristic is used)."""
+    rec = getattr(_REC, "keys", None)
+    if rec is not None:
+        rec[key] = rec.get(key, 0) + 1
     hit = _TUNED.get(key)
     if hit is not None:
         return hit
@@ -133,6 +141,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
         if hit is not None:
             return hit
         best, best_t = None, float("inf")
+        times = []
         flush = _flush_buffer()
         for c, s in candidates(M, N, K, dma, aligned64, cgemm_only):
             launch(c, s)   # warm (also sets the kernel's LDS attribute)
@@ -153,10 +162,68 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
                 samples.append(start.elapsed_time(end))
             samples.sort()
             t = samples[len(samples) // 2]
+            times.append((t, (c, s)))
             if t < best_t:
                 best, best_t = (c, s), t
+        _TUNE_TIMES[key] = sorted(times)
         _TUNED[key] = best
         return best
+
+
+@contextlib.contextmanager
+def record_tuned_keys():
+    """Collect {key: uses} of every tuned_config lookup made on this thread
+    inside the block (one program run -> the tunable launches it makes)."""
+    keys: Dict[Tuple, int] = {}
+    prev = getattr(_REC, "keys", None)
+    _REC.keys = keys
+    try:
+        yield keys
+    finally:
+        _REC.keys = prev
+
+
+def graph_tune(keys: Dict[Tuple, int], time_fn: Callable[[], float], top: int = 3, ratio: float = 1.35,
+               min_ms: float = 0.012) -> Dict[Tuple, Tuple[int, int]]:
+    """Re-pick tile configs by timing the WHOLE program (``time_fn`` captures
+    and replays it, returning ms) instead of one cold launch per kernel: inside
+    a replay a GEMM's operands arrive from the previous kernel and its
+    neighbours' tails overlap it, which the isolated timings do not see.
+
+    Coordinate descent over ``keys`` (largest estimated share first); each key
+    tries its ``top`` fastest isolated candidates within ``ratio`` of the best.
+    Keys whose isolated time is under ``min_ms`` (launch-floor bound) or that
+    were already graph-tuned are skipped.  Returns the changed picks."""
+    todo = []
+    for k, uses in keys.items():
+        times = _TUNE_TIMES.get(k)
+        if k in _GRAPH_TUNED or not times or times[0][0] < min_ms:
+            continue
+        cands = [c for t, c in times[:top] if t <= times[0][0] * ratio]
+        if len(cands) > 1:
+            todo.append((times[0][0] * uses, k, cands))
+    changed: Dict[Tuple, Tuple[int, int]] = {}
+    if not todo:
+        _GRAPH_TUNED.update(keys)
+        return changed
+    todo.sort(key=lambda x: -x[0])
+    base = time_fn()
+    for _w, k, cands in todo:
+        cur = _TUNED[k]
+        best_t, best_c = base, cur
+        for c in cands:
+            if c == cur:
+                continue
+            _TUNED[k] = c
+            t = time_fn()
+            if t < best_t * 0.995:       # ignore sub-noise wins
+                best_t, best_c = t, c
+        _TUNED[k] = best_c
+        if best_c != cur:
+            changed[k] = best_c
+            base = best_t
+    _GRAPH_TUNED.update(keys)
+    return changed
 
 
 _FLUSH: Dict[int, torch.Tensor] = {}

@@ -183,11 +183,16 @@ class GpuRunner:
                            for s in self.in_specs]
         ins = [t[:b] for t in lane.dev_in]
         # eager warm-up on the lane's stream (autotunes kernel tiles for this shape)
-        with torch.cuda.stream(lane.stream):
+        from .. import ops
+        with torch.cuda.stream(lane.stream), ops.record_tuned_keys() as keys:
             self._finish(self.program.run(ins))
             outs = self._finish(self.program.run(ins))
         lane.stream.synchronize()
         self._ensure_host_out(lane, outs)
+        if keys and self.servable.options.graph_autotune and ops.AUTOTUNE:
+            changed = ops.graph_tune(keys, lambda: self._replay_ms(lane, ins))
+            if changed:
+                log.info("graph autotune %s bucket=%d: %s", self.servable.name, b, changed)
         # compute-only graph: the H2D/D2H copies stay separate hipMemcpyAsync calls
         # so they run on the SDMA engines (copy nodes inside a graph can turn into
         # blit kernels that read host memory over PCIe from the CUs) and move only
@@ -199,6 +204,26 @@ class GpuRunner:
         lane.static_in[b] = ins
         lane.static_out[b] = outs
         log.info("captured HIP graph: %s bucket=%d (%d steps)", self.servable.name, b, len(self.program.steps))
+
+    def _replay_ms(self, lane: _Lane, ins: List[torch.Tensor], reps: int = 3, iters: int = 6) -> float:
+        """Capture the program with the current tile picks and time its replay
+        (best of ``reps`` averages over ``iters`` replays; the graph is dropped)."""
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=lane.stream, capture_error_mode="thread_local"):
+            self._finish(self.program.run(ins))
+        best = float("inf")
+        with torch.cuda.stream(lane.stream):
+            graph.replay()
+            for _ in range(reps):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(iters):
+                    graph.replay()
+                e.record()
+                e.synchronize()
+                best = min(best, s.elapsed_time(e) / iters)
+        del graph
+        return best
 
     def _launch(self, lane: _Lane, n: int) -> int:
         """H2D rows [0, b) of the lane's pinned inputs, replay, D2H; returns b."""

@@ -35,6 +35,7 @@ class ServableOptions:
     fuse: Optional[bool] = None          # default: on for GPU devices
     compute_dtype: str = "bf16"          # bf16 on GPU (fp32 on CPU always)
     hip_graphs: bool = True
+    graph_autotune: bool = True          # re-pick GEMM tiles by timing whole-graph replays (ops.graph_tune)
     lanes: int = 4                       # GPU lanes = fast-path batch slots (stream + pinned staging + graphs)
     max_batch_size: int = 32
     allowed_batch_sizes: Tuple[int, ...] = ()

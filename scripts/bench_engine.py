@@ -20,11 +20,14 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--baseline", action="store_true")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert-base"])
+    ap.add_argument("--graph-tune", type=int, default=1, help="whole-graph tile re-tuning at capture (0 = off)")
     args = ap.parse_args()
+    import logging
+    logging.basicConfig(level=logging.INFO, format="%(name)s: %(message)s")
     from rust_tensorflow_serving2_amd.models import bert, resnet
     from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
     path = os.path.join(tempfile.mkdtemp(), "1")
-    opts = ServableOptions(device="cuda:0", max_batch_size=max(args.batch))
+    opts = ServableOptions(device="cuda:0", max_batch_size=max(args.batch), graph_autotune=bool(args.graph_tune))
     if args.model == "bert-base":
         bert.export(path, seed=0)
         s = Servable("bert", 1, path, opts)
@@ -43,7 +46,9 @@ def main():
                  np.zeros((b, 128), np.int32)]
         else:
             x = [rng.random((b, 224, 224, 3), dtype=np.float32)]
+        t0 = time.perf_counter()
         r.run(x)  # capture
+        t_capture = time.perf_counter() - t0
         bucket = r._bucket(b)
         g = next(l.graphs[bucket] for l in r.lanes if bucket in l.graphs)
         torch.cuda.synchronize()
@@ -61,7 +66,7 @@ def main():
             r.run(x)
         dt_full = (time.perf_counter() - t) / (args.iters // 2)
         res[b] = {"graph_ms": dt * 1e3, "img_per_s": b / dt, "run_ms": dt_full * 1e3,
-                  "tflops": flop_per_item * b / dt / 1e12}
+                  "tflops": flop_per_item * b / dt / 1e12, "capture_s": round(t_capture, 2)}
         print(json.dumps({"model": args.model, "batch": b, **res[b]}), flush=True)
     if args.baseline and args.model == "resnet50":
         baseline(args)
