@@ -106,14 +106,28 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   // ---- softmax (rows fq*4 + r, columns nt*16 + fr)
   float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   const float* mrow = mask_bias ? mask_bias + long(b) * mask_bstride + long(q0 + fq * 4) * mask_qstride : nullptr;
+  if (mrow && mask_qstride == 0) {
+    // key mask shared by every query row (BERT's [B,1,1,S] adder): one load per key tile
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
+    for (int nt = 0; nt < NT; ++nt) {
+      const float mb = mrow[nt * 16 + fr];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float mb = mrow ? mrow[long(r) * mask_qstride + nt * 16 + fr] : 0.f;
-      const float v = s[nt][r] * scale + mb;
-      s[nt][r] = v;
-      mx[r] = fmaxf(mx[r], v);
+      for (int r = 0; r < 4; ++r) {
+        const float v = s[nt][r] * scale + mb;
+        s[nt][r] = v;
+        mx[r] = fmaxf(mx[r], v);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float mb = mrow ? mrow[long(r) * mask_qstride + nt * 16 + fr] : 0.f;
+        const float v = s[nt][r] * scale + mb;
+        s[nt][r] = v;
+        mx[r] = fmaxf(mx[r], v);
+      }
     }
   }
 #pragma unroll
@@ -149,13 +163,22 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
       o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[dt], 0, 0, 0);
     }
   }
-  // ---- normalise + store: rows q0 + fq*4 + r, cols h*D + dt*16 + fr
+  // ---- normalise, re-layout through the wave's P strip (its P reads are
+  // done: the MFMAs above consumed them) and store 16-B row chunks:
+  // rows q0 + i, cols h*D + [0, 64)
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float inv = 1.f / sum[r];
-    uint16_t* orow = ctx + (long(b) * S + q0 + fq * 4 + r) * (long(H) * D) + h * D;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) orow[dt * 16 + fr] = f32_to_bf16(o[dt][r] * inv);
+    for (int dt = 0; dt < 4; ++dt) pw[(fq * 4 + r) * P_LD + dt * 16 + fr] = f32_to_bf16(o[dt][r] * inv);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): this wave's LDS writes landed
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = j * 64 + lane, row = c >> 3, ch = c & 7;
+    *reinterpret_cast<uint4*>(ctx + (long(b) * S + q0 + row) * (long(H) * D) + h * D + ch * 8) =
+        *reinterpret_cast<const uint4*>(pw + row * P_LD + ch * 8);
   }
 }
 

@@ -7,7 +7,7 @@ namespace tfsk {
 // Config ids continue after the igemm ones so one `cfg` integer selects either
 // kernel family: cgemm configs are kCGemmCfgBase .. kCGemmCfgBase + kNumCGemmConfigs - 1.
 constexpr int kCGemmCfgBase = 32;
-constexpr int kNumCGemmConfigs = 13;
+constexpr int kNumCGemmConfigs = 16;
 
 // Operand requirements (else cgemm_launch returns hipErrorInvalidValue):
 //   dense (a_mode kADense): K % 64 == 0, lda % 8 == 0;

@@ -79,21 +79,28 @@ __device__ __forceinline__ void wait_vmcnt() {
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
 // ---- epilogue over the fp32 tile staged in LDS (8-column row chunks, NT threads)
+// NTE = the threads that take part: a multiple of the chunks per row, so a
+// thread's column is fixed (all NT unless BN / 8 does not divide NT, e.g. the
+// 96-wide tiles); EXACT = every (thread, iteration) maps inside the tile.
 template <int BM, int BN, int NT>
 struct Epi {
   static constexpr int CPR = BN / 8;
-  static constexpr int ITERS = BM * CPR / NT;
+  static constexpr int NTE = (NT / CPR) * CPR;
+  static constexpr int ITERS = (BM * CPR + NTE - 1) / NTE;
+  static constexpr bool EXACT = NTE == NT && (BM * CPR) % NT == 0;
   static constexpr int PRE = ITERS <= 8 ? ITERS : 0;
-  static_assert(NT % CPR == 0 && (BM * CPR) % NT == 0, "epilogue chunk mapping");
+  static_assert(NTE > 0, "epilogue chunk mapping");
 };
 
-// chunk `it` of thread `tid`: row-major 8-column chunks, NT apart (a thread's column is fixed)
-template <int BN, int NT>
-__device__ __forceinline__ void epi_rowcol(int tid, int it, int& row, int& col) {
-  constexpr int CPR = BN / 8;
-  const int c = tid + it * NT;
-  row = c / CPR;
-  col = (c - row * CPR) * 8;
+// chunk `it` of thread `tid`: row-major 8-column chunks, NTE apart (a thread's
+// column is fixed); false when the chunk lies outside the tile
+template <int BM, int BN, int NT>
+__device__ __forceinline__ bool epi_rowcol(int tid, int it, int& row, int& col) {
+  using E = Epi<BM, BN, NT>;
+  const int c = tid + it * E::NTE;
+  row = c / E::CPR;
+  col = (c - row * E::CPR) * 8;
+  return E::EXACT || (tid < E::NTE && row < BM);
 }
 
 template <int BM, int BN, int NT>
@@ -104,9 +111,9 @@ __device__ __forceinline__ void prefetch_residual(const IGemmArgs& p, int m0, in
 #pragma unroll
   for (int it = 0; it < E::PRE; ++it) {
     int row, col;
-    epi_rowcol<BN, NT>(tid, it, row, col);
+    const bool in = epi_rowcol<BM, BN, NT>(tid, it, row, col);
     const int m = m0 + row, n = n0 + col;
-    rpre[it] = (m < p.M && n + 8 <= p.N) ? *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n)
+    rpre[it] = (in && m < p.M && n + 8 <= p.N) ? *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n)
                                           : make_uint4(0, 0, 0, 0);
   }
 }
@@ -114,10 +121,10 @@ __device__ __forceinline__ void prefetch_residual(const IGemmArgs& p, int m0, in
 // This thread's 8 bias values (its epilogue column is fixed), loaded before the
 // K loop so the latency of the load hides under it instead of stalling the
 // epilogue of every workgroup.
-template <int BN, int NT>
+template <int BM, int BN, int NT>
 __device__ __forceinline__ void prefetch_bias(const IGemmArgs& p, int n0, int tid, float4& b0, float4& b1) {
   int row0, col0;
-  epi_rowcol<BN, NT>(tid, 0, row0, col0);
+  epi_rowcol<BM, BN, NT>(tid, 0, row0, col0);   // col0 < BN for every thread
   const int n = n0 + col0;
   b0 = b1 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (p.bias && p.splits <= 1 && p.N % 8 == 0 && n + 8 <= p.N) {
@@ -176,7 +183,7 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
 #pragma unroll
     for (int it = 0; it < E::ITERS; ++it) {
       int row, col;
-      epi_rowcol<BN, NT>(tid, it, row, col);
+      if (!epi_rowcol<BM, BN, NT>(tid, it, row, col)) continue;
       const int m = m0 + row, n = n0 + col;
       if (m >= M || n >= N) continue;
       uint4 rr = make_uint4(0, 0, 0, 0);
@@ -189,7 +196,7 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
 #pragma unroll 1
     for (int it = 0; it < E::ITERS; ++it) {
       int row, col;
-      epi_rowcol<BN, NT>(tid, it, row, col);
+      if (!epi_rowcol<BM, BN, NT>(tid, it, row, col)) continue;
       const int m = m0 + row, n = n0 + col;
       if (m >= M || n >= N) continue;
       const uint4 rr = p.residual ? *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n)
@@ -400,7 +407,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   uint4 rpre[Epi<BM, BN, G::NT>::PRE > 0 ? Epi<BM, BN, G::NT>::PRE : 1];
   prefetch_residual<BM, BN, G::NT>(p, m0, n0, tid, rpre);
   float4 bias0, bias1;
-  prefetch_bias<BN, G::NT>(p, n0, tid, bias0, bias1);
+  prefetch_bias<BM, BN, G::NT>(p, n0, tid, bias0, bias1);
 
   if (dbg & 16) {   // ablation: setup only (keep the per-lane state live)
     uint32_t keep = 0;
@@ -504,8 +511,8 @@ hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
 
 // Config table (tile BM x BN, wave grid, ring depth).  LDS per workgroup =
 // S * (BM + BN) * 128 B (or the fp32 epilogue tile if larger).
-constexpr int kBM[kNumCGemmConfigs] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256, 64, 64, 128};
-constexpr int kBN[kNumCGemmConfigs] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64, 64, 128, 64};
+constexpr int kBM[kNumCGemmConfigs] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256, 64, 64, 128, 128, 128, 64};
+constexpr int kBN[kNumCGemmConfigs] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64, 64, 128, 64, 96, 96, 96};
 
 template <int AM>
 hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
@@ -525,6 +532,12 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
     case 10: return launch_cfg<64, 64, 2, 2, 2, AM>(a, s);    // 32 KB (5 WG/CU)
     case 11: return launch_cfg<64, 128, 2, 2, 2, AM>(a, s);   // 48 KB (3 WG/CU)
     case 12: return launch_cfg<128, 64, 2, 2, 2, AM>(a, s);   // 48 KB (3 WG/CU)
+    // 96-wide tiles: N = 768 (BERT-base hidden) is 8 of them, so an M = 4096
+    // GEMM is exactly 256 tiles of 128 x 96 -- one per CU -- where 128 x 128
+    // leaves a quarter of the CUs idle (192 tiles) and 128 x 64 needs 1.5 waves
+    case 13: return launch_cfg<128, 96, 2, 2, 3, AM>(a, s);   // 84 KB, wave 64x48
+    case 14: return launch_cfg<128, 96, 2, 2, 4, AM>(a, s);   // 112 KB
+    case 15: return launch_cfg<64, 96, 2, 2, 3, AM>(a, s);    // 60 KB, wave 32x48
     default: return hipErrorInvalidValue;
   }
 }

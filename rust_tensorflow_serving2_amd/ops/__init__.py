@@ -82,7 +82,7 @@ TILE_BK = {12: 128, 13: 256, 14: 128, 15: 128, 16: 128}     # k-tile depth (defa
 # pipelined cgemm kernel (kernels/cgemm.hip; 64-aligned operands only): config id -> (BM, BN)
 CGEMM = {32: (128, 128), 33: (128, 128), 34: (64, 128), 35: (128, 64), 36: (64, 64),
          37: (256, 128), 38: (128, 256), 39: (128, 128), 40: (64, 256), 41: (256, 64),
-         42: (64, 64), 43: (64, 128), 44: (128, 64)}
+         42: (64, 64), 43: (64, 128), 44: (128, 64), 45: (128, 96), 46: (128, 96), 47: (64, 96)}
 TILES.update(CGEMM)
 
 
@@ -114,6 +114,8 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
             continue   # deep k-tiles only pay off with several of them
         if bn > 64 and N <= bn // 2 or bm > 64 and M <= bm // 2:
             continue   # mostly-empty tiles
+        if bn % 64 and N % bn:
+            continue   # 96-wide tiles: only where they divide N (BERT's 768 / 2304 / 3072)
         tiles = -(-M // bm) * -(-N // bn)
         for s in (1, 2, 4, 8, 16):
             if s > 1 and (nk // s < 2 or tiles >= 1024 or tiles * s > 4096):
@@ -183,7 +185,7 @@ def record_tuned_keys():
         _REC.keys = prev
 
 
-def graph_tune(keys: Dict[Tuple, int], time_fn: Callable[[], float], top: int = 3, ratio: float = 1.35,
+def graph_tune(keys: Dict[Tuple, int], time_fn: Callable[[], float], top: int = 4, ratio: float = 1.35,
                min_ms: float = 0.012) -> Dict[Tuple, Tuple[int, int]]:
     """Re-pick tile configs by timing the WHOLE program (``time_fn`` captures
     and replays it, returning ms) instead of one cold launch per kernel: inside
@@ -207,6 +209,7 @@ def graph_tune(keys: Dict[Tuple, int], time_fn: Callable[[], float], top: int = 
         _GRAPH_TUNED.update(keys)
         return changed
     todo.sort(key=lambda x: -x[0])
+    time_fn()                            # first capture/replay runs slow: discard it
     base = time_fn()
     for _w, k, cands in todo:
         cur = _TUNED[k]
