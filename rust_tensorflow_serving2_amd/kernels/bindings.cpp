@@ -63,6 +63,8 @@ void need(const Tensor& t, at::ScalarType st, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
+bool aligned16(const Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; }
+
 const uint16_t* bf16p(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
 uint16_t* bf16p_mut(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 
@@ -319,6 +321,7 @@ Tensor layernorm(const Tensor& x, const c10::optional<Tensor>& residual, const T
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int cols = x.size(-1);
   TORCH_CHECK(cols % 8 == 0 && gamma.numel() == cols && beta.numel() == cols, "layernorm shapes");
+  TORCH_CHECK(aligned16(gamma) && aligned16(beta), "layernorm: gamma / beta must be 16-B aligned");
   const int rows = x.numel() / cols;
   const uint16_t* r = nullptr;
   if (residual.has_value()) {
@@ -347,6 +350,7 @@ Tensor embed_ln(const Tensor& ids, const c10::optional<Tensor>& type_ids, const 
   const int64_t tokens = ids.numel(), Hd = word.size(1);
   TORCH_CHECK(Hd % 8 == 0 && Hd <= 2048, "embed_ln: hidden must be a multiple of 8 and <= 2048");
   TORCH_CHECK(gamma.numel() == Hd && beta.numel() == Hd, "embed_ln: LN params shape");
+  TORCH_CHECK(aligned16(gamma) && aligned16(beta), "embed_ln: gamma / beta must be 16-B aligned");
   TORCH_CHECK(seq > 0 && tokens % seq == 0 && tokens < (int64_t(1) << 31), "embed_ln: tokens must be batch * seq");
   const int* tt = nullptr;
   const uint16_t *pp = nullptr, *tp = nullptr;

@@ -191,7 +191,33 @@ __global__ void cast_bf16_f32_kernel(const uint16_t* __restrict__ x, float* __re
 }
 
 // ---------------------------------------------------------------- LayerNorm
-// One wave per row; two passes over the (L2-resident) row; fp32 statistics.
+// One wave per row, y = LN(x + r). Rows up to 64 * 8 * kLnChunks columns are
+// read once into registers (16-B loads), statistics are two-pass from the
+// registers, gamma/beta come in as float4 pairs; longer rows stream twice.
+constexpr int kLnChunks = 4;
+
+__device__ __forceinline__ void ln_load(const uint16_t* xr, const uint16_t* rr, int c, float* f) {
+  unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
+  if (rr) {
+    float g[8];
+    unpack8(*reinterpret_cast<const uint4*>(rr + c), g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] += g[e];
+  }
+}
+
+__device__ __forceinline__ void ln_store(uint16_t* yr, int c, const float* f, float mean, float inv,
+                                         const float* __restrict__ gamma, const float* __restrict__ beta) {
+  const float4 g0 = *reinterpret_cast<const float4*>(gamma + c), g1 = *reinterpret_cast<const float4*>(gamma + c + 4);
+  const float4 b0 = *reinterpret_cast<const float4*>(beta + c), b1 = *reinterpret_cast<const float4*>(beta + c + 4);
+  const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+  const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = (f[e] - mean) * inv * g[e] + bb[e];
+  *reinterpret_cast<uint4*>(yr + c) = pack8(o);
+}
+
 __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restrict__ x,
                                                         const uint16_t* __restrict__ r,
                                                         const float* __restrict__ gamma,
@@ -202,36 +228,50 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
   if (row >= rows) return;
   const uint16_t* xr = x + long(row) * cols;
   const uint16_t* rr = r ? r + long(row) * cols : nullptr;
+  uint16_t* yr = y + long(row) * cols;
+  if (cols <= 64 * 8 * kLnChunks) {
+    float v[kLnChunks][8];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kLnChunks; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < cols) {
+        ln_load(xr, rr, c, v[k]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += v[k][e];
+      }
+    }
+    const float mean = wave_sum(s) / cols;
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < kLnChunks; ++k)
+      if ((k * 64 + lane) * 8 < cols) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float d = v[k][e] - mean; ss += d * d; }
+      }
+    const float inv = rsqrtf(wave_sum(ss) / cols + eps);
+#pragma unroll
+    for (int k = 0; k < kLnChunks; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < cols) ln_store(yr, c, v[k], mean, inv, gamma, beta);
+    }
+    return;
+  }
   float s = 0.f, ss = 0.f;
   for (int c = lane * 8; c < cols; c += 512) {
     float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
-    if (rr) {
-      float g[8];
-      unpack8(*reinterpret_cast<const uint4*>(rr + c), g);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] += g[e];
-    }
+    ln_load(xr, rr, c, f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s += f[e]; ss += f[e] * f[e]; }
   }
   s = wave_sum(s);
   ss = wave_sum(ss);
   const float mean = s / cols;
-  const float var = fmaxf(ss / cols - mean * mean, 0.f);
-  const float inv = rsqrtf(var + eps);
+  const float inv = rsqrtf(fmaxf(ss / cols - mean * mean, 0.f) + eps);
   for (int c = lane * 8; c < cols; c += 512) {
     float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
-    if (rr) {
-      float g[8];
-      unpack8(*reinterpret_cast<const uint4*>(rr + c), g);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] += g[e];
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = (f[e] - mean) * inv * gamma[c + e] + beta[c + e];
-    *reinterpret_cast<uint4*>(y + long(row) * cols + c) = pack8(f);
+    ln_load(xr, rr, c, f);
+    ln_store(yr, c, f, mean, inv, gamma, beta);
   }
 }
 

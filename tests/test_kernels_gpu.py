@@ -297,6 +297,19 @@ def test_layernorm_and_embedding():
     assert (e.float().cpu() - ref).abs().max() < 5e-2
 
 
+@pytest.mark.parametrize("cols", [64, 520, 2048, 4104])
+def test_layernorm_register_and_streaming_paths(cols):
+    """Rows up to 2048 columns stay in registers; longer ones stream twice."""
+    x = (rnd(37, cols, seed=41) * 3 + 5).to(BF)      # offset mean: the two-pass variance matters
+    r = rnd(37, cols, seed=42).to(BF)
+    gm, bt = rnd(cols, seed=43), rnd(cols, seed=44)
+    y = hip().layernorm(x.to(DEV), r.to(DEV), gm.to(DEV), bt.to(DEV), 1e-5)
+    ref = F.layer_norm(x.float() + r.float(), (cols,), gm, bt, 1e-5)
+    assert (y.float().cpu() - ref).abs().max() < 6e-2
+    y2 = hip().layernorm(x.to(DEV), None, gm.to(DEV), bt.to(DEV), 1e-5)
+    assert (y2.float().cpu() - F.layer_norm(x.float(), (cols,), gm, bt, 1e-5)).abs().max() < 6e-2
+
+
 @pytest.mark.parametrize("hd", [64, 520, 1024, 2048])
 def test_embedding_out_of_range_rows_are_zero(hd):
     """Ids outside a table add a zero row (TF's GPU GatherV2); type ids and
