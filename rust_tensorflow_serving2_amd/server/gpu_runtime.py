@@ -200,6 +200,12 @@ class GpuRunner:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=lane.stream, capture_error_mode="thread_local"):
             outs = self._finish(self.program.run(ins))
+        # replay once now: a graph's first launch uploads it to the device
+        # (milliseconds), which must not land on the first live batch of a
+        # bucket (it showed up as a p99 spike in short benchmark windows)
+        with torch.cuda.stream(lane.stream):
+            graph.replay()
+        lane.stream.synchronize()
         lane.graphs[b] = graph
         lane.static_in[b] = ins
         lane.static_out[b] = outs
