@@ -240,16 +240,27 @@ class FusedDualConv:
 
 
 class FusedMatMul:
+    """``pad_n``: the consumers accept a row-strided [M, N] view, so an N that
+    is not a multiple of 8 (ResNet's 1001 classes) is computed as ceil8(N)
+    columns (zero weight rows) into an [M, ceil8(N)] buffer and returned as
+    its first N columns: the pipelined cgemm kernel applies (it needs N % 8 ==
+    0) instead of igemm + split-K reduce."""
+
     def __init__(self, w_kn: torch.Tensor, bias: Optional[torch.Tensor], act: str, out_f32: bool,
-                 device, use_hip: bool, name: str):
+                 device, use_hip: bool, name: str, pad_n: bool = False):
         self.k, self.n = w_kn.shape
         self.act = act
         self.out_f32 = out_f32
         self.use_hip = use_hip and self.k % 8 == 0
         self.name = name
         b = bias if bias is not None else torch.zeros(self.n)
+        self.np = -(-self.n // 8) * 8 if (pad_n and self.n % 8 and self.k % 64 == 0) else self.n
         if self.use_hip:
-            self.w = _pad_k(w_kn.t().contiguous(), 8).to(BF16).contiguous().to(device)
+            w_nk = w_kn.t().contiguous()
+            if self.np != self.n:
+                w_nk = torch.cat([w_nk, torch.zeros(self.np - self.n, self.k, dtype=w_nk.dtype)])
+                b = torch.cat([b.float().reshape(-1), torch.zeros(self.np - self.n)])
+            self.w = _pad_k(w_nk, 8).to(BF16).contiguous().to(device)
             self.b = b.float().contiguous().to(device)
         else:
             self.w_ref = w_kn.float().to(device)
@@ -270,12 +281,16 @@ class FusedMatMul:
         if res is not None:
             res = _to_bf16(res).contiguous()
         M = x.numel() // self.k
-        shape = list(x.shape[:-1]) + [self.n]
+        padded = self.np != self.n and res is None and x.dim() == 2
+        n = self.np if padded else self.n
+        w, b = (self.w, self.b) if padded or self.np == self.n else (self.w[:self.n], self.b[:self.n])
+        shape = list(x.shape[:-1]) + [n]
         out = torch.empty(shape, device=x.device, dtype=torch.float32 if self.out_f32 else BF16)
-        key = ("mm", M, self.n, self.k, res is not None, self.out_f32, self.act)
-        run = lambda c, s: H.linear(x, self.w, self.b, res, ACT[self.act], c, self.out_f32, 1.0, out, s)  # noqa
-        cfg, splits = tuned_config(key, M, self.n, run, self.k, True, self.k % 64 == 0)
-        return [run(cfg, splits)]
+        key = ("mm", M, n, self.k, res is not None, self.out_f32, self.act)
+        run = lambda c, s: H.linear(x, w, b, res, ACT[self.act], c, self.out_f32, 1.0, out, s)  # noqa
+        cfg, splits = tuned_config(key, M, n, run, self.k, True, self.k % 64 == 0)
+        y = run(cfg, splits)
+        return [y[:, :self.n] if padded else y]
 
 
 def _ref_act(y, act):
@@ -344,7 +359,9 @@ class SoftmaxArgMax:
         x = O.to_torch(ins[0])
         if self.use_hip and x.is_cuda and x.dim() == 2 and x.dtype in (torch.float32, BF16):
             from ..ops import hip
-            probs, cls = hip().softmax_argmax(x.contiguous(), True, True)
+            if x.stride(-1) != 1:
+                x = x.contiguous()
+            probs, cls = hip().softmax_argmax(x, True, True)     # row-strided views are fine
         else:
             probs = torch.softmax(x.float(), dim=-1)
             cls = torch.argmax(x.float(), dim=-1)
@@ -488,7 +505,10 @@ def fuse_matmul(g, order, fed, fetch_refs, device, opts):
                 chain.append(nxt)
                 cur = nxt
         out_f32 = _feeds_head(c, cur.name)
-        impl = FusedMatMul(w, bias, act, out_f32, device, c.use_hip, cur.name)
+        cons = c.cons.get(cur.name, [])
+        pad_n = cur.name not in c.fetch_nodes and bool(cons) and \
+            all(g.nodes[cn].op == "_SoftmaxArgMax" for cn, _p, _i in cons)
+        impl = FusedMatMul(w, bias, act, out_f32, device, c.use_hip, cur.name, pad_n)
         _finalize(g, chain, "_FusedMatMul", [n.inputs[0]] + ([residual] if residual else []), {"_impl": impl})
         c.refresh()
 

@@ -230,12 +230,17 @@ Tensor global_avgpool(const Tensor& x, const c10::optional<Tensor>& out) {
 std::vector<Tensor> softmax_argmax(const Tensor& logits, bool want_probs, bool want_classes,
                                    const c10::optional<Tensor>& probs_out,
                                    const c10::optional<Tensor>& classes_out) {
-  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous(), "logits must be contiguous GPU");
+  // rows may be strided (a [M, N] view of a GEMM output padded to ldc > N)
+  TORCH_CHECK(logits.is_cuda() && logits.dim() >= 1 && logits.stride(-1) == 1 &&
+                  (logits.is_contiguous() || logits.dim() == 2),
+              "logits must be a GPU tensor with unit column stride (contiguous, or 2-D with a row stride)");
   const bool bf = logits.scalar_type() == at::kBFloat16;
   TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "logits must be f32 or bf16");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
   const int cols = logits.size(-1);
   const int rows = logits.numel() / cols;
+  const long ld = logits.dim() == 2 ? long(logits.stride(0)) : long(cols);
+  TORCH_CHECK(ld >= cols, "logits row stride");
   Tensor probs, classes;
   if (want_probs) {
     probs = probs_out.has_value() ? *probs_out : torch::empty(logits.sizes(), logits.options().dtype(at::kFloat));
@@ -248,7 +253,7 @@ std::vector<Tensor> softmax_argmax(const Tensor& logits, bool want_probs, bool w
     need(classes, at::kLong, "classes");
   }
   check(tfsk::softmax_argmax_launch(logits.data_ptr(), bf, want_probs ? probs.data_ptr<float>() : nullptr,
-                                    want_classes ? classes.data_ptr<int64_t>() : nullptr, rows, cols,
+                                    want_classes ? classes.data_ptr<int64_t>() : nullptr, rows, cols, ld,
                                     cur_stream(logits)), "softmax_argmax");
   return {probs, classes};
 }

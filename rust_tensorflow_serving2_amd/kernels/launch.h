@@ -81,7 +81,7 @@ hipError_t global_avgpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int
                                       hipStream_t stream);
 // Row softmax (fp32 in) -> probs f32 + argmax int64 (the classifier head).
 hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, int64_t* classes,
-                                 int rows, int cols, hipStream_t stream);
+                                 int rows, int cols, long ld, hipStream_t stream);
 // fp32 -> bf16 cast (vectorized).
 hipError_t cast_f32_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t stream);
 hipError_t cast_bf16_f32_launch(const uint16_t* x, float* y, int64_t n, hipStream_t stream);

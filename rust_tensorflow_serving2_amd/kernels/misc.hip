@@ -102,7 +102,8 @@ __global__ __launch_bounds__(256) void gap_nhwc_kernel(const uint16_t* __restric
 constexpr int kSmPer = 16;
 __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restrict__ logits, int in_bf16,
                                                              float* __restrict__ probs,
-                                                             int64_t* __restrict__ classes, int rows, int cols) {
+                                                             int64_t* __restrict__ classes, int rows, int cols,
+                                                             long ld) {
   __shared__ float smx[4];
   __shared__ int sarg[4];
   __shared__ float ssum[4];
@@ -117,15 +118,15 @@ __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restr
     const int c = k * 256 + tid;
     float x = -INFINITY;
     if (c < cols)
-      x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * cols + c])
-                  : static_cast<const float*>(logits)[long(row) * cols + c];
+      x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * ld + c])
+                  : static_cast<const float*>(logits)[long(row) * ld + c];
     v[k] = x;
     if (c < cols && (x > mx || (x == mx && c < arg))) { mx = x; arg = c; }
   }
   // columns beyond the register tile (cols > 4096): strided tail, recomputed below
   for (int c = kSmPer * 256 + tid; c < cols; c += 256) {
-    const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * cols + c])
-                            : static_cast<const float*>(logits)[long(row) * cols + c];
+    const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * ld + c])
+                            : static_cast<const float*>(logits)[long(row) * ld + c];
     if (x > mx || (x == mx && c < arg)) { mx = x; arg = c; }
   }
 #pragma unroll
@@ -149,8 +150,8 @@ __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restr
     s += v[k];
   }
   for (int c = kSmPer * 256 + tid; c < cols; c += 256) {
-    const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * cols + c])
-                            : static_cast<const float*>(logits)[long(row) * cols + c];
+    const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * ld + c])
+                            : static_cast<const float*>(logits)[long(row) * ld + c];
     s += __expf(x - mx);
   }
   s = wave_sum(s);
@@ -164,8 +165,8 @@ __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restr
       if (c < cols) probs[long(row) * cols + c] = v[k] * inv;
     }
     for (int c = kSmPer * 256 + tid; c < cols; c += 256) {
-      const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * cols + c])
-                              : static_cast<const float*>(logits)[long(row) * cols + c];
+      const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * ld + c])
+                              : static_cast<const float*>(logits)[long(row) * ld + c];
       probs[long(row) * cols + c] = __expf(x - mx) * inv;
     }
   }
@@ -422,10 +423,11 @@ hipError_t global_avgpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int
 }
 
 hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, int64_t* classes, int rows,
-                                 int cols, hipStream_t s) {
+                                 int cols, long ld, hipStream_t s) {
   if (rows <= 0) return hipSuccess;
+  if (ld < cols) return hipErrorInvalidValue;
   hipLaunchKernelGGL(softmax_argmax_kernel, dim3(rows), dim3(256), 0, s, logits, in_bf16, probs, classes, rows,
-                     cols);
+                     cols, ld);
   return hipGetLastError();
 }
 

@@ -273,6 +273,34 @@ def test_softmax_argmax_shapes(rows, cols):
     assert torch.equal(c.cpu(), torch.argmax(logits, -1))
 
 
+@pytest.mark.parametrize("cols", [1001, 5000])
+def test_softmax_argmax_row_strided(cols):
+    """Logits as the first `cols` columns of a padded [rows, ceil8(cols)] GEMM
+    output (the ResNet FC with N padded to a multiple of 8)."""
+    ld = -(-cols // 8) * 8 + 8
+    full = rnd(7, ld, scale=4, seed=cols)
+    full[:, cols:] = 1e4                     # padding columns must never be read
+    view = full.to(DEV)[:, :cols]
+    p, c = hip().softmax_argmax(view)
+    logits = full[:, :cols]
+    assert torch.allclose(p.cpu(), torch.softmax(logits, -1), atol=1e-6)
+    assert torch.equal(c.cpu(), torch.argmax(logits, -1))
+
+
+def test_linear_padded_n_feeds_softmax():
+    """FusedMatMul with N = 1001 padded to 1008 (cgemm) == fp32 reference."""
+    from rust_tensorflow_serving2_amd.graph.fused import FusedMatMul
+    w = rnd(2048, 1001, scale=0.03, seed=51)
+    b = rnd(1001, scale=0.1, seed=52)
+    x = rnd(32, 2048, seed=53).to(BF)
+    mm = FusedMatMul(w, b, "none", True, torch.device(DEV), True, "fc", pad_n=True)
+    assert mm.np == 1008
+    y = mm(None, None, [x.to(DEV)])[0]
+    assert y.shape == (32, 1001) and y.stride(0) == 1008
+    ref = x.float() @ w.to(BF).float() + b
+    assert (y.cpu() - ref).abs().max() < 3e-2 * max(1.0, ref.abs().max().item())
+
+
 @pytest.mark.parametrize("n,hw,c", [(3, 1, 72), (2, 9, 520), (1, 49, 4096)])
 def test_global_avgpool_shapes(n, hw, c):
     g = rnd(n, hw, 1, c, seed=hw + c).to(BF)
