@@ -357,6 +357,7 @@ void Endpoint::complete(int slot, Server& srv) {
     s.ready.clear();
     s.reserved = s.copied = 0;
     s.state = kFree;
+    st_.consecutive_failed = 0;
     cv_free_.notify_all();
   }
   drain_queue();
@@ -372,6 +373,8 @@ void Endpoint::fail(int slot, Server& srv, int code, const std::string& msg) {
     s.ready.clear();
     s.reserved = s.copied = 0;
     s.state = kFree;
+    st_.failed++;
+    st_.consecutive_failed++;
     cv_free_.notify_all();
   }
   drain_queue();

@@ -85,6 +85,9 @@ struct Slot {
 
 struct EndpointStats {
   uint64_t requests = 0, batches = 0, rows = 0, rejected = 0;
+  // failed batches in total and since the last completed one (the replica
+  // health monitor reloads a servable whose device keeps failing)
+  uint64_t failed = 0, consecutive_failed = 0;
 };
 
 class Endpoint {

@@ -131,11 +131,15 @@ class NativeLane {
   NativeLane(Server* srv, std::shared_ptr<Endpoint> ep, int slot, int device, void* stream,
              std::vector<LaneBucket> buckets)
       : srv_(srv), ep_(std::move(ep)), slot_(slot), device_(device), stream_(stream), buckets_(std::move(buckets)) {
-    // fault injection for tests: TFSERVE_FAULT=lane_every=N fails every Nth batch
+    // fault injection for tests (same spec as utils/faults.py):
+    // TFSERVE_FAULT=lane_every=N fails every Nth batch, lane_after=N every
+    // batch after the first N of this lane (a device that went bad)
     if (const char* f = getenv("TFSERVE_FAULT")) {
       const std::string spec(f);
-      const auto k = spec.find("lane_every=");
+      auto k = spec.find("lane_every=");
       if (k != std::string::npos) fault_every_ = std::atoi(spec.c_str() + k + 11);
+      k = spec.find("lane_after=");
+      if (k != std::string::npos) fault_after_ = std::atoi(spec.c_str() + k + 11);
     }
     std::sort(buckets_.begin(), buckets_.end(), [](auto& a, auto& b) { return a.rows < b.rows; });
     // eager H2D (rows copied to the device while the batch fills) needs every
@@ -234,7 +238,9 @@ class NativeLane {
         copy_err = 0;
         continue;
       }
-      if (fault_every_ > 0 && ++seen_ % uint64_t(fault_every_) == 0) {
+      ++seen_;
+      if ((fault_every_ > 0 && seen_ % uint64_t(fault_every_) == 0) ||
+          (fault_after_ >= 0 && seen_ > uint64_t(fault_after_))) {
         errors++;
         ep_->fail(slot_, *srv_, 13 /*INTERNAL*/, "injected fault (TFSERVE_FAULT)");
         continue;
@@ -269,6 +275,7 @@ class NativeLane {
   void* copy_stream_ = nullptr;
   void* copied_ = nullptr;
   int fault_every_ = 0;
+  int fault_after_ = -1;
   uint64_t seen_ = 0;
   std::thread th_;
 };
@@ -481,6 +488,7 @@ void register_server(py::module_& m) {
         if (!ep) return d;
         auto st = ep->stats();
         d["requests"] = st.requests; d["batches"] = st.batches; d["rows"] = st.rows; d["rejected"] = st.rejected;
+        d["failed"] = st.failed; d["consecutive_failed"] = st.consecutive_failed;
         return d;
       });
 

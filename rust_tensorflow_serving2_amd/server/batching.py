@@ -227,6 +227,9 @@ class BatchingSession:
                 if target > total:
                     x = np.concatenate([x, np.repeat(x[:1], target - total, axis=0)], axis=0)
                 feeds[a] = x
+            fault = getattr(q.servable, "fault", None)
+            if fault is not None:
+                fault.check()
             outs = q.servable.run(q.sig_name, feeds, list(q.out_aliases))
             off = 0
             for t in b.tasks:

@@ -64,6 +64,9 @@ def build_parser() -> argparse.ArgumentParser:
     a("--dtype", default="bf16", choices=["bf16", "fp32"],
       help="GPU compute dtype: bf16 = fused MFMA kernels; fp32 = unfused fp32 reference path")
     a("--trace_dir", default="", help="write request/batch timelines (JSON lines) here")
+    a("--health_failure_threshold", type=int, default=8,
+      help="consecutive failed batches after which a servable is reloaded (0 = no health monitor)")
+    a("--health_max_recoveries", type=int, default=3, help="reloads of one version before it is quarantined")
     a("--log_level", default="INFO")
     return ap
 
@@ -122,7 +125,8 @@ def make_server(args, rank: int = 0, world: int = 1):
                          transport=args.transport, file_system_poll_wait_seconds=args.file_system_poll_wait_seconds,
                          io_threads=args.io_threads, batch_timeout_us=args.batch_timeout_us, servable=sopts,
                          monitoring=args.monitoring, weight_source=weight_source, replicas=replicas,
-                         trace_dir=args.trace_dir)
+                         trace_dir=args.trace_dir, health_failure_threshold=args.health_failure_threshold,
+                         health_max_recoveries=args.health_max_recoveries)
     return ModelServer(opts)
 
 

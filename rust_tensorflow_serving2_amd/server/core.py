@@ -58,6 +58,7 @@ class ServingCore:
         self.metrics = metrics
         self.replicas = None          # parallel.replicas.ReplicaControl when serving N GPU replicas
         self.tracer = None            # utils.tracing.Tracer (--trace_dir)
+        self.health = None            # server.health.HealthMonitor (device-failure detection)
         self.handlers = {
             METHOD_PREFIX_P + "Predict": self.predict,
             METHOD_PREFIX_P + "Classify": self.classify,
@@ -96,8 +97,24 @@ class ServingCore:
         return self.manager.resolve(name, version, label)
 
     def _run(self, servable, sig_name: str, inputs: Dict, out_aliases: Sequence[str]):
+        if self.health is None:
+            return self._run_raw(servable, sig_name, inputs, out_aliases)
+        try:
+            out = self._run_raw(servable, sig_name, inputs, out_aliases)
+        except BaseException as e:
+            from .health import is_device_failure
+            if is_device_failure(e):
+                self.health.record(servable.name, servable.version, False, str(e))
+            raise
+        self.health.record(servable.name, servable.version, True)
+        return out
+
+    def _run_raw(self, servable, sig_name: str, inputs: Dict, out_aliases: Sequence[str]):
         if self.batcher is not None:
             return self.batcher.run(servable, sig_name, inputs, list(out_aliases))
+        fault = getattr(servable, "fault", None)
+        if fault is not None:
+            fault.check()
         return servable.run(sig_name, inputs, list(out_aliases))
 
     @staticmethod

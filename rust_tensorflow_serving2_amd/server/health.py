@@ -1,0 +1,134 @@
+"""Replica health: detect a servable whose device keeps failing and reload it.
+
+SURVEY.md §5 "Failure detection / elastic recovery": the reference has none
+(errors bubble up as ``Box<dyn Error>``, ``src/lib.rs:11``); TF Serving marks a
+failed load ``END`` with an error status (``get_model_status.proto:50-60``).
+Serving on GPUs adds a failure mode the load path never sees: a servable that
+loaded fine starts failing every batch (a HIP error, a wedged stream, a
+corrupted graph).  Policy:
+
+* Every executed batch reports success or failure per (model, version):
+  the Python path through :meth:`HealthMonitor.record` (called by the serving
+  core around each run), the C++ fast-path lanes through their endpoint
+  counters (``failed`` / ``consecutive_failed`` in ``endpoint_stats``) which a
+  watcher thread polls.  Client errors (bad shapes, unknown aliases) are not
+  device failures and are not counted.
+* ``threshold`` consecutive failures with no success in between mark the
+  version unhealthy: the manager unloads it (draining nothing — its batches are
+  failing anyway) and loads it again from disk (:meth:`ModelManager.recover`).
+  Other versions and models keep serving throughout.
+* After ``max_recoveries`` reloads of one version it is quarantined: state
+  ``END`` with ``UNAVAILABLE`` and the last failure in its status, until a
+  config reload asks for it again.
+
+The one-process-per-GPU topology (``parallel/replicas.py``) makes this
+per-GPU: each replica process runs its own monitor over its own device.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+from typing import Callable, Dict, Iterable, List, Optional, Tuple
+
+from . import errors as E
+
+log = logging.getLogger("tfserve.health")
+
+# codes that say "the server could not run the batch", as opposed to "the
+# request was wrong" (INVALID_ARGUMENT, NOT_FOUND, FAILED_PRECONDITION, ...)
+DEVICE_FAILURE_CODES = (E.INTERNAL, E.UNKNOWN, E.DATA_LOSS)
+
+
+def is_device_failure(exc: BaseException) -> bool:
+    if isinstance(exc, E.ServingError):
+        return exc.code in DEVICE_FAILURE_CODES
+    return isinstance(exc, Exception)
+
+
+class HealthMonitor:
+    def __init__(self, manager, threshold: int = 8, max_recoveries: int = 3, poll_s: float = 0.25, metrics=None):
+        self.manager = manager
+        self.threshold = max(1, int(threshold))
+        self.max_recoveries = int(max_recoveries)
+        self.poll_s = poll_s
+        self._lock = threading.Lock()
+        self._consec: Dict[Tuple[str, int], int] = {}
+        self._native_seen: Dict[Tuple[str, int, str], int] = {}
+        self.failures: Dict[Tuple[str, int], int] = {}
+        self.recoveries: Dict[Tuple[str, int], int] = {}
+        self._sources: List[Callable[[], Iterable[Tuple[str, int, str, int, int]]]] = []
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        if metrics is not None:
+            metrics.collectors.append(self.prometheus_lines)
+
+    # --------------------------------------------------------------- reports
+    def record(self, name: str, version: int, ok: bool, why: str = "") -> None:
+        key = (name, int(version))
+        with self._lock:
+            if ok:
+                self._consec[key] = 0
+                return
+            self.failures[key] = self.failures.get(key, 0) + 1
+            n = self._consec.get(key, 0) + 1
+            self._consec[key] = n
+            trip = n >= self.threshold
+            if trip:
+                self._consec[key] = 0
+        if trip:
+            self._trip(name, int(version), f"{n} consecutive failed batches; last: {why}")
+
+    def add_source(self, fn: Callable[[], Iterable[Tuple[str, int, str, int, int]]]) -> None:
+        """``fn()`` yields ``(model, version, signature, failed_total, consecutive_failed)``
+        for native executors (polled; the C++ lanes report no per-batch callback)."""
+        self._sources.append(fn)
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._poll, name="tfs-health", daemon=True)
+            self._thread.start()
+
+    def _poll(self) -> None:
+        while not self._stop.wait(self.poll_s):
+            for src in list(self._sources):
+                try:
+                    rows = list(src())
+                except Exception:       # a source being torn down
+                    continue
+                for name, version, sig, failed, consec in rows:
+                    k = (name, int(version), sig)
+                    with self._lock:
+                        new = failed - self._native_seen.get(k, 0)
+                        self._native_seen[k] = failed
+                        if new > 0:
+                            self.failures[(name, int(version))] = self.failures.get((name, int(version)), 0) + new
+                    if consec >= self.threshold:
+                        with self._lock:
+                            self._native_seen.pop(k, None)
+                        self._trip(name, int(version), f"{consec} consecutive failed batches on the GPU fast path")
+
+    def _trip(self, name: str, version: int, why: str) -> None:
+        key = (name, version)
+        with self._lock:
+            n = self.recoveries.get(key, 0)
+            quarantine = n >= self.max_recoveries
+            if not quarantine:
+                self.recoveries[key] = n + 1
+        log.error("model %s version %d unhealthy (%s); %s", name, version, why,
+                  "quarantined" if quarantine else f"reloading (recovery {n + 1}/{self.max_recoveries})")
+        self.manager.recover(name, version, why, quarantine=quarantine)
+
+    # --------------------------------------------------------------- exports
+    def prometheus_lines(self) -> List[str]:
+        with self._lock:
+            f = dict(self.failures)
+            r = dict(self.recoveries)
+        out = ["# TYPE tfserve_batch_failures_total counter"]
+        out += [f'tfserve_batch_failures_total{{model="{m}",version="{v}"}} {n}' for (m, v), n in sorted(f.items())]
+        out.append("# TYPE tfserve_servable_recoveries_total counter")
+        out += [f'tfserve_servable_recoveries_total{{model="{m}",version="{v}"}} {n}'
+                for (m, v), n in sorted(r.items())]
+        return out
+
+    def close(self) -> None:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=2)

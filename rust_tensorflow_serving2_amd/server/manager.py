@@ -45,6 +45,8 @@ class VersionState:
     error_message: str = ""
     servable: object = None
     path: str = ""
+    recover: bool = False               # unloading because unhealthy: load again once END
+    quarantined: bool = False           # unhealthy too often: not reloaded until a config asks
 
 
 @dataclass
@@ -153,6 +155,8 @@ class ModelManager:
                             self._begin_unload(name, vs)
                         entry.versions = {v: s for v, s in entry.versions.items() if s.state != END}
                     entry.config = mc
+                    for vs in entry.versions.values():     # an explicit config lifts quarantine
+                        vs.quarantined = False
                 self._reconcile(name, entry)
         if wait:
             return self.wait_until_settled(list(new), timeout)
@@ -172,7 +176,7 @@ class ModelManager:
         aspired = set(aspired_versions(cfg, avail))
         for v in sorted(aspired):
             vs = entry.versions.get(v)
-            if vs is None or vs.state == END:
+            if vs is None or (vs.state == END and not vs.quarantined):
                 vs = VersionState(version=v, state=START, path=avail[v])
                 entry.versions[v] = vs
                 self._notify(name, v, START)
@@ -255,7 +259,30 @@ class ModelManager:
                 self._cv.notify_all()
             self._notify(name, vs.version, END)
             log.info("model %s version %d unloaded", name, vs.version)
+            if vs.recover:
+                with self._lock:
+                    entry = self._models.get(name)
+                    if entry is not None and not entry.removed:
+                        self._reconcile(name, entry)     # still aspired -> loaded again
         self._pool.submit(work)
+
+    # ------------------------------------------------------------ health
+    def recover(self, name: str, version: int, why: str, quarantine: bool = False) -> bool:
+        """Take an AVAILABLE version that keeps failing down and (unless
+        ``quarantine``) load it again from disk (server/health.py).  Other
+        versions keep serving; returns False if the version was not AVAILABLE."""
+        with self._cv:
+            entry = self._models.get(name)
+            vs = entry.versions.get(version) if entry is not None else None
+            if vs is None or entry.removed or vs.state != AVAILABLE:
+                return False
+            vs.recover = not quarantine
+            vs.quarantined = quarantine
+            vs.error_code = E.UNAVAILABLE
+            vs.error_message = ("quarantined after repeated device failures: " if quarantine else
+                                "unhealthy, reloading: ") + why
+            self._begin_unload(name, vs)
+            return True
 
     def _notify(self, name, version, state):
         for cb in list(self.listeners):

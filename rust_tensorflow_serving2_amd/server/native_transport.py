@@ -80,6 +80,8 @@ class FastEndpoint:
             if n == 0:
                 continue
             try:
+                if self.servable.fault is not None:
+                    self.servable.fault.check()
                 self.runner.run_lane(lane_idx, n)
             except Exception as e:  # report to every caller of the batch
                 log.exception("fast-path batch failed")
@@ -275,6 +277,15 @@ class NativeTransport:
             out.append(f"tfserve_fastpath_rows_total{{{lab}}} {es.get('rows', 0)}")
             out.append(f"tfserve_fastpath_rejected_total{{{lab}}} {es.get('rejected', 0)}")
         return out
+
+    def health_rows(self):
+        """(model, version, signature, failed, consecutive_failed) per fast endpoint
+        (polled by server.health.HealthMonitor)."""
+        with self._eps_lock:
+            eps = list(self._eps.items())
+        for (name, ver, sig), ep in eps:
+            es = self.srv.endpoint_stats(ep.id)
+            yield name, ver, sig, es.get("failed", 0), es.get("consecutive_failed", 0)
 
     def stats(self) -> dict:
         d = dict(self.srv.stats())

@@ -133,6 +133,9 @@ class Servable:
         self.in_flight = 0
         self._cv = threading.Condition()
         self.loaded_at = time.time()
+        from ..utils.faults import FaultPoint
+        fp = FaultPoint()
+        self.fault = fp if fp.enabled else None     # TFSERVE_FAULT injection (tests)
         self._graph_lock = threading.Lock()
 
     # ------------------------------------------------------------ graph helpers

@@ -46,6 +46,8 @@ class ServerOptions:
     model_config_file: str = ""                    # text-format ModelServerConfig
     model_config_file_poll_wait_seconds: float = 0.0
     trace_dir: str = ""                            # request/batch timeline (utils/tracing.py)
+    health_failure_threshold: int = 8              # consecutive failed batches -> reload (0 = off)
+    health_max_recoveries: int = 3                 # reloads per version before quarantine
 
 
 class ModelServer:
@@ -70,6 +72,12 @@ class ModelServer:
             from ..utils.tracing import Tracer
             self.tracer = Tracer(opts.trace_dir)
             self.core.tracer = self.tracer
+        self.health = None
+        if opts.health_failure_threshold > 0:
+            from .health import HealthMonitor
+            self.health = HealthMonitor(self.manager, opts.health_failure_threshold, opts.health_max_recoveries,
+                                        metrics=self.metrics)
+            self.core.health = self.health
         self.transports = []
         self._cfg_thread = None
         self._cfg_stop = threading.Event()
@@ -150,6 +158,8 @@ class ModelServer:
             t = GrpcTransport(self.core, self.opts.port, self.opts.host, self.opts.grpc_workers)
         self.transports.append(t.start())
         self.port = t.port
+        if self.health is not None and hasattr(t, "health_rows"):
+            self.health.add_source(t.health_rows)
         if self.tracer is not None and self.opts.transport == "native":
             self.tracer.attach_native(t.srv)
         if self.opts.rest_api_port:
@@ -170,6 +180,8 @@ class ModelServer:
         for t in self.transports:
             t.stop()
         self.transports.clear()
+        if self.health is not None:
+            self.health.close()
         if self.batcher is not None:
             self.batcher.stop()
         self.manager.stop()

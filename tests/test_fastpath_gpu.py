@@ -150,3 +150,46 @@ def test_native_lanes_and_injected_faults(tmp_path, monkeypatch):
     batches = [r for r in tracing.load(srv.tracer.path) if r["type"] == "batch"]
     assert len(batches) == 6        # the 6 successful batches (faulted ones are not traced)
     assert all(r["opened_us"] <= r["acquired_us"] <= r["done_us"] <= r["posted_us"] for r in batches)
+
+
+def test_native_lane_device_failure_reloads_servable(tmp_path, monkeypatch):
+    """A native lane whose every batch fails after the first 2 (lane_after=2,
+    a device gone bad) trips the health monitor through the endpoint's
+    consecutive-failure counter; the version is unloaded and loaded again and
+    serves OK afterwards (server/health.py)."""
+    from rust_tensorflow_serving2_amd.models import resnet
+    import time
+    monkeypatch.setenv("TFSERVE_FAULT", "lane_after=2")
+    base = str(tmp_path / "resnet")
+    resnet.export(os.path.join(base, "1"), blocks=(1, 1, 1, 1), width=16, num_classes=10, image_size=32, seed=6)
+    so = ServableOptions(device="cuda:0", max_batch_size=4, allowed_batch_sizes=(1, 2, 4), lanes=1)
+    srv = ModelServer(ServerOptions(port=0, host="127.0.0.1", model_name="resnet", model_base_path=base,
+                                    device="cuda:0", transport="native", servable=so,
+                                    file_system_poll_wait_seconds=0, batch_timeout_us=200,
+                                    health_failure_threshold=3, health_max_recoveries=10)).start()
+    try:
+        tr = srv.transports[0]
+        for _ in range(300):
+            if tr.stats().get("endpoints"):
+                break
+            time.sleep(0.05)
+        x = np.random.default_rng(7).random((1, 32, 32, 3), dtype=np.float32)
+        body = native.encode_predict_request(native.spec_tuple("resnet", None, None, ""), {"input": x})
+        codes = []
+        with grpc.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+            stub = ch.unary_unary(PREDICT)
+            for _ in range(80):
+                try:
+                    stub(body, timeout=30)
+                    codes.append("OK")
+                except grpc.RpcError as e:
+                    codes.append(e.code().name)
+                if srv.health.recoveries.get(("resnet", 1), 0) >= 1 and "OK" in codes[codes.index("INTERNAL"):]:
+                    break
+                time.sleep(0.05)
+        assert codes[:2] == ["OK", "OK"], codes
+        assert srv.health.recoveries.get(("resnet", 1), 0) >= 1, codes
+        assert "OK" in codes[codes.index("INTERNAL"):], codes      # served again after the reload
+        assert srv.health.failures[("resnet", 1)] >= 3
+    finally:
+        srv.stop()

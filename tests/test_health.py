@@ -1,0 +1,150 @@
+"""Failure detection and recovery: a servable whose batches keep
+failing is taken down and reloaded from disk, quarantined after too many
+reloads, and a config reload lifts the quarantine.  Device failures are
+injected with TFSERVE_FAULT (utils/faults.py; the C++ lanes parse the same
+spec)."""
+import asyncio
+import time
+
+import numpy as np
+import pytest
+
+from rust_tensorflow_serving2_amd.client import TensorflowServing, TFServingError
+from rust_tensorflow_serving2_amd.schema import serving
+from rust_tensorflow_serving2_amd.server import errors as E
+from rust_tensorflow_serving2_amd.server.health import HealthMonitor, is_device_failure
+from rust_tensorflow_serving2_amd.server.manager import AVAILABLE, END, ModelManager
+from rust_tensorflow_serving2_amd.server.server import ModelServer, ServerOptions
+from rust_tensorflow_serving2_amd.utils.faults import FaultPoint, InjectedFault, parse
+
+from test_manager import FakeServable, config, make_versions
+
+
+def wait_for(pred, timeout=10.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if pred():
+            return True
+        time.sleep(0.02)
+    return False
+
+
+def test_fault_spec():
+    assert parse("lane_every=3,lane_after=5, junk=1") == {"lane_every": 3, "lane_after": 5}
+    fp = FaultPoint("lane_after=2")
+    fp.check()
+    fp.check()
+    with pytest.raises(InjectedFault):
+        fp.check()
+    fp = FaultPoint("lane_every=2")
+    fp.check()
+    with pytest.raises(InjectedFault):
+        fp.check()
+    fp.check()
+    assert not FaultPoint("").enabled
+
+
+def test_device_failure_classification():
+    assert is_device_failure(E.internal("hip error"))
+    assert is_device_failure(RuntimeError("HIP error: an illegal memory access"))
+    assert not is_device_failure(E.invalid("bad shape"))
+    assert not is_device_failure(E.not_found("no such model"))
+
+
+@pytest.fixture()
+def mgr(tmp_path):
+    loads = []
+
+    def loader(name, version, path, cfg):
+        loads.append((name, version))
+        return FakeServable(name, version)
+    m = ModelManager(loader, poll_wait_seconds=0)
+    m.loads = loads
+    make_versions(tmp_path / "a", [1])
+    make_versions(tmp_path / "b", [1])
+    cfg = config("a", tmp_path / "a")
+    cfg.model_config_list.config.add(name="b", base_path=str(tmp_path / "b"))
+    m.cfg = cfg
+    assert m.apply_config(cfg) == []
+    yield m
+    m.stop()
+
+
+def test_consecutive_failures_reload_then_quarantine(mgr):
+    h = HealthMonitor(mgr, threshold=3, max_recoveries=1)
+    first = mgr.resolve("a")
+    mgr.resolve("a").release()
+    first.release()
+    # failures interleaved with a success never trip
+    for ok in (False, False, True, False, False, True):
+        h.record("a", 1, ok, "x")
+    assert mgr.loads.count(("a", 1)) == 1
+    for _ in range(3):
+        h.record("a", 1, False, "hip error")
+    # unloaded and loaded again: a new servable object serves
+    assert wait_for(lambda: mgr.loads.count(("a", 1)) == 2)
+    assert wait_for(lambda: mgr.status("a")[0].state == AVAILABLE)
+    s = mgr.resolve("a")
+    s.release()
+    assert s is not first and first.unloaded
+    assert h.recoveries[("a", 1)] == 1
+    # model b was never touched
+    assert mgr.loads.count(("b", 1)) == 1 and mgr.status("b")[0].state == AVAILABLE
+    # the second trip exceeds max_recoveries -> quarantined, not reloaded
+    for _ in range(3):
+        h.record("a", 1, False, "hip error again")
+    assert wait_for(lambda: mgr.status("a")[0].state == END)
+    st = mgr.status("a")[0]
+    assert st.error_code == E.UNAVAILABLE and "quarantined" in st.error_message
+    mgr.poll_once()                               # the file-system poll does not revive it
+    time.sleep(0.1)
+    assert mgr.status("a")[0].state == END and mgr.loads.count(("a", 1)) == 2
+    with pytest.raises(E.ServingError):
+        mgr.resolve("a")
+    # an explicit config reload asks for it again
+    assert mgr.apply_config(mgr.cfg) == []
+    assert mgr.status("a")[0].state == AVAILABLE and mgr.loads.count(("a", 1)) == 3
+    lines = "\n".join(h.prometheus_lines())
+    assert 'tfserve_servable_recoveries_total{model="a",version="1"} 1' in lines
+
+
+def test_native_source_polled(mgr):
+    rows = {"v": [("a", 1, "serving_default", 0, 0)]}
+    h = HealthMonitor(mgr, threshold=4, max_recoveries=2, poll_s=0.02)
+    h.add_source(lambda: rows["v"])
+    time.sleep(0.1)
+    assert mgr.loads.count(("a", 1)) == 1
+    rows["v"] = [("a", 1, "serving_default", 5, 5)]
+    assert wait_for(lambda: mgr.loads.count(("a", 1)) == 2)
+    assert h.failures[("a", 1)] == 5
+    h.close()
+
+
+def test_server_recovers_from_injected_device_faults(hpt_path, monkeypatch):
+    """half_plus_two over gRPC: after 2 good batches every batch fails
+    (lane_after=2); 3 failures trip the monitor, the version is reloaded (the
+    reload's fault counter starts again), so clients see the outage end."""
+    monkeypatch.setenv("TFSERVE_FAULT", "lane_after=2")
+    cfg = serving.ModelServerConfig()
+    cfg.model_config_list.config.add(name="hpt", base_path=hpt_path, model_platform="tensorflow")
+    srv = ModelServer(ServerOptions(port=0, model_config=cfg, file_system_poll_wait_seconds=0,
+                                    health_failure_threshold=3, health_max_recoveries=5)).start()
+    try:
+        async def go():
+            c = await TensorflowServing.new().hostname("127.0.0.1").port(srv.port).build()
+            x = {"x": np.array([[1.0]], np.float32)}
+            oks, errs = 0, 0
+            for _ in range(12):
+                try:
+                    out = await c.predict_tensors("hpt", x)
+                    np.testing.assert_allclose(out["y"].reshape(-1), [2.5])
+                    oks += 1
+                except TFServingError:
+                    errs += 1
+                    await asyncio.sleep(0.3)          # reload in progress
+            return oks, errs
+        oks, errs = asyncio.run(go())
+        assert oks >= 4 and errs >= 3, (oks, errs)
+        assert srv.health.recoveries[("hpt", 1)] >= 1
+    finally:
+        srv.stop()
