@@ -48,8 +48,9 @@ PREDICT = "/tensorflow.serving.PredictionService/Predict"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=1000,
+                    help="timed steps (a step is < 1 ms: 100-step windows measured with +-20 %% spread)")
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="seconds of untimed traffic before the warmup steps (steady-state GPU/CPU clocks, TCP "
                          "windows and first-touch of the transport's buffers; a serving step is < 1 ms, so a few "

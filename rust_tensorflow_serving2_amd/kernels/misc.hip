@@ -26,34 +26,40 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 }
 
 // ---------------------------------------------------------------- max pool
+// One block row per output row (n, ho): threads cover that row's Wo * C/8
+// 16-byte chunks, so the only per-thread index math is one 32-bit division by
+// C/8 (the grid-stride version spent three 64-bit div/mods per output chunk,
+// emulated in ~40 VALU ops each).  Rows beyond the grid's y extent loop.
 __global__ __launch_bounds__(256) void maxpool_nhwc_kernel(const uint16_t* __restrict__ x,
                                                            uint16_t* __restrict__ y, int N, int H, int W,
                                                            int C, int KH, int KW, int SH, int SW, int PT,
                                                            int PL, int Ho, int Wo) {
   const int C8 = C / 8;
-  const long total = long(N) * Ho * Wo * C8;
-  for (long i = blockIdx.x * long(blockDim.x) + threadIdx.x; i < total; i += long(gridDim.x) * blockDim.x) {
-    const int c8 = int(i % C8);
-    long t = i / C8;
-    const int wo = int(t % Wo); t /= Wo;
-    const int ho = int(t % Ho);
-    const int n = int(t / Ho);
+  const int row_items = Wo * C8;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= row_items) return;
+  const int wo = j / C8;
+  const int c8 = j - wo * C8;
+  for (int r = blockIdx.y; r < N * Ho; r += gridDim.y) {
+    const int n = r / Ho;
+    const int ho = r - n * Ho;
     float m[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
     for (int kh = 0; kh < KH; ++kh) {
       const int hi = ho * SH - PT + kh;
       if ((unsigned)hi >= (unsigned)H) continue;
+      const uint16_t* xrow = x + (long(n) * H + hi) * long(W) * C + c8 * 8;
       for (int kw = 0; kw < KW; ++kw) {
         const int wi = wo * SW - PL + kw;
         if ((unsigned)wi >= (unsigned)W) continue;
         float f[8];
-        unpack8(*reinterpret_cast<const uint4*>(x + ((long(n) * H + hi) * W + wi) * C + c8 * 8), f);
+        unpack8(*reinterpret_cast<const uint4*>(xrow + long(wi) * C), f);
 #pragma unroll
         for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
       }
     }
-    *reinterpret_cast<uint4*>(y + i * 8) = pack8(m);
+    *reinterpret_cast<uint4*>(y + (long(r) * Wo * C8 + j) * 8) = pack8(m);
   }
 }
 
@@ -410,9 +416,13 @@ int grid_for(long work, int block) {
 
 hipError_t maxpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int KH, int KW,
                                int SH, int SW, int PT, int PL, int Ho, int Wo, hipStream_t s) {
-  const long work = long(N) * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(maxpool_nhwc_kernel, dim3(grid_for(work, 256)), dim3(256), 0, s, x, y, N, H, W, C, KH, KW,
-                     SH, SW, PT, PL, Ho, Wo);
+  if (C % 8 || N <= 0 || Ho <= 0 || Wo <= 0) return N <= 0 || Ho <= 0 || Wo <= 0 ? hipSuccess : hipErrorInvalidValue;
+  const long row_items = long(Wo) * (C / 8);
+  if (row_items > (1L << 30)) return hipErrorInvalidValue;
+  const long rows = long(N) * Ho;
+  if (rows > (1L << 30)) return hipErrorInvalidValue;
+  const dim3 grid(unsigned((row_items + 255) / 256), unsigned(rows < 65535 ? rows : 65535));
+  hipLaunchKernelGGL(maxpool_nhwc_kernel, grid, dim3(256), 0, s, x, y, N, H, W, C, KH, KW, SH, SW, PT, PL, Ho, Wo);
   return hipGetLastError();
 }
 

@@ -250,6 +250,15 @@ def test_linear_matches_fp32(m, n, k, act, cfg, splits):
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
 
 
+@pytest.mark.parametrize("n,h,w,c,k,st,pt,pb", [(2, 9, 13, 8, 3, 2, 1, 1), (3, 17, 5, 520, 2, 2, 0, 1),
+                                                 (1, 30, 30, 2048, 3, 1, 1, 1), (32, 112, 112, 64, 3, 2, 0, 1)])
+def test_maxpool_shapes(n, h, w, c, k, st, pt, pb):
+    x = rnd(n, h, w, c, seed=h * w + c).to(BF)
+    y = hip().maxpool(x.to(DEV), k, k, st, st, pt, pb, pt, pb)
+    ref = F.max_pool2d(F.pad(x.float().permute(0, 3, 1, 2), [pt, pb, pt, pb], value=-1e30), k, st)
+    assert torch.equal(y.float().cpu(), ref.permute(0, 2, 3, 1))
+
+
 def test_pools_and_head():
     x = rnd(4, 112, 112, 64, seed=11).to(BF)
     y = hip().maxpool(x.to(DEV), 3, 3, 2, 2, 0, 1, 0, 1)
