@@ -389,20 +389,29 @@ __global__ void ingest_rgb4_kernel(const float4* __restrict__ x, uint4* __restri
 // fp32 NHWC (C <= 4) -> bf16 RGBA into a zero-bordered [N][Hp][Wp][4] buffer
 // (image at row pt, column pl): the stem conv then runs without padding, so
 // every 16-B operand chunk it DMAs (2 pixels x 4 channels) is in bounds.
-__global__ void ingest_c4_pad_kernel(const float* __restrict__ x, uint2* __restrict__ y, int N, int H, int W, int C,
-                                     int Hp, int Wp, int pt, int pl) {
-  const long total = long(N) * Hp * Wp;
-  for (long i = blockIdx.x * long(blockDim.x) + threadIdx.x; i < total; i += long(gridDim.x) * blockDim.x) {
-    const int xo = int(i % Wp);
-    const long r = i / Wp;
-    const int yo = int(r % Hp), n = int(r / Hp);
-    const int yi = yo - pt, xi = xo - pl;
+// One block row per padded output row (n, yo), threads across its Wp pixels:
+// 32-bit index math only, and border rows / columns store zeros without loads.
+__global__ __launch_bounds__(256) void ingest_c4_pad_kernel(const float* __restrict__ x, uint2* __restrict__ y,
+                                                            int N, int H, int W, int C, int Hp, int Wp, int pt,
+                                                            int pl) {
+  const int xo = blockIdx.x * blockDim.x + threadIdx.x;
+  if (xo >= Wp) return;
+  const int xi = xo - pl;
+  for (int r = blockIdx.y; r < N * Hp; r += gridDim.y) {
+    const int n = r / Hp;
+    const int yi = r - n * Hp - pt;
     uint16_t v[4] = {0, 0, 0, 0};
     if ((unsigned)yi < (unsigned)H && (unsigned)xi < (unsigned)W) {
       const float* src = x + ((long(n) * H + yi) * W + xi) * C;
-      for (int c = 0; c < C; ++c) v[c] = f32_to_bf16(src[c]);
+      if (C == 3) {
+        v[0] = f32_to_bf16(src[0]);
+        v[1] = f32_to_bf16(src[1]);
+        v[2] = f32_to_bf16(src[2]);
+      } else {
+        for (int c = 0; c < C; ++c) v[c] = f32_to_bf16(src[c]);
+      }
     }
-    y[i] = make_uint2(v[0] | (uint32_t(v[1]) << 16), v[2] | (uint32_t(v[3]) << 16));
+    y[long(r) * Wp + xo] = make_uint2(v[0] | (uint32_t(v[1]) << 16), v[2] | (uint32_t(v[3]) << 16));
   }
 }
 
@@ -460,9 +469,12 @@ hipError_t ingest_c4_launch(const float* x, uint16_t* y, int64_t pixels, int C, 
 
 hipError_t ingest_c4_pad_launch(const float* x, uint16_t* y, int N, int H, int W, int C, int Hp, int Wp, int pt,
                                int pl, hipStream_t s) {
-  const long total = long(N) * Hp * Wp;
-  hipLaunchKernelGGL(ingest_c4_pad_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, x,
-                     reinterpret_cast<uint2*>(y), N, H, W, C, Hp, Wp, pt, pl);
+  if (N <= 0 || Hp <= 0 || Wp <= 0) return hipSuccess;
+  const long rows = long(N) * Hp;
+  if (rows > (1L << 30) || Wp > (1 << 30)) return hipErrorInvalidValue;
+  const dim3 grid(unsigned((Wp + 255) / 256), unsigned(rows < 65535 ? rows : 65535));
+  hipLaunchKernelGGL(ingest_c4_pad_kernel, grid, dim3(256), 0, s, x, reinterpret_cast<uint2*>(y), N, H, W, C, Hp,
+                     Wp, pt, pl);
   return hipGetLastError();
 }
 

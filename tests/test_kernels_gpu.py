@@ -219,6 +219,16 @@ def test_cgemm_padded_rgba_stem(k, c, s, cfg):
     assert (y.float().cpu() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("n,h,w,c,hp,wp,pt,pl", [(3, 37, 29, 3, 44, 40, 3, 3), (2, 5, 300, 4, 7, 310, 1, 2),
+                                                  (32, 224, 224, 3, 230, 232, 3, 3), (1, 3, 3, 1, 3, 3, 0, 0)])
+def test_ingest_c4_padded_exact(n, h, w, c, hp, wp, pt, pl):
+    x = torch.rand(n, h, w, c) * 4 - 2
+    y = hip().ingest_c4_padded(x.to(DEV), hp, wp, pt, pl).cpu()
+    ref = torch.zeros(n, hp, wp, 4, dtype=BF)
+    ref[:, pt:pt + h, pl:pl + w, :c] = x.to(BF)
+    assert y.shape == ref.shape and torch.equal(y.view(torch.int16), ref.view(torch.int16))
+
+
 def test_asymmetric_identity_gemm():
     """A = I, asymmetric B: catches a transposed C write (guide §3)."""
     m = n = 64
