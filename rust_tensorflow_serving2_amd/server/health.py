@@ -101,20 +101,23 @@ class HealthMonitor:
                         if new > 0:
                             self.failures[(name, int(version))] = self.failures.get((name, int(version)), 0) + new
                     if consec >= self.threshold:
-                        with self._lock:
-                            self._native_seen.pop(k, None)
                         self._trip(name, int(version), f"{consec} consecutive failed batches on the GPU fast path")
 
     def _trip(self, name: str, version: int, why: str) -> None:
         key = (name, version)
         with self._lock:
             n = self.recoveries.get(key, 0)
-            quarantine = n >= self.max_recoveries
-            if not quarantine:
-                self.recoveries[key] = n + 1
+        quarantine = n >= self.max_recoveries
+        # only a version that is AVAILABLE is taken down; repeated trips while
+        # it is already unloading / reloading (the poller still sees the old
+        # endpoint's counters) are no-ops and are not counted
+        if not self.manager.recover(name, version, why, quarantine=quarantine):
+            return
+        if not quarantine:
+            with self._lock:
+                self.recoveries[key] = self.recoveries.get(key, 0) + 1
         log.error("model %s version %d unhealthy (%s); %s", name, version, why,
                   "quarantined" if quarantine else f"reloading (recovery {n + 1}/{self.max_recoveries})")
-        self.manager.recover(name, version, why, quarantine=quarantine)
 
     # --------------------------------------------------------------- exports
     def prometheus_lines(self) -> List[str]:

@@ -109,6 +109,8 @@ def test_consecutive_failures_reload_then_quarantine(mgr):
 
 
 def test_native_source_polled(mgr):
+    """Endpoint counters polled: one trip per outage even though the poller
+    keeps seeing the failing counters until the old endpoint is gone."""
     rows = {"v": [("a", 1, "serving_default", 0, 0)]}
     h = HealthMonitor(mgr, threshold=4, max_recoveries=2, poll_s=0.02)
     h.add_source(lambda: rows["v"])
@@ -116,8 +118,23 @@ def test_native_source_polled(mgr):
     assert mgr.loads.count(("a", 1)) == 1
     rows["v"] = [("a", 1, "serving_default", 5, 5)]
     assert wait_for(lambda: mgr.loads.count(("a", 1)) == 2)
+    rows["v"] = [("a", 1, "serving_default", 0, 0)]      # the reloaded endpoint: fresh counters
+    time.sleep(0.1)
+    assert mgr.loads.count(("a", 1)) == 2 and h.recoveries[("a", 1)] == 1
     assert h.failures[("a", 1)] == 5
+    assert mgr.status("a")[0].state == AVAILABLE
     h.close()
+
+
+def test_trips_while_unloading_are_not_counted(mgr):
+    h = HealthMonitor(mgr, threshold=1, max_recoveries=1)
+    s = mgr.resolve("a")                 # held: the unload drains until released
+    for _ in range(5):
+        h.record("a", 1, False, "hip error")
+    assert h.recoveries[("a", 1)] == 1   # the 4 trips during UNLOADING were no-ops
+    s.release()
+    assert wait_for(lambda: mgr.loads.count(("a", 1)) == 2)
+    assert wait_for(lambda: mgr.status("a")[0].state == AVAILABLE)
 
 
 def test_server_recovers_from_injected_device_faults(hpt_path, monkeypatch):
