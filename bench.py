@@ -71,6 +71,9 @@ def parse():
                     help="resnet50 = headline config; bert-base = BASELINE config 3 (seq 128); "
                          "tiny = same 224x224x3 payload, negligible compute (transport ceiling probe)")
     ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--c1-requests", type=int, default=200,
+                    help="after the timed window: batch-1 round trips at concurrency 1 over one connection "
+                         "(reported as p50_c1_ms; 0 = skip)")
     ap.add_argument("--cpu-report", action="store_true",
                     help="add per-thread-group CPU seconds of the timed window (from /proc) to the JSON")
     return ap.parse_args()
@@ -180,22 +183,22 @@ def main():
     conc = args.concurrency or 4 * args.batch
     per_step = max(1, args.batch // args.request_batch)
 
-    # one persistent client: connections (TCP + HTTP/2 handshakes, window
-    # ramp-up) are set up before warmup and reused by the timed run, as a
-    # serving client keeps its channel open
+    # one persistent client, kept running from pre-warm through warmup into the
+    # timed window: connections (TCP + HTTP/2 handshakes, window ramp-up) are
+    # set up once, and the `conc` calls in flight never drain at a boundary, so
+    # the timed window sees the steady-state pipeline whatever --steps is
     loadgen = _C.LoadGen("127.0.0.1", server.port, PREDICT, bodies, conc, args.connections, args.client_threads)
+    loadgen.start()
 
-    def drive(n):
-        return loadgen.run(n, 600.0)
+    def check(res, what):
+        if res["errors"] or res["first_error"]:
+            loadgen.stop(10.0)
+            raise SystemExit(f"{what} errors: {res['errors']} {res['first_error']}")
 
     t_pre = time.perf_counter()
     while time.perf_counter() - t_pre < args.prewarm_s:
-        p = drive(64 * per_step)
-        if p["errors"]:
-            raise SystemExit(f"pre-warm errors: {p['first_error']}")
-    w = drive(max(per_step, args.warmup * per_step))
-    if w["errors"]:
-        raise SystemExit(f"warmup errors: {w['first_error']}")
+        check(loadgen.window(64 * per_step, 600.0), "pre-warm")
+    check(loadgen.window(max(per_step, args.warmup * per_step), 600.0), "warmup")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -203,7 +206,7 @@ def main():
     io0 = server.transports[0].stats() if args.cpu_report and args.transport == "native" else None
     ru0 = os.times()
     t0 = time.perf_counter()
-    r = drive(args.steps * per_step)
+    r = loadgen.window(args.steps * per_step, 600.0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -218,17 +221,29 @@ def main():
         cpu_report = {k: round(v / elapsed, 2) for k, v in sorted(groups.items(), key=lambda x: -x[1]) if v > 0.01}
         ru1 = os.times()
         cpu_report["process_total"] = round((ru1.user + ru1.system - ru0.user - ru0.system) / elapsed, 2)
-        cpu_report["loadgen_cores"] = round(r.get("cpu_s", 0.0) / elapsed, 2)
         if io0 is not None:
             io1 = server.transports[0].stats()
             nreq = max(1, io1["requests"] - io0["requests"])
             for k in ("io_s_recv", "io_s_h2", "io_s_dispatch", "io_s_send"):
                 cpu_report[k.replace("io_s_", "io_us_per_req_")] = round((io1[k] - io0[k]) / nreq * 1e6, 1)
+    loadgen.stop(30.0)
+    check(r, "timed window")
+
+    # latency mode: one client, one connection, one call in flight (the
+    # reference's examples/prediction.rs pattern): p50 of batch-1 round trips
+    p50_c1 = None
+    if args.c1_requests > 0:
+        lg1 = _C.LoadGen("127.0.0.1", server.port, PREDICT, bodies, 1, 1, 1)
+        lg1.run(max(10, args.c1_requests // 10), 120.0)
+        r1 = lg1.run(args.c1_requests, 120.0)
+        if r1["latency_us"]:
+            p50_c1 = float(np.percentile(np.asarray(r1["latency_us"]), 50)) / 1e3
+        del lg1
     lat = np.asarray(r["latency_us"], dtype=np.float64)
     if os.environ.get("TFSERVE_BENCH_DUMP") and rank == 0:
         np.save(os.environ["TFSERVE_BENCH_DUMP"], lat)      # completion-order latencies (diagnostics)
     mine = torch.tensor([elapsed, float(r["ok"]), float(r["errors"]), np.percentile(lat, 50) if lat.size else 0,
-                         np.percentile(lat, 99) if lat.size else 0], dtype=torch.float64,
+                         np.percentile(lat, 99) if lat.size else 0, p50_c1 or 0.0], dtype=torch.float64,
                         device=device if backend == "nccl" else "cpu")
     if world > 1:
         allv = [torch.zeros_like(mine) for _ in range(world)]
@@ -263,6 +278,7 @@ def main():
             "p50_latency_ms": round(float(np.median(allv[:, 3])) / 1e3, 3),
             "p99_latency_ms": round(float(allv[:, 4].max()) / 1e3, 3),
             "errors": int(allv[:, 2].sum()),
+            "p50_c1_ms": round(float(np.median(allv[:, 5])), 3) if allv.shape[1] > 5 and allv[0, 5] > 0 else None,
             "load_s": round(t_load, 2), "prewarm_s": args.prewarm_s,
             "cpu_cores_by_thread": cpu_report,
             "fast_path_share": round(stats.get("fast_path", 0) / max(1, stats.get("requests", 1)), 3) if stats else None,

@@ -286,6 +286,7 @@ int Endpoint::acquire(int slot, int timeout_ms, std::vector<std::pair<int, int>>
     }
     if (s.state == kReady && s.reserved > 0 && s.copied == s.reserved) {
       s.state = kRunning;
+      ++running_;
       st_.batches++;
       st_.rows += s.reserved;
       return s.reserved;
@@ -303,7 +304,7 @@ int Endpoint::acquire(int slot, int timeout_ms, std::vector<std::pair<int, int>>
     }
     if (s.state == kOpen && s.reserved > 0) {
       const auto due = s.first + std::chrono::microseconds(timeout_us);
-      if (now >= due) {
+      if (now >= due || (idle_dispatch_ && running_ == 0 && s.copied == s.reserved)) {
         s.state = kReady;
         if (open_ == slot) open_ = -1;
         continue;
@@ -356,8 +357,10 @@ void Endpoint::complete(int slot, Server& srv) {
     s.reqs.clear();
     s.ready.clear();
     s.reserved = s.copied = 0;
+    if (s.state == kRunning) --running_;
     s.state = kFree;
     st_.consecutive_failed = 0;
+    if (running_ == 0 && open_ >= 0) slots_[open_].cv->notify_all();   // idle dispatch
     cv_free_.notify_all();
   }
   drain_queue();
@@ -372,9 +375,11 @@ void Endpoint::fail(int slot, Server& srv, int code, const std::string& msg) {
     s.reqs.clear();
     s.ready.clear();
     s.reserved = s.copied = 0;
+    if (s.state == kRunning) --running_;
     s.state = kFree;
     st_.failed++;
     st_.consecutive_failed++;
+    if (running_ == 0 && open_ >= 0) slots_[open_].cv->notify_all();
     cv_free_.notify_all();
   }
   drain_queue();

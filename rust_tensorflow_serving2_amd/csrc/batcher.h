@@ -103,6 +103,14 @@ class Endpoint {
   void commit_stream(SlotStream& r, std::unique_ptr<Call> call);
   void abandon_stream(SlotStream& r);
   void set_server(Server* srv) { srv_ = srv; }
+  // Idle dispatch: a partly filled batch runs right away when no batch of
+  // this endpoint is executing (the device would otherwise idle for the
+  // batch timeout); under load some batch is always running, so batches
+  // still fill up to max_rows / the timeout.
+  void set_idle_dispatch(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    idle_dispatch_ = on;
+  }
   // GPU worker side.  With `ranges`, rows that completed since the last call
   // are appended to it (the worker copies them to the device right away) and
   // the call also returns 0 early whenever new rows are available.
@@ -147,6 +155,8 @@ class Endpoint {
   std::vector<Slot> slots_;
   int open_ = -1;
   int next_ = 0;
+  int running_ = 0;          // slots in kRunning
+  bool idle_dispatch_ = true;
   bool closed_ = false;
   EndpointStats st_;
 };

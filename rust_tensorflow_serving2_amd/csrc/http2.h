@@ -156,9 +156,19 @@ class LoadGen {
           int concurrency, int connections, int threads);
   ~LoadGen();
   LoadGenResult run(uint64_t total, double timeout_s);
+  // Continuous mode: keep `concurrency` calls in flight until stop(), so a
+  // benchmark's warmup and timed windows see a pipeline that never drains.
+  void start();
+  // Block until the next `n` completions (counted from the call) have
+  // arrived; their latencies / errors and the wall time of the window.
+  LoadGenResult window(uint64_t n, double timeout_s);
+  uint64_t completed() const;
+  // Stop submitting, drain in-flight calls, join; totals since start().
+  LoadGenResult stop(double timeout_s);
   struct Worker;
 
  private:
+  std::vector<std::thread> threads_;
   std::shared_ptr<void> sh_;       // shared request state (type private to the .cpp)
   void* cbs_ = nullptr;            // nghttp2_session_callbacks*
   std::vector<std::unique_ptr<Worker>> workers_;

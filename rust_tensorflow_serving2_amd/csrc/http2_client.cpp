@@ -35,10 +35,22 @@ namespace {
 struct Shared {
   std::vector<std::string> framed;
   std::string path, authority;
-  uint64_t total;
+  std::atomic<uint64_t> total{0};
   std::atomic<uint64_t> issued{0};
   std::atomic<uint64_t> finished{0};
+  // continuous mode (LoadGen::start): no request budget and no deadline; the
+  // workers run until stop(), every completion gets a global sequence number
+  // so a timed window can pick out exactly its completions
+  std::atomic<bool> continuous{false};
+  std::atomic<bool> stopping{false};
   Clock::time_point deadline;
+};
+
+// One completion in continuous mode: (sequence number, latency, ok)
+struct Done {
+  uint64_t seq;
+  double us;
+  bool ok;
 };
 
 struct Req {
@@ -78,6 +90,9 @@ struct ClientConn {
   std::string* first_error;
   uint64_t* bytes_sent;
   uint64_t* bytes_recv;
+  // continuous mode: completions are logged here (under done_mu) instead
+  std::mutex* done_mu = nullptr;
+  std::vector<Done>* done = nullptr;
 };
 
 ssize_t read_body(nghttp2_session*, int32_t, uint8_t*, size_t length, uint32_t* flags, nghttp2_data_source* src,
@@ -149,9 +164,14 @@ int on_close(nghttp2_session* s, int32_t sid, uint32_t err, void* ud) {
   if (!r) return 0;
   const double us = std::chrono::duration<double, std::micro>(Clock::now() - r->t0).count();
   *c->bytes_recv += r->bytes;
-  if (err == 0 && r->http_status == 200 && r->grpc_status == 0) {
+  const bool good = err == 0 && r->http_status == 200 && r->grpc_status == 0;
+  if (c->sh->continuous.load(std::memory_order_relaxed)) {
+    std::lock_guard<std::mutex> g(*c->done_mu);
+    c->done->push_back(Done{c->sh->finished.fetch_add(1), us, good});
+  }
+  if (good) {
     (*c->ok)++;
-    c->lat->push_back(us);
+    if (!c->sh->continuous.load(std::memory_order_relaxed)) c->lat->push_back(us);
   } else {
     (*c->err)++;
     if (c->first_error->empty())
@@ -160,7 +180,7 @@ int on_close(nghttp2_session* s, int32_t sid, uint32_t err, void* ud) {
   }
   delete r;
   c->inflight--;
-  c->sh->finished++;
+  if (!c->sh->continuous.load(std::memory_order_relaxed)) c->sh->finished++;
   submit_one(c);
   return 0;
 }
@@ -168,8 +188,11 @@ int on_close(nghttp2_session* s, int32_t sid, uint32_t err, void* ud) {
 bool submit_one(ClientConn* c) {
   Shared* sh = c->sh;
   if (c->inflight >= c->target) return false;
+  if (sh->continuous.load(std::memory_order_relaxed)) {
+    if (sh->stopping.load(std::memory_order_relaxed)) return false;
+  }
   const uint64_t k = sh->issued.fetch_add(1);
-  if (k >= sh->total) {
+  if (!sh->continuous.load(std::memory_order_relaxed) && k >= sh->total) {
     sh->issued.fetch_sub(1);
     return false;
   }
@@ -293,6 +316,8 @@ struct LoadGen::Worker {
   std::vector<std::unique_ptr<ClientConn>> conns;
   LoadGenResult part;
   std::string connect_error;
+  std::mutex done_mu;
+  std::vector<Done> done;   // continuous mode completions not yet consumed by a window
   ~Worker() {
     for (auto& c : conns) {
       if (c->sess) nghttp2_session_del(c->sess);
@@ -351,6 +376,7 @@ LoadGen::LoadGen(const std::string& host, int port, const std::string& method,
 }
 
 LoadGen::~LoadGen() {
+  if (!threads_.empty()) stop(10.0);
   workers_.clear();
   if (cbs_) nghttp2_session_callbacks_del(static_cast<nghttp2_session_callbacks*>(cbs_));
 }
@@ -371,6 +397,8 @@ void worker_loop(LoadGen::Worker* w, Shared* sh) {
     c->first_error = &out->first_error;
     c->bytes_sent = &out->bytes_sent;
     c->bytes_recv = &out->bytes_recv;
+    c->done_mu = &w->done_mu;
+    c->done = &w->done;
   }
   for (size_t i = 0; i < conns.size(); ++i) {
     if (conns[i]->dead) continue;
@@ -384,7 +412,8 @@ void worker_loop(LoadGen::Worker* w, Shared* sh) {
     for (auto& c : conns)
       if (!c->dead && (c->inflight > 0)) any_live = true;
     if (!any_live) break;
-    if (Clock::now() > sh->deadline) {
+    if ((!sh->continuous.load(std::memory_order_relaxed) || sh->stopping.load(std::memory_order_acquire)) &&
+        Clock::now() > sh->deadline) {
       if (out->first_error.empty()) out->first_error = "load generator timed out";
       break;
     }
@@ -421,6 +450,8 @@ void worker_loop(LoadGen::Worker* w, Shared* sh) {
 
 LoadGenResult LoadGen::run(uint64_t total, double timeout_s) {
   Shared* sh = static_cast<Shared*>(sh_.get());
+  if (!threads_.empty()) throw std::logic_error("LoadGen::run while a continuous run is active (stop() first)");
+  sh->continuous = false;
   sh->total = total;
   sh->issued = 0;
   sh->finished = 0;
@@ -450,6 +481,108 @@ LoadGenResult LoadGen::run(uint64_t total, double timeout_s) {
     res.bytes_recv += p.bytes_recv;
     res.cpu_s += p.cpu_s;
     res.latency_us.insert(res.latency_us.end(), p.latency_us.begin(), p.latency_us.end());
+    if (res.first_error.empty()) res.first_error = p.first_error;
+  }
+  return res;
+}
+
+void LoadGen::start() {
+  Shared* sh = static_cast<Shared*>(sh_.get());
+  if (!threads_.empty()) return;
+  sh->continuous = true;
+  sh->stopping = false;
+  sh->issued = 0;
+  sh->finished = 0;
+  for (auto& wp : workers_) {
+    wp->part = LoadGenResult();
+    {
+      std::lock_guard<std::mutex> g(wp->done_mu);
+      wp->done.clear();
+    }
+    LoadGen::Worker* w = wp.get();
+    threads_.emplace_back([w, sh] {
+      pthread_setname_np(pthread_self(), "tfs-loadgen");
+      timespec a{}, b{};
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &a);
+      worker_loop(w, sh);
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &b);
+      w->part.cpu_s = double(b.tv_sec - a.tv_sec) + 1e-9 * double(b.tv_nsec - a.tv_nsec);
+    });
+  }
+}
+
+uint64_t LoadGen::completed() const {
+  return static_cast<Shared*>(sh_.get())->finished.load();
+}
+
+LoadGenResult LoadGen::window(uint64_t n, double timeout_s) {
+  Shared* sh = static_cast<Shared*>(sh_.get());
+  if (threads_.empty()) throw std::logic_error("LoadGen::window needs start()");
+  LoadGenResult res;
+  const uint64_t s0 = sh->finished.load();
+  const auto t0 = Clock::now();
+  const auto deadline = t0 + std::chrono::microseconds(int64_t(timeout_s * 1e6));
+  // drop completions older than the window so the logs stay bounded
+  for (auto& w : workers_) {
+    std::lock_guard<std::mutex> g(w->done_mu);
+    w->done.erase(std::remove_if(w->done.begin(), w->done.end(), [&](const Done& d) { return d.seq < s0; }),
+                  w->done.end());
+  }
+  // the window ends at the completion with sequence number s0 + n - 1
+  for (;;) {
+    if (sh->finished.load() >= s0 + n) break;
+    if (Clock::now() > deadline) {
+      res.first_error = "load generator window timed out";
+      break;
+    }
+    bool alive = false;
+    for (auto& w : workers_)
+      for (auto& c : w->conns)
+        if (!c->dead) alive = true;
+    if (!alive) {
+      res.first_error = "every connection was lost";
+      break;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  res.elapsed_s = std::chrono::duration<double>(Clock::now() - t0).count();
+  for (auto& w : workers_) {
+    std::lock_guard<std::mutex> g(w->done_mu);
+    for (auto& d : w->done) {
+      if (d.seq < s0 || d.seq >= s0 + n) continue;
+      if (d.ok) {
+        res.ok++;
+        res.latency_us.push_back(d.us);
+      } else {
+        res.errors++;
+      }
+    }
+  }
+  if (res.first_error.empty() && res.errors)
+    for (auto& w : workers_)
+      if (!w->part.first_error.empty()) {
+        res.first_error = w->part.first_error;
+        break;
+      }
+  return res;
+}
+
+LoadGenResult LoadGen::stop(double timeout_s) {
+  Shared* sh = static_cast<Shared*>(sh_.get());
+  LoadGenResult res;
+  if (threads_.empty()) return res;
+  sh->deadline = Clock::now() + std::chrono::microseconds(int64_t(timeout_s * 1e6));
+  sh->stopping.store(true, std::memory_order_release);   // no new submissions; workers drain and exit
+  for (auto& t : threads_) t.join();
+  threads_.clear();
+  sh->continuous = false;
+  for (auto& w : workers_) {
+    const LoadGenResult& p = w->part;
+    res.ok += p.ok;
+    res.errors += p.errors;
+    res.bytes_sent += p.bytes_sent;
+    res.bytes_recv += p.bytes_recv;
+    res.cpu_s += p.cpu_s;
     if (res.first_error.empty()) res.first_error = p.first_error;
   }
   return res;

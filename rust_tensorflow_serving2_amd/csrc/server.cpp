@@ -448,6 +448,11 @@ void register_server(py::module_& m) {
         return s.fast->add_endpoint(ep);
       }, py::arg("model"), py::arg("version"), py::arg("signature"), py::arg("inputs"), py::arg("outputs"),
          py::arg("max_rows"), py::arg("timeout_us"), py::arg("max_wait_ms") = 200)
+      .def("set_idle_dispatch", [](PyServer& s, int id, bool on) {
+        auto ep = s.fast->endpoint(id);
+        if (!ep) throw std::invalid_argument("no such endpoint");
+        ep->set_idle_dispatch(on);
+      })
       .def("endpoint_io_order", [](PyServer& s, int id) {
         auto ep = s.fast->endpoint(id);
         if (!ep) throw std::invalid_argument("no such endpoint");
@@ -566,7 +571,34 @@ void register_server(py::module_& m) {
         d["latency_us"] = r.latency_us; d["first_error"] = r.first_error;
         d["bytes_sent"] = r.bytes_sent; d["bytes_recv"] = r.bytes_recv; d["cpu_s"] = r.cpu_s;
         return d;
-      }, py::arg("total"), py::arg("timeout_s") = 120.0);
+      }, py::arg("total"), py::arg("timeout_s") = 120.0)
+      .def("start", [](LoadGen& lg) {
+        py::gil_scoped_release nogil;
+        lg.start();
+      })
+      .def("completed", [](LoadGen& lg) { return lg.completed(); })
+      .def("window", [](LoadGen& lg, uint64_t n, double timeout_s) {
+        LoadGenResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = lg.window(n, timeout_s);
+        }
+        py::dict d;
+        d["ok"] = r.ok; d["errors"] = r.errors; d["elapsed_s"] = r.elapsed_s;
+        d["latency_us"] = r.latency_us; d["first_error"] = r.first_error;
+        return d;
+      }, py::arg("n"), py::arg("timeout_s") = 120.0)
+      .def("stop", [](LoadGen& lg, double timeout_s) {
+        LoadGenResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = lg.stop(timeout_s);
+        }
+        py::dict d;
+        d["ok"] = r.ok; d["errors"] = r.errors; d["first_error"] = r.first_error;
+        d["bytes_sent"] = r.bytes_sent; d["bytes_recv"] = r.bytes_recv; d["cpu_s"] = r.cpu_s;
+        return d;
+      }, py::arg("timeout_s") = 30.0);
 
   m.def("run_loadgen", [](const std::string& host, int port, const std::string& method, const py::list& bodies,
                           uint64_t total, int concurrency, int connections, int threads, double timeout_s) {

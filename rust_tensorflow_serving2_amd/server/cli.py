@@ -59,6 +59,9 @@ def build_parser() -> argparse.ArgumentParser:
       help="native = C++ HTTP/2 front end with the Predict fast path; grpc = grpcio server")
     a("--io_threads", type=int, default=4, help="native transport epoll threads (per replica)")
     a("--batch_timeout_us", type=int, default=2000, help="fast-path batch window when batching params unset")
+    a("--idle_dispatch", type=_bool, nargs="?", const=True, default=True,
+      help="fast path: run a partly filled batch immediately when no batch of its model is executing "
+           "(batch-1 latency without the batch window; under load batches still fill)")
     a("--max_batch_size", type=int, default=32, help="fast-path GPU batch (HIP-graph bucket) limit")
     a("--hip_graphs", type=_bool, nargs="?", const=True, default=True)
     a("--dtype", default="bf16", choices=["bf16", "fp32"],
@@ -123,7 +126,8 @@ def make_server(args, rank: int = 0, world: int = 1):
                          model_config_file_poll_wait_seconds=args.model_config_file_poll_wait_seconds,
                          device=device, enable_batching=args.enable_batching, batching_parameters=batching,
                          transport=args.transport, file_system_poll_wait_seconds=args.file_system_poll_wait_seconds,
-                         io_threads=args.io_threads, batch_timeout_us=args.batch_timeout_us, servable=sopts,
+                         io_threads=args.io_threads, batch_timeout_us=args.batch_timeout_us,
+                         idle_dispatch=args.idle_dispatch, servable=sopts,
                          monitoring=args.monitoring, weight_source=weight_source, replicas=replicas,
                          trace_dir=args.trace_dir, health_failure_threshold=args.health_failure_threshold,
                          health_max_recoveries=args.health_max_recoveries)

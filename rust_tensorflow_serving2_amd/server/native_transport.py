@@ -48,6 +48,7 @@ class FastEndpoint:
         ins = [(a, in_specs[a].dtype, list(in_specs[a].shape[1:])) for a in in_aliases]
         outs = [(a, out_specs[a].dtype, list(out_specs[a].shape[1:])) for a in out_aliases]
         self.id = srv.add_endpoint(servable.name, servable.version, sig_name, ins, outs, self.max_rows, timeout_us)
+        srv.set_idle_dispatch(self.id, transport.idle_dispatch)
         io_in, io_out = srv.endpoint_io_order(self.id)
         assert list(io_in) == in_aliases and list(io_out) == out_aliases
         self.workers: List[threading.Thread] = []
@@ -101,7 +102,7 @@ class FastEndpoint:
 class NativeTransport:
     def __init__(self, core, port: int, host: str = "0.0.0.0", batcher=None, io_threads: int = 4,
                  py_workers: int = 16, fast_path: bool = True, batch_timeout_us: int = 2000,
-                 max_message: int = 2 ** 31 - 1, metrics=None):
+                 max_message: int = 2 ** 31 - 1, metrics=None, idle_dispatch: bool = True):
         self.core = core
         self.srv = _C.Http2Server(host, port, io_threads, max_message)
         self.port = self.srv.port
@@ -109,6 +110,7 @@ class NativeTransport:
         if self.metrics is not None:
             self.metrics.collectors.append(self.prometheus_lines)
         self.fast_path = fast_path
+        self.idle_dispatch = idle_dispatch
         self.batch_timeout_us = batch_timeout_us
         if batcher is not None:
             self.batch_timeout_us = int(getattr(batcher, "timeout_us", batch_timeout_us))

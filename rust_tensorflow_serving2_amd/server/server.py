@@ -39,6 +39,7 @@ class ServerOptions:
     grpc_workers: int = 64
     io_threads: int = 4                            # native transport epoll threads
     batch_timeout_us: int = 2000                   # native fast-path batch window
+    idle_dispatch: bool = True                     # run a partial batch at once when the device idles
     servable: ServableOptions = field(default_factory=ServableOptions)
     monitoring: bool = True
     weight_source: Optional[object] = None         # parallel.weights.ReplicatedWeightSource (N replicas)
@@ -152,7 +153,8 @@ class ModelServer:
         if self.opts.transport == "native":
             from .native_transport import NativeTransport
             t = NativeTransport(self.core, self.opts.port, self.opts.host, batcher=self.batcher,
-                                io_threads=self.opts.io_threads, batch_timeout_us=self.opts.batch_timeout_us)
+                                io_threads=self.opts.io_threads, batch_timeout_us=self.opts.batch_timeout_us,
+                                idle_dispatch=self.opts.idle_dispatch)
         else:
             from .grpc_transport import GrpcTransport
             t = GrpcTransport(self.core, self.opts.port, self.opts.host, self.opts.grpc_workers)

@@ -82,6 +82,30 @@ def test_persistent_loadgen_reuses_connections(nserver):
     del lg
 
 
+def test_continuous_loadgen_windows(nserver):
+    """bench.py's steady-state mode: the load generator keeps `concurrency`
+    calls in flight from start() to stop(); each window counts exactly its own
+    n completions (latency per completion), whatever n is."""
+    body = native.encode_predict_request(native.spec_tuple("hpt", None, None, ""), {"x": np.ones((2, 1), np.float32)})
+    lg = _C.LoadGen("127.0.0.1", nserver.port, "/tensorflow.serving.PredictionService/Predict", [body], 16, 4, 2)
+    lg.start()
+    done0 = lg.completed()
+    for n in (5, 100, 1, 37):
+        r = lg.window(n, 60.0)
+        assert r["ok"] == n and r["errors"] == 0, r["first_error"]
+        assert len(r["latency_us"]) == n and min(r["latency_us"]) > 0
+        assert r["elapsed_s"] > 0
+    assert lg.completed() >= done0 + 143
+    tot = lg.stop(30.0)
+    assert tot["errors"] == 0 and tot["ok"] >= 143
+    with pytest.raises(RuntimeError):
+        lg.window(1, 1.0)             # needs start()
+    assert lg.run(10, 60.0)["ok"] == 10   # the connections stay usable for batch runs
+    lg.start()
+    assert lg.window(20, 60.0)["ok"] == 20
+    del lg                            # destructor stops a running generator
+
+
 def test_native_loadgen_large_bodies(nserver):
     """Multi-frame (zero-copy DATA) requests of different sizes on shared connections."""
     bodies = [native.encode_predict_request(native.spec_tuple("hpt", None, None, ""),
