@@ -195,8 +195,9 @@ class FusedConv:
         dma = not self.c4 and self.cin % 8 == 0      # bf16 dense/im2col operands -> DMA-ring configs apply
         # pipelined cgemm kernel applies (im2col / dense with C % 64, or the padded RGBA stem)
         aligned = (dma and self.cin % 64 == 0) or self.c4
+        halo = aligned and not self.c4 and kh == 3 and kw == 3 and self.sh == 1 and self.sw == 1
         cfg, splits = tuned_config(key, M, self.cout, lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s), K,
-                                   dma, aligned)
+                                   dma, aligned, halo=halo)
         return [H.conv2d(*args, cfg=cfg, out=out, splits=splits)]
 
 

@@ -15,6 +15,7 @@
 //                           so staging is 16-B loads and 16-B LDS stores
 // S <= 256, S % 32 == 0, D == 64.  The S x S matrix never touches HBM.
 #include "common.h"
+#include "gemm_common.h"
 #include "launch.h"
 
 namespace tfsk {
@@ -188,13 +189,8 @@ hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, 
   constexpr int QB = qb_for(S);
   constexpr int lds = (S * D + D * (S + 8) + (QB / 16) * 16 * (S + 8)) * 2;
   static_assert(S % QB == 0 && lds <= 160 * 1024, "attention tile");
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<S, QB>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&attention_kernel<S, QB>), lds);
+  if (e != hipSuccess) return e;
   const int grid = B * H * (S / QB);
   hipLaunchKernelGGL((attention_kernel<S, QB>), dim3(grid), dim3(QB * 4), lds, st, qkv, mb, ctx, H, scale, bs, qs);
   return hipGetLastError();

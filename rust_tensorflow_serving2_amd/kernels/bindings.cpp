@@ -30,15 +30,25 @@ bool is_cgemm_cfg(int64_t cfg) {
   return cfg >= tfsk::kCGemmCfgBase && cfg < tfsk::kCGemmCfgBase + tfsk::kNumCGemmConfigs;
 }
 
+// halo-tiled 3x3 stride-1 conv configs (halo.hip)
+bool is_halo_cfg(int64_t cfg) {
+  return cfg >= tfsk::kHaloCfgBase && cfg < tfsk::kHaloCfgBase + tfsk::kNumHaloConfigs;
+}
+
 hipError_t launch_any(const tfsk::IGemmArgs& a, int a_mode, int64_t cfg, hipStream_t st) {
+  if (is_halo_cfg(cfg)) return tfsk::halo_launch(a, int(cfg), st);
   return is_cgemm_cfg(cfg) ? tfsk::cgemm_launch(a, a_mode, int(cfg), st) : tfsk::igemm_launch(a, a_mode, int(cfg), st);
 }
 
 void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, const Tensor& like, hipStream_t st) {
-  TORCH_CHECK((cfg >= 0 && cfg < tfsk::kNumIGemmConfigs) || is_cgemm_cfg(cfg), "bad tile config ", cfg);
+  TORCH_CHECK((cfg >= 0 && cfg < tfsk::kNumIGemmConfigs) || is_cgemm_cfg(cfg) || is_halo_cfg(cfg),
+              "bad tile config ", cfg);
   TORCH_CHECK(!is_cgemm_cfg(cfg) || tfsk::cgemm_supported(a, a_mode),
               "tile config ", cfg, " needs 64-aligned operands (K % 64, C % 64)");
-  const int nk = (a.K + 63) / 64;
+  TORCH_CHECK(!is_halo_cfg(cfg) || (a_mode == tfsk::kAIm2col && tfsk::halo_supported(a)),
+              "halo config ", cfg, " needs a 3x3 stride-1 conv with C % 64 == 0");
+  // split-K granule: 64-deep k-tiles, or 64-channel chunks (9 taps each) for the halo conv
+  const int nk = is_halo_cfg(cfg) ? a.C / 64 : (a.K + 63) / 64;
   if (splits > nk) splits = nk;
   if (splits <= 1) {
     a.splits = 1;
@@ -449,7 +459,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (int c = 0; c < tfsk::kNumCGemmConfigs; ++c) v.push_back(tfsk::kCGemmCfgBase + c);
     return v;
   });
+  m.def("halo_configs", []() {
+    std::vector<int> v;
+    for (int c = 0; c < tfsk::kNumHaloConfigs; ++c) v.push_back(tfsk::kHaloCfgBase + c);
+    return v;
+  });
   m.def("config_tile", [](int cfg) {
+    if (is_halo_cfg(cfg)) return std::make_pair(tfsk::halo_config_bm(cfg), tfsk::halo_config_bn(cfg));
     if (is_cgemm_cfg(cfg)) return std::make_pair(tfsk::cgemm_config_bm(cfg), tfsk::cgemm_config_bn(cfg));
     return std::make_pair(tfsk::igemm_config_bm(cfg), tfsk::igemm_config_bn(cfg));
   });

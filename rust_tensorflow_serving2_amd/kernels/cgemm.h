@@ -20,4 +20,16 @@ int cgemm_config_bm(int cfg);
 int cgemm_config_bn(int cfg);
 hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t stream);
 
+// Halo-tiled 3x3 stride-1 conv (halo.hip): an NHWC bf16 input with C % 64 == 0
+// and the im2col weight layout ([Cout][9 * C]); the workgroup tile is a block
+// of output pixels (TH x TW, picked by the launcher) x a BN slice of Cout.
+// Config ids kHaloCfgBase .. + kNumHaloConfigs - 1; split-K splits the channel
+// chunks (kt_per_split counts 64-channel chunks).
+constexpr int kHaloCfgBase = 48;
+constexpr int kNumHaloConfigs = 6;
+bool halo_supported(const IGemmArgs& a);
+int halo_config_bm(int cfg);
+int halo_config_bn(int cfg);
+hipError_t halo_launch(const IGemmArgs& a, int cfg, hipStream_t stream);
+
 }  // namespace tfsk

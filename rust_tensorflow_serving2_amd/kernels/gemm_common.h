@@ -1,0 +1,126 @@
+// Device helpers shared by the pipelined MFMA GEMM kernels (cgemm.hip,
+// halo.hip) and the host-side per-device LDS attribute cache.
+#pragma once
+#include <mutex>
+#include <set>
+#include <tuple>
+
+#include "common.h"
+#include "launch.h"
+
+namespace tfsk {
+
+// hipFuncAttributeMaxDynamicSharedMemorySize is per (kernel, device): a
+// process that drives several GPUs must set it on each.  Thread-safe; a set
+// lookup under a mutex per launch (host side only, never inside a graph replay).
+inline hipError_t ensure_dyn_lds(const void* fn, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  static std::mutex mu;
+  static std::set<std::tuple<const void*, int, int>> done;
+  std::lock_guard<std::mutex> g(mu);
+  const auto key = std::make_tuple(fn, dev, bytes);
+  if (done.count(key)) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done.insert(key);
+  return e;
+}
+
+namespace gemm {
+
+constexpr int KT = 64;                    // k-tile depth (bf16) = 128 B per LDS row
+constexpr uint32_t kOOB = 0x80000000u;    // voffset beyond any buffer: the DMA returns zeros
+
+// a / d for 0 <= a < 2^24, d >= 1 via the float reciprocal `inv` = 1/d (one
+// multiply + a +-1 fix-up, ~8 VALU instead of the ~35 of an integer division).
+__device__ __forceinline__ int fdiv(int a, int d, float inv) {
+  int q = int(float(a) * inv);
+  const int r = a - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
+// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt at their maxima; gfx9 encoding).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// Barrier without the vmcnt(0) drain __syncthreads' fence would add.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// ---- epilogue over the fp32 tile staged in LDS (8-column row chunks, NT threads)
+// NTE = the threads that take part: a multiple of the chunks per row, so a
+// thread's column is fixed (all NT unless BN / 8 does not divide NT, e.g. the
+// 96-wide tiles); EXACT = every (thread, iteration) maps inside the tile.
+template <int BM, int BN, int NT>
+struct Epi {
+  static constexpr int CPR = BN / 8;
+  static constexpr int NTE = (NT / CPR) * CPR;
+  static constexpr int ITERS = (BM * CPR + NTE - 1) / NTE;
+  static constexpr bool EXACT = NTE == NT && (BM * CPR) % NT == 0;
+  static constexpr int PRE = ITERS <= 8 ? ITERS : 0;
+  static_assert(NTE > 0, "epilogue chunk mapping");
+};
+
+// chunk `it` of thread `tid`: row-major 8-column chunks, NTE apart (a thread's
+// column is fixed); false when the chunk lies outside the tile
+template <int BM, int BN, int NT>
+__device__ __forceinline__ bool epi_rowcol(int tid, int it, int& row, int& col) {
+  using E = Epi<BM, BN, NT>;
+  const int c = tid + it * E::NTE;
+  row = c / E::CPR;
+  col = (c - row * E::CPR) * 8;
+  return E::EXACT || (tid < E::NTE && row < BM);
+}
+
+// This thread's 8 bias values (its epilogue column is fixed), loaded before the
+// K loop so the latency of the load hides under it.
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void prefetch_bias(const IGemmArgs& p, int n0, int tid, float4& b0, float4& b1) {
+  int row0, col0;
+  epi_rowcol<BM, BN, NT>(tid, 0, row0, col0);   // col0 < BN for every thread
+  const int n = n0 + col0;
+  b0 = b1 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.bias && p.splits <= 1 && p.N % 8 == 0 && n + 8 <= p.N) {
+    b0 = *reinterpret_cast<const float4*>(p.bias + n);
+    b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+  }
+}
+
+// Two floats -> packed bf16 pair (round-to-nearest-even; a plain __bf16 cast
+// compiles to one v_cvt_pk_bf16_f32 on gfx950 and keeps NaNs NaN).
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const __bf16 lo = static_cast<__bf16>(a), hi = static_cast<__bf16>(b);
+  return uint32_t(__builtin_bit_cast(uint16_t, lo)) | (uint32_t(__builtin_bit_cast(uint16_t, hi)) << 16);
+}
+
+// One 8-column chunk: alpha * acc + bias (+ residual) -> act -> 16-B bf16 (or
+// 2 x 16-B f32) store.  The launchers guarantee N, ldc, ldr % 8 == 0.
+template <int ACT>
+__device__ __forceinline__ void epi_chunk(const IGemmArgs& p, const float* src, int m, int n, const float (&bv)[8],
+                                          const uint4 rr) {
+  const float4 lo = *reinterpret_cast<const float4*>(src);
+  const float4 hi = *reinterpret_cast<const float4*>(src + 4);
+  float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+  const float alpha = p.alpha;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = act_fn<ACT>(v[2 * e] * alpha + bv[2 * e] + __uint_as_float(w[e] << 16));
+    v[2 * e + 1] = act_fn<ACT>(v[2 * e + 1] * alpha + bv[2 * e + 1] + __uint_as_float(w[e] & 0xffff0000u));
+  }
+  if (p.out_f32) {
+    float* o = static_cast<float*>(p.out) + size_t(m) * p.ldc + n;
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.out) + size_t(m) * p.ldc + n) =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                   pack_bf16x2(v[6], v[7]));
+  }
+}
+
+}  // namespace gemm
+}  // namespace tfsk

@@ -1,0 +1,350 @@
+// Halo-tiled 3x3 stride-1 convolution for MI355X (gfx950): bf16 NHWC operands,
+// fp32 MFMA accumulate, the cgemm epilogue (bias / residual / act, split-K).
+//
+// Why: the implicit-GEMM (im2col) path streams every input pixel into LDS nine
+// times (once per filter tap).  Per-CU LDS-DMA intake tops out at ~70 GB/s
+// (MI355X_MICROARCH.md, "indexed rows" / ldsdma-fill), and the round-1
+// rocprofv3 replay (profiles/r50_b32_replay_round1_final.txt) put the ResNet-50
+// 3x3 layers at 10-13 TB/s of chip-wide intake: 115-236 MB per layer at b32,
+// i.e. intake-bound at 3-8x their MFMA time.  Here a workgroup owns a TH x TW
+// block of output pixels of one image (+ a BN slice of output channels); per
+// 64-channel chunk it DMAs the (TH+2) x (TW+2) input halo into LDS ONCE and
+// runs all nine taps against it — the A operand of tap (kh, kw) is the halo
+// shifted by kh*(TW+2) + kw rows.  A-intake drops ~9x -> ~1.3-1.9x of the
+// input; only the weight slices (B) stream per tap.
+//
+//   * K loop = (chunk c, tap u) steps, the 9 taps unrolled; B ring of 3 slots
+//     (9 % 3 == 0: slot indices are compile-time), two B tiles in flight;
+//   * the halo of chunk c+1 is DMA'd into the other halo buffer while chunk c
+//     computes (one buffer when C == 64: no next chunk);
+//   * counted vmcnt waits (the per-step count of younger DMAs is known at
+//     compile time except at the tails, which take the exact smaller counts);
+//   * LDS rows are 128 B with 16-B chunks XOR-swizzled by (row & 7), the same
+//     conflict-free image as cgemm; A fragment reads re-derive the swizzle per
+//     tap from the shifted halo row (5 VALU per fragment, hidden under MFMA);
+//   * tile -> workgroup: XCD-aware remap, output-channel slices innermost so
+//     the workgroups sharing one halo run on one XCD (shared L2);
+//   * split-K over channel chunks (gridDim.y), partial slabs indexed by the
+//     output pixel row, reduced by splitk_reduce like every other GEMM.
+#include <type_traits>
+
+#include "gemm_common.h"
+#include "cgemm.h"
+
+namespace tfsk {
+
+namespace {
+
+using namespace gemm;
+
+template <int BM, int BN, int WGM, int WGN, int HR>
+struct HG {
+  static constexpr int NW = WGM * WGN, NT = 64 * NW;
+  static constexpr int WM = BM / WGM, WN = BN / WGN;
+  static constexpr int TM = WM / 16, TN = WN / 16;
+  static constexpr int HPW = HR / (8 * NW);        // halo 1-KB DMA pieces per wave per chunk
+  static constexpr int BPW = BN / (8 * NW);        // B pieces per wave per step
+  static constexpr int S = 3;                      // B ring depth
+  static constexpr int HALO_B = HR * 128;          // bytes of one halo buffer
+  static constexpr int B_B = BN * 128;             // bytes of one B ring slot
+  static constexpr int CS_LD = BN + 4;
+  static constexpr int LDS_EPI = BM * CS_LD * 4;
+  static constexpr int lds(int nbuf) {
+    return (nbuf * HALO_B + S * B_B) > LDS_EPI ? (nbuf * HALO_B + S * B_B) : LDS_EPI;
+  }
+  static_assert(HPW >= 1 && HR % (8 * NW) == 0, "halo DMA split");
+  static_assert(BPW >= 1 && BN % (8 * NW) == 0, "B DMA split");
+  static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
+  static_assert(HPW + BPW < 64, "vmcnt range");
+  static_assert(lds(2) <= 160 * 1024, "LDS budget");
+};
+
+template <int BM, int BN, int WGM, int WGN, int HR>
+__global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) {
+  using G = HG<BM, BN, WGM, WGN, HR>;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  char* const smem = reinterpret_cast<char*>(smem_raw);
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+  const int TH = p.TH, TW = p.TW, HW2 = TW + 2;
+  const int Ho = p.Ho, Wo = p.Wo, H = p.H, W = p.W, C = p.C;
+  const int tph = (Ho + TH - 1) / TH, tpw = (Wo + TW - 1) / TW;
+  const int nbn = (p.N + BN - 1) / BN;
+
+  // ---- tile of this workgroup: (image, tile row, tile col, channel slice)
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int bn = wg % nbn;
+  int r_ = wg / nbn;
+  const int tw = r_ % tpw;
+  r_ /= tpw;
+  const int th = r_ % tph;
+  const int img = r_ / tph;
+  const int h0 = th * TH, w0 = tw * TW, n0 = bn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int prow = lane >> 3;
+  const uint32_t kc = uint32_t(((lane & 7) ^ prow) * 8);
+
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.a), 0, int(p.a_bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.b), 0, int(p.b_bytes), 0x00020000);
+
+  // ---- per-lane halo DMA offsets: halo row r = pixel (h0 - PT + r / HW2, w0 - PL + r % HW2)
+  const int hrows = (TH + 2) * HW2;
+  const float inv_hw2 = 1.f / float(HW2);
+  uint32_t h_off[G::HPW];
+#pragma unroll
+  for (int j = 0; j < G::HPW; ++j) {
+    const int r = (wid * G::HPW + j) * 8 + prow;
+    const int rr = fdiv(r, HW2, inv_hw2);
+    const int hh = h0 - p.PT + rr, ww = w0 - p.PL + (r - rr * HW2);
+    const bool ok = r < hrows && unsigned(hh) < unsigned(H) && unsigned(ww) < unsigned(W);
+    h_off[j] = ok ? (uint32_t((img * H + hh) * W + ww) * uint32_t(C) + kc) * 2u : kOOB;
+  }
+  uint32_t b_off[G::BPW];
+#pragma unroll
+  for (int j = 0; j < G::BPW; ++j) {
+    const int n = n0 + (wid * G::BPW + j) * 8 + prow;
+    b_off[j] = n < p.N ? (uint32_t(n) * uint32_t(p.ldb) + kc) * 2u : kOOB;
+  }
+
+  // ---- channel-chunk range (split-K: blockIdx.y selects a slice of chunks)
+  const int nch = C / KT;
+  int c0 = 0, c1 = nch;
+  if (p.splits > 1) {
+    c0 = blockIdx.y * p.kt_per_split;
+    c1 = min(nch, c0 + p.kt_per_split);
+  }
+  const int nbuf = (c1 - c0) > 1 ? 2 : 1;
+  char* const ring = smem + nbuf * G::HALO_B;
+
+  auto issue_halo = [&](int c) {
+    char* dst = smem + ((c - c0) & 1) * G::HALO_B;
+    const uint32_t soff = uint32_t(c) * (KT * 2);
+#pragma unroll
+    for (int j = 0; j < G::HPW; ++j) {
+      const uint32_t v = h_off[j];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(dst + (wid * G::HPW + j) * 1024), 16, v, soff, 0, 0);
+    }
+  };
+  // weights k = tap * C + channel
+  auto issue_b = [&](int c, int u, int slot) {
+    const uint32_t soff = uint32_t(u * C + c * KT) * 2u;
+#pragma unroll
+    for (int j = 0; j < G::BPW; ++j) {
+      const uint32_t v = b_off[j];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_ptr_t)(ring + slot * G::B_B + (wid * G::BPW + j) * 1024),
+                                               16, v, soff, 0, 0);
+    }
+  };
+
+  // ---- consumer fragments: A rows are output pixels -> halo rows (tap (0,0))
+  const int fr = lane & 15, fq = lane >> 4;
+  int hrow0[G::TM];
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i) {
+    const int px = wm * G::WM + i * 16 + fr;
+    const int ph = px / TW;
+    hrow0[i] = px < TH * TW ? ph * HW2 + (px - ph * TW) : 0;
+  }
+  const uint32_t rb0 = uint32_t(((wn * G::WN + fr) * KT + ((fq ^ (fr & 7)) * 8)) * 2);
+  const uint32_t rb1 = uint32_t(((wn * G::WN + fr) * KT + (((4 + fq) ^ (fr & 7)) * 8)) * 2);
+
+  f32x4 acc[G::TM][G::TN];
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const char* hb, const char* sb, int tap_off) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[G::TM], bfr[G::TN];
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i) {
+        const int hr = hrow0[i] + tap_off;
+        const uint32_t addr = uint32_t(hr) * 128u + ((uint32_t((kk * 4 + fq) ^ (hr & 7))) << 4);
+        af[i] = *reinterpret_cast<const bf16x8*>(hb + addr);
+      }
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sb + (kk ? rb1 : rb0) + j * 16 * KT * 2);
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  float4 bias0, bias1;
+  prefetch_bias<BM, BN, G::NT>(p, n0, tid, bias0, bias1);
+
+  // ---- prologue: halo of the first chunk, two B tiles
+  issue_halo(c0);
+  issue_b(c0, 0, 0);
+  issue_b(c0, 1, 1);
+
+  for (int c = c0; c < c1; ++c) {
+    const bool hasH = c + 1 < c1;      // this chunk's tap-0 step issues the next halo
+    const char* hb = smem + ((c - c0) & 1) * G::HALO_B;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      // younger DMAs than B(step) = what the previous step issued: B(step + 1)
+      // (absent at the last step) and, after a tap-0 step, the next halo
+      const bool hasB1 = !(c + 1 == c1 && u == 8);
+      if (u == 1) {
+        if (hasH) {
+          if (hasB1) wait_vmcnt<G::HPW + G::BPW>(); else wait_vmcnt<G::HPW>();
+        } else {
+          if (hasB1) wait_vmcnt<G::BPW>(); else wait_vmcnt<0>();
+        }
+      } else {
+        if (hasB1) wait_vmcnt<G::BPW>(); else wait_vmcnt<0>();
+      }
+      lds_barrier();   // every wave's DMAs landed; the slot / buffer about to be refilled is read-free
+      if (u == 0 && hasH) issue_halo(c + 1);
+      // B of step + 2: (c, u + 2) or (c + 1, u - 7)
+      if (u + 2 < 9) issue_b(c, u + 2, (u + 2) % 3);
+      else if (c + 1 < c1) issue_b(c + 1, u - 7, (u + 2) % 3);
+      compute(hb, ring + (u % 3) * G::B_B, (u / 3) * HW2 + (u % 3));
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  // ---- epilogue: fp32 tile staged in LDS; row = output pixel of the block
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * G::WM + i * 16 + fq * 4 + r) * G::CS_LD + wn * G::WN + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+
+  auto out_row = [&](int row) -> int {   // global GEMM row of tile row `row`, or -1
+    if (row >= TH * TW) return -1;
+    const int ph = row / TW, pw = row - ph * TW;
+    const int h = h0 + ph, w = w0 + pw;
+    if (h >= Ho || w >= Wo) return -1;
+    return (img * Ho + h) * Wo + w;
+  };
+
+  using E = Epi<BM, BN, G::NT>;
+  if (p.splits > 1) {
+    const float alpha = p.alpha;
+    float* ws = p.ws + size_t(blockIdx.y) * p.M * p.N;
+#pragma unroll 1
+    for (int it = 0; it < E::ITERS; ++it) {
+      int row, col;
+      if (!epi_rowcol<BM, BN, G::NT>(tid, it, row, col)) continue;
+      const int m = out_row(row), n = n0 + col;
+      if (m < 0 || n >= p.N) continue;
+      const float* src = Cs + row * G::CS_LD + col;
+      float4 a = *reinterpret_cast<const float4*>(src);
+      float4 b = *reinterpret_cast<const float4*>(src + 4);
+      a.x *= alpha; a.y *= alpha; a.z *= alpha; a.w *= alpha;
+      b.x *= alpha; b.y *= alpha; b.z *= alpha; b.w *= alpha;
+      float* dst = ws + size_t(m) * p.N + n;
+      *reinterpret_cast<float4*>(dst) = a;
+      *reinterpret_cast<float4*>(dst + 4) = b;
+    }
+    return;
+  }
+  const float bv[8] = {bias0.x, bias0.y, bias0.z, bias0.w, bias1.x, bias1.y, bias1.z, bias1.w};
+  auto run = [&](auto act_tag) {
+    constexpr int ACT = decltype(act_tag)::value;
+#pragma unroll 2
+    for (int it = 0; it < E::ITERS; ++it) {
+      int row, col;
+      if (!epi_rowcol<BM, BN, G::NT>(tid, it, row, col)) continue;
+      const int m = out_row(row), n = n0 + col;
+      if (m < 0 || n >= p.N) continue;
+      const uint4 rr = p.residual ? *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n)
+                                  : make_uint4(0, 0, 0, 0);
+      epi_chunk<ACT>(p, Cs + row * G::CS_LD + col, m, n, bv, rr);
+    }
+  };
+  switch (p.act) {
+    case kActRelu: run(std::integral_constant<int, kActRelu>{}); break;
+    case kActGeluTanh: run(std::integral_constant<int, kActGeluTanh>{}); break;
+    case kActGeluErf: run(std::integral_constant<int, kActGeluErf>{}); break;
+    case kActTanh: run(std::integral_constant<int, kActTanh>{}); break;
+    default: run(std::integral_constant<int, kActNone>{}); break;
+  }
+}
+
+// Output block (TH, TW) for a BM-pixel tile whose halo fits HR rows: fewest
+// tiles first, then the smallest halo (least re-read input).
+bool pick_block(int Ho, int Wo, int BM, int HR, int& TH, int& TW) {
+  long best_tiles = -1, best_halo = 0;
+  for (int tw = 1; tw <= Wo; ++tw) {
+    int th = BM / tw < Ho ? BM / tw : Ho;
+    while (th >= 1 && (th + 2) * (tw + 2) > HR) --th;
+    if (th < 1) continue;
+    const long tiles = long((Ho + th - 1) / th) * ((Wo + tw - 1) / tw);
+    const long halo = long(th + 2) * (tw + 2);
+    if (best_tiles < 0 || tiles < best_tiles || (tiles == best_tiles && halo < best_halo)) {
+      best_tiles = tiles;
+      best_halo = halo;
+      TH = th;
+      TW = tw;
+    }
+  }
+  return best_tiles > 0;
+}
+
+template <int BM, int BN, int WGM, int WGN, int HR>
+hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
+  using G = HG<BM, BN, WGM, WGN, HR>;
+  IGemmArgs a = a0;
+  if (!pick_block(a.Ho, a.Wo, BM, HR, a.TH, a.TW)) return hipErrorInvalidValue;
+  const int nch = a.C / KT;
+  const int splits = a.splits > 1 ? a.splits : 1;
+  if (splits > 1 && a.kt_per_split <= 0) return hipErrorInvalidValue;
+  const int per = splits > 1 ? a.kt_per_split : nch;
+  const int nimg = a.M / (a.Ho * a.Wo);
+  const long tiles = long(nimg) * ((a.Ho + a.TH - 1) / a.TH) * ((a.Wo + a.TW - 1) / a.TW) * ((a.N + BN - 1) / BN);
+  if (tiles == 0) return hipSuccess;
+  if (tiles >= (1L << 31)) return hipErrorInvalidValue;
+  const int lds = G::lds(per > 1 ? 2 : 1);
+  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&halo_conv_kernel<BM, BN, WGM, WGN, HR>), G::lds(2));
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((halo_conv_kernel<BM, BN, WGM, WGN, HR>), dim3(unsigned(tiles), splits), dim3(G::NT), lds, s, a);
+  return hipGetLastError();
+}
+
+constexpr int kHBM[kNumHaloConfigs] = {256, 128, 128, 64, 256, 64};
+constexpr int kHBN[kNumHaloConfigs] = {64, 128, 64, 64, 128, 128};
+
+}  // namespace
+
+bool halo_supported(const IGemmArgs& a) {
+  return a.KH == 3 && a.KW == 3 && a.SH == 1 && a.SW == 1 && a.C % KT == 0 && a.K == 9 * a.C && a.ldb >= a.K &&
+         a.ldb % 8 == 0 && a.N % 8 == 0 && a.ldc % 8 == 0 && (!a.residual || a.ldr % 8 == 0) && a.PT >= 0 &&
+         a.PT <= 2 && a.PL >= 0 && a.PL <= 2 && a.Ho > 0 && a.Wo > 0 && a.M % (a.Ho * a.Wo) == 0 &&
+         a.M < (1 << 23) && int64_t(a.M / (a.Ho * a.Wo)) * a.H * a.W * a.C < (1LL << 30);
+}
+
+int halo_config_bm(int cfg) { return kHBM[cfg - kHaloCfgBase]; }
+int halo_config_bn(int cfg) { return kHBN[cfg - kHaloCfgBase]; }
+
+hipError_t halo_launch(const IGemmArgs& a, int cfg, hipStream_t s) {
+  if (cfg < kHaloCfgBase || cfg >= kHaloCfgBase + kNumHaloConfigs || !halo_supported(a)) return hipErrorInvalidValue;
+  switch (cfg - kHaloCfgBase) {
+    case 0: return launch_halo_cfg<256, 64, 4, 1, 320>(a, s);    // 104 KB (64 KB for C == 64), waves 64x64
+    case 1: return launch_halo_cfg<128, 128, 2, 2, 192>(a, s);   // 96 KB, waves 64x64
+    case 2: return launch_halo_cfg<128, 64, 2, 2, 192>(a, s);    // 72 KB (48 KB), waves 64x32
+    case 3: return launch_halo_cfg<64, 64, 2, 2, 128>(a, s);     // 56 KB (40 KB), waves 32x32
+    case 4: return launch_halo_cfg<256, 128, 4, 2, 320>(a, s);   // 135 KB, 8 waves of 64x64
+    case 5: return launch_halo_cfg<64, 128, 2, 2, 128>(a, s);    // 80 KB, waves 32x64
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace tfsk

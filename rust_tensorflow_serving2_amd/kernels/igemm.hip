@@ -21,6 +21,7 @@
 //   * epilogue staged through LDS as fp32 so bias/residual/activation work on
 //     coalesced 16-B row chunks (residual read once, output written once).
 #include "common.h"
+#include "gemm_common.h"
 #include "launch.h"
 
 namespace tfsk {
@@ -587,13 +588,9 @@ hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
   }
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<BM, BN, AMODE, NSTAGE, WAVES_M, BKT>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&igemm_kernel<BM, BN, AMODE, NSTAGE, WAVES_M, BKT>),
+                                G::LDS);
+  if (e != hipSuccess) return e;
   const int splits = a.splits > 1 ? a.splits : 1;
   hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE, NSTAGE, WAVES_M, BKT>), dim3(tiles, splits), dim3(kThreads), G::LDS, s, a);
   return hipGetLastError();

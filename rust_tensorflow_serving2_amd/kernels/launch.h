@@ -42,6 +42,8 @@ struct IGemmArgs {
   const void* a2;
   int64_t a2_bytes;
   int K1;
+  // halo conv (halo.hip): output pixel block per workgroup (set by the launcher)
+  int TH, TW;
 };
 
 // kAStem7x7x3: fp32 NHWC input with C == 3 and a 7-wide filter (the ResNet

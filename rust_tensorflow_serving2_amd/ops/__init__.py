@@ -84,6 +84,9 @@ CGEMM = {32: (128, 128), 33: (128, 128), 34: (64, 128), 35: (128, 64), 36: (64, 
          37: (256, 128), 38: (128, 256), 39: (128, 128), 40: (64, 256), 41: (256, 64),
          42: (64, 64), 43: (64, 128), 44: (128, 64), 45: (128, 96), 46: (128, 96), 47: (64, 96)}
 TILES.update(CGEMM)
+# halo-tiled 3x3 stride-1 conv (kernels/halo.hip): config id -> (output pixels per tile, BN)
+HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 128), 53: (64, 128)}
+TILES.update(HALO)
 
 
 def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
@@ -96,14 +99,29 @@ def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
     return s
 
 
-def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False, cgemm_only: bool = False):
+def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
+               halo: bool = False):
     """(tile config, split-K) pairs worth timing for an M x N x K problem
     (``dma``: the operand mode uses the direct-to-LDS path, so the deeper
     DMA-ring configs apply; ``aligned64``: K and the conv channels are
-    multiples of 64, so the pipelined cgemm configs apply)."""
+    multiples of 64, so the pipelined cgemm configs apply; ``halo``: a 3x3
+    stride-1 conv with C % 64 == 0, so the halo-tiled configs apply too —
+    their split-K granule is a 64-channel chunk of 9 taps)."""
     nk = -(-K // 64)
     out = []
+    if halo and aligned64 and K % 576 == 0 and N % 8 == 0:
+        nch = K // 576
+        for cfg, (bm, bn) in HALO.items():
+            if bn > 64 and N <= bn // 2:
+                continue
+            tiles = -(-M // bm) * -(-N // bn)
+            for s in (1, 2, 4, 8):
+                if s > 1 and (nch // s < 1 or tiles >= 512 or tiles * s > 2048):
+                    continue
+                out.append((cfg, s))
     for cfg, (bm, bn) in TILES.items():
+        if cfg in HALO:
+            continue
         if cfg in DMA_ONLY and (not dma or (cfg in (4, 5, 6, 7) and nk < 3)):
             continue
         if cfg in CGEMM and not (aligned64 and K % 64 == 0 and N % 8 == 0):
@@ -125,7 +143,8 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
 
 
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
-                 dma: bool = True, aligned64: bool = False, cgemm_only: bool = False) -> Tuple[int, int]:
+                 dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
+                 halo: bool = False) -> Tuple[int, int]:
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
     heuristic is used)."""
@@ -145,7 +164,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
         best, best_t = None, float("inf")
         times = []
         flush = _flush_buffer()
-        for c, s in candidates(M, N, K, dma, aligned64, cgemm_only):
+        for c, s in candidates(M, N, K, dma, aligned64, cgemm_only, halo):
             launch(c, s)   # warm (also sets the kernel's LDS attribute)
             samples = []
             for _rep in range(5):

@@ -104,6 +104,63 @@ def test_cgemm_conv_matches_fp32(shape, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
 
 
+HALO_CFGS = list(range(48, 54))
+HALO_SHAPES = [
+    # N, H, W, Cin, Cout, pads            (3x3 stride 1; ResNet-50 stages + edge cases)
+    (2, 56, 56, 64, 64, (1, 1, 1, 1)),
+    (2, 28, 28, 128, 128, (1, 1, 1, 1)),
+    (3, 14, 14, 256, 256, (1, 1, 1, 1)),
+    (2, 7, 7, 512, 512, (1, 1, 1, 1)),
+    (1, 13, 17, 192, 72, (1, 1, 1, 1)),    # odd image, 3 chunks, N tail (72 % BN != 0)
+    (2, 9, 11, 64, 136, (0, 0, 0, 0)),     # VALID (no padding)
+    (1, 5, 6, 128, 64, (2, 0, 1, 1)),      # asymmetric top pad
+]
+
+
+@pytest.mark.parametrize("shape", HALO_SHAPES)
+@pytest.mark.parametrize("cfg", HALO_CFGS)
+def test_halo_conv_matches_fp32(shape, cfg):
+    """Halo-tiled 3x3 stride-1 conv (one input halo per 64-channel chunk, nine
+    shifted taps from LDS) vs fp32 conv, with bias + residual + ReLU and split-K."""
+    n, h, w, cin, cout, pads = shape
+    x = rnd(n, h, w, cin, seed=11).to(BF)
+    wt = rnd(3, 3, cin, cout, scale=1 / math.sqrt(9 * cin), seed=12).to(BF).float()
+    b = rnd(cout, scale=0.1, seed=13)
+    ho = h + pads[0] + pads[1] - 2
+    wo = w + pads[2] + pads[3] - 2
+    res = rnd(n, ho, wo, cout, seed=14).to(BF)
+    ref = ref_conv(x, wt, b, 1, pads, res, "relu")
+    for splits in (1, 2, 3):
+        y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), 3, 3, 1, 1, *pads, act=ACT["relu"],
+                         cfg=cfg, splits=splits)
+        torch.cuda.synchronize()
+        err = (y.float().cpu() - ref).abs().max().item()
+        assert y.shape == (n, ho, wo, cout)
+        assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
+
+
+def test_halo_exact_identity_taps():
+    """Integer-valued operands (exact in bf16 and fp32): every output pixel of
+    every tile position, tap and channel chunk must match bit for bit — catches
+    a mis-shifted halo row or a wrong swizzle that tolerances could hide."""
+    n, h, w, cin, cout = 2, 19, 23, 128, 64
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(-3, 4, (n, h, w, cin), generator=g).float()
+    wt = torch.randint(-2, 3, (3, 3, cin, cout), generator=g).float()
+    ref = ref_conv(x, wt, torch.zeros(cout), 1, (1, 1, 1, 1))
+    for cfg in HALO_CFGS:
+        y = hip().conv2d(x.to(BF).to(DEV), pack_w(wt), None, None, 3, 3, 1, 1, 1, 1, 1, 1, act=0, cfg=cfg,
+                         out_f32=True)
+        assert torch.equal(y.cpu(), ref), cfg
+
+
+def test_halo_rejects_non_3x3():
+    x = torch.zeros(1, 8, 8, 64, device=DEV, dtype=BF)
+    w = torch.zeros(64, 64 * 9, device=DEV, dtype=BF)
+    with pytest.raises(RuntimeError, match="halo config"):
+        hip().conv2d(x, w, None, None, 3, 3, 2, 2, 1, 1, 1, 1, act=0, cfg=48)
+
+
 @pytest.mark.parametrize("m,n,k", [(32, 1000, 2048), (256, 2304, 768), (1000, 768, 3072), (8, 72, 64)])
 @pytest.mark.parametrize("cfg", CGEMM_CFGS)
 def test_cgemm_linear_matches_fp32(m, n, k, cfg):
