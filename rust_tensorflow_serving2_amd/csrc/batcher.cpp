@@ -146,12 +146,14 @@ int Endpoint::offer(std::unique_ptr<Call>& call, PredictRequestView& req) {
       s.state = kReady;
       open_ = -1;
     }
+    ++copying_;
   }
   // copy outside the lock: IO threads fill different rows of a slot in parallel
   copy_rows(slot, r0, n, src);
   return 0;
 }
 
+// Caller incremented copying_ under mu_ when it reserved the rows.
 void Endpoint::copy_rows(int slot, int r0, int n, const std::vector<const uint8_t*>& src) {
   Slot& s = slots_[slot];
   for (size_t i = 0; i < inputs.size(); ++i)
@@ -160,6 +162,7 @@ void Endpoint::copy_rows(int slot, int r0, int n, const std::vector<const uint8_
   s.copied += n;
   s.ready.emplace_back(r0, n);
   s.cv->notify_all();
+  if (--copying_ == 0 && closed_) cv_free_.notify_all();
 }
 
 void Endpoint::drain_queue() {
@@ -190,6 +193,7 @@ void Endpoint::drain_queue() {
       }
       queue_.pop_front();
       jobs.push_back(std::move(j));
+      ++copying_;
     }
   }
   for (auto& j : jobs) copy_rows(j.slot, j.r0, j.n, j.src);
@@ -385,18 +389,50 @@ void Endpoint::fail(int slot, Server& srv, int code, const std::string& msg) {
   drain_queue();
 }
 
+void Endpoint::fail_dead(int slot, Server& srv, int code, const std::string& msg) {
+  Slot& s = slots_[slot];
+  for (auto& p : s.reqs)
+    if (p.call) srv.respond(*p.call, code, msg, std::string());
+  std::lock_guard<std::mutex> g(mu_);
+  s.reqs.clear();
+  s.ready.clear();
+  if (s.state == kRunning) --running_;
+  s.state = kDead;
+  st_.failed++;
+  st_.consecutive_failed++;
+  cv_free_.notify_all();
+}
+
 void Endpoint::close(Server* srv) {
   std::deque<Queued> left;
+  std::vector<std::unique_ptr<Call>> unstarted;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::mutex> g(mu_);
     closed_ = true;
     for (auto& s : slots_) abandon_stalled_locked(s);
     left.swap(queue_);
+    // requests sitting in slots no lane has started: their lanes see
+    // acquire() < 0 and exit, so nobody else would ever answer them
+    for (auto& s : slots_) {
+      if (s.state != kOpen && s.state != kReady) continue;
+      for (auto& p : s.reqs)
+        if (p.call) unstarted.push_back(std::move(p.call));
+      s.reqs.clear();
+      s.ready.clear();
+      s.reserved = s.copied = 0;
+      s.state = kFree;
+    }
+    open_ = -1;
     for (auto& sl : slots_) sl.cv->notify_all();
     cv_free_.notify_all();
+    // IO threads may still be copying rows (reserved before closed_ was set)
+    // into the pinned buffers: the caller frees those once this returns
+    cv_free_.wait(g, [this] { return copying_ == 0; });
   }
-  if (srv)
+  if (srv) {
     for (auto& q : left) srv->respond(*q.call, 14 /*UNAVAILABLE*/, "Servable is being unloaded", std::string());
+    for (auto& c : unstarted) srv->respond(*c, 14 /*UNAVAILABLE*/, "Servable is being unloaded", std::string());
+  }
 }
 
 EndpointStats Endpoint::stats() {
@@ -464,10 +500,13 @@ int FastPath::add_endpoint(std::shared_ptr<Endpoint> ep) {
   return ep->id;
 }
 
-std::shared_ptr<Endpoint> FastPath::endpoint(int id) {
+std::shared_ptr<Endpoint> FastPath::endpoint(int id, bool retired) {
   std::shared_lock<std::shared_mutex> g(mu_);
   auto it = eps_.find(id);
-  return it == eps_.end() ? nullptr : it->second;
+  if (it != eps_.end()) return it->second;
+  if (!retired) return nullptr;
+  auto r = retired_.find(id);
+  return r == retired_.end() ? nullptr : r->second;
 }
 
 void FastPath::remove_endpoint(int id) {
@@ -482,6 +521,11 @@ void FastPath::remove_endpoint(int id) {
     if (it != eps_.end()) {
       ep = it->second;
       eps_.erase(it);
+      for (auto r = retired_.begin(); r != retired_.end();) {   // drop the ones nobody holds any more
+        if (!r->second->busy()) r = retired_.erase(r);
+        else ++r;
+      }
+      retired_[id] = ep;
     }
   }
   if (ep) ep->close(srv_);

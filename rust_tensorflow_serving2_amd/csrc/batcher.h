@@ -64,7 +64,9 @@ struct Queued {
   std::vector<std::string> owned;      // kOwned tensors (non-packed encodings)
 };
 
-enum SlotState : int { kFree = 0, kOpen = 1, kReady = 2, kRunning = 3 };
+// kDead: the lane gave the slot's batch up (device hang); the GPU may still
+// write its pinned output rows, so the slot is never handed out again.
+enum SlotState : int { kFree = 0, kOpen = 1, kReady = 2, kRunning = 3, kDead = 4 };
 
 struct Slot {
   std::vector<uint8_t*> in_base;     // per input: pinned [max_rows][row]
@@ -122,7 +124,14 @@ class Endpoint {
   }
   void complete(int slot, Server& srv);
   void fail(int slot, Server& srv, int code, const std::string& msg);
-  // Responds UNAVAILABLE to requests still queued when `srv` is given.
+  // Like fail(), but the slot is retired (kDead) instead of freed: its batch
+  // timed out on the device, whose late writes must not land in a reused slot.
+  void fail_dead(int slot, Server& srv, int code, const std::string& msg);
+  // Closes the endpoint.  With `srv`, every request that has not started on
+  // the device (queued, or in an open / ready slot) is answered UNAVAILABLE;
+  // running batches are left to their lanes.  Returns after every in-flight
+  // row copy into the slots' pinned buffers has finished, so the caller may
+  // release those buffers once the lanes are joined.
   void close(Server* srv = nullptr);
 
   const int id;
@@ -134,6 +143,10 @@ class Endpoint {
   const int64_t timeout_us;
   const int max_wait_ms;
   EndpointStats stats();
+  bool busy() {
+    std::lock_guard<std::mutex> g(mu_);
+    return running_ > 0;
+  }
 
  private:
   int open_slot_locked(int n);
@@ -156,6 +169,7 @@ class Endpoint {
   int open_ = -1;
   int next_ = 0;
   int running_ = 0;          // slots in kRunning
+  int copying_ = 0;          // copy_rows() calls writing into slot buffers outside mu_
   bool idle_dispatch_ = true;
   bool closed_ = false;
   EndpointStats st_;
@@ -168,7 +182,9 @@ class FastPath {
   std::shared_ptr<Endpoint> route(const ModelSpecView& spec);
   std::shared_ptr<StreamRes> reserve_stream(const ProbeInfo& pi);
   int add_endpoint(std::shared_ptr<Endpoint> ep);
-  std::shared_ptr<Endpoint> endpoint(int id);
+  // `retired`: also endpoints already removed — a lane that finishes a batch
+  // after its endpoint closed must still reach it to answer that batch
+  std::shared_ptr<Endpoint> endpoint(int id, bool retired = false);
   void remove_endpoint(int id);
   // route (model, signature) [+version] to an endpoint; version < 0 = "latest"
   void set_route(const std::string& model, const std::string& signature, int64_t version, int ep_id);
@@ -180,6 +196,9 @@ class FastPath {
   Server* srv_;
   std::shared_mutex mu_;
   std::map<int, std::shared_ptr<Endpoint>> eps_;
+  // removed endpoints, kept until no batch of theirs is running (pruned on
+  // the next removal): they own no buffers, only their bookkeeping
+  std::map<int, std::shared_ptr<Endpoint>> retired_;
   std::map<std::string, int> routes_;   // key = model \0 signature \0 version|"L"
   int ids_ = 0;
 };

@@ -76,6 +76,7 @@ constexpr int kHipMemcpyHostToDevice = 1, kHipMemcpyDeviceToHost = 2;
 constexpr unsigned kHipEventDisableTiming = 0x2;
 constexpr unsigned kHipStreamNonBlocking = 0x1;
 constexpr int kHipErrorNotReady = 600;
+constexpr int kLaneHung = -2;   // NativeLane::wait gave up (not a hipError_t)
 
 HipRt& hip_rt() {
   static HipRt rt;
@@ -174,6 +175,8 @@ class NativeLane {
       if (k != std::string::npos) fault_every_ = std::atoi(spec.c_str() + k + 11);
       k = spec.find("lane_after=");
       if (k != std::string::npos) fault_after_ = std::atoi(spec.c_str() + k + 11);
+      k = spec.find("lane_hang=");
+      if (k != std::string::npos) fault_hang_ = std::atoi(spec.c_str() + k + 10);
     }
     std::sort(buckets_.begin(), buckets_.end(), [](auto& a, auto& b) { return a.rows < b.rows; });
     // eager H2D (rows copied to the device while the batch fills) needs every
@@ -188,6 +191,7 @@ class NativeLane {
       for (size_t i = 0; eager_ && i < b.in.size(); ++i)
         if (b.in[i].dst != buckets_.back().in[i].dst || b.in[i].src != buckets_.back().in[i].src) eager_ = false;
     }
+    if (const char* t = getenv("TFSERVE_LANE_TIMEOUT_MS")) timeout_floor_ms_ = std::max(1, std::atoi(t));
     const char* eager_env = getenv("TFSERVE_EAGER_H2D");
     eager_ = eager_ && eager_env && std::atoi(eager_env) != 0;
     th_ = std::thread([this] { run(); });
@@ -198,6 +202,7 @@ class NativeLane {
   }
   int endpoint_id() const { return ep_->id; }
   std::atomic<uint64_t> batches{0}, errors{0};
+  std::atomic<bool> dead{false};   // gave up on a hung batch and exited
 
  private:
   int batch(HipRt& rt, void* done, int n) {
@@ -238,7 +243,7 @@ class NativeLane {
       rx.pop();
       rx.push("tfs.gpu_wait");
     }
-    if (!e) e = wait(rt, done);
+    if (!e) e = wait(rt, done, deadline_from(Clock::now()));
     if (rx.on()) {
       rx.pop();
       rx.pop();
@@ -247,14 +252,25 @@ class NativeLane {
   }
   // Poll the batch's completion event: a short yield phase, then 40 us naps.
   // (hipEventSynchronize busy-waits a core per lane for the whole ~1 ms batch;
-  // the IO threads need those cores.)
-  static int wait(HipRt& rt, void* ev) {
+  // the IO threads need those cores.)  Gives up after `deadline` (a hung
+  // kernel or wedged stream): returns kLaneHung.
+  static int wait(HipRt& rt, void* ev, Clock::time_point deadline) {
     for (int i = 0;; ++i) {
       const int e = rt.event_query(ev);
       if (e != kHipErrorNotReady) return e;
-      if (i < 16) std::this_thread::yield();
-      else std::this_thread::sleep_for(std::chrono::microseconds(40));
+      if (i < 16) {
+        std::this_thread::yield();
+      } else {
+        if ((i & 63) == 0 && Clock::now() > deadline) return kLaneHung;
+        std::this_thread::sleep_for(std::chrono::microseconds(40));
+      }
     }
+  }
+  // Batch deadline: 50x the lane's running mean batch time, never under the
+  // floor (first batches include lazy device init; TFSERVE_LANE_TIMEOUT_MS).
+  Clock::time_point deadline_from(Clock::time_point t0) const {
+    const double ms = std::max(double(timeout_floor_ms_), 50.0 * mean_ms_);
+    return t0 + std::chrono::microseconds(int64_t(ms * 1e3));
   }
   // H2D of rows that just completed in the pinned slot (row ranges from acquire)
   int copy_rows(HipRt& rt, const std::vector<std::pair<int, int>>& ranges) {
@@ -279,6 +295,7 @@ class NativeLane {
       eager_ = false;
     std::vector<std::pair<int, int>> ranges;
     int copy_err = 0;
+    bool hung = false;
     for (;;) {
       ranges.clear();
       const int n = ep_->acquire(slot_, 100, eager_ ? &ranges : nullptr);
@@ -292,6 +309,14 @@ class NativeLane {
         continue;
       }
       ++seen_;
+      if (fault_hang_ >= 0 && seen_ > uint64_t(fault_hang_)) {
+        // simulated wedged device: the batch never completes within the deadline
+        std::this_thread::sleep_for(std::chrono::milliseconds(timeout_floor_ms_));
+        errors++;
+        hung = true;
+        ep_->fail_dead(slot_, *srv_, 14 /*UNAVAILABLE*/, "GPU batch timed out (device not responding)");
+        break;
+      }
       if ((fault_every_ > 0 && seen_ % uint64_t(fault_every_) == 0) ||
           (fault_after_ >= 0 && seen_ > uint64_t(fault_after_))) {
         errors++;
@@ -301,6 +326,15 @@ class NativeLane {
       const bool tracing = trace_buf().on.load(std::memory_order_relaxed);
       const auto t_acq = Clock::now();
       const int e = done ? batch(rt, done, n) : -1;
+      if (e == kLaneHung) {
+        // the device stopped making progress: answer the batch, retire the
+        // slot (late GPU writes may still land in it) and end this lane so an
+        // unload can join it; the health monitor sees the failure counters
+        errors++;
+        hung = true;
+        ep_->fail_dead(slot_, *srv_, 14 /*UNAVAILABLE*/, "GPU batch timed out (device not responding)");
+        break;
+      }
       if (e != 0) {
         errors++;
         std::string why = e > 0 && rt.err ? std::string(rt.err(e)) : std::string("no graph for this batch");
@@ -309,12 +343,16 @@ class NativeLane {
       }
       batches++;
       const auto t_done = Clock::now();
+      const double ms = std::chrono::duration<double, std::milli>(t_done - t_acq).count();
+      mean_ms_ = batches == 1 ? ms : 0.9 * mean_ms_ + 0.1 * ms;
       const auto t_open = tracing ? ep_->slot_opened(slot_) : t_done;
       ep_->complete(slot_, *srv_);
       if (tracing)
         trace_buf().add({ep_->id, slot_, n, us_of(t_open), us_of(t_acq), us_of(t_acq), us_of(t_done),
                          us_of(Clock::now())});
     }
+    dead = hung;
+    if (hung) return;   // the wedged stream still references these: leak them rather than block
     if (done) rt.event_destroy(done);
     if (copied_) rt.event_destroy(copied_);
     if (copy_stream_ && rt.stream_destroy) rt.stream_destroy(copy_stream_);
@@ -329,6 +367,9 @@ class NativeLane {
   void* copied_ = nullptr;
   int fault_every_ = 0;
   int fault_after_ = -1;
+  int fault_hang_ = -1;
+  int timeout_floor_ms_ = 10000;
+  double mean_ms_ = 0.0;
   uint64_t seen_ = 0;
   std::thread th_;
 };
@@ -519,23 +560,24 @@ void register_server(py::module_& m) {
       .def("native_lane_stats", [](PyServer& s) {
         std::lock_guard<std::mutex> g(s.lmu);
         py::list out;
-        for (auto& l : s.lanes) out.append(py::make_tuple(l->endpoint_id(), l->batches.load(), l->errors.load()));
+        for (auto& l : s.lanes)
+          out.append(py::make_tuple(l->endpoint_id(), l->batches.load(), l->errors.load(), l->dead.load()));
         return out;
       })
       .def("acquire", [](PyServer& s, int id, int slot, int timeout_ms) {
-        auto ep = s.fast->endpoint(id);
+        auto ep = s.fast->endpoint(id, true);
         if (!ep) return -1;
         py::gil_scoped_release nogil;
         return ep->acquire(slot, timeout_ms);
       })
       .def("complete", [](PyServer& s, int id, int slot) {
-        auto ep = s.fast->endpoint(id);
+        auto ep = s.fast->endpoint(id, true);
         if (!ep) return;
         py::gil_scoped_release nogil;
         ep->complete(slot, *s.srv);
       })
       .def("fail", [](PyServer& s, int id, int slot, int code, const std::string& msg) {
-        auto ep = s.fast->endpoint(id);
+        auto ep = s.fast->endpoint(id, true);
         if (!ep) return;
         py::gil_scoped_release nogil;
         ep->fail(slot, *s.srv, code, msg);

@@ -243,8 +243,13 @@ class BatchingSession:
                     res[a] = v[off:off + t.size]
                 t.result = res
                 off += t.size
-        except BaseException as e:     # every task of the batch gets the error
-            err = e if isinstance(e, E.ServingError) else E.internal(f"{type(e).__name__}: {e}")
+        except BaseException as e:     # every task of the batch gets the (same) error
+            if isinstance(e, E.ServingError):
+                err = e
+            else:
+                from .health import is_device_failure
+                err = E.internal(f"{type(e).__name__}: {e}")
+                err.device_failure = is_device_failure(e)     # host bugs are not device failures
             for t in b.tasks:
                 t.error = err
         finally:

@@ -105,7 +105,13 @@ class ServingCore:
             out = self._run_raw(servable, sig_name, inputs, out_aliases)
         except BaseException as e:
             from .health import is_device_failure
-            if is_device_failure(e):
+            # one failed batch fails every request in it with the SAME error
+            # object (server/batching.py): count the batch once, not per request
+            if is_device_failure(e) and not getattr(e, "_health_counted", False):
+                try:
+                    e._health_counted = True
+                except AttributeError:
+                    pass
                 self.health.record(getattr(servable, "name", "?"), getattr(servable, "version", 0), False, str(e))
             raise
         self.health.record(getattr(servable, "name", "?"), getattr(servable, "version", 0), True)

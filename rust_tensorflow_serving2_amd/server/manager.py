@@ -99,6 +99,8 @@ class ModelManager:
         self._poller: Optional[threading.Thread] = None
         self._stop = threading.Event()
         self.listeners: List[Callable[[str, int, int], None]] = []   # (model, version, state)
+        # called with each model name an explicit config (apply_config) lists
+        self.config_listeners: List[Callable[[str], None]] = []
 
     # ------------------------------------------------------------ config
     def config(self):
@@ -158,6 +160,12 @@ class ModelManager:
                     for vs in entry.versions.values():     # an explicit config lifts quarantine
                         vs.quarantined = False
                 self._reconcile(name, entry)
+        for name in new:
+            for cb in list(self.config_listeners):
+                try:
+                    cb(name)
+                except Exception:
+                    log.exception("config listener failed")
         if wait:
             return self.wait_until_settled(list(new), timeout)
         return []

@@ -37,6 +37,21 @@ class FastEndpoint:
         self.t = transport
         self.servable = servable
         self.sig = sig_name
+        self._closed = False
+        # the lanes replay graphs and read/write pinned buffers the servable
+        # owns: hold a reference until close() has joined them, so the
+        # manager's unload (which drains references) cannot free them early
+        servable.acquire()
+        try:
+            self._setup(transport, servable, sig_name, timeout_us)
+        except BaseException:
+            self.close()
+            raise
+
+    def _setup(self, transport, servable, sig_name: str, timeout_us: int):
+        self.id = -1
+        self.workers: List[threading.Thread] = []
+        self._stop = threading.Event()
         srv = transport.srv
         sig = servable.signatures[sig_name]
         in_specs = servable.input_specs(sig_name)
@@ -51,8 +66,6 @@ class FastEndpoint:
         srv.set_idle_dispatch(self.id, transport.idle_dispatch)
         io_in, io_out = srv.endpoint_io_order(self.id)
         assert list(io_in) == in_aliases and list(io_out) == out_aliases
-        self.workers: List[threading.Thread] = []
-        self._stop = threading.Event()
         lanes = self.runner.fast_lanes()
         for lane_idx in lanes:
             in_ptrs, out_ptrs = self.runner.lane_host_pointers(lane_idx)
@@ -93,10 +106,19 @@ class FastEndpoint:
                 self.t.metrics.observe_batch(n, 0.0, str(self.servable.options.device))
 
     def close(self):
+        """Close the endpoint (requests that have not started are answered
+        UNAVAILABLE), join its lanes, then drop the servable reference."""
+        if self._closed:
+            return
+        self._closed = True
         self._stop.set()
-        self.t.srv.remove_endpoint(self.id)
-        for th in self.workers:
-            th.join(timeout=5)
+        try:
+            if self.id >= 0:
+                self.t.srv.remove_endpoint(self.id)
+            for th in self.workers:
+                th.join(timeout=5)
+        finally:
+            self.servable.release()
 
 
 class NativeTransport:
@@ -124,6 +146,10 @@ class NativeTransport:
         # stop() waits for them so no capture outlives the transport
         self._reg_threads: List[threading.Thread] = []
         self._cancelled: set = set()
+        # endpoint teardown (closing + joining lanes) runs off the manager's
+        # listener call, which holds the manager lock: only the route removal
+        # is synchronous, so resolve() / GetModelStatus never wait on a lane
+        self._teardown: List[threading.Thread] = []
 
     # ------------------------------------------------------------ slow path
     def _serve(self):
@@ -224,8 +250,13 @@ class NativeTransport:
         for k, ep in zip(keys, eps):
             self.srv.set_route(name, k[2], version, -1)
         self._refresh_latest(name)
-        for ep in eps:
-            ep.close()
+        if not eps:
+            return
+        th = threading.Thread(target=lambda: [ep.close() for ep in eps], daemon=True,
+                              name=f"tfs-teardown-{name}-{version}")
+        with self._eps_lock:
+            self._teardown = [t for t in self._teardown if t.is_alive()] + [th]
+        th.start()
 
     # ------------------------------------------------------------ lifecycle
     def start(self):
@@ -247,8 +278,11 @@ class NativeTransport:
         with self._eps_lock:
             eps = list(self._eps.values())
             self._eps.clear()
+            teardown = list(self._teardown)
         for ep in eps:
             ep.close()
+        for th in teardown:
+            th.join(timeout=60)
         self.srv.stop()
         for w in self._workers:
             w.join(timeout=2)
@@ -281,13 +315,13 @@ class NativeTransport:
         return out
 
     def health_rows(self):
-        """(model, version, signature, failed, consecutive_failed) per fast endpoint
-        (polled by server.health.HealthMonitor)."""
+        """(model, version, signature, failed, consecutive_failed, batches) per
+        fast endpoint (polled by server.health.HealthMonitor)."""
         with self._eps_lock:
             eps = list(self._eps.items())
         for (name, ver, sig), ep in eps:
             es = self.srv.endpoint_stats(ep.id)
-            yield name, ver, sig, es.get("failed", 0), es.get("consecutive_failed", 0)
+            yield name, ver, sig, es.get("failed", 0), es.get("consecutive_failed", 0), es.get("batches", 0)
 
     def stats(self) -> dict:
         d = dict(self.srv.stats())

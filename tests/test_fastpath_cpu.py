@@ -164,3 +164,73 @@ def test_deadline_exceeded_is_not_computed_twice():
         srv.remove_endpoint(ep)
         th.join(timeout=5)
         srv.stop()
+
+
+def test_close_answers_every_unstarted_request():
+    """Endpoint close (a version unloading) while requests sit in the FIFO
+    queue, in an open batch and in a ready batch no lane has started: every
+    one is answered (OK if its batch ran, UNAVAILABLE otherwise) -- none is
+    left hanging until the client deadline."""
+    srv = _C.Http2Server("127.0.0.1", 0, 2)
+    ep = srv.add_endpoint("m", 1, "serving_default", [("x", T.DT_FLOAT, [16])], [("y", T.DT_FLOAT, [16])], 4, 1000000)
+    bufs = []
+    for k in range(2):
+        xin, yout = np.zeros((4, 16), np.float32), np.zeros((4, 16), np.float32)
+        srv.set_slot_buffers(ep, k, [xin.ctypes.data], [yout.ctypes.data])
+        bufs.append((xin, yout))
+    srv.set_route("m", "serving_default", -1, ep)
+    started = threading.Event()
+
+    def lane():                        # serves slot 0 once, slowly; slot 1 never runs
+        while True:
+            n = srv.acquire(ep, 0, 50)
+            if n < 0:
+                return
+            if n == 0:
+                continue
+            started.set()
+            time.sleep(0.5)
+            bufs[0][1][:n] = bufs[0][0][:n] + 1
+            srv.complete(ep, 0)
+
+    def slow_path():                   # stands in for the Python core: model unloaded
+        while not done.is_set():
+            c = srv.next_call(50)
+            if c is not None:
+                srv.respond(c, 14, "Servable not found", b"")
+
+    done = threading.Event()
+    th = threading.Thread(target=lane, daemon=True)
+    py = threading.Thread(target=slow_path, daemon=True)
+    srv.start()
+    th.start()
+    py.start()
+    spec = native.spec_tuple("m", None, None, "serving_default")
+    body = native.encode_predict_request(spec, {"x": np.ones((1, 16), np.float32)})
+    codes = []
+    try:
+        with grpc.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+            stub = ch.unary_unary(PREDICT)
+            with cf.ThreadPoolExecutor(16) as ex:
+                futs = [ex.submit(stub, body, timeout=20) for _ in range(4)]   # fills slot 0 -> runs
+                assert started.wait(5)
+                futs += [ex.submit(stub, body, timeout=20) for _ in range(10)]  # slot 1 (ready) + queue
+                time.sleep(0.3)
+                t0 = time.time()
+                srv.remove_endpoint(ep)
+                for f in futs:
+                    try:
+                        f.result()
+                        codes.append("OK")
+                    except grpc.RpcError as e:
+                        codes.append(e.code().name)
+                assert time.time() - t0 < 10
+    finally:
+        done.set()
+        th.join(timeout=5)
+        py.join(timeout=5)
+        srv.stop()
+    # the first batch (idle dispatch: whatever had arrived) ran; everything
+    # later was still waiting when the endpoint closed
+    assert len(codes) == 14 and set(codes) <= {"OK", "UNAVAILABLE"}, codes
+    assert 1 <= codes.count("OK") <= 4 and codes.count("UNAVAILABLE") >= 10, codes

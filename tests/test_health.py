@@ -106,6 +106,63 @@ def test_consecutive_failures_reload_then_quarantine(mgr):
     assert mgr.status("a")[0].state == AVAILABLE and mgr.loads.count(("a", 1)) == 3
     lines = "\n".join(h.prometheus_lines())
     assert 'tfserve_servable_recoveries_total{model="a",version="1"} 1' in lines
+    # the config reload also reset the recovery window: the next trip reloads
+    # the version again instead of quarantining it at once
+    for _ in range(3):
+        h.record("a", 1, False, "hip error after the config reload")
+    assert wait_for(lambda: mgr.loads.count(("a", 1)) == 4)
+    assert wait_for(lambda: mgr.status("a")[0].state == AVAILABLE)
+    assert h.recoveries[("a", 1)] == 1 and h.recoveries_total[("a", 1)] == 2
+
+
+def test_clean_run_forgives_recoveries(mgr):
+    """After a reload, enough good batches reset the recovery count: faults
+    far apart never accumulate into a quarantine."""
+    h = HealthMonitor(mgr, threshold=2, max_recoveries=1, clean_batches=5)
+    for _ in range(2):
+        h.record("a", 1, False, "hip error")
+    assert wait_for(lambda: mgr.loads.count(("a", 1)) == 2)
+    assert wait_for(lambda: mgr.status("a")[0].state == AVAILABLE)
+    for _ in range(5):
+        h.record("a", 1, True)
+    assert h.recoveries.get(("a", 1), 0) == 0
+    for _ in range(2):                     # would have quarantined without the reset
+        h.record("a", 1, False, "hip error, much later")
+    assert wait_for(lambda: mgr.loads.count(("a", 1)) == 3)
+    assert wait_for(lambda: mgr.status("a")[0].state == AVAILABLE)
+
+
+def test_batch_failure_counted_once_and_host_errors_ignored():
+    """One failed batch fails all its requests with the same error object: the
+    serving core counts it once.  Host-side bugs are not device failures."""
+    from rust_tensorflow_serving2_amd.server.core import ServingCore
+
+    class Mon:
+        def __init__(self):
+            self.calls = []
+
+        def record(self, name, version, ok, why=""):
+            self.calls.append(ok)
+
+    class S:
+        name, version = "m", 1
+
+    err = E.internal("RuntimeError: HIP error: an illegal memory access")
+    core = ServingCore.__new__(ServingCore)
+    core.health = Mon()
+
+    def boom(*a):
+        raise err
+    core._run_raw = boom
+    for _ in range(8):                     # 8 requests of one failed batch
+        with pytest.raises(E.ServingError):
+            core._run(S(), "sig", {}, [])
+    assert core.health.calls == [False]
+    host = E.internal("IndexError: index 3 is out of bounds")
+    host.device_failure = False
+    assert not is_device_failure(host)
+    assert not is_device_failure(IndexError("index 3 is out of bounds"))
+    assert is_device_failure(InjectedFault("injected fault (TFSERVE_FAULT)"))
 
 
 def test_native_source_polled(mgr):
