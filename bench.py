@@ -74,6 +74,10 @@ def parse():
     ap.add_argument("--c1-requests", type=int, default=200,
                     help="after the timed window: batch-1 round trips at concurrency 1 over one connection "
                          "(reported as p50_c1_ms; 0 = skip)")
+    ap.add_argument("--ref-client-requests", type=int, default=2000,
+                    help="after the timed window: rank 0 drives this many Predicts over 2 HTTP/2 connections "
+                         "(the reference client's channel pattern, src/lib.rs:132-138) while every rank serves; "
+                         "reported as ref_client_rps + the share each GPU served (per-stream routing; 0 = skip)")
     ap.add_argument("--cpu-report", action="store_true",
                     help="add per-thread-group CPU seconds of the timed window (from /proc) to the JSON")
     return ap.parse_args()
@@ -147,11 +151,15 @@ def main():
     sopts = ServableOptions(device=str(device), max_batch_size=args.batch, lanes=args.lanes,
                             allowed_batch_sizes=tuple(sorted({1, 2, 4, 8, 16, args.batch})))
     port = (args.port + local) if args.port else 0
+    # N > 1: every rank's front end may route single Predicts to the least-loaded
+    # GPU over shared-memory rings (csrc/router.h); balanced ranks keep their own
+    route_group = f"b{os.environ.get('MASTER_PORT', '0')}" if world > 1 else None
     server = ModelServer(ServerOptions(port=port, host="127.0.0.1", model_name=model_name, model_base_path=base,
                                        device=str(device), transport=args.transport, servable=sopts,
                                        io_threads=args.io_threads, batch_timeout_us=args.batch_timeout_us,
                                        file_system_poll_wait_seconds=0, weight_source=weight_source,
-                                       monitoring=False))
+                                       monitoring=False,
+                                       router=(route_group, rank, world) if route_group else None))
     t_load = time.perf_counter()
     server.start()
     t_load = time.perf_counter() - t_load
@@ -229,6 +237,42 @@ def main():
     loadgen.stop(30.0)
     check(r, "timed window")
 
+    # reference-client mode: ONE client with 2 connections (the Rust client's
+    # two channels) on rank 0's port while every rank serves; the router
+    # spreads its streams over the GPUs
+    ref = None
+    if args.ref_client_requests > 0 and args.transport == "native":
+        srvc = server.transports[0].srv
+
+        def served():
+            st, rs = srvc.stats(), srvc.router_stats()
+            return st["requests"] - (rs.get("forwarded", 0) if rs else 0)
+        if world > 1:
+            dist.barrier()
+        s0 = served()
+        if rank == 0:
+            lg2 = _C.LoadGen("127.0.0.1", server.port, PREDICT, bodies, min(conc, 128), 2, 1)
+            lg2.run(max(64, args.ref_client_requests // 10), 120.0)
+            s0 = served()
+            r2 = lg2.run(args.ref_client_requests, 300.0)
+            ref = {"ok": r2["ok"], "errors": r2["errors"], "elapsed_s": r2["elapsed_s"]}
+            del lg2
+        if world > 1:
+            dist.barrier()
+        share = torch.tensor([float(served() - s0)], dtype=torch.float64,
+                             device=device if backend == "nccl" else "cpu")
+        if world > 1:
+            parts = [torch.zeros_like(share) for _ in range(world)]
+            dist.all_gather(parts, share)
+            share_v = [float(p.item()) for p in parts]
+        else:
+            share_v = [float(share.item())]
+        if ref is not None:
+            tot = max(1.0, sum(share_v))
+            ref = {"ref_client_rps": round(ref["ok"] / max(ref["elapsed_s"], 1e-9), 1),
+                   "ref_client_errors": ref["errors"],
+                   "ref_client_gpu_share": [round(v / tot, 3) for v in share_v]}
+
     # latency mode: one client, one connection, one call in flight (the
     # reference's examples/prediction.rs pattern): p50 of batch-1 round trips
     p50_c1 = None
@@ -283,10 +327,15 @@ def main():
             "cpu_cores_by_thread": cpu_report,
             "fast_path_share": round(stats.get("fast_path", 0) / max(1, stats.get("requests", 1)), 3) if stats else None,
         }
+        if ref is not None:
+            out.update(ref)
         print(json.dumps(out), flush=True)
     server.stop()
     if world > 1:
         dist.barrier()
+        if rank == 0 and route_group:
+            from rust_tensorflow_serving2_amd.parallel.replicas import shm_cleanup
+            shm_cleanup(route_group)
         dist.destroy_process_group()
 
 

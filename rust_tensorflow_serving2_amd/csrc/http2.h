@@ -29,6 +29,16 @@ namespace tfs {
 
 using Clock = std::chrono::steady_clock;
 
+struct Call;
+
+// Answers calls that another replica placed in this replica's shared-memory
+// ring (router.h): the answer goes back through the ring, not a socket.
+class RemoteSink {
+ public:
+  virtual ~RemoteSink() = default;
+  virtual void respond_remote(const Call& c, int status, const std::string& msg, const std::string& body) = 0;
+};
+
 // One completed unary request waiting for its answer.
 struct Call {
   uint64_t conn_id = 0;
@@ -39,8 +49,16 @@ struct Call {
   // `off`) so the 602 KB request buffer moves into the Call without a copy
   std::string body;
   size_t off = 0;
-  const uint8_t* data() const { return reinterpret_cast<const uint8_t*>(body.data()) + off; }
-  size_t size() const { return body.size() - off; }
+  // a message held outside `body`: the cell of a cross-replica call (router.h)
+  const uint8_t* ext = nullptr;
+  size_t ext_len = 0;
+  RemoteSink* remote = nullptr;   // answer through this sink (cell index below)
+  uint32_t cell = 0;
+  bool routed = false;            // placed by the router already: never forwarded again
+  // outstanding-call counter this call was counted in (decremented when answered)
+  std::atomic<int64_t>* load = nullptr;
+  const uint8_t* data() const { return ext ? ext : reinterpret_cast<const uint8_t*>(body.data()) + off; }
+  size_t size() const { return ext ? ext_len : body.size() - off; }
   Clock::time_point arrival;
   int64_t timeout_us = 0;  // grpc-timeout, 0 = none
   // the client's deadline (grpc-timeout) has passed: answer DEADLINE_EXCEEDED, skip the work
@@ -69,6 +87,8 @@ struct StreamRes {
   virtual void commit(std::unique_ptr<Call> call) = 0;
   // The IO side gives up (stream reset, protocol error).
   virtual void abandon() = 0;
+  // The row lives in another replica's ring (router.h), not a local batch slot.
+  virtual bool remote() const { return false; }
   // Copy the next chunk; false once the batcher has abandoned the row (too slow).
   bool write(const uint8_t* p, size_t n) {
     writers.fetch_add(1);
@@ -96,6 +116,7 @@ struct ServerStats {
 };
 
 class IoThread;
+class Router;
 
 class Server {
  public:
@@ -112,8 +133,27 @@ class Server {
   void respond(uint64_t conn_id, int io_index, int32_t stream_id, int status, std::string message,
                std::string body);
   void respond(const Call& c, int status, std::string message, std::string body) {
+    if (c.load) c.load->fetch_sub(1, std::memory_order_relaxed);
+    if (c.remote) {
+      c.remote->respond_remote(c, status, message, body);
+      return;
+    }
     respond(c.conn_id, c.io_index, c.stream_id, status, std::move(message), std::move(body));
   }
+  // Cross-replica routing (router.h); null = every call stays local.  Set
+  // before start().
+  void set_router(Router* r);
+  Router* router() const { return router_; }
+  // A streamed Predict's row: on a peer (router) or in a local batch slot.
+  std::shared_ptr<StreamRes> reserve_stream(const ProbeInfo& pi, const uint8_t* head, size_t head_len,
+                                            const std::string& method);
+  // Count a call in this replica's load (answered calls uncount themselves).
+  void count(Call& c) {
+    if (c.load) return;
+    c.load = load_;
+    c.load->fetch_add(1, std::memory_order_relaxed);
+  }
+  int64_t load() const { return load_->load(std::memory_order_relaxed); }
   // Slow path queue for the Python control plane.
   std::unique_ptr<Call> next_call(int timeout_ms);
   void push_call(std::unique_ptr<Call> c);
@@ -130,6 +170,9 @@ class Server {
   std::vector<std::unique_ptr<IoThread>> io_;
   FastDispatch fast_;
   StreamReserve reserve_;
+  Router* router_ = nullptr;
+  std::atomic<int64_t> own_load_{0};
+  std::atomic<int64_t>* load_ = &own_load_;
   std::mutex qmu_;
   std::condition_variable qcv_;
   std::deque<std::unique_ptr<Call>> queue_;

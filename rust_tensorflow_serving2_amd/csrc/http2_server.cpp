@@ -15,6 +15,7 @@
 
 #include "http2.h"
 #include "nghttp2_min.h"
+#include "router.h"
 
 namespace tfs {
 
@@ -297,7 +298,7 @@ class IoThread {
       return 0;
     }
     if (st->mode == kProbeMode) {
-      if (st->path != kPredictMethod || !self->srv_->stream_reserve()) {
+      if (st->path != kPredictMethod || !(self->srv_->stream_reserve() || self->srv_->router())) {
         st->mode = kBufferMode;
       } else {
         const size_t before = st->body.size();
@@ -306,7 +307,8 @@ class IoThread {
         ProbeInfo pi;
         Probe pr = probe_predict_header((const uint8_t*)st->body.data(), st->body.size(), kStreamMin, pi);
         if (pr == Probe::kFound) {
-          std::shared_ptr<StreamRes> res = self->srv_->stream_reserve()(pi);
+          std::shared_ptr<StreamRes> res =
+              self->srv_->reserve_stream(pi, (const uint8_t*)st->body.data(), st->body.size(), st->path);
           if (res) {
             // payload = framed-message bytes [payload_off, payload_off + len): part may sit in
             // the header buffer, the rest in this chunk (data[take..] is message offset before+take..)
@@ -409,6 +411,7 @@ class IoThread {
       call->method = st->path;
       call->arrival = Clock::now();
       call->timeout_us = st->timeout_us;
+      if (!r->remote()) srv_->count(*call);   // a remote row counts in its replica's load
       srv_->stats.requests++;
       srv_->stats.fast_path++;
       srv_->stats.streamed++;
@@ -732,7 +735,23 @@ void Server::respond(uint64_t conn_id, int io_index, int32_t stream_id, int stat
   io_[io_index]->post(Outgoing{conn_id, stream_id, status, std::move(message), std::move(body)});
 }
 
+void Server::set_router(Router* r) {
+  router_ = r;
+  load_ = r ? r->load_word() : &own_load_;
+}
+
+std::shared_ptr<StreamRes> Server::reserve_stream(const ProbeInfo& pi, const uint8_t* head, size_t head_len,
+                                                  const std::string& method) {
+  if (router_) {
+    auto r = router_->reserve_stream(pi, head, head_len, method);
+    if (r) return r;
+  }
+  return reserve_ ? reserve_(pi) : nullptr;
+}
+
 void Server::dispatch(std::unique_ptr<Call> c) {
+  if (router_ && !c->routed && c->method == kPredictMethod && router_->forward(c)) return;
+  count(*c);
   if (fast_) {
     const auto t0 = Clock::now();
     const bool taken = fast_(c);

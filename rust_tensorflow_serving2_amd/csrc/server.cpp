@@ -15,6 +15,7 @@
 
 #include "batcher.h"
 #include "http2.h"
+#include "router.h"
 
 namespace py = pybind11;
 using namespace tfs;
@@ -375,6 +376,9 @@ class NativeLane {
 };
 
 struct PyServer {
+  // declared first: destroyed last, after every lane / endpoint that may
+  // still answer a call another replica placed in its ring
+  std::unique_ptr<Router> router;
   std::unique_ptr<Server> srv;
   std::unique_ptr<FastPath> fast;
   std::mutex lmu;
@@ -548,6 +552,31 @@ void register_server(py::module_& m) {
                                                        reinterpret_cast<void*>(stream), std::move(bs)));
         return true;
       }, py::arg("endpoint"), py::arg("slot"), py::arg("device"), py::arg("stream"), py::arg("buckets"))
+      .def("enable_router", [](PyServer& s, const std::string& group, int rank, int world, int ncells,
+                               size_t req_cap, size_t resp_cap, int margin) {
+        if (s.router) throw std::runtime_error("router already enabled");
+        s.router = std::make_unique<Router>(s.srv.get(), group, rank, world, ncells, req_cap, resp_cap, margin);
+        s.srv->set_router(s.router.get());
+        s.router->start();
+      }, py::arg("group"), py::arg("rank"), py::arg("world"), py::arg("ncells") = 64,
+         py::arg("req_cap") = size_t(1) << 20, py::arg("resp_cap") = size_t(64) << 10, py::arg("margin") = 8)
+      .def("stop_router", [](PyServer& s) {
+        py::gil_scoped_release nogil;
+        if (s.router) s.router->stop();
+      })
+      .def("router_stats", [](PyServer& s) {
+        py::dict d;
+        if (!s.router) return d;
+        auto& st = s.router->stats;
+        d["forwarded"] = st.forwarded.load(); d["streamed"] = st.streamed.load();
+        d["ingested"] = st.ingested.load(); d["returned"] = st.returned.load();
+        d["reclaimed"] = st.reclaimed.load(); d["lost"] = st.lost.load(); d["no_cell"] = st.no_cell.load();
+        d["peers_alive"] = s.router->peers_alive();
+        d["loads"] = s.router->loads();
+        d["rank"] = s.router->rank();
+        return d;
+      })
+      .def("load", [](PyServer& s) { return s.srv->load(); })
       .def("set_tracing", [](PyServer&, bool on) { trace_buf().on = on; })
       .def("drain_trace", [](PyServer&) {
         py::list out;

@@ -205,8 +205,19 @@ class ReplicatedWeightSource:
         for k in [k for k, (t, _) in self._parked.items() if now - t > ttl]:
             del self._parked[k]
 
+    def group_broken(self) -> bool:
+        """A replica died (the supervisor says so): the collective can no
+        longer complete, every rank loads from disk from now on."""
+        try:
+            return self.store.check(["tfs/group_broken"])
+        except Exception:
+            return True
+
     # ------------------------------------------------------------ API
     def load(self, name: str, version: int, path: str):
+        if self.group_broken():
+            self.stats["disk_loads"] = self.stats.get("disk_loads", 0) + 1
+            return sm.load(path)
         if self.is_leader:
             return self._publish_and_broadcast(name, version, path)
         k = (name, int(version))
@@ -220,12 +231,17 @@ class ReplicatedWeightSource:
             if isinstance(parked[1], Exception):
                 raise parked[1]
             return parked[1]
-        try:
-            return fut.result(timeout=self.load_timeout)
-        except FutureTimeout:
-            with self._lock:
-                self._pending.pop(k, None)
-            raise LoadError(f"timed out waiting for the leader rank to broadcast {name} version {version}")
+        deadline = time.time() + self.load_timeout
+        while True:
+            try:
+                return fut.result(timeout=0.5)
+            except FutureTimeout:
+                if self.group_broken() or time.time() > deadline:
+                    with self._lock:
+                        self._pending.pop(k, None)
+                    if self.group_broken():     # the leader may be the replica that died
+                        return sm.load(path)
+                    raise LoadError(f"timed out waiting for the leader rank to broadcast {name} version {version}")
 
     def close(self):
         self._stop.set()

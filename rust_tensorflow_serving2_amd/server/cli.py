@@ -70,6 +70,9 @@ def build_parser() -> argparse.ArgumentParser:
     a("--health_failure_threshold", type=int, default=8,
       help="consecutive failed batches after which a servable is reloaded (0 = no health monitor)")
     a("--health_max_recoveries", type=int, default=3, help="reloads of one version before it is quarantined")
+    a("--route_streams", type=_bool, nargs="?", const=True, default=True,
+      help="replicas: route individual Predicts to the least-loaded replica over shared memory "
+           "(one client connection still uses every GPU)")
     a("--log_level", default="INFO")
     return ap
 
@@ -100,7 +103,7 @@ def make_server(args, rank: int = 0, world: int = 1):
     batching = None
     if args.enable_batching and args.batching_parameters_file:
         batching = _read_text_proto(args.batching_parameters_file, serving.BatchingParameters())
-    weight_source = replicas = None
+    weight_source = replicas = router = None
     if world > 1:
         import torch.distributed as dist
         from ..parallel.replicas import ReplicaControl
@@ -108,15 +111,31 @@ def make_server(args, rank: int = 0, world: int = 1):
         dev = torch.device(device)
         if dev.type == "cuda":
             torch.cuda.set_device(dev)
-        if not dist.is_initialized():
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            if dev.type == "cuda":
-                dist.init_process_group("nccl", device_id=dev)
-            else:
-                dist.init_process_group("gloo")
-        store = dist.distributed_c10d._get_default_store()
-        weight_source = ReplicatedWeightSource(store, device=dev)
-        replicas = ReplicaControl(store, rank, world)
+        restarts = int(os.environ.get("TFSERVE_RESTARTS", "0"))
+        store_addr = os.environ.get("TFSERVE_STORE", "")
+        store = None
+        if store_addr:
+            # the supervisor's store (parallel/replicas.py launch): outlives any replica
+            from datetime import timedelta
+            host, sport = store_addr.rsplit(":", 1)
+            store = dist.TCPStore(host, int(sport), is_master=False, timeout=timedelta(seconds=120))
+        if restarts == 0:
+            if not dist.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                backend = "nccl" if dev.type == "cuda" else "gloo"
+                kw = {"device_id": dev} if dev.type == "cuda" else {}
+                if store is not None:
+                    dist.init_process_group(backend, store=dist.PrefixStore("tfs/pg", store), rank=rank,
+                                            world_size=world, **kw)
+                else:
+                    dist.init_process_group(backend, **kw)
+            if store is None:
+                store = dist.distributed_c10d._get_default_store()
+            weight_source = ReplicatedWeightSource(store, device=dev)
+        # a replacement replica (restarted by the supervisor) is not a member of
+        # the weight-broadcast group: it loads from disk
+        replicas = ReplicaControl(store, rank, world, restarted=restarts > 0)
+        router = (os.environ.get("TFSERVE_ROUTE_GROUP") or f"p{os.environ.get('MASTER_PORT', '0')}", rank, world)
     sopts = ServableOptions(device=device, hip_graphs=args.hip_graphs, warmup=args.enable_model_warmup,
                             max_batch_size=args.max_batch_size, compute_dtype=args.dtype,
                             fuse=False if args.dtype == "fp32" else None)
@@ -130,8 +149,27 @@ def make_server(args, rank: int = 0, world: int = 1):
                          idle_dispatch=args.idle_dispatch, servable=sopts,
                          monitoring=args.monitoring, weight_source=weight_source, replicas=replicas,
                          trace_dir=args.trace_dir, health_failure_threshold=args.health_failure_threshold,
-                         health_max_recoveries=args.health_max_recoveries)
+                         health_max_recoveries=args.health_max_recoveries,
+                         router=router if args.route_streams else None)
     return ModelServer(opts)
+
+
+def _write_stats(server, stats_dir: str, rank: int):
+    """Per-replica counters at shutdown (TFSERVE_STATS_DIR; multi-replica tests)."""
+    import json
+    d = {"rank": rank, "pid": os.getpid(), "restarts": int(os.environ.get("TFSERVE_RESTARTS", "0"))}
+    for t in server.transports:
+        if hasattr(t, "srv") and hasattr(t.srv, "router_stats"):
+            st = t.srv.stats()
+            rs = dict(t.srv.router_stats())
+            d["requests"] = st["requests"]
+            d["router"] = rs
+            d["served"] = st["requests"] - rs.get("forwarded", 0)   # answered by this replica's device
+    os.makedirs(stats_dir, exist_ok=True)
+    path = os.path.join(stats_dir, f"replica{rank}.{os.getpid()}.json")
+    with open(path + ".tmp", "w") as f:
+        json.dump(d, f)
+    os.replace(path + ".tmp", path)
 
 
 def serve(args, rank: int = 0, world: int = 1, ready: Optional[threading.Event] = None,
@@ -140,7 +178,7 @@ def serve(args, rank: int = 0, world: int = 1, ready: Optional[threading.Event] 
     server.start()
     log.info("replica %d/%d serving gRPC on %s:%d%s", rank, world, args.host, server.port,
              f", REST on {server.rest_port}" if getattr(server, "rest_port", None) else "")
-    print(f"[tfserve] replica {rank}/{world} ready: grpc={server.port}"
+    print(f"[tfserve] replica {rank}/{world} ready: pid={os.getpid()} grpc={server.port}"
           + (f" rest={server.rest_port}" if getattr(server, "rest_port", None) else ""), flush=True)
     stop = stop or threading.Event()
     signalled = []
@@ -151,8 +189,15 @@ def serve(args, rank: int = 0, world: int = 1, ready: Optional[threading.Event] 
             signal.signal(s, lambda *_: signalled.append(1))
     if ready is not None:
         ready.set()
+    stats_dir = os.environ.get("TFSERVE_STATS_DIR")
+    n = 0
     while not signalled and not stop.is_set():
         time.sleep(0.1)
+        n += 1
+        if stats_dir and n % 5 == 0:
+            _write_stats(server, stats_dir, rank)
+    if stats_dir:
+        _write_stats(server, stats_dir, rank)
     server.stop()
     if world > 1:
         import torch.distributed as dist

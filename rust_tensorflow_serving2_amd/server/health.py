@@ -27,6 +27,7 @@ per-GPU: each replica process runs its own monitor over its own device.
 from __future__ import annotations
 
 import logging
+import os
 import threading
 import time
 from typing import Callable, Dict, Iterable, List, Optional, Tuple
@@ -38,6 +39,14 @@ log = logging.getLogger("tfserve.health")
 # codes that say "the server could not run the batch", as opposed to "the
 # request was wrong" (INVALID_ARGUMENT, NOT_FOUND, FAILED_PRECONDITION, ...)
 DEVICE_FAILURE_CODES = (E.INTERNAL, E.UNKNOWN, E.DATA_LOSS)
+STICKY_EXIT = 75      # exit status of a replica that gave its poisoned GPU context up
+_STICKY_WORDS = ("illegal address", "illegal memory", "hardware exception", "device not responding",
+                 "timed out (device")
+
+
+def is_sticky(why: str) -> bool:
+    w = why.lower()
+    return any(k in w for k in _STICKY_WORDS)
 
 
 _DEVICE_WORDS = ("hip", "cuda", "gpu", "device", "hsa", "illegal memory", "illegal address")
@@ -131,7 +140,10 @@ class HealthMonitor:
             if trip:
                 self._consec[key] = 0
         if trip:
-            self._trip(name, int(version), f"{n} consecutive failed batches; last: {why}")
+            if is_sticky(why):
+                self._sticky(name, int(version), f"{n} consecutive failed batches; last: {why}")
+            else:
+                self._trip(name, int(version), f"{n} consecutive failed batches; last: {why}")
 
     def add_source(self, fn: Callable[[], Iterable[Tuple[str, int, str, int, int]]]) -> None:
         """``fn()`` yields ``(model, version, signature, failed_total, consecutive_failed)``
@@ -151,6 +163,9 @@ class HealthMonitor:
                 for row in rows:
                     name, version, sig, failed, consec = row[:5]
                     batches = row[5] if len(row) > 5 else None
+                    dead_lanes = row[6] if len(row) > 6 else 0
+                    if dead_lanes:
+                        self._sticky(name, int(version), f"{dead_lanes} GPU lane(s) timed out (device hang)")
                     k = (name, int(version), sig)
                     with self._lock:
                         new = failed - self._native_seen.get(k, 0)
@@ -165,6 +180,18 @@ class HealthMonitor:
                                 self._good_batches((name, int(version)), good)
                     if consec >= self.threshold:
                         self._trip(name, int(version), f"{consec} consecutive failed batches on the GPU fast path")
+
+    def _sticky(self, name: str, version: int, why: str) -> None:
+        """A failure an in-process reload cannot fix (a hung queue, an illegal
+        address: the HIP context is poisoned).  Under the replica supervisor
+        (parallel/replicas.py, TFSERVE_SUPERVISED=1) the process exits so a
+        fresh one takes the GPU; unsupervised, fall back to a reload."""
+        if os.environ.get("TFSERVE_SUPERVISED") == "1":
+            log.critical("model %s version %d: %s; exiting so the supervisor restarts this replica",
+                         name, version, why)
+            logging.shutdown()
+            os._exit(STICKY_EXIT)
+        self._trip(name, version, why)
 
     def _trip(self, name: str, version: int, why: str) -> None:
         key = (name, version)

@@ -124,10 +124,20 @@ class FastEndpoint:
 class NativeTransport:
     def __init__(self, core, port: int, host: str = "0.0.0.0", batcher=None, io_threads: int = 4,
                  py_workers: int = 16, fast_path: bool = True, batch_timeout_us: int = 2000,
-                 max_message: int = 2 ** 31 - 1, metrics=None, idle_dispatch: bool = True):
+                 max_message: int = 2 ** 31 - 1, metrics=None, idle_dispatch: bool = True,
+                 router: Optional[tuple] = None):
         self.core = core
         self.srv = _C.Http2Server(host, port, io_threads, max_message)
         self.port = self.srv.port
+        if router is not None:
+            # (group, rank, world): per-stream routing over shared memory rings
+            # (csrc/router.h); sizes from the environment for unusual models
+            group, rank, world = router
+            self.srv.enable_router(group, int(rank), int(world),
+                                   ncells=int(os.environ.get("TFSERVE_ROUTE_CELLS", "64")),
+                                   req_cap=int(os.environ.get("TFSERVE_ROUTE_REQ_BYTES", str(1 << 20))),
+                                   resp_cap=int(os.environ.get("TFSERVE_ROUTE_RESP_BYTES", str(256 << 10))),
+                                   margin=int(os.environ.get("TFSERVE_ROUTE_MARGIN", "8")))
         self.metrics = metrics if metrics is not None else getattr(core, "metrics", None)
         if self.metrics is not None:
             self.metrics.collectors.append(self.prometheus_lines)
@@ -283,6 +293,7 @@ class NativeTransport:
             ep.close()
         for th in teardown:
             th.join(timeout=60)
+        self.srv.stop_router()          # peers see this replica go; its forwarded calls are answered
         self.srv.stop()
         for w in self._workers:
             w.join(timeout=2)
@@ -315,16 +326,24 @@ class NativeTransport:
         return out
 
     def health_rows(self):
-        """(model, version, signature, failed, consecutive_failed, batches) per
-        fast endpoint (polled by server.health.HealthMonitor)."""
+        """(model, version, signature, failed, consecutive_failed, batches,
+        dead_lanes) per fast endpoint (polled by server.health.HealthMonitor)."""
         with self._eps_lock:
             eps = list(self._eps.items())
+        dead = {}
+        for ep_id, _b, _e, is_dead in self.srv.native_lane_stats():
+            if is_dead:
+                dead[ep_id] = dead.get(ep_id, 0) + 1
         for (name, ver, sig), ep in eps:
             es = self.srv.endpoint_stats(ep.id)
-            yield name, ver, sig, es.get("failed", 0), es.get("consecutive_failed", 0), es.get("batches", 0)
+            yield (name, ver, sig, es.get("failed", 0), es.get("consecutive_failed", 0), es.get("batches", 0),
+                   dead.get(ep.id, 0))
 
     def stats(self) -> dict:
         d = dict(self.srv.stats())
+        rs = self.srv.router_stats()
+        if rs:
+            d["router"] = dict(rs)
         with self._eps_lock:
             d["endpoints"] = {f"{k[0]}/v{k[1]}/{k[2]}": self.srv.endpoint_stats(ep.id) for k, ep in self._eps.items()}
         return d

@@ -49,6 +49,7 @@ class ServerOptions:
     trace_dir: str = ""                            # request/batch timeline (utils/tracing.py)
     health_failure_threshold: int = 8              # consecutive failed batches -> reload (0 = off)
     health_max_recoveries: int = 3                 # reloads per version before quarantine
+    router: Optional[tuple] = None                 # (group, rank, world): cross-replica stream routing
 
 
 class ModelServer:
@@ -154,7 +155,7 @@ class ModelServer:
             from .native_transport import NativeTransport
             t = NativeTransport(self.core, self.opts.port, self.opts.host, batcher=self.batcher,
                                 io_threads=self.opts.io_threads, batch_timeout_us=self.opts.batch_timeout_us,
-                                idle_dispatch=self.opts.idle_dispatch)
+                                idle_dispatch=self.opts.idle_dispatch, router=self.opts.router)
         else:
             from .grpc_transport import GrpcTransport
             t = GrpcTransport(self.core, self.opts.port, self.opts.host, self.opts.grpc_workers)

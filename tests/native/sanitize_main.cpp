@@ -5,7 +5,11 @@
 //     the streaming header probe on every prefix;
 //   * the SSTable writer/reader with corruption;
 //   * the batcher: concurrent offers + streamed rows (commit / abandon) against
-//     a lane thread acquiring and completing, through a real Server instance.
+//     a lane thread acquiring and completing, through a real Server instance;
+//   * the cross-replica router: two front ends in one process sharing a
+//     routing group (shared-memory rings), buffered and streamed calls routed
+//     both ways while responders answer them, then one router stops.
+// Built twice: ASan + UBSan, and TSan (the IO / lane / router threads).
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -13,8 +17,11 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "batcher.h"
 #include "http2.h"
+#include "router.h"
 #include "sstable.h"
 #include "wire.h"
 
@@ -194,10 +201,104 @@ static void stress_batcher() {
   CHECK(batches.load() > 0);
 }
 
+static void stress_router() {
+  const std::string group = "san" + std::to_string(getpid());
+  Server a("127.0.0.1", 0, 1, size_t(1) << 30), b("127.0.0.1", 0, 1, size_t(1) << 30);
+  auto ra = std::make_unique<Router>(&a, group, 0, 2, 8, 4096, 4096, 0);
+  auto rb = std::make_unique<Router>(&b, group, 1, 2, 8, 4096, 4096, 0);
+  a.set_router(ra.get());
+  b.set_router(rb.get());
+  ra->start();
+  rb->start();
+  std::atomic<bool> stop{false};
+  std::atomic<int> answered{0};
+  std::vector<std::thread> th;
+  for (Server* s : {&a, &b})
+    for (int k = 0; k < 2; ++k)
+      th.emplace_back([&, s] {
+        while (!stop) {
+          auto c = s->next_call(2);
+          if (!c) continue;
+          CHECK(c->size() >= 1 && c->data()[0] == 'p');
+          std::this_thread::sleep_for(std::chrono::microseconds(200));
+          s->respond(*c, 0, std::string(), std::string(c->size() > 64 ? 64 : c->size(), 'r'));
+          answered++;
+        }
+      });
+  std::this_thread::sleep_for(std::chrono::milliseconds(300));   // routers map each other
+  std::vector<std::thread> drivers;
+  for (int t = 0; t < 4; ++t)
+    drivers.emplace_back([&, t] {
+      std::mt19937 rng(77 + t);
+      Server& s = t % 2 ? b : a;
+      for (int i = 0; i < 300; ++i) {
+        if (rng() % 3) {   // a buffered call
+          auto c = std::make_unique<Call>();
+          c->method = "/tensorflow.serving.PredictionService/Predict";
+          c->body.assign(5, '\0');
+          c->body += "p" + std::string(1 + rng() % 2000, char('a' + i % 26));
+          c->off = 5;
+          c->arrival = Clock::now();
+          s.dispatch(std::move(c));
+        } else {           // a streamed call whose payload lands in whichever row the router picks
+          std::string head(5, '\0');
+          head += "p" + std::string(20, 'h');
+          ProbeInfo pi;
+          pi.payload_off = head.size();
+          pi.payload_len = 1 + rng() % 1500;
+          auto r = s.reserve_stream(pi, reinterpret_cast<const uint8_t*>(head.data()), head.size(),
+                                    "/tensorflow.serving.PredictionService/Predict");
+          if (!r) continue;     // stays local: no batch slots in this harness
+          std::vector<uint8_t> payload(r->len, uint8_t('z'));
+          size_t left = r->len;
+          while (left) {
+            const size_t n = std::min<size_t>(left, 1 + rng() % 400);
+            r->write(payload.data() + (r->len - left), n);
+            left -= n;
+          }
+          if (rng() % 9 == 0) {
+            r->abandon();
+          } else {
+            auto c = std::make_unique<Call>();
+            c->method = "/tensorflow.serving.PredictionService/Predict";
+            c->arrival = Clock::now();
+            r->commit(std::move(c));
+          }
+        }
+      }
+    });
+  for (auto& d : drivers) d.join();
+  std::this_thread::sleep_for(std::chrono::milliseconds(500));
+  CHECK(ra->stats.forwarded.load() + rb->stats.forwarded.load() > 0);
+  CHECK(ra->stats.returned.load() == ra->stats.forwarded.load());
+  CHECK(rb->stats.returned.load() == rb->stats.forwarded.load());
+  rb->stop();                      // a peer goes away with the other still routing
+  for (int i = 0; i < 50; ++i) {
+    auto c = std::make_unique<Call>();
+    c->method = "/tensorflow.serving.PredictionService/Predict";
+    c->body = std::string(5, '\0') + "pzz";
+    c->off = 5;
+    c->arrival = Clock::now();
+    a.dispatch(std::move(c));
+  }
+  std::this_thread::sleep_for(std::chrono::milliseconds(300));
+  stop = true;
+  for (auto& t : th) t.join();
+  ra->stop();
+  a.set_router(nullptr);
+  b.set_router(nullptr);
+  ra.reset();
+  rb.reset();
+  const std::string dir = "/dev/shm/tfs_" + group + "_dir";
+  std::remove(dir.c_str());
+  CHECK(answered.load() > 0);
+}
+
 int main() {
   fuzz_codec();
   fuzz_sstable();
   stress_batcher();
+  stress_router();
   if (failures) {
     std::fprintf(stderr, "%d check(s) failed\n", failures);
     return 1;

@@ -239,3 +239,25 @@ def test_roctx_ranges_noop_and_enabled(tmp_path):
     env["TFSERVE_ROCTX"] = "1"
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
     assert out.stdout.strip() in ("True", "False")      # False only where the library is absent
+
+
+def test_sticky_failure_exits_only_when_supervised(mgr, monkeypatch):
+    """A hung lane / poisoned HIP context cannot be reloaded in-process: a
+    supervised replica exits (the supervisor restarts it); unsupervised it
+    falls back to a reload."""
+    import rust_tensorflow_serving2_amd.server.health as H
+    exits = []
+    monkeypatch.setattr(H.os, "_exit", lambda code: exits.append(code))
+    h = HealthMonitor(mgr, threshold=2, max_recoveries=3)
+    monkeypatch.delenv("TFSERVE_SUPERVISED", raising=False)
+    for _ in range(2):
+        h.record("a", 1, False, "GPU batch timed out (device not responding)")
+    assert not exits and wait_for(lambda: mgr.loads.count(("a", 1)) == 2)
+    assert wait_for(lambda: mgr.status("a")[0].state == AVAILABLE)
+    monkeypatch.setenv("TFSERVE_SUPERVISED", "1")
+    for _ in range(2):
+        h.record("a", 1, False, "HIP error: an illegal memory access was encountered")
+    assert exits == [H.STICKY_EXIT]
+    exits.clear()
+    h.record("a", 1, False, "plain failure")        # not sticky: the normal path
+    assert not exits

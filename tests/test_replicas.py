@@ -114,3 +114,109 @@ def test_cli_two_replicas_shared_port_and_reload(hpt_path, tmp_path):
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, 9)
             proc.wait()
+
+
+def _stats(d):
+    import json
+    out = {}
+    for f in sorted(os.listdir(d)):
+        if f.endswith(".json"):
+            with open(os.path.join(d, f)) as fh:
+                s = json.load(fh)
+            out[(s["rank"], s["pid"])] = s
+    return out
+
+
+def test_four_replicas_one_connection_and_replica_restart(hpt_path, tmp_path):
+    """Four CPU replicas (gloo), ONE client connection (the reference client's
+    pattern): the front end that owns the connection routes Predicts to the
+    least-loaded replica over shared memory, so every replica serves >= 15%
+    of 400 calls.  Then `kill -9` of one replica: the others keep serving,
+    a config reload issued during the outage completes, the supervisor
+    restarts only the dead replica, which rejoins (applies the new config,
+    takes routed calls)."""
+    import json
+    import signal as sig
+    from rust_tensorflow_serving2_amd.client import TensorflowServing, TFServingError
+    from rust_tensorflow_serving2_amd.schema import serving
+    port = _free_port()
+    logf = str(tmp_path / "replicas.log")
+    stats_dir = str(tmp_path / "stats")
+    env = dict(os.environ, PYTHONPATH=ROOT, TFSERVE_STATS_DIR=stats_dir, TFSERVE_ROUTE_CELLS="16",
+               TFSERVE_ROUTE_MARGIN="2")
+    env.pop("WORLD_SIZE", None)
+    proc = subprocess.Popen([sys.executable, "-m", "rust_tensorflow_serving2_amd.server", f"--port={port}",
+                             "--model_name=a", f"--model_base_path={hpt_path}", "--num_gpus=4", "--device=cpu",
+                             "--host=127.0.0.1", "--file_system_poll_wait_seconds=0", "--log_level=WARNING",
+                             "--io_threads=1"],
+                            env=env, stdout=open(logf, "w"), stderr=subprocess.STDOUT, text=True,
+                            start_new_session=True)
+
+    def ready_count():
+        return open(logf).read().count("ready:")
+
+    async def burst(model, n, conc=32):
+        c = await TensorflowServing.new().hostname("127.0.0.1").port(port).build()   # one channel
+        x = {"x": np.array([[2.0]], np.float32)}
+        sem = asyncio.Semaphore(conc)
+
+        async def one():
+            async with sem:
+                return (await c.clone().predict_tensors(model, x))["y"].reshape(-1).tolist()
+        return await asyncio.gather(*[one() for _ in range(n)])
+
+    try:
+        deadline = time.time() + 240
+        while time.time() < deadline and proc.poll() is None and ready_count() < 4:
+            time.sleep(0.2)
+        assert ready_count() == 4, open(logf).read()[-3000:]
+        time.sleep(1.0)                                  # routers see their peers
+        out = asyncio.run(burst("a", 400))
+        assert all(v == [3.0] for v in out)
+        time.sleep(1.0)                                  # stats files refresh every 0.5 s
+        st = _stats(stats_dir)
+        served = {r: s["served"] for (r, _p), s in st.items()}
+        assert len(served) == 4 and sum(served.values()) >= 400, st
+        for r, n in served.items():
+            assert n >= 0.15 * 400, (served, st)
+
+        # ---- kill -9 one replica: the rest keep serving on fresh connections
+        victim = 2
+        vpid = next(p for (r, p) in st if r == victim)
+        os.kill(vpid, sig.SIGKILL)
+        time.sleep(0.5)
+        for _ in range(6):
+            assert asyncio.run(burst("a", 10, conc=4)) == [[3.0]] * 10
+
+        # ---- a reload during the outage completes (the dead replica is not waited for)
+        async def reload():
+            c = await TensorflowServing.new().hostname("127.0.0.1").port(port).build()
+            return await c.reload([serving.ModelConfig(name="b", base_path=hpt_path, model_platform="tensorflow")])
+        t0 = time.time()
+        resp = asyncio.run(reload())
+        assert resp.status.error_code == 0, resp.status.error_message
+        assert time.time() - t0 < 60
+
+        # ---- the supervisor restarted only the victim; it rejoins with the new config
+        deadline = time.time() + 240
+        while time.time() < deadline and ready_count() < 5:
+            time.sleep(0.2)
+        log_text = open(logf).read()
+        assert ready_count() == 5 and "replica 2 exited" in log_text, log_text[-3000:]
+        time.sleep(1.5)
+        out = asyncio.run(burst("b", 400))
+        assert all(v == [3.0] for v in out)
+        with pytest.raises(TFServingError):
+            asyncio.run(burst("a", 1, conc=1))
+        time.sleep(1.0)
+        st2 = _stats(stats_dir)
+        new = [s for (r, p), s in st2.items() if r == victim and p != vpid]
+        assert new and new[0]["restarts"] == 1 and new[0]["served"] > 0, st2
+        assert proc.poll() is None                       # the group is still up
+    finally:
+        os.killpg(proc.pid, 15)
+        try:
+            proc.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, 9)
+            proc.wait()
