@@ -67,8 +67,9 @@ def parse():
     ap.add_argument("--batch-timeout-us", type=int, default=2000)
     ap.add_argument("--distinct-requests", type=int, default=64, help="distinct pre-encoded request bodies")
     ap.add_argument("--lanes", type=int, default=4, help="GPU lanes (batch slots in flight) per rank")
-    ap.add_argument("--model", default="resnet50", choices=["resnet50", "tiny", "bert-base"],
-                    help="resnet50 = headline config; bert-base = BASELINE config 3 (seq 128); "
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "resnet50-v2", "tiny", "bert-base"],
+                    help="resnet50 = headline config (v1.5); resnet50-v2 = the pre-activation ResNet the reference "
+                         "serves (serving/fetch.sh:7); bert-base = BASELINE config 3 (seq 128); "
                          "tiny = same 224x224x3 payload, negligible compute (transport ceiling probe)")
     ap.add_argument("--seq-len", type=int, default=128)
     ap.add_argument("--c1-requests", type=int, default=200,
@@ -134,6 +135,8 @@ def main():
     if rank == 0 and not os.path.exists(os.path.join(base, "1", "saved_model.pb")):
         if args.model == "resnet50":
             resnet.export(os.path.join(base, "1"), seed=0, image_size=args.image_size)
+        elif args.model == "resnet50-v2":
+            resnet.export(os.path.join(base, "1"), version="v2", seed=0, image_size=args.image_size)
         elif args.model == "bert-base":
             from rust_tensorflow_serving2_amd.models import bert
             bert.export(os.path.join(base, "1"), bert.BertConfig(seq_len=args.seq_len), seed=0)
@@ -302,10 +305,11 @@ def main():
         value = total_ok / t_max
         metric = METRIC if args.model != "bert-base" else \
             f"Predict RPCs/sec + p50 latency, BERT-base seq={args.seq_len} dynamic batching on MI355X"
-        model_label = {"resnet50": "ResNet-50 v1.5", "tiny": "tiny-transport-probe",
+        model_label = {"resnet50": "ResNet-50 v1.5", "resnet50-v2": "ResNet-50 v2", "tiny": "tiny-transport-probe",
                        "bert-base": f"BERT-base seq {args.seq_len}"}[args.model]
         data = ("synthetic 224x224x3 f32 images (float_val, batch-1 PredictRequests as the Rust client sends), "
-                "random-init ResNet-50 v1.5 weights") if args.model != "bert-base" else \
+                f"random-init {'ResNet-50 v2' if args.model == 'resnet50-v2' else 'ResNet-50 v1.5'} weights") \
+            if args.model != "bert-base" else \
             "synthetic int32 token ids / masks, random-init BERT-base weights"
         out = {
             "metric": metric, "value": round(value, 1), "unit": "Predict RPCs/s", "n_gpus": world,

@@ -148,6 +148,20 @@ class FusedConv:
             self.w_ref = w_hwio.float().to(device)
             self.b_ref = bias.float().to(device)
 
+    # ---- post-activation output (ResNet v2 pre-activation of the next block)
+    post = None          # (scale [Cout], shift [Cout], act) on the device / CPU
+    post_mode = None     # "dual": [raw, post]; "only": [post]
+
+    def set_post(self, scale: torch.Tensor, shift: torch.Tensor, act: str, mode: str):
+        dev = self.device if self.use_hip else (self.w_ref.device if hasattr(self, "w_ref") else "cpu")
+        self.post = (scale.float().contiguous().to(dev), shift.float().contiguous().to(dev), act)
+        self.post_mode = mode
+
+    def post_ok(self) -> bool:
+        """The fused kernels write the post output only on the cgemm / halo
+        paths (64-aligned channels); the CPU reference always can."""
+        return not self.use_hip or (not self.c4 and self.cin % 64 == 0 and self.cout % 8 == 0)
+
     def pads_for(self, h, w):
         if self.padding == "SAME":
             return O.tf_same_pads(h, self.kh, self.sh) + O.tf_same_pads(w, self.kw, self.sw)
@@ -165,7 +179,7 @@ class FusedConv:
             y = y.permute(0, 2, 3, 1) + self.b_ref
             if res is not None:
                 y = y + res.float()
-            return [_ref_act(y, self.act).contiguous()]
+            return _with_post(self, _ref_act(y, self.act).contiguous())
         from ..ops import ACT, hip, tuned_config
         if self.c4:
             # fp32 RGB request -> zero-bordered bf16 RGBA sized for the padded
@@ -190,15 +204,18 @@ class FusedConv:
         M = n * ho * wo
         args = (x, self.w, self.b, res, kh, kw, self.sh, self.sw, pt, pb, pl, pr, ACT[self.act])
         out = torch.empty((n, ho, wo, self.cout), device=x.device, dtype=BF16)
-        key = ("conv", tuple(x.shape), x.dtype, self.cout, kh, kw, self.sh, res is not None, self.act)
+        key = ("conv", tuple(x.shape), x.dtype, self.cout, kh, kw, self.sh, res is not None, self.act, self.post_mode)
         K = kh * 32 if self.c4 else kh * kw * self.cin
         dma = not self.c4 and self.cin % 8 == 0      # bf16 dense/im2col operands -> DMA-ring configs apply
         # pipelined cgemm kernel applies (im2col / dense with C % 64, or the padded RGBA stem)
         aligned = (dma and self.cin % 64 == 0) or self.c4
         halo = aligned and not self.c4 and kh == 3 and kw == 3 and self.sh == 1 and self.sw == 1
-        cfg, splits = tuned_config(key, M, self.cout, lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s), K,
-                                   dma, aligned, halo=halo)
-        return [H.conv2d(*args, cfg=cfg, out=out, splits=splits)]
+        kw_post, outs = _post_kwargs(self, out)
+        run = lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s, **kw_post)  # noqa
+        cfg, splits = tuned_config(key, M, self.cout, run, K, dma, aligned, halo=halo,
+                                   cgemm_only=self.post is not None)
+        run(cfg, splits)
+        return outs
 
 
 class FusedDualConv:
@@ -214,6 +231,7 @@ class FusedDualConv:
         self.act = act
         self.use_hip = use_hip
         self.name = name
+        self.device = device
         if use_hip:
             w = torch.cat([conv_h.w[:, :self.c1], conv_x.w[:, :self.c2]], dim=1)   # [Cout][C1 + C2] bf16
             self.w = _pad_k(w.cpu(), 8).contiguous().to(device)
@@ -222,22 +240,32 @@ class FusedDualConv:
             self.w1, self.w2 = conv_h.w_ref, conv_x.w_ref
             self.b_ref = conv_h.b_ref + conv_x.b_ref
 
+    post = None
+    post_mode = None
+    set_post = FusedConv.set_post
+
+    def post_ok(self) -> bool:
+        return self.cout % 8 == 0
+
     def __call__(self, ctx, node, ins):
         h, x = O.to_torch(ins[0]), O.to_torch(ins[1])
         if not self.use_hip:
             y = h.float() @ self.w1.reshape(self.c1, self.cout)
             xs = x.float()[:, ::self.sh, ::self.sw, :]
             y = y + xs @ self.w2.reshape(self.c2, self.cout) + self.b_ref
-            return [_ref_act(y, self.act).contiguous()]
+            return _with_post(self, _ref_act(y, self.act).contiguous())
         from ..ops import ACT, hip, tuned_config
         H = hip()
         h, x = _to_bf16(h).contiguous(), _to_bf16(x).contiguous()
         n, ho, wo, _ = h.shape
         out = torch.empty((n, ho, wo, self.cout), device=h.device, dtype=BF16)
-        key = ("dual", tuple(h.shape), tuple(x.shape), self.cout, self.sh, self.act)
-        run = lambda c, s: H.conv2d_dual(h, x, self.w, self.b, self.sh, self.sw, ACT[self.act], c, out, s)  # noqa
+        key = ("dual", tuple(h.shape), tuple(x.shape), self.cout, self.sh, self.act, self.post_mode)
+        kw_post, outs = _post_kwargs(self, out)
+        run = lambda c, s: H.conv2d_dual(h, x, self.w, self.b, self.sh, self.sw, ACT[self.act], c, out, s,  # noqa
+                                         **kw_post)
         cfg, splits = tuned_config(key, n * ho * wo, self.cout, run, self.c1 + self.c2, True, True, cgemm_only=True)
-        return [run(cfg, splits)]
+        run(cfg, splits)
+        return outs
 
 
 class FusedMatMul:
@@ -294,6 +322,27 @@ class FusedMatMul:
         return [y[:, :self.n] if padded else y]
 
 
+def _with_post(impl, y: torch.Tensor) -> list:
+    """CPU reference of the post-activation output: [y] / [y, post] / [post]."""
+    if impl.post is None:
+        return [y]
+    scale, shift, act = impl.post
+    z = _ref_act(y * scale.to(y.device) + shift.to(y.device), act).contiguous()
+    return [y, z] if impl.post_mode == "dual" else [z]
+
+
+def _post_kwargs(impl, out: torch.Tensor):
+    """(kernel kwargs, op outputs) for the fused post-activation output."""
+    if impl.post is None:
+        return {}, [out]
+    from ..ops import ACT
+    scale, shift, act = impl.post
+    if impl.post_mode == "dual":
+        out2 = torch.empty_like(out)
+        return dict(post_scale=scale, post_shift=shift, post_act=ACT[act], out2=out2), [out, out2]
+    return dict(post_scale=scale, post_shift=shift, post_act=ACT[act], post_only=True), [out]
+
+
 def _ref_act(y, act):
     if act == "relu":
         return torch.relu(y)
@@ -336,6 +385,17 @@ class MaxPool:
         self.sh, self.sw = strides
         self.padding = padding
         self.use_hip = use_hip
+        self.post = None
+        self.post_mode = None
+
+    def set_post(self, scale, shift, act, mode, device=None):
+        # on the device up front: a host->device copy inside HIP-graph capture is illegal
+        dev = device if (self.use_hip and device is not None) else "cpu"
+        self.post = (scale.float().contiguous().to(dev), shift.float().contiguous().to(dev), act)
+        self.post_mode = mode
+
+    def post_ok(self) -> bool:
+        return True
 
     def __call__(self, ctx, node, ins):
         x = O.to_torch(ins[0])
@@ -344,11 +404,17 @@ class MaxPool:
             (pt, pb), (pl, pr) = O.tf_same_pads(h, self.kh, self.sh), O.tf_same_pads(w, self.kw, self.sw)
         else:
             pt = pb = pl = pr = 0
-        if self.use_hip and x.is_cuda and x.shape[-1] % 8 == 0:
-            from ..ops import hip
-            return [hip().maxpool(_to_bf16(x).contiguous(), self.kh, self.kw, self.sh, self.sw, pt, pb, pl, pr)]
+        if self.use_hip and x.is_cuda and x.shape[-1] % 8 == 0 and self.post_mode != "dual":
+            from ..ops import ACT, hip
+            kw = {}
+            if self.post is not None:    # folded BN (+ReLU) after the max, same kernel
+                sc, sh, act = self.post
+                kw = dict(post_scale=sc, post_shift=sh, post_act=ACT[act])
+            return [hip().maxpool(_to_bf16(x).contiguous(), self.kh, self.kw, self.sh, self.sw, pt, pb, pl, pr,
+                                  **kw)]
         xc = F.pad(x.permute(0, 3, 1, 2), [pl, pr, pt, pb], value=float("-inf"))
-        return [F.max_pool2d(xc, (self.kh, self.kw), (self.sh, self.sw)).permute(0, 2, 3, 1).contiguous()]
+        y = F.max_pool2d(xc, (self.kh, self.kw), (self.sh, self.sw)).permute(0, 2, 3, 1).contiguous()
+        return _with_post(self, y)
 
 
 class SoftmaxArgMax:
@@ -427,6 +493,18 @@ def fuse_conv(g, order, fed, fetch_refs, device, opts):
                 scale = gamma * torch.rsqrt(var + float(nxt.attr("epsilon", 1e-3)))
                 w = w * scale
                 bias = (bias - mean) * scale + beta
+                chain.append(nxt)
+                cur = nxt
+                nxt = c.only_consumer(cur.name)
+        # a constant per-channel / scalar scale (ResNet v2's residual scale):
+        # folded into the weights and bias
+        if nxt is not None and nxt.op == "Mul" and len(nxt.inputs) == 2 and (cur.name, 0) in nxt.inputs:
+            other = nxt.inputs[1] if nxt.inputs[0] == (cur.name, 0) else nxt.inputs[0]
+            sv = _const(g, other)
+            if sv is not None and sv.numel() in (1, cout) and other != (cur.name, 0):
+                sv = sv.float().reshape(-1)
+                w = w * sv
+                bias = bias * sv
                 chain.append(nxt)
                 cur = nxt
                 nxt = c.only_consumer(cur.name)
@@ -608,6 +686,73 @@ def fuse_dual_conv(g, order, fed, fetch_refs, device, opts):
         c.refresh()
 
 
+def _bn_affine(g: Graph, c: _Ctx, bn: Node):
+    """(scale, shift) of an inference FusedBatchNorm with constant params whose
+    only used output is y, else None."""
+    if bn.op not in ("FusedBatchNorm", "FusedBatchNormV2", "FusedBatchNormV3") or bn.attr("is_training", False) \
+            or bn.sattr("data_format", "NHWC") != "NHWC" or bn.name in c.fetch_nodes:
+        return None
+    params = [_const(g, r) for r in bn.inputs[1:5]]
+    if any(p is None for p in params) or {i for _c, _p, i in c.cons.get(bn.name, [])} - {0}:
+        return None
+    gamma, beta, mean, var = (p.float().reshape(-1) for p in params)
+    scale = gamma * torch.rsqrt(var + float(bn.attr("epsilon", 1e-3)))
+    return scale, beta - mean * scale
+
+
+def fuse_post_activation(g, order, fed, fetch_refs, device, opts):
+    """ResNet v2 pre-activation: ``P -> FusedBatchNorm -> [Relu]`` where P is a
+    fused conv / dual conv / max-pool becomes a second output of P written by
+    the same kernel's epilogue: P then yields ``[sum, relu(bn(sum))]`` when the
+    raw sum has other consumers (the next block's identity shortcut), or just
+    ``[relu(bn(sum))]`` when it does not (a projecting next block; the final
+    post-norm before the global pool).  SURVEY.md §2.7 K1's dual-output
+    epilogue; the model is the reference's ``resnet_v2_fp32_savedmodel_NHWC``
+    (``serving/fetch.sh:7``)."""
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    for name in order:
+        p = g.nodes.get(name)
+        if p is None or p.op not in ("_FusedConv2D", "_FusedDualConv", "_MaxPool"):
+            continue
+        impl = p.attrs["_impl"]
+        if impl.post is not None or not impl.post_ok() or name in c.fetch_nodes:
+            continue
+        cons = c.cons.get(name, [])
+        if any(i != 0 for _c, _p, i in cons):
+            continue
+        bns = [g.nodes[cn] for cn, _pos, _i in cons
+               if g.nodes[cn].op.startswith("FusedBatchNorm") and g.nodes[cn].inputs[0] == (name, 0)]
+        if len(bns) != 1:
+            continue
+        bn = bns[0]
+        aff = _bn_affine(g, c, bn)
+        if aff is None or aff[0].numel() != getattr(impl, "cout", aff[0].numel()):
+            continue
+        out_node, act = bn, "none"
+        relu = c.only_consumer(bn.name)
+        if relu is not None and relu.op == "Relu" and relu.name not in c.fetch_nodes:
+            out_node, act = relu, "relu"
+        elif bn.name in c.fetch_nodes:
+            continue
+        others = [cn for cn, _pos, _i in cons if cn != bn.name]
+        if isinstance(impl, MaxPool) and others:
+            continue                  # the pooling kernel writes one output
+        mode = "dual" if others else "only"
+        if isinstance(impl, MaxPool):
+            impl.set_post(aff[0], aff[1], act, mode, device=c.device)
+        else:
+            impl.set_post(aff[0], aff[1], act, mode)
+        new_ref = (name, 1 if mode == "dual" else 0)
+        for cn, pos, _i in c.cons.get(out_node.name, []):
+            g.nodes[cn].inputs[pos] = new_ref
+        p.ctrl = _merge_ctrl([p, bn] + ([out_node] if out_node is not bn else []))
+        del g.nodes[bn.name]
+        if out_node is not bn:
+            del g.nodes[out_node.name]
+        c.refresh()
+
+
 def default_passes(options=None):
     from .patterns import bert_passes
-    return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_dual_conv, fuse_matmul]
+    return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_dual_conv, fuse_post_activation,
+                                                                 fuse_matmul]

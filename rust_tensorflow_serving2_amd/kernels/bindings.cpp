@@ -76,13 +76,47 @@ void need(const Tensor& t, at::ScalarType st, const char* name) {
 bool aligned16(const Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; }
 
 const uint16_t* bf16p(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+
+// Post-activation output (ResNet v2): out2 = act2(y * scale + shift) per output
+// channel, written by the same GEMM epilogue.  post_only: `y` itself receives
+// the post-activated values (the raw sum is not stored).  cgemm / halo configs
+// (or split-K, whose reduce applies the epilogue) only.
+void set_post(tfsk::IGemmArgs& a, const c10::optional<Tensor>& scale, const c10::optional<Tensor>& shift,
+              int64_t act2, const c10::optional<Tensor>& out2, bool post_only, const Tensor& y, int64_t cfg,
+              int64_t splits, int cout) {
+  if (!scale.has_value()) {
+    TORCH_CHECK(!shift.has_value() && !out2.has_value() && !post_only, "post output needs post_scale");
+    return;
+  }
+  TORCH_CHECK(shift.has_value(), "post_scale needs post_shift");
+  need(*scale, at::kFloat, "post_scale");
+  need(*shift, at::kFloat, "post_shift");
+  TORCH_CHECK(scale->numel() == cout && shift->numel() == cout, "post scale / shift must have Cout entries");
+  TORCH_CHECK(aligned16(*scale) && aligned16(*shift), "post scale / shift must be 16-B aligned");
+  TORCH_CHECK(cfg >= tfsk::kCGemmCfgBase || splits > 1, "the post-activation output needs a cgemm / halo config");
+  a.scale2 = scale->data_ptr<float>();
+  a.shift2 = shift->data_ptr<float>();
+  a.act2 = int(act2);
+  if (post_only) {
+    TORCH_CHECK(!out2.has_value(), "post_only writes the post output to `out`");
+    a.out2 = y.data_ptr();
+    a.out = nullptr;
+  } else {
+    TORCH_CHECK(out2.has_value(), "dual output needs out2");
+    TORCH_CHECK(out2->scalar_type() == y.scalar_type() && out2->numel() == y.numel() && out2->is_contiguous(),
+                "out2 must match the output");
+    a.out2 = out2->data_ptr();
+  }
+}
 uint16_t* bf16p_mut(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 
 // x: NHWC bf16 (or fp32 when stem=true), w: [Cout][ldb] bf16, bias: [Cout] f32
 Tensor conv2d(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
               const c10::optional<Tensor>& residual, int64_t KH, int64_t KW, int64_t SH, int64_t SW,
               int64_t PT, int64_t PB, int64_t PL, int64_t PR, int64_t act, int64_t cfg,
-              const c10::optional<Tensor>& out, bool out_f32, int64_t splits) {
+              const c10::optional<Tensor>& out, bool out_f32, int64_t splits,
+              const c10::optional<Tensor>& post_scale, const c10::optional<Tensor>& post_shift, int64_t post_act,
+              const c10::optional<Tensor>& out2, bool post_only) {
   const bool stem = x.scalar_type() == at::kFloat;
   need(x, stem ? at::kFloat : at::kBFloat16, "x");
   need(w, at::kBFloat16, "w");
@@ -130,6 +164,7 @@ Tensor conv2d(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
     a.ldr = Cout;
   }
   a.act = act; a.out = y.data_ptr(); a.ldc = Cout; a.out_f32 = out_f32; a.alpha = 1.f;
+  set_post(a, post_scale, post_shift, post_act, out2, post_only, y, cfg, splits, Cout);
   run_igemm(a, a_mode, cfg, splits, x, cur_stream(x));
   return y;
 }
@@ -139,7 +174,9 @@ Tensor conv2d(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
 // h: NHWC [N][Ho][Wo][C_h] bf16 (dense rows), x: NHWC [N][H][W][C_x] bf16
 // sampled at (ho*SH, wo*SW).  cgemm configs only (C_h, C_x % 64 == 0).
 Tensor conv2d_dual(const Tensor& h, const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
-                   int64_t SH, int64_t SW, int64_t act, int64_t cfg, const c10::optional<Tensor>& out, int64_t splits) {
+                   int64_t SH, int64_t SW, int64_t act, int64_t cfg, const c10::optional<Tensor>& out, int64_t splits,
+                   const c10::optional<Tensor>& post_scale, const c10::optional<Tensor>& post_shift,
+                   int64_t post_act, const c10::optional<Tensor>& out2, bool post_only) {
   need(h, at::kBFloat16, "h");
   need(x, at::kBFloat16, "x");
   need(w, at::kBFloat16, "w");
@@ -169,6 +206,7 @@ Tensor conv2d_dual(const Tensor& h, const Tensor& x, const Tensor& w, const c10:
     a.bias = bias->data_ptr<float>();
   }
   a.act = act; a.out = y.data_ptr(); a.ldc = Cout; a.out_f32 = 0; a.alpha = 1.f;
+  set_post(a, post_scale, post_shift, post_act, out2, post_only, y, cfg, splits, Cout);
   run_igemm(a, tfsk::kADual, cfg, splits, h, cur_stream(h));
   return y;
 }
@@ -212,7 +250,8 @@ Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
 }
 
 Tensor maxpool(const Tensor& x, int64_t KH, int64_t KW, int64_t SH, int64_t SW, int64_t PT, int64_t PB,
-               int64_t PL, int64_t PR, const c10::optional<Tensor>& out) {
+               int64_t PL, int64_t PR, const c10::optional<Tensor>& out, const c10::optional<Tensor>& post_scale,
+               const c10::optional<Tensor>& post_shift, int64_t post_act) {
   need(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "maxpool: NHWC with C % 8 == 0");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -221,8 +260,18 @@ Tensor maxpool(const Tensor& x, int64_t KH, int64_t KW, int64_t SH, int64_t SW, 
   Tensor y = out.has_value() ? *out : torch::empty({N, Ho, Wo, C}, x.options());
   need(y, at::kBFloat16, "out");
   TORCH_CHECK(y.numel() == int64_t(N) * Ho * Wo * C, "out has the wrong size");
+  const float* sc = nullptr;
+  const float* sh = nullptr;
+  if (post_scale.has_value()) {
+    TORCH_CHECK(post_shift.has_value(), "post_scale needs post_shift");
+    need(*post_scale, at::kFloat, "post_scale");
+    need(*post_shift, at::kFloat, "post_shift");
+    TORCH_CHECK(post_scale->numel() == C && post_shift->numel() == C, "post scale / shift must have C entries");
+    sc = post_scale->data_ptr<float>();
+    sh = post_shift->data_ptr<float>();
+  }
   check(tfsk::maxpool_nhwc_launch(bf16p(x), bf16p_mut(y), N, H, W, C, KH, KW, SH, SW, PT, PL, Ho, Wo,
-                                  cur_stream(x)), "maxpool");
+                                  cur_stream(x), sc, sh, int(post_act)), "maxpool");
   return y;
 }
 
@@ -427,15 +476,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d", &conv2d, "NHWC implicit-GEMM conv (+bias +residual +act)", py::arg("x"), py::arg("w"),
         py::arg("bias"), py::arg("residual"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
         py::arg("pt"), py::arg("pb"), py::arg("pl"), py::arg("pr"), py::arg("act") = 0, py::arg("cfg") = 0,
-        py::arg("out") = py::none(), py::arg("out_f32") = false, py::arg("splits") = 1);
+        py::arg("out") = py::none(), py::arg("out_f32") = false, py::arg("splits") = 1,
+        py::arg("post_scale") = py::none(), py::arg("post_shift") = py::none(), py::arg("post_act") = 0,
+        py::arg("out2") = py::none(), py::arg("post_only") = false);
   m.def("conv2d_dual", &conv2d_dual, "act(conv1x1(h) + conv1x1_stride(x) + bias) as one K-concatenated GEMM",
         py::arg("h"), py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"), py::arg("sw"), py::arg("act") = 0,
-        py::arg("cfg") = 36, py::arg("out") = py::none(), py::arg("splits") = 1);
+        py::arg("cfg") = 36, py::arg("out") = py::none(), py::arg("splits") = 1,
+        py::arg("post_scale") = py::none(), py::arg("post_shift") = py::none(), py::arg("post_act") = 0,
+        py::arg("out2") = py::none(), py::arg("post_only") = false);
   m.def("linear", &linear,"x @ w^T (+bias +residual +act)", py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("residual") = py::none(), py::arg("act") = 0, py::arg("cfg") = 0, py::arg("out_f32") = false,
         py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("splits") = 1);
   m.def("maxpool", &maxpool, py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
-        py::arg("pt"), py::arg("pb"), py::arg("pl"), py::arg("pr"), py::arg("out") = py::none());
+        py::arg("pt"), py::arg("pb"), py::arg("pl"), py::arg("pr"), py::arg("out") = py::none(),
+        py::arg("post_scale") = py::none(), py::arg("post_shift") = py::none(), py::arg("post_act") = 0);
   m.def("global_avgpool", &global_avgpool, py::arg("x"), py::arg("out") = py::none());
   m.def("softmax_argmax", &softmax_argmax, py::arg("logits"), py::arg("want_probs") = true,
         py::arg("want_classes") = true, py::arg("probs_out") = py::none(), py::arg("classes_out") = py::none());

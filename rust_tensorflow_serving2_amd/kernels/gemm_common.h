@@ -96,8 +96,43 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return uint32_t(__builtin_bit_cast(uint16_t, lo)) | (uint32_t(__builtin_bit_cast(uint16_t, hi)) << 16);
 }
 
+// 8 values -> one 16-B bf16 (or 2 x 16-B f32) store at row m, column n of `out`
+// (nullptr: nothing stored).
+__device__ __forceinline__ void store_chunk(const IGemmArgs& p, void* out, int m, int n, const float (&v)[8]) {
+  if (!out) return;
+  if (p.out_f32) {
+    float* o = static_cast<float*>(out) + size_t(m) * p.ldc + n;
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(out) + size_t(m) * p.ldc + n) =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                   pack_bf16x2(v[6], v[7]));
+  }
+}
+
+// The post-activation output: out2 = act2(v * scale2 + shift2) (per channel;
+// scale2 / shift2 are L2-resident and read per chunk rather than prefetched,
+// so kernels without a second output pay no registers for it).
+__device__ __forceinline__ void post_chunk(const IGemmArgs& p, int m, int n, const float (&v)[8]) {
+  const float4 s0 = *reinterpret_cast<const float4*>(p.scale2 + n);
+  const float4 s1 = *reinterpret_cast<const float4*>(p.scale2 + n + 4);
+  const float4 t0 = *reinterpret_cast<const float4*>(p.shift2 + n);
+  const float4 t1 = *reinterpret_cast<const float4*>(p.shift2 + n + 4);
+  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float sh[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+  float w[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = v[e] * sc[e] + sh[e];
+    w[e] = p.act2 == kActRelu ? fmaxf(x, 0.f) : x;
+  }
+  store_chunk(p, p.out2, m, n, w);
+}
+
 // One 8-column chunk: alpha * acc + bias (+ residual) -> act -> 16-B bf16 (or
-// 2 x 16-B f32) store.  The launchers guarantee N, ldc, ldr % 8 == 0.
+// 2 x 16-B f32) store (+ the post-activation output).  The launchers
+// guarantee N, ldc, ldr % 8 == 0.
 template <int ACT>
 __device__ __forceinline__ void epi_chunk(const IGemmArgs& p, const float* src, int m, int n, const float (&bv)[8],
                                           const uint4 rr) {
@@ -111,15 +146,8 @@ __device__ __forceinline__ void epi_chunk(const IGemmArgs& p, const float* src, 
     v[2 * e] = act_fn<ACT>(v[2 * e] * alpha + bv[2 * e] + __uint_as_float(w[e] << 16));
     v[2 * e + 1] = act_fn<ACT>(v[2 * e + 1] * alpha + bv[2 * e + 1] + __uint_as_float(w[e] & 0xffff0000u));
   }
-  if (p.out_f32) {
-    float* o = static_cast<float*>(p.out) + size_t(m) * p.ldc + n;
-    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-    *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
-  } else {
-    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.out) + size_t(m) * p.ldc + n) =
-        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                   pack_bf16x2(v[6], v[7]));
-  }
+  store_chunk(p, p.out, m, n, v);
+  if (p.out2) post_chunk(p, m, n, v);
 }
 
 }  // namespace gemm

@@ -621,8 +621,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(IGemmArgs p) {
       if (p.bias) x += p.bias[n + e];
       if (p.residual) x += bf16_to_f32(p.residual[size_t(m) * p.ldr + n + e]);
       x = apply_act(x, p.act);
-      if (p.out_f32) static_cast<float*>(p.out)[size_t(m) * p.ldc + n + e] = x;
-      else static_cast<uint16_t*>(p.out)[size_t(m) * p.ldc + n + e] = f32_to_bf16(x);
+      if (p.out) {
+        if (p.out_f32) static_cast<float*>(p.out)[size_t(m) * p.ldc + n + e] = x;
+        else static_cast<uint16_t*>(p.out)[size_t(m) * p.ldc + n + e] = f32_to_bf16(x);
+      }
+      if (p.out2) {   // post-activation output (ResNet v2 pre-activation of the next block)
+        float y = x * p.scale2[n + e] + p.shift2[n + e];
+        if (p.act2 == kActRelu) y = fmaxf(y, 0.f);
+        if (p.out_f32) static_cast<float*>(p.out2)[size_t(m) * p.ldc + n + e] = y;
+        else static_cast<uint16_t*>(p.out2)[size_t(m) * p.ldc + n + e] = f32_to_bf16(y);
+      }
     }
   }
 }

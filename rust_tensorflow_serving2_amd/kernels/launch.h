@@ -44,6 +44,14 @@ struct IGemmArgs {
   int K1;
   // halo conv (halo.hip): output pixel block per workgroup (set by the launcher)
   int TH, TW;
+  // post-activation output (cgemm / halo / split-K reduce): out2 = act2(v *
+  // scale2 + shift2) per output channel, v = the epilogue value stored to
+  // `out` — a ResNet v2 block's sum and the next block's pre-activation
+  // relu(bn(sum)) from ONE kernel.  out == nullptr: only out2 is written.
+  void* out2;
+  const float* scale2;
+  const float* shift2;
+  int act2;
 };
 
 // kAStem7x7x3: fp32 NHWC input with C == 3 and a 7-wide filter (the ResNet
@@ -74,10 +82,13 @@ int igemm_config_stages(int cfg);
 int igemm_config_bk(int cfg);
 hipError_t igemm_launch(const IGemmArgs& args, int a_mode, int cfg, hipStream_t stream);
 
-// NHWC bf16 max-pool (TF SAME/VALID padding given explicitly).
+// NHWC bf16 max-pool (TF SAME/VALID padding given explicitly).  With `scale`
+// (and `shift`): y = act(max * scale[c] + shift[c]) — a folded inference
+// BatchNorm (+ ReLU when act == 1) applied after the pooling.
 hipError_t maxpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int H, int W, int C,
                                int KH, int KW, int SH, int SW, int PT, int PL, int Ho, int Wo,
-                               hipStream_t stream);
+                               hipStream_t stream, const float* scale = nullptr, const float* shift = nullptr,
+                               int act = 0);
 // Mean over H,W of NHWC bf16 -> [N][C] (bf16).
 hipError_t global_avgpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int HW, int C,
                                       hipStream_t stream);

@@ -33,13 +33,22 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 __global__ __launch_bounds__(256) void maxpool_nhwc_kernel(const uint16_t* __restrict__ x,
                                                            uint16_t* __restrict__ y, int N, int H, int W,
                                                            int C, int KH, int KW, int SH, int SW, int PT,
-                                                           int PL, int Ho, int Wo) {
+                                                           int PL, int Ho, int Wo,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, int act) {
   const int C8 = C / 8;
   const int row_items = Wo * C8;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= row_items) return;
   const int wo = j / C8;
   const int c8 = j - wo * C8;
+  // optional folded BN (+ReLU) after the max: this thread's 8 channels are fixed
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = scale ? scale[c8 * 8 + e] : 1.f;
+    sh[e] = scale ? shift[c8 * 8 + e] : 0.f;
+  }
   for (int r = blockIdx.y; r < N * Ho; r += gridDim.y) {
     const int n = r / Ho;
     const int ho = r - n * Ho;
@@ -57,6 +66,13 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_kernel(const uint16_t* __res
         unpack8(*reinterpret_cast<const uint4*>(xrow + long(wi) * C), f);
 #pragma unroll
         for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
+      }
+    }
+    if (scale) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        m[e] = m[e] * sc[e] + sh[e];
+        if (act == kActRelu) m[e] = fmaxf(m[e], 0.f);
       }
     }
     *reinterpret_cast<uint4*>(y + (long(r) * Wo * C8 + j) * 8) = pack8(m);
@@ -424,14 +440,17 @@ int grid_for(long work, int block) {
 }  // namespace
 
 hipError_t maxpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int KH, int KW,
-                               int SH, int SW, int PT, int PL, int Ho, int Wo, hipStream_t s) {
+                               int SH, int SW, int PT, int PL, int Ho, int Wo, hipStream_t s, const float* scale,
+                               const float* shift, int act) {
+  if ((scale == nullptr) != (shift == nullptr)) return hipErrorInvalidValue;
   if (C % 8 || N <= 0 || Ho <= 0 || Wo <= 0) return N <= 0 || Ho <= 0 || Wo <= 0 ? hipSuccess : hipErrorInvalidValue;
   const long row_items = long(Wo) * (C / 8);
   if (row_items > (1L << 30)) return hipErrorInvalidValue;
   const long rows = long(N) * Ho;
   if (rows > (1L << 30)) return hipErrorInvalidValue;
   const dim3 grid(unsigned((row_items + 255) / 256), unsigned(rows < 65535 ? rows : 65535));
-  hipLaunchKernelGGL(maxpool_nhwc_kernel, grid, dim3(256), 0, s, x, y, N, H, W, C, KH, KW, SH, SW, PT, PL, Ho, Wo);
+  hipLaunchKernelGGL(maxpool_nhwc_kernel, grid, dim3(256), 0, s, x, y, N, H, W, C, KH, KW, SH, SW, PT, PL, Ho, Wo,
+                     scale, shift, act);
   return hipGetLastError();
 }
 

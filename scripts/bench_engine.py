@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[1, 32])
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--baseline", action="store_true")
-    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert-base"])
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "resnet50-v2", "bert-base"])
     ap.add_argument("--graph-tune", type=int, default=1, help="whole-graph tile re-tuning at capture (0 = off)")
     args = ap.parse_args()
     import logging
@@ -34,7 +34,7 @@ def main():
         r = s.runner("serving_default", ["input_ids", "input_mask", "segment_ids"], ["pooled_output", "probabilities"])
         flop_per_item = 2 * 85e6 * 128 + 4 * 12 * 128 * 128 * 768   # encoder GEMMs + attention, seq 128
     else:
-        resnet.export(path)
+        resnet.export(path, version="v2" if args.model == "resnet50-v2" else "v1.5")
         s = Servable("resnet", 1, path, opts)
         r = s.runner("serving_default", ["input"], ["classes", "probabilities"])
         flop_per_item = 2 * 4.1e9

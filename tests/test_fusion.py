@@ -35,6 +35,32 @@ def test_resnet_fusion_exact(tiny_resnet_path):
     assert hist["_SoftmaxArgMax"] == 1 and hist["_GlobalAvgPool"] == 1 and hist["_MaxPool"] == 1
 
 
+@pytest.fixture(scope="module")
+def tiny_resnet_v2_path(models_dir):
+    from rust_tensorflow_serving2_amd.models import resnet
+    base = os.path.join(str(models_dir), "tiny_resnet_v2")
+    resnet.export(os.path.join(base, "1"), version="v2", blocks=(2, 2, 1, 1), width=8, num_classes=11,
+                  image_size=32, seed=4)
+    return base
+
+
+def test_resnet_v2_preactivation_fully_fused(tiny_resnet_v2_path):
+    """ResNet v2 (the reference's model, serving/fetch.sh:7): every
+    pre-activation BN + ReLU rides on the producing conv / dual conv / pool as
+    its post-activation output, the residual scale folds into conv3's weights:
+    no FusedBatchNorm, Relu or Mul node is left."""
+    ref, fused = _pair(os.path.join(tiny_resnet_v2_path, "1"))
+    x = np.random.default_rng(1).random((3, 32, 32, 3), dtype=np.float32)
+    a = ref.run("serving_default", {"input": x}, ["classes", "probabilities"])
+    b = fused.run("serving_default", {"input": x}, ["classes", "probabilities"])
+    np.testing.assert_allclose(a["probabilities"], b["probabilities"], atol=1e-5)
+    np.testing.assert_array_equal(a["classes"], b["classes"])
+    hist = fused.runner("serving_default", ["input"], ["classes", "probabilities"]).program.op_histogram()
+    for op in ("FusedBatchNormV3", "Relu", "Mul", "Conv2D", "AddV2"):
+        assert op not in hist, hist
+    assert hist["_MaxPool"] == 1 and hist["_GlobalAvgPool"] == 1 and hist["_SoftmaxArgMax"] == 1
+
+
 def test_bert_fusion_exact(tiny_bert):
     ref, fused = _pair(tiny_bert)
     rng = np.random.default_rng(0)

@@ -456,3 +456,77 @@ def test_attention_matches_fp32(s):
     att2 = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(d) + full, -1)
     ref2 = (att2 @ v).permute(0, 2, 1, 3).reshape(b, s, h * d)
     assert (y2.float().cpu() - ref2).abs().max() < 3e-2
+
+
+@pytest.mark.parametrize("cfg,splits,shape", [
+    (42, 1, (2, 14, 14, 256, 256, 1, 1, (0, 0, 0, 0))),
+    (36, 3, (2, 14, 14, 256, 256, 1, 1, (0, 0, 0, 0))),     # split-K: the reduce kernel writes both
+    (44, 1, (2, 28, 28, 128, 128, 3, 2, (1, 1, 1, 1))),     # im2col, strided
+    (48, 1, (2, 28, 28, 128, 128, 3, 1, (1, 1, 1, 1))),     # halo 3x3
+    (51, 2, (1, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1))),       # halo, split over channel chunks
+])
+def test_conv_post_activation_outputs(cfg, splits, shape):
+    """ResNet v2 epilogue: one conv writes the block sum y (+bias +residual)
+    AND relu(y * s + t) (the next block's pre-activation), or only the latter."""
+    n, h, w, cin, cout, k, s, pads = shape
+    x = rnd(n, h, w, cin, seed=31).to(BF)
+    wt = rnd(k, k, cin, cout, scale=1 / math.sqrt(k * k * cin), seed=32).to(BF).float()
+    b = rnd(cout, scale=0.1, seed=33)
+    ho = (h + pads[0] + pads[1] - k) // s + 1
+    wo = (w + pads[2] + pads[3] - k) // s + 1
+    res = rnd(n, ho, wo, cout, seed=34).to(BF)
+    sc, sh = rnd(cout, seed=35) * 0.5 + 1.0, rnd(cout, seed=36) * 0.2
+    ref = ref_conv(x, wt, b, s, pads, res, "none")
+    ref2 = torch.relu(ref * sc + sh)
+    out2 = torch.empty(n, ho, wo, cout, device=DEV, dtype=BF)
+    y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), k, k, s, s, *pads, act=0, cfg=cfg, splits=splits,
+                     post_scale=sc.to(DEV), post_shift=sh.to(DEV), post_act=ACT["relu"], out2=out2)
+    torch.cuda.synchronize()
+    tol = 3e-2 * max(1.0, ref.abs().max().item())
+    assert (y.float().cpu() - ref).abs().max().item() < tol
+    assert (out2.float().cpu() - ref2).abs().max().item() < tol
+    only = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), k, k, s, s, *pads, act=0, cfg=cfg,
+                        splits=splits, post_scale=sc.to(DEV), post_shift=sh.to(DEV), post_act=ACT["relu"],
+                        post_only=True)
+    torch.cuda.synchronize()
+    assert (only.float().cpu() - ref2).abs().max().item() < tol
+
+
+def test_conv_post_rejects_igemm():
+    x = torch.zeros(1, 8, 8, 64, device=DEV, dtype=BF)
+    w = torch.zeros(64, 64, device=DEV, dtype=BF)
+    sc = torch.ones(64, device=DEV)
+    with pytest.raises(RuntimeError, match="post-activation output needs"):
+        hip().conv2d(x, w, None, None, 1, 1, 1, 1, 0, 0, 0, 0, act=0, cfg=3, post_scale=sc, post_shift=sc,
+                     post_only=True)
+
+
+def test_conv2d_dual_post_output():
+    n, ho, c1, hh, c2, s, cout = 2, 14, 256, 28, 512, 2, 1024
+    h = rnd(n, ho, ho, c1, seed=41).to(BF)
+    x = rnd(n, hh, hh, c2, seed=42).to(BF)
+    w1 = rnd(cout, c1, scale=1 / math.sqrt(c1), seed=43).to(BF)
+    w2 = rnd(cout, c2, scale=1 / math.sqrt(c2), seed=44).to(BF)
+    b = rnd(cout, scale=0.1, seed=45)
+    sc, sh = rnd(cout, seed=46) * 0.5 + 1.0, rnd(cout, seed=47) * 0.2
+    ref = h.float() @ w1.float().t() + x.float()[:, ::s, ::s, :] @ w2.float().t() + b
+    w = torch.cat([w1, w2], 1).contiguous().to(DEV)
+    out2 = torch.empty(n, ho, ho, cout, device=DEV, dtype=BF)
+    y = hip().conv2d_dual(h.to(DEV), x.to(DEV), w, b.to(DEV), s, s, 0, 43, None, 1, post_scale=sc.to(DEV),
+                          post_shift=sh.to(DEV), post_act=ACT["relu"], out2=out2)
+    torch.cuda.synchronize()
+    tol = 3e-2 * max(1.0, ref.abs().max().item())
+    assert (y.float().cpu() - ref).abs().max().item() < tol
+    assert (out2.float().cpu() - torch.relu(ref * sc + sh)).abs().max().item() < tol
+
+
+def test_maxpool_post_affine():
+    x = rnd(2, 112, 112, 64, seed=51).to(BF)
+    sc, sh = rnd(64, seed=52) * 0.5, rnd(64, seed=53) * 0.2     # negative scales included
+    y = hip().maxpool(x.to(DEV), 3, 3, 2, 2, 0, 1, 0, 1, post_scale=sc.to(DEV), post_shift=sh.to(DEV),
+                      post_act=ACT["relu"])
+    xp = F.pad(x.float().permute(0, 3, 1, 2), [0, 1, 0, 1], value=float("-inf"))
+    ref = F.max_pool2d(xp, 3, 2).permute(0, 2, 3, 1)
+    ref = torch.relu(ref * sc + sh)
+    torch.cuda.synchronize()
+    assert (y.float().cpu() - ref).abs().max().item() < 2e-2
