@@ -149,8 +149,9 @@ def main():
     weight_source = None
     if world > 1:
         from rust_tensorflow_serving2_amd.parallel.weights import ReplicatedWeightSource
-        weight_source = ReplicatedWeightSource(dist.distributed_c10d._get_default_store(),
-                                               device=device if backend == "nccl" else torch.device("cpu"))
+        # the leader compiles + tunes once; the other ranks bind its packed bf16
+        # device weights (RCCL broadcast; the gloo rehearsal stages via the host)
+        weight_source = ReplicatedWeightSource(dist.distributed_c10d._get_default_store(), device=device)
     sopts = ServableOptions(device=str(device), max_batch_size=args.batch, lanes=args.lanes,
                             allowed_batch_sizes=tuple(sorted({1, 2, 4, 8, 16, args.batch})))
     port = (args.port + local) if args.port else 0

@@ -23,6 +23,7 @@ import torch
 
 from ..utils import tensors as T
 from . import ops as O
+from .placement import to_device
 from .ir import Graph, Node, fmt_ref, parse_ref
 
 NON_FOLDABLE = {"Placeholder", "PlaceholderWithDefault", "ParseExample", "ParseExampleV2", "NoOp",
@@ -54,6 +55,8 @@ def const_value(node: Node):
 
 
 def array_to_value(a: np.ndarray, dt: int):
+    if isinstance(a, torch.Tensor):      # a meta (shape-only) weight: parallel/weights.py followers
+        return a
     if dt == T.DT_BFLOAT16:
         return torch.from_numpy(np.array(a, dtype=np.uint16).view(np.int16)).view(torch.bfloat16)
     if dt == T.DT_STRING:
@@ -185,9 +188,12 @@ def cse(graph: Graph, order: Sequence[str], fed_nodes: Set[str], fetch_refs) -> 
         if name in fetch_nodes or name in fed_nodes or n.ctrl:
             continue
         key = None
-        if n.op == "Const":
+        if n.op == "Const" and not n.attrs.get("_variable"):
+            # (model variables are never merged: a replica compiling on shape-only
+            # weights must build the same program as the one holding the values)
             v = n.value[0] if n.value else const_value(n)
-            if isinstance(v, torch.Tensor) and v.numel() <= 64 and (not n.value or len(n.value) == 1):
+            if isinstance(v, torch.Tensor) and not v.is_meta and v.numel() <= 64 and \
+                    (not n.value or len(n.value) == 1):
                 key = ("Const", str(v.dtype), tuple(v.shape), v.detach().cpu().numpy().tobytes())
         elif n.op in _CSE_OPS:
             ak = _attrs_key(n.attrs)
@@ -262,7 +268,7 @@ def compile_program(graph: Graph, feeds: Sequence[str], fetches: Sequence[str],
             for i in needed.get(name, ()):
                 v = node.value[i]
                 if isinstance(v, torch.Tensor) and device.type != "cpu" and _device_resident(v):
-                    v = v.to(device)
+                    v = to_device(v, device)
                     node.value[i] = v
                 const_slots.append((slot((name, i)), v))
             continue

@@ -32,6 +32,7 @@ import torch.nn.functional as F
 from ..utils import tensors as T
 from . import ops as O
 from .ir import Graph, Node
+from .placement import to_device, zeros
 
 BF16 = torch.bfloat16
 
@@ -100,7 +101,7 @@ def _pad_k(w_nk: torch.Tensor, mult: int = 64) -> torch.Tensor:
     n, k = w_nk.shape
     kp = -(-k // mult) * mult
     if kp != k:
-        w_nk = torch.cat([w_nk, torch.zeros(n, kp - k, dtype=w_nk.dtype)], dim=1)
+        w_nk = torch.cat([w_nk, torch.zeros(n, kp - k, dtype=w_nk.dtype, device=w_nk.device)], dim=1)
     return w_nk
 
 
@@ -136,17 +137,17 @@ class FusedConv:
         self.khp = self.kh + (self.kh % 2) if self.c4 else self.kh
         if use_hip:
             if self.c4:
-                w4 = torch.zeros(self.khp, 8, 4, self.cout)
+                w4 = torch.zeros(self.khp, 8, 4, self.cout, device=w_hwio.device)
                 w4[:self.kh, :self.kw, :self.cin, :] = w_hwio.float()
                 w_nk = w4.permute(3, 0, 1, 2).reshape(self.cout, self.khp * 32)
             else:
                 k = self.kh * self.kw * self.cin
                 w_nk = w_hwio.permute(3, 0, 1, 2).reshape(self.cout, k)
-            self.w = _pad_k(w_nk).to(BF16).contiguous().to(device)
-            self.b = bias.float().contiguous().to(device)
+            self.w = to_device(_pad_k(w_nk).to(BF16), device)
+            self.b = to_device(bias.float(), device)
         else:
-            self.w_ref = w_hwio.float().to(device)
-            self.b_ref = bias.float().to(device)
+            self.w_ref = to_device(w_hwio.float(), device)
+            self.b_ref = to_device(bias.float(), device)
 
     # ---- post-activation output (ResNet v2 pre-activation of the next block)
     post = None          # (scale [Cout], shift [Cout], act) on the device / CPU
@@ -154,7 +155,7 @@ class FusedConv:
 
     def set_post(self, scale: torch.Tensor, shift: torch.Tensor, act: str, mode: str):
         dev = self.device if self.use_hip else (self.w_ref.device if hasattr(self, "w_ref") else "cpu")
-        self.post = (scale.float().contiguous().to(dev), shift.float().contiguous().to(dev), act)
+        self.post = (to_device(scale.float(), dev), to_device(shift.float(), dev), act)
         self.post_mode = mode
 
     def post_ok(self) -> bool:
@@ -233,8 +234,9 @@ class FusedDualConv:
         self.name = name
         self.device = device
         if use_hip:
-            w = torch.cat([conv_h.w[:, :self.c1], conv_x.w[:, :self.c2]], dim=1)   # [Cout][C1 + C2] bf16
-            self.w = _pad_k(w.cpu(), 8).contiguous().to(device)
+            # [Cout][C1 + C2] bf16, concatenated on the device (no host round trip)
+            w = torch.cat([conv_h.w[:, :self.c1], conv_x.w[:, :self.c2]], dim=1)
+            self.w = to_device(_pad_k(w, 8), device)
             self.b = (conv_h.b + conv_x.b).contiguous()
         else:
             self.w1, self.w2 = conv_h.w_ref, conv_x.w_ref
@@ -282,18 +284,18 @@ class FusedMatMul:
         self.out_f32 = out_f32
         self.use_hip = use_hip and self.k % 8 == 0
         self.name = name
-        b = bias if bias is not None else torch.zeros(self.n)
+        b = bias if bias is not None else zeros(self.n, w_kn)
         self.np = -(-self.n // 8) * 8 if (pad_n and self.n % 8 and self.k % 64 == 0) else self.n
         if self.use_hip:
             w_nk = w_kn.t().contiguous()
             if self.np != self.n:
-                w_nk = torch.cat([w_nk, torch.zeros(self.np - self.n, self.k, dtype=w_nk.dtype)])
-                b = torch.cat([b.float().reshape(-1), torch.zeros(self.np - self.n)])
-            self.w = _pad_k(w_nk, 8).to(BF16).contiguous().to(device)
-            self.b = b.float().contiguous().to(device)
+                w_nk = torch.cat([w_nk, torch.zeros(self.np - self.n, self.k, dtype=w_nk.dtype, device=w_nk.device)])
+                b = torch.cat([b.float().reshape(-1), zeros(self.np - self.n, b)])
+            self.w = to_device(_pad_k(w_nk, 8).to(BF16), device)
+            self.b = to_device(b.float(), device)
         else:
-            self.w_ref = w_kn.float().to(device)
-            self.b_ref = b.float().to(device)
+            self.w_ref = to_device(w_kn.float(), device)
+            self.b_ref = to_device(b.float(), device)
 
     def __call__(self, ctx, node, ins):
         x = O.to_torch(ins[0])
@@ -391,7 +393,7 @@ class MaxPool:
     def set_post(self, scale, shift, act, mode, device=None):
         # on the device up front: a host->device copy inside HIP-graph capture is illegal
         dev = device if (self.use_hip and device is not None) else "cpu"
-        self.post = (scale.float().contiguous().to(dev), shift.float().contiguous().to(dev), act)
+        self.post = (to_device(scale.float(), dev), to_device(shift.float(), dev), act)
         self.post_mode = mode
 
     def post_ok(self) -> bool:
@@ -470,7 +472,7 @@ def fuse_conv(g, order, fed, fetch_refs, device, opts):
         strides = n.attr("strides", [1, 1, 1, 1])
         w = w.float()
         cout = w.shape[3]
-        bias = torch.zeros(cout)
+        bias = zeros(cout, w)
         chain.append(n)
         cur = n
         residual = None

@@ -26,6 +26,7 @@ import torch
 import torch.nn.functional as F
 
 from . import ops as O
+from .placement import to_device
 from .ir import Graph, Node
 
 BF16 = torch.bfloat16
@@ -98,8 +99,8 @@ class LayerNormOp:
     def __init__(self, gamma, beta, eps, device, use_hip):
         self.eps = float(eps)
         self.use_hip = use_hip
-        self.g = gamma.float().reshape(-1).contiguous().to(device)
-        self.b = beta.float().reshape(-1).contiguous().to(device)
+        self.g = to_device(gamma.float().reshape(-1), device)
+        self.b = to_device(beta.float().reshape(-1), device)
 
     def __call__(self, ctx, node, ins):
         x = O.to_torch(ins[0])
@@ -326,7 +327,7 @@ def _dense_src(g, c, ref):
         w = w.t()
     nodes.append(n)
     if bias is None:
-        bias = torch.zeros(w.shape[1])
+        bias = torch.zeros(w.shape[1], device=w.device)
     return n.inputs[0], w, bias, nodes
 
 
@@ -441,16 +442,16 @@ class EmbeddingLNOp:
         self.seq, self.eps, self.use_hip = int(seq), float(eps), use_hip
         self.tables_f = [t.float().contiguous() for t in tables]
         self.pos_f = None if pos is None else pos.float().reshape(-1, tables[0].shape[1]).contiguous()
-        self.g = gamma.float().reshape(-1).contiguous().to(device)
-        self.b = beta.float().reshape(-1).contiguous().to(device)
+        self.g = to_device(gamma.float().reshape(-1), device)
+        self.b = to_device(beta.float().reshape(-1), device)
         self.hip_ok = use_hip and device.type == "cuda" and len(tables) <= 2
         if self.hip_ok:
-            self.tables = [t.to(device=device, dtype=BF16).contiguous() for t in tables]
-            self.pos = None if pos is None else self.pos_f.to(device=device, dtype=BF16).contiguous()
+            self.tables = [to_device(t, device, BF16) for t in tables]
+            self.pos = None if pos is None else to_device(self.pos_f, device, BF16)
             self.tables_f = self.pos_f = None     # only the bf16 copies stay resident
         else:
-            self.tables_f = [t.to(device) for t in self.tables_f]
-            self.pos_f = None if self.pos_f is None else self.pos_f.to(device)
+            self.tables_f = [to_device(t, device) for t in self.tables_f]
+            self.pos_f = None if self.pos_f is None else to_device(self.pos_f, device)
 
     def __call__(self, ctx, node, ins):
         idx = [O.to_torch(v) for v in ins]
@@ -548,7 +549,7 @@ def fuse_embedding(g, order, fed, fetch_refs, device, opts):
             ln.op = "_EmbeddingLN"
             ln.inputs = [gt[1] for gt in gathers]
             ln.ctrl = []
-            ln.attrs = {"_impl": EmbeddingLNOp([gt[0] for gt in gathers], p, S, impl.g.cpu(), impl.b.cpu(), impl.eps,
+            ln.attrs = {"_impl": EmbeddingLNOp([gt[0] for gt in gathers], p, S, impl.g, impl.b, impl.eps,
                                                device, c.use_hip)}
             c.refresh()
 

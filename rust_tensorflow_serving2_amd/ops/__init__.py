@@ -56,6 +56,20 @@ AUTOTUNE = os.environ.get("TFSERVE_AUTOTUNE", "1") != "0"
 _TUNE_TIMES: Dict[Tuple, List[Tuple[float, Tuple[int, int]]]] = {}
 _GRAPH_TUNED: set = set()
 _REC = threading.local()
+# tile picks another replica made (parallel/weights.py: the leader tunes, the
+# followers install its table) keyed by repr(key): used instead of tuning
+_REMOTE: Dict[str, Tuple[int, int]] = {}
+
+
+def install_remote_tuned(table: Dict[str, list]) -> None:
+    with _TUNE_LOCK:
+        for k, v in table.items():
+            _REMOTE[k] = (int(v[0]), int(v[1]))
+
+
+def tuned_table_for(keys) -> Dict[str, list]:
+    """{repr(key): [cfg, splits]} of the picks made for ``keys`` (to publish)."""
+    return {repr(k): list(_TUNED[k]) for k in keys if k in _TUNED}
 
 
 def heuristic_config(M: int, N: int) -> int:
@@ -154,6 +168,12 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
     hit = _TUNED.get(key)
     if hit is not None:
         return hit
+    remote = _REMOTE.get(repr(key)) if _REMOTE else None
+    if remote is not None:
+        with _TUNE_LOCK:
+            _TUNED[key] = remote
+            _GRAPH_TUNED.add(key)          # the leader already graph-tuned it
+        return remote
     if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
         c = 42 if cgemm_only else heuristic_config(M, N)
         return c, heuristic_splits(M, N, K, c)

@@ -81,6 +81,9 @@ class GpuRunner:
         with torch.cuda.device(self.device):
             self.program = compile_program(g, [s.name for s in in_specs], [s.name for s in out_specs],
                                            self.device, servable.passes(), opts.extra)
+            from .servable import runner_key, share_weights
+            share_weights(servable, in_specs, out_specs, self.program)
+        self._key = runner_key(in_specs, out_specs)
         self.batched = all(s.shape is not None and len(s.shape) >= 1 and s.shape[0] == -1 and
                            all(d >= 0 for d in s.shape[1:]) and s.dtype != T.DT_STRING for s in in_specs)
         self.use_graphs = opts.hip_graphs and self.batched
@@ -182,8 +185,14 @@ class GpuRunner:
             lane.dev_in = [torch.zeros([bmax] + list(s.shape[1:]), dtype=_torch_dtype(s.dtype), device=dev)
                            for s in self.in_specs]
         ins = [t[:b] for t in lane.dev_in]
-        # eager warm-up on the lane's stream (autotunes kernel tiles for this shape)
         from .. import ops
+        src = getattr(self.servable, "weight_source", None)
+        if src is not None:
+            # a follower replica uses the leader's tile picks for this bucket
+            table = src.wait_tuned(self.servable.name, self.servable.version, self._key, b)
+            if table:
+                ops.install_remote_tuned(table)
+        # eager warm-up on the lane's stream (autotunes kernel tiles for this shape)
         with torch.cuda.stream(lane.stream), ops.record_tuned_keys() as keys:
             self._finish(self.program.run(ins))
             outs = self._finish(self.program.run(ins))
@@ -193,6 +202,8 @@ class GpuRunner:
             changed = ops.graph_tune(keys, lambda: self._replay_ms(lane, ins))
             if changed:
                 log.info("graph autotune %s bucket=%d: %s", self.servable.name, b, changed)
+        if src is not None and keys:
+            src.publish_tuned(self.servable.name, self.servable.version, self._key, b, ops.tuned_table_for(keys))
         # compute-only graph: the H2D/D2H copies stay separate hipMemcpyAsync calls
         # so they run on the SDMA engines (copy nodes inside a graph can turn into
         # blit kernels that read host memory over PCIe from the CUs) and move only

@@ -82,6 +82,7 @@ class Runner:
         self.program: Program = compile_program(
             g, [s.name for s in in_specs], [s.name for s in out_specs],
             servable.options.torch_device, passes, servable.options.extra)
+        share_weights(servable, in_specs, out_specs, self.program)
 
     def run(self, inputs: Sequence) -> List:
         dev = self.servable.options.torch_device
@@ -95,6 +96,27 @@ class Runner:
                 t = t.to(dev, non_blocking=True)
             feeds.append(t)
         return self.program.run(feeds)
+
+
+def runner_key(in_specs, out_specs) -> str:
+    return "|".join(s.name for s in in_specs) + ">" + "|".join(s.name for s in out_specs)
+
+
+def share_weights(servable, in_specs, out_specs, program) -> None:
+    """Replicas: the leader broadcasts ``program``'s packed device weights; a
+    follower (compiled on shapes only) binds them (parallel/weights.py)."""
+    src = getattr(servable, "weight_source", None)
+    if src is None:
+        return
+
+    def recompile():
+        real = sm.load(servable.path, verify=servable.options.verify_checksums)
+        g = from_graph_def(real.graph_def)
+        bind_variables(g, real.bundle)
+        servable.bundle = real
+        return compile_program(g, [s.name for s in in_specs], [s.name for s in out_specs],
+                               servable.options.torch_device, servable.passes(), servable.options.extra)
+    src.share_program(servable.name, servable.version, runner_key(in_specs, out_specs), program, recompile)
 
 
 def _np_to_torch(a: np.ndarray, dt: int) -> torch.Tensor:
@@ -121,11 +143,14 @@ class Servable:
     """One loaded version of one model."""
 
     def __init__(self, name: str, version: int, path: str, options: ServableOptions,
-                 bundle: Optional[sm.SavedModelBundle] = None):
+                 bundle: Optional[sm.SavedModelBundle] = None, weight_source=None):
         self.name = name
         self.version = version
         self.path = path
         self.options = options
+        # parallel/weights.py ReplicatedWeightSource: compiled programs share
+        # the leader's device weight blob (a follower's bundle is shape-only)
+        self.weight_source = weight_source
         self.bundle = bundle or sm.load(path, verify=options.verify_checksums)
         self.signatures = self.bundle.signatures
         self._runners: Dict[tuple, Runner] = {}

@@ -93,7 +93,7 @@ class ModelServer:
         bundle = None
         if self.opts.weight_source is not None:
             bundle = self.opts.weight_source.load(name, version, path)
-        s = Servable(name, version, path, so, bundle)
+        s = Servable(name, version, path, so, bundle, weight_source=self.opts.weight_source)
         s.warmup()
         if cfg is not None and cfg.HasField("logging_config"):
             self.request_logs.configure(name, cfg.logging_config)

@@ -25,18 +25,28 @@ def _weights_worker(rank, world, port, model_dir, out_q):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
+    from rust_tensorflow_serving2_amd.graph import placement
     from rust_tensorflow_serving2_amd.parallel.weights import LoadError, ReplicatedWeightSource
+    from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     store = dist.distributed_c10d._get_default_store()
-    ws = ReplicatedWeightSource(store, device=torch.device("cpu"), load_timeout=60)
+    ws = ReplicatedWeightSource(store, device=torch.device("cpu"), load_timeout=60, share=True)
     res = {}
     if rank == 0:
         time.sleep(0.5)                         # followers ask first: they must wait for the leader
-    b = ws.load("m", 1, os.path.join(model_dir, "1"))
+    path = os.path.join(model_dir, "1")
+    b = ws.load("m", 1, path)
     res["keys"] = sorted(b.bundle.keys())
-    res["sum"] = float(sum(np.asarray(b.bundle[k], np.float64).sum() for k in res["keys"]))
+    # followers hold no weight values: float variables are shape-only
+    res["meta"] = sum(1 for k in res["keys"] if isinstance(b.bundle[k], torch.Tensor) and b.bundle[k].is_meta)
     res["sigs"] = sorted(b.signatures)
+    # compile on every rank; the followers' program binds the leader's packed weights
+    s = Servable("m", 1, path, ServableOptions(device="cpu", fuse=True), b, weight_source=ws)
+    x = np.random.default_rng(0).random((2, 32, 32, 3), dtype=np.float32)
+    out = s.run("serving_default", {"input": x}, ["classes", "probabilities"])
+    res["probs"] = out["probabilities"].tolist()
+    res["bound"] = ws.stats.get("bound_bytes", 0)
     try:
         ws.load("m", 2, os.path.join(model_dir, "does_not_exist"))
         res["err"] = None
@@ -49,6 +59,9 @@ def _weights_worker(rank, world, port, model_dir, out_q):
 
 
 def test_replicated_weight_source_gloo(tiny_resnet_path):
+    """Leader reads + compiles, followers get a shape-only bundle and bind
+    their compiled program to the leader's broadcast weight blob; outputs are
+    identical on every rank."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -60,8 +73,10 @@ def test_replicated_weight_source_gloo(tiny_resnet_path):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert out[0]["keys"] == out[1]["keys"] and len(out[0]["keys"]) > 10
-    assert out[0]["sum"] == pytest.approx(out[1]["sum"])
+    assert out[0]["meta"] == 0 and out[1]["meta"] > 10
     assert out[0]["sigs"] == out[1]["sigs"]
+    np.testing.assert_array_equal(np.asarray(out[0]["probs"]), np.asarray(out[1]["probs"]))
+    assert out[1]["bound"] > 0 and out[0]["bound"] == 0
     assert out[0]["err"] and out[1]["err"] and out[0]["err"] == out[1]["err"]
 
 
@@ -143,7 +158,7 @@ def test_four_replicas_one_connection_and_replica_restart(hpt_path, tmp_path):
     logf = str(tmp_path / "replicas.log")
     stats_dir = str(tmp_path / "stats")
     env = dict(os.environ, PYTHONPATH=ROOT, TFSERVE_STATS_DIR=stats_dir, TFSERVE_ROUTE_CELLS="16",
-               TFSERVE_ROUTE_MARGIN="2")
+               TFSERVE_ROUTE_MARGIN="2", TFSERVE_SHARE_WAIT_S="2")
     env.pop("WORLD_SIZE", None)
     proc = subprocess.Popen([sys.executable, "-m", "rust_tensorflow_serving2_amd.server", f"--port={port}",
                              "--model_name=a", f"--model_base_path={hpt_path}", "--num_gpus=4", "--device=cpu",

@@ -1,0 +1,104 @@
+"""Device-resident weight replication on the MI355X (parallel/weights.py).
+
+* nccl (RCCL) at world size 1: the leader's load / compile / pack / broadcast
+  path runs on the hardware.
+* gloo at world size 2 on ONE GPU (two replicas sharing the device; RCCL
+  refuses two ranks per GPU): the follower compiles ResNet-50 on shapes only,
+  binds its program to the leader's packed bf16 device blob, installs the
+  leader's tile picks -- zero host->device weight copies, no autotuning of
+  its own -- and returns bit-identical outputs."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import torch.multiprocessing as mp  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, backend, port, path, out_q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from rust_tensorflow_serving2_amd import ops
+    from rust_tensorflow_serving2_amd.graph import placement
+    from rust_tensorflow_serving2_amd.parallel.weights import ReplicatedWeightSource
+    from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        ws = ReplicatedWeightSource(dist.distributed_c10d._get_default_store(), device=dev, load_timeout=300)
+        h2d0 = placement.H2D_BYTES
+        b = ws.load("resnet", 1, path)
+        s = Servable("resnet", 1, path, ServableOptions(device="cuda:0", max_batch_size=4,
+                                                         allowed_batch_sizes=(4,)), b, weight_source=ws)
+        x = np.random.default_rng(7).random((4, 224, 224, 3), dtype=np.float32)
+        out = s.run("serving_default", {"input": x}, ["classes", "probabilities"])
+        res = {"probs": out["probabilities"], "classes": out["classes"], "h2d": placement.H2D_BYTES - h2d0,
+               "bound": ws.stats.get("bound_bytes", 0), "bcast": ws.stats.get("broadcast_bytes", 0),
+               "tuned_here": len(ops._TUNE_TIMES), "remote": len(ops._REMOTE)}
+        ws.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        out_q.put((rank, res))
+    except Exception as e:  # pragma: no cover - reported to the test
+        import traceback
+        out_q.put((rank, {"error": f"{e}\n{traceback.format_exc()}"}))
+
+
+def _run(world, backend, path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, backend, port, path, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for r, v in out.items():
+        assert "error" not in v, v["error"]
+    return out
+
+
+@pytest.fixture(scope="module")
+def r50(tmp_path_factory):
+    from rust_tensorflow_serving2_amd.models import resnet
+    base = str(tmp_path_factory.mktemp("r50w"))
+    resnet.export(os.path.join(base, "1"), seed=5)
+    return os.path.join(base, "1")
+
+
+def test_rccl_world1_leader_path(r50):
+    out = _run(1, "nccl", r50)
+    r = out[0]
+    assert r["bcast"] > 20e6                       # ResNet-50's packed bf16 program weights went through RCCL
+    np.testing.assert_allclose(r["probs"].sum(1), 1.0, atol=1e-4)
+
+
+def test_follower_binds_leader_blob_without_host_copies(r50):
+    out = _run(2, "gloo", r50)
+    lead, fol = out[0], out[1]
+    np.testing.assert_array_equal(lead["probs"], fol["probs"])
+    np.testing.assert_array_equal(lead["classes"], fol["classes"])
+    assert lead["h2d"] > 20e6                      # the leader uploaded the folded weights once
+    assert fol["h2d"] == 0                         # the follower: not one weight byte host -> device
+    assert fol["bound"] >= 0.9 * lead["bcast"] and fol["bound"] > 20e6
+    assert fol["tuned_here"] == 0 and fol["remote"] > 0     # the leader's tile picks, no own autotune
