@@ -123,6 +123,28 @@ def to_image(img):
     raise TypeError(f"cannot convert {type(img).__name__} to an image")
 
 
+def _preprocess_lut(preprocessing_fn: Callable) -> np.ndarray:
+    """``preprocessing_fn`` at the 256 values a u8 pixel can take (as f32, the
+    way src/lib.rs:237-242 feeds it): the whole per-pixel map as a table."""
+    vals = np.arange(256, dtype=np.float32)
+    try:
+        out = np.asarray(preprocessing_fn(vals), dtype=np.float32)
+        if out.shape != vals.shape:
+            raise ValueError
+    except Exception:
+        out = np.array([preprocessing_fn(float(v)) for v in vals], dtype=np.float32)
+    return np.ascontiguousarray(out)
+
+
+def _image_request(spec, img, preprocessing_fn: Callable, alias: str = "input") -> bytes:
+    """The reference's predict_with_preprocessing request (src/lib.rs:226-263)
+    built natively: u8 pixels -> table lookup -> packed float_val, one pass."""
+    im = to_image(img)
+    w, h = im.size
+    px = np.ascontiguousarray(np.asarray(im, dtype=np.uint8)).reshape(-1)
+    return native.encode_image_request(spec, alias, px, [1, w, h, 3], _preprocess_lut(preprocessing_fn))
+
+
 def _image_tensor(img, preprocessing_fn: Callable) -> np.ndarray:
     """Pixels exactly as the reference builds them: dims ``[1, width, height, 3]``
     (src/lib.rs:229-235 — width/height in that order) over ``raw_pixels()`` in
@@ -201,8 +223,6 @@ class TensorflowServing:
         self._channel = channel
         self.signature_name_ = signature_name
         self._calls = {}
-        for svc in (PREDICTION_SERVICE, MODEL_SERVICE):
-            pass
 
     @staticmethod
     def new() -> TensorflowServingBuilder:
@@ -292,9 +312,9 @@ class TensorflowServing:
 
     async def predict_with_preprocessing(self, img, model_description, preprocessing_fn: Callable,
                                          timeout=None):
-        pixels, dims = _image_tensor(img, preprocessing_fn)
-        # shape is set from dims; float_val carries raw pixels (reference quirks preserved)
-        body = _encode_float_request(self._spec_tuple(model_description), "input", pixels, dims)
+        # shape [1, w, h, 3] from the image, float_val = fn(pixel) for every raw
+        # pixel (reference quirks preserved), encoded by the native image encoder
+        body = _image_request(self._spec_tuple(model_description), img, preprocessing_fn)
         return await self._call(PREDICTION_SERVICE, "Predict", body, serving.PredictResponse, timeout)
 
     async def predict(self, img, model_description, timeout=None):
@@ -338,10 +358,10 @@ def _encode_float_request(spec, alias: str, values: np.ndarray, dims: List[int])
     ``dims`` regardless of len(values) (the reference may send mismatching
     counts, e.g. RGBA images — the server must reject, not crash)."""
     from ..schema import serving as S
-    # encode values with the native packer, then patch the shape
-    body = native.encode_predict_request(spec, {alias: values.reshape(-1)})
     if int(np.prod(dims)) == values.size:
         return native.encode_predict_request(spec, {alias: values.reshape(dims)})
+    # the count disagrees with the shape: encode the values, then patch the shape
+    body = native.encode_predict_request(spec, {alias: values.reshape(-1)})
     req = S.PredictRequest.FromString(body)
     t = req.inputs[alias]
     del t.tensor_shape.dim[:]

@@ -3,6 +3,7 @@
 //   (TensorBundle index), mmap'd bundle shards, the HTTP/2 gRPC front end
 //   and the dynamic batcher (see server.cpp / batcher.cpp).
 #include <pthread.h>
+#include <cstring>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -143,6 +144,37 @@ py::bytes encode_request(const py::object& spec, const py::list& inputs, const p
   return py::bytes(out);
 }
 
+// The reference's image hot loop (src/lib.rs:237-242: raw_pixels() u8 -> f32
+// -> preprocessing_fn -> float_val) in one native pass: `lut` holds the
+// preprocessing function's value for each of the 256 possible pixel values
+// (any f32 -> f32 function of a u8 pixel is exactly a 256-entry table), so
+// every pixel is one table lookup written straight into the float_val array.
+// `dims` is the shape the reference sends ([1, width, height, 3]) even when
+// the pixel count disagrees (grayscale / RGBA: the server must reject it).
+py::bytes encode_image_request(const py::object& spec, const std::string& alias, const py::buffer& pixels,
+                               const std::vector<int64_t>& dims, const py::buffer& lut) {
+  ConstBuf px = get_buf(pixels);
+  ConstBuf lb = get_buf(lut);
+  if (lb.len != 256 * sizeof(float)) throw std::invalid_argument("lut must hold 256 float32 values");
+  ModelSpecView s = spec_from_py(spec);
+  std::string out;
+  {
+    py::gil_scoped_release nogil;
+    std::vector<float> vals(px.len);
+    float table[256];
+    std::memcpy(table, lb.ptr, sizeof(table));
+    for (size_t i = 0; i < px.len; ++i) vals[i] = table[px.ptr[i]];
+    OutTensor t;
+    t.alias = alias;
+    t.dtype = DT_FLOAT;
+    t.shape = dims;
+    t.data = vals.data();
+    t.count = vals.size();
+    out = encode_predict_request(s, {t}, {}, false);
+  }
+  return py::bytes(out);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -156,6 +188,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("use_tensor_content") = false);
   m.def("encode_predict_request", &encode_request, py::arg("spec"), py::arg("inputs"),
         py::arg("output_filter") = py::list(), py::arg("use_tensor_content") = false);
+  m.def("encode_image_request", &encode_image_request, py::arg("spec"), py::arg("alias"), py::arg("pixels"),
+        py::arg("dims"), py::arg("lut"),
+        "PredictRequest of one DT_FLOAT float_val tensor from u8 pixels mapped through a 256-entry table");
 
   m.def("set_thread_name", [](const std::string& name) {
     // OS-level thread name (<= 15 chars), visible in /proc/<pid>/task/*/comm

@@ -98,3 +98,10 @@ def decode_tensor_proto(data: bytes) -> np.ndarray:
 MappedFile = _C.MappedFile
 sstable_build = _C.sstable_build
 sstable_read = _C.sstable_read
+
+
+def encode_image_request(spec: tuple, alias: str, pixels: np.ndarray, dims, lut: np.ndarray) -> bytes:
+    """PredictRequest with one DT_FLOAT ``float_val`` tensor: ``lut[pixels]``
+    (u8 -> f32 through a 256-entry table) with shape ``dims`` (C++)."""
+    return _C.encode_image_request(spec, alias, np.ascontiguousarray(pixels, dtype=np.uint8).reshape(-1),
+                                   [int(d) for d in dims], np.ascontiguousarray(lut, dtype=np.float32))

@@ -166,6 +166,31 @@ class ReplicaControl:
                 t.join(timeout=5)
 
 
+def count_gpus() -> int:
+    """GPUs visible to this process, counted without touching the HIP runtime
+    (the supervisor must never initialise a device): KFD topology nodes with
+    SIMDs, narrowed by ROCR/HIP/CUDA_VISIBLE_DEVICES."""
+    n = 0
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for node in os.listdir(base):
+            try:
+                with open(os.path.join(base, node, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        n = 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids)) if n else len(ids)
+    return n
+
+
 def free_port(host: str = "127.0.0.1") -> int:
     with socket.socket() as s:
         s.bind((host, 0))

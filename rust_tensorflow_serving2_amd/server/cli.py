@@ -218,8 +218,9 @@ def main(argv: Optional[List[str]] = None) -> int:
         return serve(args, int(os.environ.get("RANK", "0")), world_env)
     n = args.num_gpus
     if n == 0:
-        import torch                         # device_count() does not initialise the GPU
-        n = max(1, torch.cuda.device_count())
+        # sysfs KFD topology: the supervisor never initialises the HIP runtime
+        from ..parallel.replicas import count_gpus
+        n = max(1, count_gpus())
     if n > 1:
         from ..parallel.replicas import launch
         return launch(argv, n)

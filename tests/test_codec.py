@@ -163,3 +163,27 @@ def test_upb_built_tensors_decode_natively(dt, shape, form, seed):
     got = arrays["x"]
     assert dts["x"] == dt and got.dtype == np.dtype(npdt) and got.shape == tuple(shape)
     np.testing.assert_array_equal(got, want)
+
+
+def test_native_image_encoder_matches_reference_loop():
+    """N3: the native u8 -> fn(f32) -> float_val encoder (one table lookup per
+    pixel) produces the same bytes as the reference's per-pixel loop
+    (src/lib.rs:237-242) for RGB, grayscale and RGBA images (the last two keep
+    the reference's [1, w, h, 3] shape with a mismatching count), with a
+    vectorisable and a scalar-only preprocessing function."""
+    import math
+
+    from PIL import Image
+
+    from rust_tensorflow_serving2_amd import native
+    from rust_tensorflow_serving2_amd.client import _encode_float_request, _image_request, _image_tensor
+    rng = np.random.default_rng(3)
+    spec = native.spec_tuple("resnet", 7, None, "serving_default")
+    fns = [lambda v: v / 255.0, lambda v: math.sqrt(v) - 3.0 if isinstance(v, float) else (_ for _ in ()).throw(TypeError)]
+    for mode, c in (("RGB", 3), ("L", 1), ("RGBA", 4)):
+        arr = rng.integers(0, 256, (5, 7, c), dtype=np.uint8).squeeze()
+        im = Image.fromarray(arr, mode)
+        for fn in fns:
+            px, dims = _image_tensor(im, fn)
+            ref = _encode_float_request(spec, "input", px, dims)
+            assert _image_request(spec, im, fn) == ref, (mode, fn)
