@@ -112,6 +112,9 @@ class LayerNormOp:
         return [y if not x.is_cuda else y.to(x.dtype)]
 
 
+MAX_ATTENTION_SEQ = 4096      # kernels/launch.h kMaxAttentionSeq
+
+
 class AttentionOp:
     def __init__(self, heads: int, head_dim: int, seq: int, scale: float, use_hip: bool):
         self.h, self.d, self.s, self.scale, self.use_hip = heads, head_dim, seq, scale, use_hip
@@ -124,7 +127,7 @@ class AttentionOp:
         if adder is not None:
             if adder.dim() != 4 or adder.shape[1] != 1 or adder.shape[-1] != S:
                 raise O.Unsupported("attention mask must be [B|1, 1, S|1, S]")
-        if (self.use_hip and qkv.is_cuda and D == 64 and S in (64, 128, 192, 256)):
+        if self.use_hip and qkv.is_cuda and D == 64 and 1 <= S <= MAX_ATTENTION_SEQ:
             from ..ops import hip
             from .fused import _to_bf16
             q3 = _to_bf16(qkv).reshape(B, S, 3 * H * D).contiguous()

@@ -13,7 +13,9 @@
 //                           rows padded by 16 B) so B fragments are 16-B reads;
 //                           the transpose is done in registers on 8x8 blocks
 //                           so staging is 16-B loads and 16-B LDS stores
-// S <= 256, S % 32 == 0, D == 64.  The S x S matrix never touches HBM.
+// S in {64, 128, 192, 256} (the whole key row in registers; D == 64), and
+// attention_flash_kernel below for any other S up to
+// kMaxAttentionSeq.  The S x S matrix never touches HBM.
 #include "common.h"
 #include "gemm_common.h"
 #include "launch.h"
@@ -183,6 +185,171 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   }
 }
 
+// ---------------------------------------------------------------- long sequences
+// S up to 512 (BERT-QA's 384, full 512) or any other S the fixed-S kernel
+// above does not cover: a KV-block loop with an online softmax (running row
+// max / sum, O rescaled per block), so registers hold one 64-key block of
+// scores instead of the whole row and LDS holds one K / V block.  Keys past S
+// in the last block are masked to -inf; query rows past S are never stored.
+constexpr int FQB = 64, FKB = 64;
+
+__global__ __launch_bounds__(256) void attention_flash_kernel(const uint16_t* __restrict__ qkv,
+                                                              const float* __restrict__ mask_bias,
+                                                              uint16_t* __restrict__ ctx, int S, int H, float scale,
+                                                              long mask_bstride, long mask_qstride) {
+  constexpr int VT_LD = FKB + 8, P_LD = FKB + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[FKB * D];       // [key][64] swizzled
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[D * VT_LD];     // [d][key]
+  __shared__ __attribute__((aligned(16))) uint16_t Ps[4 * 16 * P_LD]; // per-wave P / output strips
+
+  const int qblocks = (S + FQB - 1) / FQB;
+  const int bid = blockIdx.x;
+  const int qb = bid % qblocks;
+  const int h = (bid / qblocks) % H;
+  const int b = bid / (qblocks * H);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const long row_stride = 3L * H * D;
+  const uint16_t* base = qkv + long(b) * S * row_stride;
+
+  const int q0 = qb * FQB + wid * 16;
+  bf16x8 qf[2];
+  const int qrow = min(q0 + fr, S - 1);            // rows past S load a valid row, never stored
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+    qf[kk] = *reinterpret_cast<const bf16x8*>(base + long(qrow) * row_stride + h * D + kk * 32 + fq * 8);
+
+  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, l[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint16_t* pw = Ps + wid * 16 * P_LD;
+  const float* mrow = mask_bias ? mask_bias + long(b) * mask_bstride : nullptr;
+
+  for (int k0 = 0; k0 < S; k0 += FKB) {
+    // ---- stage this block's K (swizzled rows) and V (transposed); keys past S read key S-1
+    for (int c = tid; c < FKB * 8; c += 256) {
+      const int key = c >> 3, ch = c & 7;
+      const int kg = min(k0 + key, S - 1);
+      const uint4 kv = *reinterpret_cast<const uint4*>(base + long(kg) * row_stride + H * D + h * D + ch * 8);
+      *reinterpret_cast<uint4*>(Ks + key * D + ((ch ^ (key & 7)) * 8)) = kv;
+    }
+    for (int blk = tid; blk < (FKB / 8) * 8; blk += 256) {
+      const int kgrp = blk >> 3, ch = blk & 7;
+      uint32_t w[8][4];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int kg = min(k0 + kgrp * 8 + k, S - 1);
+        const uint4 v = *reinterpret_cast<const uint4*>(base + long(kg) * row_stride + 2 * H * D + h * D + ch * 8);
+        w[k][0] = v.x; w[k][1] = v.y; w[k][2] = v.z; w[k][3] = v.w;
+      }
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        uint32_t ov[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t lo = (d & 1) ? (w[2 * j][d >> 1] >> 16) : (w[2 * j][d >> 1] & 0xffffu);
+          const uint32_t hi = (d & 1) ? (w[2 * j + 1][d >> 1] & 0xffff0000u) : (w[2 * j + 1][d >> 1] << 16);
+          ov[j] = lo | hi;
+        }
+        *reinterpret_cast<uint4*>(Vt + (ch * 8 + d) * VT_LD + kgrp * 8) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+      }
+    }
+    __syncthreads();
+    // ---- scores of this block
+    f32x4 sc[FKB / 16];
+#pragma unroll
+    for (int nt = 0; nt < FKB / 16; ++nt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int key = nt * 16 + fr;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + fq;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + key * D + ((ch ^ (key & 7)) * 8));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[kk], kf, acc, 0, 0, 0);
+      }
+      sc[nt] = acc;
+    }
+    // ---- online softmax update (rows fq*4 + r, key k0 + nt*16 + fr)
+    float bm[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int nt = 0; nt < FKB / 16; ++nt) {
+      const int key = k0 + nt * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v;
+        if (key < S) {
+          const float mb = mrow ? mrow[long(min(q0 + fq * 4 + r, S - 1)) * mask_qstride + key] : 0.f;
+          v = sc[nt][r] * scale + mb;
+        } else {
+          v = -INFINITY;
+        }
+        sc[nt][r] = v;
+        bm[r] = fmaxf(bm[r], v);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) bm[r] = fmaxf(bm[r], __shfl_xor(bm[r], off, 64));
+    float alpha[4], bs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float mn = fmaxf(m[r], bm[r]);
+      alpha[r] = __expf(m[r] - mn);            // exp(-inf) = 0 on the first block
+      m[r] = mn;
+      bs[r] = 0.f;
+    }
+#pragma unroll
+    for (int nt = 0; nt < FKB / 16; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __expf(sc[nt][r] - m[r]);
+        bs[r] += e;
+        pw[(fq * 4 + r) * P_LD + nt * 16 + fr] = f32_to_bf16(e);
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) bs[r] += __shfl_xor(bs[r], off, 64);
+      l[r] = l[r] * alpha[r] + bs[r];
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dt][r] *= alpha[r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);       // this wave's P strip writes landed
+    __builtin_amdgcn_wave_barrier();
+    // ---- o += P V over the block's 64 keys
+#pragma unroll
+    for (int ks = 0; ks < FKB / 32; ++ks) {
+      const bf16x8 pa = *reinterpret_cast<const bf16x8*>(pw + fr * P_LD + ks * 32 + fq * 8);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vt + (dt * 16 + fr) * VT_LD + ks * 32 + fq * 8);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[dt], 0, 0, 0);
+      }
+    }
+    __syncthreads();                          // every wave is done with Ks / Vt before the next block
+  }
+  // ---- normalise and store (through the wave's strip for 16-B row chunks)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float inv = 1.f / l[r];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) pw[(fq * 4 + r) * P_LD + dt * 16 + fr] = f32_to_bf16(o[dt][r] * inv);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = j * 64 + lane, row = c >> 3, ch = c & 7;
+    if (q0 + row < S)
+      *reinterpret_cast<uint4*>(ctx + (long(b) * S + q0 + row) * (long(H) * D) + h * D + ch * 8) =
+          *reinterpret_cast<const uint4*>(pw + row * P_LD + ch * 8);
+  }
+}
+
 template <int S>
 hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, int H, float scale, long bs, long qs,
                     hipStream_t st) {
@@ -207,7 +374,14 @@ hipError_t attention_launch(const uint16_t* qkv, const float* mask_bias, uint16_
     case 128: return launch_s<128>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
     case 192: return launch_s<192>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
     case 256: return launch_s<256>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
-    default: return hipErrorInvalidValue;
+    default: {
+      if (S <= 0 || S > kMaxAttentionSeq) return hipErrorInvalidValue;
+      const long grid = long(B) * H * ((S + FQB - 1) / FQB);
+      if (grid >= (1L << 31)) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(attention_flash_kernel, dim3(unsigned(grid)), dim3(256), 0, st, qkv, mask_bias, ctx, S, H,
+                         scale, bs, qs);
+      return hipGetLastError();
+    }
   }
 }
 

@@ -451,7 +451,7 @@ Tensor attention(const Tensor& qkv, const c10::optional<Tensor>& mask_bias, int6
   TORCH_CHECK(HD3 % (3 * heads) == 0, "qkv width must be 3*heads*head_dim");
   const int D = HD3 / (3 * heads);
   TORCH_CHECK(D == 64, "attention kernel supports head_dim 64");
-  TORCH_CHECK(S == 64 || S == 128 || S == 192 || S == 256, "attention kernel supports S in {64,128,192,256}");
+  TORCH_CHECK(S >= 1 && S <= tfsk::kMaxAttentionSeq, "attention kernel supports 1 <= S <= ", tfsk::kMaxAttentionSeq);
   const float* mb = nullptr;
   if (mask_bias.has_value()) {
     need(*mask_bias, at::kFloat, "mask_bias");

@@ -109,6 +109,7 @@ hipError_t embed_ln_launch(const int* ids, const int* type_ids, const uint16_t* 
                            const uint16_t* pos, const uint16_t* type, const float* gamma,
                            const float* beta, uint16_t* y, int tokens, int seq, int hidden,
                            int vocab, int ntypes, float eps, hipStream_t stream);
+constexpr int kMaxAttentionSeq = 4096;
 // Fused multi-head attention over a packed QKV buffer [B*S][3*H*D] (bf16):
 // ctx[b,q,h,:] = softmax(Q K^T * scale + mask[b*bstride + q*qstride + key]) V
 // (additive f32 mask; strides 0 broadcast, e.g. BERT's [B,1,S,S] adder or a [B,S] key mask)

@@ -41,3 +41,38 @@ def test_bert_base_gpu_matches_cpu(bert_base):
     hist = runner.program.op_histogram()
     assert hist["_Attention"] == 12 and hist["_FusedQKV"] == 12 and hist["_LayerNorm"] == 24
     assert hist["_EmbeddingLN"] == 1 and hist["_KeyMaskAdder"] == 1 and "GatherV2" not in hist
+
+
+@pytest.mark.parametrize("seq", [384, 512])
+def test_bert_long_sequence_uses_hip_attention(tmp_path, seq):
+    """BERT-QA's seq 384 and the full 512 positions: the fused attention runs
+    the KV-block kernel (no fp32 torch fallback) and matches the CPU program."""
+    from rust_tensorflow_serving2_amd.models import bert
+    from rust_tensorflow_serving2_amd.ops import hip
+    from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
+    cfg = bert.BertConfig(vocab_size=2000, layers=2, seq_len=seq)
+    path = os.path.join(str(tmp_path), "1")
+    bert.export(path, cfg, seed=1)
+    mod = hip()
+    orig = mod.attention
+    seqs = []
+
+    def spy(qkv, *a):
+        seqs.append(qkv.shape[1])
+        return orig(qkv, *a)
+    mod.attention = spy
+    try:
+        gpu = Servable("bert", 1, path, ServableOptions(device="cuda:0", max_batch_size=4))
+        rng = np.random.default_rng(1)
+        ids = rng.integers(0, 2000, (2, seq)).astype(np.int32)
+        mask = np.ones((2, seq), np.int32)
+        mask[1, seq - 100:] = 0
+        feeds = {"input_ids": ids, "input_mask": mask, "segment_ids": np.zeros((2, seq), np.int32)}
+        outs = ["pooled_output", "probabilities"]
+        g = gpu.run("serving_default", feeds, outs)
+    finally:
+        mod.attention = orig
+    assert seqs and set(seqs) == {seq}, seqs          # the HIP kernel ran (not the torch fallback)
+    c = Servable("bert", 1, path, ServableOptions(device="cpu")).run("serving_default", feeds, outs)
+    assert np.abs(g["pooled_output"] - c["pooled_output"]).max() < 5e-2
+    assert np.abs(g["probabilities"] - c["probabilities"]).max() < 1e-2

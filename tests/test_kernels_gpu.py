@@ -439,7 +439,8 @@ def test_embedding_out_of_range_rows_are_zero(hd):
         hip().embed_ln(ids.to(DEV), None, word.to(DEV), None, None, gm.to(DEV), bt.to(DEV), 1e-6, 5)   # 32 % 5
 
 
-@pytest.mark.parametrize("s", [64, 128, 256])
+@pytest.mark.parametrize("s", [64, 128, 256,
+                               32, 100, 320, 384, 512])     # KV-block (online softmax) kernel, partial blocks
 def test_attention_matches_fp32(s):
     b, h, d = 3, 12, 64
     qkv = rnd(b, s, 3 * h * d, seed=21).to(BF)
