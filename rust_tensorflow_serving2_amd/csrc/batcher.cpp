@@ -202,6 +202,7 @@ void Endpoint::drain_queue() {
 // ---------------------------------------------------------------- streaming rows
 void SlotStream::commit(std::unique_ptr<Call> call) { ep->commit_stream(*this, std::move(call)); }
 void SlotStream::abandon() { ep->abandon_stream(*this); }
+bool SlotStream::keep_header() const { return ep->logging(); }
 
 std::shared_ptr<StreamRes> Endpoint::reserve_stream(const std::shared_ptr<Endpoint>& self, const ProbeInfo& pi) {
   // the same acceptance rules as offer(), on the header alone
@@ -332,6 +333,11 @@ void Endpoint::complete(int slot, Server& srv) {
   spec.signature_name = signature;
   std::vector<OutTensor> outs;
   const auto now = Clock::now();
+  std::shared_ptr<RequestLog> log;
+  if (logging()) {
+    std::lock_guard<std::mutex> g(mu_);
+    log = log_;
+  }
   for (auto& p : s.reqs) {
     if (!p.call) continue;   // abandoned streaming row
     if (p.call->expired(now)) {
@@ -354,6 +360,18 @@ void Endpoint::complete(int slot, Server& srv) {
       outs.push_back(std::move(t));
     }
     std::string body = encode_predict_response(&spec, outs, false);
+    if (log && log->sample()) {
+      // the request message as received: a streamed one is its header bytes +
+      // the payload sitting in this slot's row (not yet reused)
+      if (p.sres) {
+        if (p.call->head.size() > 5)
+          log->submit_predict(spec, p.call->head.substr(5),
+                              std::string(reinterpret_cast<const char*>(p.sres->dst), p.sres->len), body);
+      } else {
+        log->submit_predict(spec, std::string(reinterpret_cast<const char*>(p.call->data()), p.call->size()),
+                            std::string(), body);
+      }
+    }
     srv.respond(*p.call, 0, std::string(), std::move(body));
   }
   {

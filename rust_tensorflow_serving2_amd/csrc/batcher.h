@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "http2.h"
+#include "request_log.h"
 #include "wire.h"
 
 namespace tfs {
@@ -44,6 +45,7 @@ struct SlotStream final : StreamRes {
   int slot = -1, idx = -1, n = 0;
   void commit(std::unique_ptr<Call> call) override;
   void abandon() override;
+  bool keep_header() const override;
 };
 
 struct Pending {
@@ -143,6 +145,13 @@ class Endpoint {
   const int64_t timeout_us;
   const int max_wait_ms;
   EndpointStats stats();
+  // Request logging (null: off).  Sampled pairs go to the log's writer thread.
+  void set_log(std::shared_ptr<RequestLog> log) {
+    std::lock_guard<std::mutex> g(mu_);
+    log_ = std::move(log);
+    logging_.store(log_ != nullptr);
+  }
+  bool logging() const { return logging_.load(std::memory_order_relaxed); }
   bool busy() {
     std::lock_guard<std::mutex> g(mu_);
     return running_ > 0;
@@ -173,6 +182,8 @@ class Endpoint {
   bool idle_dispatch_ = true;
   bool closed_ = false;
   EndpointStats st_;
+  std::shared_ptr<RequestLog> log_;
+  std::atomic<bool> logging_{false};
 };
 
 class FastPath {

@@ -52,6 +52,9 @@ struct Call {
   // a message held outside `body`: the cell of a cross-replica call (router.h)
   const uint8_t* ext = nullptr;
   size_t ext_len = 0;
+  // a streamed request's header bytes (length prefix + everything before the
+  // payload), kept only when its endpoint logs requests (request_log.h)
+  std::string head;
   RemoteSink* remote = nullptr;   // answer through this sink (cell index below)
   uint32_t cell = 0;
   bool routed = false;            // placed by the router already: never forwarded again
@@ -89,6 +92,8 @@ struct StreamRes {
   virtual void abandon() = 0;
   // The row lives in another replica's ring (router.h), not a local batch slot.
   virtual bool remote() const { return false; }
+  // The committed Call should keep the request's header bytes (Call::head).
+  virtual bool keep_header() const { return false; }
   // Copy the next chunk; false once the batcher has abandoned the row (too slow).
   bool write(const uint8_t* p, size_t n) {
     writers.fetch_add(1);

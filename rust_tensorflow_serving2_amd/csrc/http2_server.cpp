@@ -417,6 +417,7 @@ class IoThread {
       srv_->stats.streamed++;
       srv_->stats.bytes_in += st->body.size() - 5 + r->len;
       st->committed = true;
+      if (r->keep_header()) call->head = std::move(st->body);
       std::string().swap(st->body);
       r->commit(std::move(call));
       return;

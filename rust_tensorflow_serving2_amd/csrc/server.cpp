@@ -436,6 +436,29 @@ void register_server(py::module_& m) {
       .def_property_readonly("timeout_us", [](const PyCall& c) { return c.call->timeout_us; })
       .def_property_readonly("expired", [](const PyCall& c) { return c.call->expired(); });
 
+  py::class_<RequestLog, std::shared_ptr<RequestLog>>(m, "RequestLog")
+      .def(py::init([](const std::string& path, double rate, size_t max_pending) {
+             return std::make_shared<RequestLog>(path, rate, max_pending);
+           }),
+           py::arg("path"), py::arg("sampling_rate"), py::arg("max_pending") = size_t(256) << 20)
+      .def_readonly("path", &RequestLog::path)
+      .def_readonly("sampling_rate", &RequestLog::rate)
+      .def("sample", &RequestLog::sample)
+      .def("submit_record", [](RequestLog& l, const py::bytes& rec) { return l.submit_record(std::string(rec)); })
+      .def("flush", [](RequestLog& l) {
+        py::gil_scoped_release nogil;
+        l.flush();
+      })
+      .def("close", [](RequestLog& l) {
+        py::gil_scoped_release nogil;
+        l.close();
+      })
+      .def("stats", [](RequestLog& l) {
+        py::dict d;
+        d["written"] = l.written.load(); d["dropped"] = l.dropped.load(); d["bytes"] = l.bytes.load();
+        return d;
+      });
+
   py::class_<PyServer>(m, "Http2Server")
       .def(py::init([](const std::string& host, int port, int io_threads, size_t max_message) {
              auto p = std::make_unique<PyServer>();
@@ -498,6 +521,11 @@ void register_server(py::module_& m) {
         if (!ep) throw std::invalid_argument("no such endpoint");
         ep->set_idle_dispatch(on);
       })
+      .def("set_endpoint_log", [](PyServer& s, int id, std::shared_ptr<RequestLog> log) {
+        auto ep = s.fast->endpoint(id);
+        if (!ep) throw std::invalid_argument("no such endpoint");
+        ep->set_log(std::move(log));
+      }, py::arg("endpoint"), py::arg("log").none(true))
       .def("endpoint_io_order", [](PyServer& s, int id) {
         auto ep = s.fast->endpoint(id);
         if (!ep) throw std::invalid_argument("no such endpoint");

@@ -64,6 +64,9 @@ class FastEndpoint:
         outs = [(a, out_specs[a].dtype, list(out_specs[a].shape[1:])) for a in out_aliases]
         self.id = srv.add_endpoint(servable.name, servable.version, sig_name, ins, outs, self.max_rows, timeout_us)
         srv.set_idle_dispatch(self.id, transport.idle_dispatch)
+        lg = transport.request_logs.get(servable.name) if transport.request_logs is not None else None
+        if lg is not None:            # logging_config: the lanes sample and submit natively
+            srv.set_endpoint_log(self.id, lg.native)
         io_in, io_out = srv.endpoint_io_order(self.id)
         assert list(io_in) == in_aliases and list(io_out) == out_aliases
         lanes = self.runner.fast_lanes()
@@ -142,6 +145,7 @@ class NativeTransport:
         if self.metrics is not None:
             self.metrics.collectors.append(self.prometheus_lines)
         self.fast_path = fast_path
+        self.request_logs = getattr(core, "request_logger", None)
         self.idle_dispatch = idle_dispatch
         self.batch_timeout_us = batch_timeout_us
         if batcher is not None:
@@ -268,8 +272,20 @@ class NativeTransport:
             self._teardown = [t for t in self._teardown if t.is_alive()] + [th]
         th.start()
 
+    def _on_log_config(self, name: str, lg):
+        """A model's logging_config changed: its fast-path endpoints follow."""
+        with self._eps_lock:
+            eps = [ep for (n, _v, _s), ep in self._eps.items() if n == name]
+        for ep in eps:
+            try:
+                self.srv.set_endpoint_log(ep.id, lg.native if lg is not None else None)
+            except ValueError:
+                pass                  # removed meanwhile
+
     # ------------------------------------------------------------ lifecycle
     def start(self):
+        if self.request_logs is not None:
+            self.request_logs.listeners.append(self._on_log_config)
         self.srv.start()
         for w in self._workers:
             w.start()
@@ -281,6 +297,8 @@ class NativeTransport:
 
     def stop(self, grace: Optional[float] = 1.0):
         self._stop.set()
+        if self.request_logs is not None and self._on_log_config in self.request_logs.listeners:
+            self.request_logs.listeners.remove(self._on_log_config)
         with self._eps_lock:
             regs = list(self._reg_threads)
         for th in regs:   # in-flight registrations see _stop and close what they built

@@ -20,6 +20,7 @@
 #include <unistd.h>
 
 #include "batcher.h"
+#include "request_log.h"
 #include "http2.h"
 #include "router.h"
 #include "sstable.h"
@@ -139,8 +140,18 @@ static void stress_batcher() {
   for (int s = 0; s < SLOTS; ++s)
     ep->set_slot_buffers(s, {reinterpret_cast<uint8_t*>(bufs[2 * s].data())},
                          {reinterpret_cast<const uint8_t*>(bufs[2 * s + 1].data())});
+  // request logging on, toggled off / on while lanes submit (writer thread + lane threads)
+  const std::string log_path = "/tmp/sanitize_reqlog_" + std::to_string(getpid()) + ".tfrecord";
+  auto rlog = std::make_shared<RequestLog>(log_path, 0.5);
+  ep->set_log(rlog);
   std::atomic<bool> stop{false};
   std::atomic<int> batches{0};
+  std::thread toggler([&] {
+    for (int k = 0; !stop; ++k) {
+      ep->set_log(k % 3 == 2 ? nullptr : rlog);
+      std::this_thread::sleep_for(std::chrono::milliseconds(3));
+    }
+  });
   std::vector<std::thread> lanes;
   for (int s = 0; s < SLOTS; ++s)
     lanes.emplace_back([&, s] {
@@ -188,6 +199,7 @@ static void stress_batcher() {
             r->abandon();
           } else {
             auto call = std::make_unique<Call>();
+            if (r->keep_header()) call->head = "\0\0\0\0\0hdr";   // what request_done keeps
             r->commit(std::move(call));
           }
         }
@@ -198,7 +210,12 @@ static void stress_batcher() {
   stop = true;
   ep->close(&srv);
   for (auto& t : lanes) t.join();
+  toggler.join();
+  rlog->flush();
+  rlog->close();
   CHECK(batches.load() > 0);
+  CHECK(rlog->written.load() > 0);
+  std::remove(log_path.c_str());
 }
 
 static void stress_router() {

@@ -193,3 +193,54 @@ def test_native_lane_device_failure_reloads_servable(tmp_path, monkeypatch):
         assert srv.health.failures[("resnet", 1)] >= 3
     finally:
         srv.stop()
+
+
+def test_request_logging_on_the_gpu_fast_path(tmp_path):
+    """logging_config sampling_rate=1.0 on a GPU model: every Predict served by
+    the native fast path (streamed 300 KB images included) is read back as a
+    valid PredictionLog TFRecord holding the request as sent and the response
+    as received."""
+    from rust_tensorflow_serving2_amd.models import resnet
+    from rust_tensorflow_serving2_amd.utils.request_log import read_tfrecords
+    import time
+    base = str(tmp_path / "resnet")
+    resnet.export(os.path.join(base, "1"), blocks=(1, 1, 1, 1), width=16, num_classes=10, image_size=160, seed=8)
+    cfg = serving.ModelServerConfig()
+    mc = cfg.model_config_list.config.add(name="resnet", base_path=base, model_platform="tensorflow")
+    mc.logging_config.log_collector_config.filename_prefix = str(tmp_path / "logs" / "resnet")
+    mc.logging_config.sampling_config.sampling_rate = 1.0
+    so = ServableOptions(device="cuda:0", max_batch_size=4, allowed_batch_sizes=(1, 2, 4))
+    srv = ModelServer(ServerOptions(port=0, host="127.0.0.1", model_config=cfg, device="cuda:0", transport="native",
+                                    servable=so, file_system_poll_wait_seconds=0, batch_timeout_us=300)).start()
+    try:
+        tr = srv.transports[0]
+        for _ in range(300):
+            if tr.stats().get("endpoints"):
+                break
+            time.sleep(0.05)
+        assert tr.stats()["endpoints"]
+        rng = np.random.default_rng(9)
+        spec = native.spec_tuple("resnet", None, None, "")
+        bodies = [native.encode_predict_request(spec, {"input": rng.random((1 + i % 2, 160, 160, 3),
+                                                                           dtype=np.float32)})
+                  for i in range(12)]
+
+        async def go():
+            async with grpc.aio.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+                stub = ch.unary_unary(PREDICT)
+                return await asyncio.gather(*[stub(b) for b in bodies])
+        outs = asyncio.run(go())
+        st = tr.srv.stats()
+        assert st["fast_path"] == 12 and st["streamed"] >= 1 and st["slow_path"] == 0, st
+        lg = srv.request_logs.get("resnet")
+        lg.flush()
+        recs = [serving.PredictionLog.FromString(r) for r in read_tfrecords(lg.path)]
+        assert len(recs) == 12
+        sent = dict(zip(bodies, outs))
+        for pl in recs:
+            req = pl.predict_log.request.SerializeToString()
+            assert req in sent and pl.predict_log.response.SerializeToString() == sent[req]
+            assert pl.log_metadata.model_spec.name == "resnet" and pl.log_metadata.model_spec.version.value == 1
+        assert lg.stats()["dropped"] == 0
+    finally:
+        srv.stop()
