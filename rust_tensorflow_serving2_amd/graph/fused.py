@@ -437,7 +437,86 @@ class SoftmaxArgMax:
         return [probs, cls if self.cdt == torch.int64 else cls.to(self.cdt)]
 
 
+class ClassifierHead:
+    """``_GlobalAvgPool -> _FusedMatMul (no act) -> _SoftmaxArgMax`` (the ResNet
+    head) as two launches (``hip().classifier_head``: pooled split-K partial
+    dot products, then bias + partial sums + softmax/argmax) instead of three
+    with a 16-workgroup, 2048-deep serial GEMM in the middle."""
+
+    def __init__(self, mm: FusedMatMul, classes_dtype, use_hip: bool):
+        self.n = mm.n
+        self.cdt = classes_dtype
+        self.use_hip = use_hip and mm.use_hip and mm.k in (512, 1024, 2048, 4096)
+        if mm.use_hip:
+            self.w, self.b = mm.w, mm.b                     # bf16 [Np][K], f32 [Np]
+        else:
+            self.w_ref, self.b_ref = mm.w_ref, mm.b_ref     # f32 [K][N], [N]
+
+    def __call__(self, ctx, node, ins):
+        x = O.to_torch(ins[0])
+        if self.use_hip and x.is_cuda and x.dim() == 4 and x.shape[-1] == self.w.shape[1]:
+            from ..ops import hip
+            probs, cls = hip().classifier_head(_to_bf16(x).contiguous(), self.w, self.b, self.n)
+        else:
+            pooled = x.float().mean(dim=(1, 2))
+            if hasattr(self, "w_ref"):
+                logits = pooled @ self.w_ref.to(x.device) + self.b_ref.to(x.device)
+            else:
+                logits = (pooled @ self.w.float().t().to(x.device) + self.b.to(x.device))[:, :self.n]
+            probs = torch.softmax(logits, dim=-1)
+            cls = torch.argmax(logits, dim=-1)
+        return [probs, cls if self.cdt == torch.int64 else cls.to(self.cdt)]
+
+
+O.OPS["_ClassifierHead"] = _impl_op
+
+_PASSTHROUGH = ("Identity", "Squeeze", "Reshape")
+
+
 # ------------------------------------------------------------------ passes
+def fuse_classifier_head(g, order, fed, fetch_refs, device, opts):
+    """_SoftmaxArgMax(dense(mean_hw(x))) -> _ClassifierHead(x); every node in
+    between must have that single consumer and not be fetched."""
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+
+    def single(node) -> bool:
+        return node.name not in c.fetch_nodes and len(c.cons.get(node.name, [])) == 1
+
+    def walk(ref, chain):
+        n = g.nodes.get(ref[0])
+        while n is not None and n.op in _PASSTHROUGH and ref[1] == 0 and single(n) and n.inputs:
+            chain.append(n)
+            ref = n.inputs[0]
+            n = g.nodes.get(ref[0])
+        return ref, n
+
+    for name in order:
+        sm = g.nodes.get(name)
+        if sm is None or sm.op != "_SoftmaxArgMax" or not sm.inputs:
+            continue
+        chain: List[Node] = []
+        ref, mm = walk(sm.inputs[0], chain)
+        if mm is None or mm.op != "_FusedMatMul" or ref[1] != 0 or len(mm.inputs) != 1 or not single(mm):
+            continue
+        impl = mm.attrs["_impl"]
+        if impl.act != "none":
+            continue
+        chain.append(mm)
+        ref, gap = walk(mm.inputs[0], chain)
+        if gap is None or gap.op != "_GlobalAvgPool" or ref[1] != 0 or not single(gap):
+            continue
+        chain.append(gap)
+        sm_impl = sm.attrs["_impl"]
+        head = ClassifierHead(impl, sm_impl.cdt, c.use_hip)
+        sm.op = "_ClassifierHead"
+        sm.inputs = [gap.inputs[0]]
+        sm.attrs = {"_impl": head}
+        sm.ctrl = _merge_ctrl(chain + [sm])
+        for n in chain:
+            del g.nodes[n.name]
+        c.refresh()
+
+
 def fuse_conv(g, order, fed, fetch_refs, device, opts):
     c = _Ctx(g, order, fed, fetch_refs, device, opts)
     for name in order:
@@ -757,4 +836,4 @@ def fuse_post_activation(g, order, fed, fetch_refs, device, opts):
 def default_passes(options=None):
     from .patterns import bert_passes
     return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_dual_conv, fuse_post_activation,
-                                                                 fuse_matmul]
+                                                                 fuse_matmul, fuse_classifier_head]

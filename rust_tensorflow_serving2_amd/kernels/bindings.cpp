@@ -317,6 +317,28 @@ std::vector<Tensor> softmax_argmax(const Tensor& logits, bool want_probs, bool w
   return {probs, classes};
 }
 
+// ResNet-style head: probs, classes = softmax/argmax(mean_hw(x) @ w^T + bias)[:, :n]
+std::vector<Tensor> classifier_head(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t n) {
+  need(x, at::kBFloat16, "x");
+  need(w, at::kBFloat16, "w");
+  need(bias, at::kFloat, "bias");
+  TORCH_CHECK(x.dim() == 4, "classifier_head: x must be NHWC");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int M = x.size(0), HW = x.size(1) * x.size(2), K = x.size(3);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && (K == 512 || K == 1024 || K == 2048 || K == 4096),
+              "classifier_head: w [Np][K] with K in {512, 1024, 2048, 4096}");
+  const int Np = w.size(0);
+  TORCH_CHECK(bias.numel() == Np && n >= 1 && n <= Np, "classifier_head: bias [Np], 1 <= n <= Np");
+  Tensor part = torch::empty({int64_t(tfsk::classifier_head_ws_floats(M, K, Np))}, x.options().dtype(at::kFloat));
+  Tensor probs = torch::empty({M, n}, x.options().dtype(at::kFloat));
+  Tensor classes = torch::empty({M}, x.options().dtype(at::kLong));
+  check(tfsk::classifier_head_launch(bf16p(x), bf16p(w), bias.data_ptr<float>(), part.data_ptr<float>(),
+                                     probs.data_ptr<float>(), classes.data_ptr<int64_t>(), M, HW, K, Np, int(n),
+                                     cur_stream(x)),
+        "classifier_head");
+  return {probs, classes};
+}
+
 Tensor ingest_c4(const Tensor& x, const c10::optional<Tensor>& out) {
   need(x, at::kFloat, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) <= 4, "ingest_c4: NHWC with C <= 4");
@@ -491,6 +513,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pt"), py::arg("pb"), py::arg("pl"), py::arg("pr"), py::arg("out") = py::none(),
         py::arg("post_scale") = py::none(), py::arg("post_shift") = py::none(), py::arg("post_act") = 0);
   m.def("global_avgpool", &global_avgpool, py::arg("x"), py::arg("out") = py::none());
+  m.def("classifier_head", &classifier_head, "softmax/argmax(mean_hw(x) @ w^T + bias)[:, :n]", py::arg("x"),
+        py::arg("w"), py::arg("bias"), py::arg("n"));
   m.def("softmax_argmax", &softmax_argmax, py::arg("logits"), py::arg("want_probs") = true,
         py::arg("want_classes") = true, py::arg("probs_out") = py::none(), py::arg("classes_out") = py::none());
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("out") = py::none());

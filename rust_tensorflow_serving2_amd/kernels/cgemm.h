@@ -26,7 +26,7 @@ hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t str
 // Config ids kHaloCfgBase .. + kNumHaloConfigs - 1; split-K splits the channel
 // chunks (kt_per_split counts 64-channel chunks).
 constexpr int kHaloCfgBase = 48;
-constexpr int kNumHaloConfigs = 6;
+constexpr int kNumHaloConfigs = 9;
 bool halo_supported(const IGemmArgs& a);
 int halo_config_bm(int cfg);
 int halo_config_bn(int cfg);

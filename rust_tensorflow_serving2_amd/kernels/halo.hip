@@ -13,12 +13,17 @@
 // shifted by kh*(TW+2) + kw rows.  A-intake drops ~9x -> ~1.3-1.9x of the
 // input; only the weight slices (B) stream per tap.
 //
-//   * K loop = (chunk c, tap u) steps, the 9 taps unrolled; B ring of 3 slots
-//     (9 % 3 == 0: slot indices are compile-time), two B tiles in flight;
+//   * K loop = (chunk c, tap u) steps; B ring of S = 3 or 9 slots with S - 1
+//     weight tiles in flight.  Depth matters: a CU takes in ~55 GB/s with 16 KB of
+//     LDS-DMA in flight but 100-125 GB/s with 32-64 KB
+//     (scripts/intake_bench.hip, profiles/round2/intake_bench.log); the first
+//     version kept two 8-KB B tiles in flight and ran the 3x3 layers B-bound;
 //   * the halo of chunk c+1 is DMA'd into the other halo buffer while chunk c
 //     computes (one buffer when C == 64: no next chunk);
-//   * counted vmcnt waits (the per-step count of younger DMAs is known at
-//     compile time except at the tails, which take the exact smaller counts);
+//   * counted vmcnt waits: with the taps unrolled and a separate body for the
+//     last chunk, the number of DMAs issued after B(step) is a compile-time
+//     constant per tap (a run-time switch over it cost ~12 scalar branches per
+//     step and made the kernel slower than the 2-deep original);
 //   * LDS rows are 128 B with 16-B chunks XOR-swizzled by (row & 7), the same
 //     conflict-free image as cgemm; A fragment reads re-derive the swizzle per
 //     tap from the shifted halo row (5 VALU per fragment, hidden under MFMA);
@@ -37,14 +42,15 @@ namespace {
 
 using namespace gemm;
 
-template <int BM, int BN, int WGM, int WGN, int HR>
+template <int BM, int BN, int WGM, int WGN, int HR, int S_>
 struct HG {
   static constexpr int NW = WGM * WGN, NT = 64 * NW;
   static constexpr int WM = BM / WGM, WN = BN / WGN;
   static constexpr int TM = WM / 16, TN = WN / 16;
   static constexpr int HPW = HR / (8 * NW);        // halo 1-KB DMA pieces per wave per chunk
   static constexpr int BPW = BN / (8 * NW);        // B pieces per wave per step
-  static constexpr int S = 3;                      // B ring depth
+  static constexpr int S = S_;                     // B ring depth (S - 1 tiles in flight)
+  static_assert(S == 3 || S == 9, "ring depth must divide the 9 taps (static slots)");
   static constexpr int HALO_B = HR * 128;          // bytes of one halo buffer
   static constexpr int B_B = BN * 128;             // bytes of one B ring slot
   static constexpr int CS_LD = BN + 4;
@@ -55,13 +61,13 @@ struct HG {
   static_assert(HPW >= 1 && HR % (8 * NW) == 0, "halo DMA split");
   static_assert(BPW >= 1 && BN % (8 * NW) == 0, "B DMA split");
   static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
-  static_assert(HPW + BPW < 64, "vmcnt range");
+  static_assert(HPW + BPW * (S - 2) <= 39, "vmcnt immediate range");
   static_assert(lds(2) <= 160 * 1024, "LDS budget");
 };
 
-template <int BM, int BN, int WGM, int WGN, int HR>
+template <int BM, int BN, int WGM, int WGN, int HR, int S>
 __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) {
-  using G = HG<BM, BN, WGM, WGN, HR>;
+  using G = HG<BM, BN, WGM, WGN, HR, S>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   char* const smem = reinterpret_cast<char*>(smem_raw);
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -183,36 +189,44 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
   float4 bias0, bias1;
   prefetch_bias<BM, BN, G::NT>(p, n0, tid, bias0, bias1);
 
-  // ---- prologue: halo of the first chunk, two B tiles
+  // ---- steps t = (chunk c0 + t / 9, tap u = t % 9); B(t) lands in slot
+  // t % S = u % S (S divides 9), D = S - 1 tiles issued ahead.  Every chunk but
+  // the last has the same DMA schedule, so the taps are unrolled and every
+  // wait count is an immediate: DMAs younger than B(t) are B(t+1 .. t+D-1)
+  // (fewer in the last chunk's tail) plus this chunk's halo issue when it went
+  // out after B(t), i.e. at tap 0 with 1 <= u < D.
+  constexpr int D = G::S - 1;
+  const int nck = c1 - c0;
   issue_halo(c0);
-  issue_b(c0, 0, 0);
-  issue_b(c0, 1, 1);
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < nck * 9) issue_b(c0 + j / 9, j % 9, j % G::S);
 
-  for (int c = c0; c < c1; ++c) {
-    const bool hasH = c + 1 < c1;      // this chunk's tap-0 step issues the next halo
+  auto chunk = [&](auto last_tag, int c) {
+    constexpr bool LAST = decltype(last_tag)::value;
     const char* hb = smem + ((c - c0) & 1) * G::HALO_B;
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
-      // younger DMAs than B(step) = what the previous step issued: B(step + 1)
-      // (absent at the last step) and, after a tap-0 step, the next halo
-      const bool hasB1 = !(c + 1 == c1 && u == 8);
-      if (u == 1) {
-        if (hasH) {
-          if (hasB1) wait_vmcnt<G::HPW + G::BPW>(); else wait_vmcnt<G::HPW>();
-        } else {
-          if (hasB1) wait_vmcnt<G::BPW>(); else wait_vmcnt<0>();
-        }
-      } else {
-        if (hasB1) wait_vmcnt<G::BPW>(); else wait_vmcnt<0>();
+      const int nb = LAST ? (D - 1 < 8 - u ? D - 1 : 8 - u) : D - 1;
+      const int younger = G::BPW * nb + ((!LAST && u >= 1 && u < D) ? G::HPW : 0);
+      switch (younger) {   // folds to one immediate per unrolled tap
+#define TFSK_W(k) case k: wait_vmcnt<k>(); break;
+        TFSK_W(0) TFSK_W(1) TFSK_W(2) TFSK_W(3) TFSK_W(4) TFSK_W(5) TFSK_W(6) TFSK_W(7) TFSK_W(8) TFSK_W(9)
+        TFSK_W(10) TFSK_W(11) TFSK_W(12) TFSK_W(13) TFSK_W(14) TFSK_W(15) TFSK_W(16) TFSK_W(17) TFSK_W(18)
+        TFSK_W(19) TFSK_W(20) TFSK_W(21) TFSK_W(22) TFSK_W(23) TFSK_W(24) TFSK_W(25) TFSK_W(26) TFSK_W(27)
+        TFSK_W(28) TFSK_W(29) TFSK_W(30) TFSK_W(31) TFSK_W(32) TFSK_W(33) TFSK_W(34) TFSK_W(35) TFSK_W(36)
+        TFSK_W(37) TFSK_W(38) TFSK_W(39)
+#undef TFSK_W
+        default: wait_vmcnt<40>(); break;
       }
       lds_barrier();   // every wave's DMAs landed; the slot / buffer about to be refilled is read-free
-      if (u == 0 && hasH) issue_halo(c + 1);
-      // B of step + 2: (c, u + 2) or (c + 1, u - 7)
-      if (u + 2 < 9) issue_b(c, u + 2, (u + 2) % 3);
-      else if (c + 1 < c1) issue_b(c + 1, u - 7, (u + 2) % 3);
-      compute(hb, ring + (u % 3) * G::B_B, (u / 3) * HW2 + (u % 3));
+      if (!LAST && u == 0) issue_halo(c + 1);
+      if (!LAST || u + D < 9) issue_b(c + (u + D) / 9, (u + D) % 9, (u + D) % G::S);
+      compute(hb, ring + (u % G::S) * G::B_B, (u / 3) * HW2 + (u % 3));
     }
-  }
+  };
+  for (int c = c0; c < c1 - 1; ++c) chunk(std::false_type{}, c);
+  chunk(std::true_type{}, c1 - 1);
   wait_vmcnt<0>();
   __syncthreads();
 
@@ -299,9 +313,9 @@ bool pick_block(int Ho, int Wo, int BM, int HR, int& TH, int& TW) {
   return best_tiles > 0;
 }
 
-template <int BM, int BN, int WGM, int WGN, int HR>
+template <int BM, int BN, int WGM, int WGN, int HR, int S>
 hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
-  using G = HG<BM, BN, WGM, WGN, HR>;
+  using G = HG<BM, BN, WGM, WGN, HR, S>;
   IGemmArgs a = a0;
   if (!pick_block(a.Ho, a.Wo, BM, HR, a.TH, a.TW)) return hipErrorInvalidValue;
   const int nch = a.C / KT;
@@ -313,14 +327,15 @@ hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
   if (tiles == 0) return hipSuccess;
   if (tiles >= (1L << 31)) return hipErrorInvalidValue;
   const int lds = G::lds(per > 1 ? 2 : 1);
-  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&halo_conv_kernel<BM, BN, WGM, WGN, HR>), G::lds(2));
+  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&halo_conv_kernel<BM, BN, WGM, WGN, HR, S>), G::lds(2));
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((halo_conv_kernel<BM, BN, WGM, WGN, HR>), dim3(unsigned(tiles), splits), dim3(G::NT), lds, s, a);
+  hipLaunchKernelGGL((halo_conv_kernel<BM, BN, WGM, WGN, HR, S>), dim3(unsigned(tiles), splits), dim3(G::NT), lds, s,
+                     a);
   return hipGetLastError();
 }
 
-constexpr int kHBM[kNumHaloConfigs] = {256, 128, 128, 64, 256, 64};
-constexpr int kHBN[kNumHaloConfigs] = {64, 128, 64, 64, 128, 128};
+constexpr int kHBM[kNumHaloConfigs] = {256, 128, 128, 64, 256, 64, 64, 128, 256};
+constexpr int kHBN[kNumHaloConfigs] = {64, 128, 64, 64, 128, 128, 64, 64, 64};
 
 }  // namespace
 
@@ -337,12 +352,17 @@ int halo_config_bn(int cfg) { return kHBN[cfg - kHaloCfgBase]; }
 hipError_t halo_launch(const IGemmArgs& a, int cfg, hipStream_t s) {
   if (cfg < kHaloCfgBase || cfg >= kHaloCfgBase + kNumHaloConfigs || !halo_supported(a)) return hipErrorInvalidValue;
   switch (cfg - kHaloCfgBase) {
-    case 0: return launch_halo_cfg<256, 64, 4, 1, 320>(a, s);    // 104 KB (64 KB for C == 64), waves 64x64
-    case 1: return launch_halo_cfg<128, 128, 2, 2, 192>(a, s);   // 96 KB, waves 64x64
-    case 2: return launch_halo_cfg<128, 64, 2, 2, 192>(a, s);    // 72 KB (48 KB), waves 64x32
-    case 3: return launch_halo_cfg<64, 64, 2, 2, 128>(a, s);     // 56 KB (40 KB), waves 32x32
-    case 4: return launch_halo_cfg<256, 128, 4, 2, 320>(a, s);   // 135 KB, 8 waves of 64x64
-    case 5: return launch_halo_cfg<64, 128, 2, 2, 128>(a, s);    // 80 KB, waves 32x64
+    // LDS = 2 halo buffers (HR x 128 B; one when C == 64) + S B slots (BN x 128 B)
+    case 0: return launch_halo_cfg<256, 64, 4, 1, 320, 3>(a, s);    // 104 KB (64 KB for C == 64), waves 64x64
+    case 1: return launch_halo_cfg<128, 128, 2, 2, 192, 3>(a, s);   // 96 KB, waves 64x64
+    case 2: return launch_halo_cfg<128, 64, 2, 2, 192, 3>(a, s);    // 72 KB (48 KB), waves 64x32
+    case 3: return launch_halo_cfg<64, 64, 2, 2, 128, 3>(a, s);     // 56 KB (40 KB), waves 32x32
+    case 4: return launch_halo_cfg<256, 128, 4, 2, 320, 3>(a, s);   // 135 KB, 8 waves of 64x64
+    case 5: return launch_halo_cfg<64, 128, 2, 2, 128, 3>(a, s);    // 80 KB, waves 32x64
+    // 9-slot rings: 8 weight tiles in flight (16 x 1-KB DMAs per wave)
+    case 6: return launch_halo_cfg<64, 64, 2, 2, 128, 9>(a, s);     // 104 KB, waves 32x32
+    case 7: return launch_halo_cfg<128, 64, 2, 2, 192, 9>(a, s);    // 120 KB, waves 64x32
+    case 8: return launch_halo_cfg<256, 64, 4, 1, 320, 9>(a, s);    // 152 KB, waves 64x64
     default: return hipErrorInvalidValue;
   }
 }

@@ -93,6 +93,14 @@ hipError_t maxpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int H, int
 hipError_t global_avgpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int HW, int C,
                                       hipStream_t stream);
 // Row softmax (fp32 in) -> probs f32 + argmax int64 (the classifier head).
+// GlobalAvgPool + dense + softmax/argmax (misc.hip): x [M][HW][K] bf16 (NHWC
+// feature map, K % 256 == 0), w [Np][K] bf16, bias [Np] f32, ws = f32
+// workspace of classifier_head_ws_floats(M, K, Np); probs [M][N] f32 and
+// classes [M] for the first N <= Np columns.
+hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const float* bias, float* ws,
+                                  float* probs, int64_t* classes, int M, int HW, int K, int Np, int N,
+                                  hipStream_t s);
+size_t classifier_head_ws_floats(int M, int K, int Np);
 hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, int64_t* classes,
                                  int rows, int cols, long ld, hipStream_t stream);
 // fp32 -> bf16 cast (vectorized).

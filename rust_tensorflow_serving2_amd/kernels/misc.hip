@@ -2,6 +2,7 @@
 // LayerNorm, embedding+LN.  All bf16 traffic is 16-B vectorised (8 elements
 // per lane), reductions are wave64 shuffles.
 #include "common.h"
+#include "gemm_common.h"
 #include "launch.h"
 
 namespace tfsk {
@@ -121,17 +122,32 @@ __global__ __launch_bounds__(256) void gap_nhwc_kernel(const uint16_t* __restric
 // registers (up to 16 per thread, i.e. rows of <= 4096 classes stay in
 // registers), max/argmax and the exp-sum are block reductions (wave shuffles
 // + LDS).  ArgMax ties resolve to the smallest index (TF semantics).
+// With `parts`, a logit is bias[c] + the sum of `nparts` split-K partial rows
+// (parts[p * part_stride + row * ld + c]): the classifier head's reduction.
 constexpr int kSmPer = 16;
+template <int NPARTS>
 __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restrict__ logits, int in_bf16,
                                                              float* __restrict__ probs,
                                                              int64_t* __restrict__ classes, int rows, int cols,
-                                                             long ld) {
+                                                             long ld, const float* __restrict__ parts,
+                                                             long part_stride, const float* __restrict__ bias) {
   __shared__ float smx[4];
   __shared__ int sarg[4];
   __shared__ float ssum[4];
   const int row = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (row >= rows) return;
+  auto load = [&](int c) -> float {
+    if constexpr (NPARTS > 0) {
+      float a = bias[c];
+      const float* q = parts + long(row) * ld + c;
+#pragma unroll
+      for (int p = 0; p < NPARTS; ++p) a += q[p * part_stride];
+      return a;
+    }
+    return in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * ld + c])
+                   : static_cast<const float*>(logits)[long(row) * ld + c];
+  };
   float v[kSmPer];
   float mx = -INFINITY;
   int arg = 0x7fffffff;
@@ -139,16 +155,13 @@ __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restr
   for (int k = 0; k < kSmPer; ++k) {
     const int c = k * 256 + tid;
     float x = -INFINITY;
-    if (c < cols)
-      x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * ld + c])
-                  : static_cast<const float*>(logits)[long(row) * ld + c];
+    if (c < cols) x = load(c);
     v[k] = x;
     if (c < cols && (x > mx || (x == mx && c < arg))) { mx = x; arg = c; }
   }
   // columns beyond the register tile (cols > 4096): strided tail, recomputed below
   for (int c = kSmPer * 256 + tid; c < cols; c += 256) {
-    const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * ld + c])
-                            : static_cast<const float*>(logits)[long(row) * ld + c];
+    const float x = load(c);
     if (x > mx || (x == mx && c < arg)) { mx = x; arg = c; }
   }
 #pragma unroll
@@ -171,11 +184,7 @@ __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restr
     v[k] = (k * 256 + tid < cols) ? __expf(v[k] - mx) : 0.f;
     s += v[k];
   }
-  for (int c = kSmPer * 256 + tid; c < cols; c += 256) {
-    const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * ld + c])
-                            : static_cast<const float*>(logits)[long(row) * ld + c];
-    s += __expf(x - mx);
-  }
+  for (int c = kSmPer * 256 + tid; c < cols; c += 256) s += __expf(load(c) - mx);
   s = wave_sum(s);
   if (lane == 0) ssum[w] = s;
   __syncthreads();
@@ -186,13 +195,121 @@ __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restr
       const int c = k * 256 + tid;
       if (c < cols) probs[long(row) * cols + c] = v[k] * inv;
     }
-    for (int c = kSmPer * 256 + tid; c < cols; c += 256) {
-      const float x = in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * ld + c])
-                              : static_cast<const float*>(logits)[long(row) * ld + c];
-      probs[long(row) * cols + c] = __expf(x - mx) * inv;
-    }
+    for (int c = kSmPer * 256 + tid; c < cols; c += 256) probs[long(row) * cols + c] = __expf(load(c) - mx) * inv;
   }
   if (classes && tid == 0) classes[row] = arg;
+}
+
+// ---------------------------------------------------------------- classifier head
+// GlobalAvgPool -> dense -> (softmax + argmax), the ResNet head, as three short
+// launches that each fill the chip, instead of gap + a 16-workgroup GEMM with
+// a 2048-deep serial K loop (17.6 us at b32) + softmax:
+//   1. gap_rows: workgroup (row, 64-channel slice), 32 lane groups split the
+//      HW positions (<= 2 loads per lane for 7x7), bf16 pooled rows [M][K];
+//   2. fc_partial: workgroup (K slice, 32 columns), one v_mfma 16x16x32 tile
+//      pair per 32 rows, operands straight from global (every load of the
+//      slice in flight at once), 4 waves split the slice and meet in LDS ->
+//      f32 partial rows [KS][M][Np];
+//   3. softmax_argmax<KS> above: bias + the KS partials per logit.
+// Deterministic (no atomics).  Measured on the way (b32, rocprofv3): a fused
+// pool + 32-slice VALU version took 15 + 35 us, a VALU dot-product version
+// 27 us (LDS-read bound) for the middle kernel.
+constexpr int kHeadKS = 4, kHeadCols = 32;
+__global__ __launch_bounds__(256) void gap_rows_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ pooled,
+                                                       int HW, int K, float inv_hw) {
+  __shared__ float part[32][8][9];
+  const int m = blockIdx.x, k0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, cg = tid & 7, hs = tid >> 3;
+  float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint16_t* p = x + long(m) * HW * K + k0 + cg * 8;
+  for (int hw = hs; hw < HW; hw += 32) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(p + long(hw) * K), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s8[e] += f[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[hs][cg][e] = s8[e];
+  __syncthreads();
+  if (tid < 64) {
+    const int g = tid >> 3, e = tid & 7;
+    float a = 0.f;
+#pragma unroll 8
+    for (int h = 0; h < 32; ++h) a += part[h][g][e];
+    pooled[long(m) * K + k0 + tid] = f32_to_bf16(a * inv_hw);
+  }
+}
+
+// K slice = K / kHeadKS channels, split over the 4 waves (kw = K slice / 4 each,
+// a multiple of 32); a wave holds 2 x 2 16x16 accumulators (32 rows x 32 cols).
+template <int KSTEPS>
+__global__ __launch_bounds__(256) void fc_partial_kernel(const uint16_t* __restrict__ pooled,
+                                                         const uint16_t* __restrict__ w, float* __restrict__ part,
+                                                         int M, int K, int Np) {
+  __shared__ float red[3][32][33];
+  const int ks = blockIdx.x, ns = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int kslice = K / kHeadKS, kw = kslice / 4;
+  const int k0 = ks * kslice + wid * kw;
+  const int n0 = ns * kHeadCols;
+  // B fragments of this wave's K range: rows n0 + j*16 + fr (zero past Np)
+  bf16x8 bfr[KSTEPS][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + j * 16 + fr;
+#pragma unroll
+    for (int t = 0; t < KSTEPS; ++t)
+      bfr[t][j] = n < Np ? *reinterpret_cast<const bf16x8*>(w + long(n) * K + k0 + t * 32 + fq * 8)
+                         : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  for (int m0 = 0; m0 < M; m0 += 32) {
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 afr[KSTEPS][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = m0 + i * 16 + fr;
+#pragma unroll
+      for (int t = 0; t < KSTEPS; ++t)
+        afr[t][i] = m < M ? *reinterpret_cast<const bf16x8*>(pooled + long(m) * K + k0 + t * 32 + fq * 8)
+                          : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int t = 0; t < KSTEPS; ++t)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[t][i], bfr[t][j], acc[i][j], 0, 0, 0);
+    // waves 1..3 hand their tiles to wave 0 (C layout: row fq*4 + r, column fr)
+    if (wid > 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[wid - 1][i * 16 + fq * 4 + r][j * 16 + fr] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (wid == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int rr = i * 16 + fq * 4 + r, cc = j * 16 + fr;
+            const int m = m0 + rr, n = n0 + cc;
+            if (m < M && n < Np)
+              part[(long(ks) * M + m) * Np + n] = acc[i][j][r] + red[0][rr][cc] + red[1][rr][cc] + red[2][rr][cc];
+          }
+    }
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------- casts
@@ -464,9 +581,38 @@ hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, 
                                  int cols, long ld, hipStream_t s) {
   if (rows <= 0) return hipSuccess;
   if (ld < cols) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(softmax_argmax_kernel, dim3(rows), dim3(256), 0, s, logits, in_bf16, probs, classes, rows,
-                     cols, ld);
+  hipLaunchKernelGGL(softmax_argmax_kernel<0>, dim3(rows), dim3(256), 0, s, logits, in_bf16, probs, classes, rows,
+                     cols, ld, static_cast<const float*>(nullptr), 0L, static_cast<const float*>(nullptr));
   return hipGetLastError();
+}
+
+hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const float* bias, float* ws, float* probs,
+                                  int64_t* classes, int M, int HW, int K, int Np, int N, hipStream_t s) {
+  if (M <= 0) return hipSuccess;
+  if (K % (kHeadKS * 4 * 32) || N > Np || N <= 0 || HW <= 0) return hipErrorInvalidValue;
+  const int ksteps = K / kHeadKS / 4 / 32;        // 32-deep MFMA steps per wave
+  uint16_t* pooled = reinterpret_cast<uint16_t*>(ws);
+  float* part = ws + (size_t(M) * K + 1) / 2;
+  hipLaunchKernelGGL(gap_rows_kernel, dim3(M, K / 64), dim3(256), 0, s, x, pooled, HW, K, 1.f / float(HW));
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const dim3 grid(kHeadKS, (Np + kHeadCols - 1) / kHeadCols);
+  switch (ksteps) {
+    case 1: hipLaunchKernelGGL(fc_partial_kernel<1>, grid, dim3(256), 0, s, pooled, w, part, M, K, Np); break;
+    case 2: hipLaunchKernelGGL(fc_partial_kernel<2>, grid, dim3(256), 0, s, pooled, w, part, M, K, Np); break;
+    case 4: hipLaunchKernelGGL(fc_partial_kernel<4>, grid, dim3(256), 0, s, pooled, w, part, M, K, Np); break;
+    case 8: hipLaunchKernelGGL(fc_partial_kernel<8>, grid, dim3(256), 0, s, pooled, w, part, M, K, Np); break;
+    default: return hipErrorInvalidValue;
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(softmax_argmax_kernel<kHeadKS>, dim3(M), dim3(256), 0, s, static_cast<const void*>(nullptr), 0,
+                     probs, classes, M, N, long(Np), static_cast<const float*>(part), long(M) * Np, bias);
+  return hipGetLastError();
+}
+
+size_t classifier_head_ws_floats(int M, int K, int Np) {
+  return (size_t(M) * K + 1) / 2 + size_t(kHeadKS) * M * Np;   // bf16 pooled rows + f32 partials
 }
 
 hipError_t cast_f32_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t s) {

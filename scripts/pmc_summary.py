@@ -1,28 +1,75 @@
-"""Per-kernel PMC counter averages from a rocprofv3 --pmc run (rocpd sqlite or counter CSV)."""
+"""Per-kernel PMC counter averages from a rocprofv3 --pmc run (rocpd sqlite).
+
+    python scripts/pmc_summary.py /tmp/prof_pmc                 # averages per kernel name
+    python scripts/pmc_summary.py /tmp/prof_pmc --replay ingest  # one graph replay, per dispatch
+
+``--replay FIRST`` lists the dispatches of the last complete replay (between the
+last two launches of the kernel whose name contains FIRST) in order, one row
+per layer, with MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x
+kernel cycles), kernel cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums GRBM over
+the 8 XCDs; MI355X_MICROARCH.md 'DVFS give-back').
+"""
+import argparse
 import glob
 import sqlite3
-import sys
 from collections import defaultdict
 
 
+def _short(k: str) -> str:
+    return k.replace("void ", "").replace("tfsk::(anonymous namespace)::", "").split("(tfsk")[0].split("(")[0][:60]
+
+
+def _columns(c, table):
+    return [r[1] for r in c.execute(f"pragma table_info({table})")]
+
+
 def main():
-    path = sys.argv[1]
-    dbs = glob.glob(path + "/**/*.db", recursive=True) if not path.endswith(".db") else [path]
-    agg = defaultdict(lambda: defaultdict(list))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("path")
+    ap.add_argument("--replay", default=None, help="substring of the replay's first kernel")
+    a = ap.parse_args()
+    dbs = glob.glob(a.path + "/**/*.db", recursive=True) if not a.path.endswith(".db") else [a.path]
+    per_dispatch = {}        # (db, dispatch) -> [name, {counter: value}]
     for db in dbs:
         c = sqlite3.connect(db)
         tabs = [r[0] for r in c.execute("select name from sqlite_master where type in ('table','view')")]
-        if "counters_collection" in tabs:
-            q = "select kernel_name, counter_name, value from counters_collection"
-        else:
+        if "counters_collection" not in tabs:
             print("tables:", tabs)
             return
-        for k, n, v in c.execute(q):
-            agg[k][n].append(v)
-    for k, d in sorted(agg.items()):
-        short = k.replace("void ", "").replace("tfsk::(anonymous namespace)::", "").split("(tfsk")[0][:70]
-        vals = " ".join(f"{n}={sum(v)/len(v):.4g}" for n, v in sorted(d.items()))
-        print(f"{short}: {vals}")
+        cols = _columns(c, "counters_collection")
+        did = "dispatch_id" if "dispatch_id" in cols else ("correlation_id" if "correlation_id" in cols else None)
+        sel = f"kernel_name, counter_name, value, {did}" if did else "kernel_name, counter_name, value, rowid"
+        for k, n, v, d in c.execute(f"select {sel} from counters_collection"):
+            ent = per_dispatch.setdefault((db, d), [k, defaultdict(float)])
+            ent[1][n] += v
+    if a.replay is None:
+        agg = defaultdict(lambda: defaultdict(list))
+        for k, d in per_dispatch.values():
+            for n, v in d.items():
+                agg[k][n].append(v)
+        for k, d in sorted(agg.items()):
+            vals = " ".join(f"{n}={sum(v)/len(v):.4g}" for n, v in sorted(d.items()))
+            print(f"{_short(k)}: {vals}")
+        return
+    rows = [per_dispatch[key] for key in sorted(per_dispatch, key=lambda x: (x[0], x[1]))]
+    idx = [i for i, (k, _d) in enumerate(rows) if a.replay in k]
+    if len(idx) < 2:
+        raise SystemExit(f"need two dispatches of {a.replay!r}, found {len(idx)}")
+    rep = rows[idx[-2]:idx[-1]]
+    tot_busy = tot_cyc = 0.0
+    print(f"{'#':>3} {'kernel':60s} {'kcycles':>9} {'mfma%':>6} {'wait%':>6} {'active%':>7}")
+    for i, (k, d) in enumerate(rep):
+        cyc = d.get("GRBM_GUI_ACTIVE", 0.0) / 8
+        busy = d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        util = busy / (1024 * cyc) if cyc else 0.0
+        wc = d.get("SQ_WAVE_CYCLES", 0.0)
+        wait = d.get("SQ_WAIT_ANY", 0.0) / wc if wc else 0.0
+        act = d.get("SQ_ACTIVE_INST_ANY", 0.0) / wc if wc else 0.0
+        tot_busy += busy
+        tot_cyc += cyc
+        print(f"{i:3d} {_short(k):60s} {cyc / 1e3:9.1f} {100 * util:6.1f} {100 * wait:6.1f} {100 * act:7.1f}")
+    print(f"replay: {len(rep)} dispatches, {tot_cyc / 1e3:.1f} kcycles, "
+          f"MFMA busy {100 * tot_busy / (1024 * tot_cyc) if tot_cyc else 0:.1f}% of SIMD-cycles")
 
 
 if __name__ == "__main__":

@@ -104,7 +104,7 @@ def test_cgemm_conv_matches_fp32(shape, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
 
 
-HALO_CFGS = list(range(48, 54))
+HALO_CFGS = list(range(48, 57))
 HALO_SHAPES = [
     # N, H, W, Cin, Cout, pads            (3x3 stride 1; ResNet-50 stages + edge cases)
     (2, 56, 56, 64, 64, (1, 1, 1, 1)),
@@ -437,6 +437,26 @@ def test_embedding_out_of_range_rows_are_zero(hd):
     assert (e2.float().cpu() - F.layer_norm(wz[wi], (hd,), gm, bt, 1e-6)).abs().max() < 5e-2
     with pytest.raises(RuntimeError):
         hip().embed_ln(ids.to(DEV), None, word.to(DEV), None, None, gm.to(DEV), bt.to(DEV), 1e-6, 5)   # 32 % 5
+
+
+@pytest.mark.parametrize("m,hw,k,np_,n", [(32, 49, 2048, 1001, 1001), (32, 49, 2048, 1008, 1001), (1, 49, 2048, 1001, 1001),
+                                         (3, 4, 512, 10, 10), (70, 9, 1024, 300, 257), (5, 1, 4096, 33, 33)])
+def test_classifier_head_matches_fp32(m, hw, k, np_, n):
+    """mean_hw -> dense -> softmax/argmax in two launches (split-K partial rows,
+    then bias + partial sums + softmax) vs fp32; rows in several 32-row chunks,
+    a weight matrix padded past the n classes read."""
+    x = rnd(m, hw, 1, k, seed=41).to(BF)
+    w = rnd(np_, k, scale=0.05, seed=42).to(BF)
+    b = rnd(np_, scale=0.1, seed=43)
+    probs, cls = hip().classifier_head(x.to(DEV), w.to(DEV), b.to(DEV), n)
+    pooled = x.float().mean(dim=(1, 2)).to(BF).float()        # the kernel pools into bf16 (MFMA operand)
+    logits = (pooled @ w.float().t() + b)[:, :n]
+    ref = torch.softmax(logits, -1)
+    assert probs.shape == (m, n) and cls.shape == (m,)
+    assert (probs.cpu() - ref).abs().max() < 1e-4
+    top2 = logits.topk(2, -1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 1e-3                 # rows whose argmax is not a near-tie
+    assert torch.equal(cls.cpu()[clear], logits.argmax(-1)[clear])
 
 
 @pytest.mark.parametrize("s", [64, 128, 256,
