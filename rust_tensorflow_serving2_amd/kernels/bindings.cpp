@@ -27,7 +27,7 @@ void check(hipError_t e, const char* what) {
 // cfg < kNumIGemmConfigs: igemm.hip (any operand mode); cfg in [kCGemmCfgBase,
 // kCGemmCfgBase + kNumCGemmConfigs): the pipelined cgemm.hip kernel (64-aligned operands).
 bool is_cgemm_cfg(int64_t cfg) {
-  return cfg >= tfsk::kCGemmCfgBase && cfg < tfsk::kCGemmCfgBase + tfsk::kNumCGemmConfigs;
+  return cfg >= 0 && cfg < (1 << 20) && tfsk::cgemm_cfg_id(int(cfg));
 }
 
 // halo-tiled 3x3 stride-1 conv configs (halo.hip)
@@ -535,6 +535,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cgemm_configs", []() {
     std::vector<int> v;
     for (int c = 0; c < tfsk::kNumCGemmConfigs; ++c) v.push_back(tfsk::kCGemmCfgBase + c);
+    for (int c = 0; c < tfsk::kNumCGemmConfigs2; ++c) v.push_back(tfsk::kCGemmCfgBase2 + c);
     return v;
   });
   m.def("halo_configs", []() {

@@ -8,6 +8,13 @@ namespace tfsk {
 // kernel family: cgemm configs are kCGemmCfgBase .. kCGemmCfgBase + kNumCGemmConfigs - 1.
 constexpr int kCGemmCfgBase = 32;
 constexpr int kNumCGemmConfigs = 16;
+// a second id range (after the halo ids): 2-wave and 3-deep variants
+constexpr int kCGemmCfgBase2 = 64;
+constexpr int kNumCGemmConfigs2 = 8;
+inline bool cgemm_cfg_id(int cfg) {
+  return (cfg >= kCGemmCfgBase && cfg < kCGemmCfgBase + kNumCGemmConfigs) ||
+         (cfg >= kCGemmCfgBase2 && cfg < kCGemmCfgBase2 + kNumCGemmConfigs2);
+}
 
 // Operand requirements (else cgemm_launch returns hipErrorInvalidValue):
 //   dense (a_mode kADense): K % 64 == 0, lda % 8 == 0;

@@ -412,8 +412,16 @@ hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
 
 // Config table (tile BM x BN, wave grid, ring depth).  LDS per workgroup =
 // S * (BM + BN) * 128 B (or the fp32 epilogue tile if larger).
-constexpr int kBM[kNumCGemmConfigs] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256, 64, 64, 128, 128, 128, 64};
-constexpr int kBN[kNumCGemmConfigs] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64, 64, 128, 64, 96, 96, 96};
+constexpr int kAll = kNumCGemmConfigs + kNumCGemmConfigs2;
+constexpr int kBM[kAll] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256, 64, 64, 128, 128, 128, 64,
+                           64, 64, 64, 128, 64, 128, 64, 64};
+constexpr int kBN[kAll] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64, 64, 128, 64, 96, 96, 96,
+                           64, 64, 64, 64, 128, 64, 128, 64};
+
+// config id -> index into the tables (both id ranges)
+int cfg_index(int cfg) {
+  return cfg < kCGemmCfgBase2 ? cfg - kCGemmCfgBase : kNumCGemmConfigs + (cfg - kCGemmCfgBase2);
+}
 
 template <int AM>
 hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
@@ -439,6 +447,17 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
     case 13: return launch_cfg<128, 96, 2, 2, 3, AM>(a, s);   // 84 KB, wave 64x48
     case 14: return launch_cfg<128, 96, 2, 2, 4, AM>(a, s);   // 112 KB
     case 15: return launch_cfg<64, 96, 2, 2, 3, AM>(a, s);    // 60 KB, wave 32x48
+    // two waves per workgroup: a 64x64 tile as two 64x32 wave tiles reads 24 KB
+    // of LDS fragments per k-step instead of the 32 KB four 32x32 waves read
+    // (whose LDS reads take as long as their MFMAs at 256 B/clk)
+    case 16: return launch_cfg<64, 64, 1, 2, 2, AM>(a, s);    // 32 KB, wave 64x32
+    case 17: return launch_cfg<64, 64, 1, 2, 3, AM>(a, s);    // 48 KB
+    case 18: return launch_cfg<64, 64, 2, 1, 3, AM>(a, s);    // 48 KB, wave 32x64
+    case 19: return launch_cfg<128, 64, 2, 1, 2, AM>(a, s);   // 48 KB, wave 64x64
+    case 20: return launch_cfg<64, 128, 1, 2, 2, AM>(a, s);   // 48 KB, wave 64x64
+    case 21: return launch_cfg<128, 64, 2, 1, 3, AM>(a, s);   // 72 KB, wave 64x64
+    case 22: return launch_cfg<64, 128, 1, 2, 3, AM>(a, s);   // 72 KB, wave 64x64
+    case 23: return launch_cfg<64, 64, 2, 2, 3, AM>(a, s);    // 48 KB, wave 32x32
     default: return hipErrorInvalidValue;
   }
 }
@@ -462,13 +481,12 @@ bool cgemm_supported(const IGemmArgs& a, int a_mode) {
   return false;
 }
 
-int cgemm_config_bm(int cfg) { return kBM[cfg - kCGemmCfgBase]; }
-int cgemm_config_bn(int cfg) { return kBN[cfg - kCGemmCfgBase]; }
+int cgemm_config_bm(int cfg) { return kBM[cfg_index(cfg)]; }
+int cgemm_config_bn(int cfg) { return kBN[cfg_index(cfg)]; }
 
 hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) {
-  if (cfg < kCGemmCfgBase || cfg >= kCGemmCfgBase + kNumCGemmConfigs || !cgemm_supported(a, a_mode))
-    return hipErrorInvalidValue;
-  cfg -= kCGemmCfgBase;
+  if (!cgemm_cfg_id(cfg) || !cgemm_supported(a, a_mode)) return hipErrorInvalidValue;
+  cfg = cfg_index(cfg);
   switch (a_mode) {
     case kAIm2col: return launch_mode<1>(a, cfg, s);
     case kADual: return launch_mode<2>(a, cfg, s);
