@@ -415,6 +415,64 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
   }
 }
 
+// Exact-fit rows (cols == LPR * 8 * CH, e.g. BERT-base 768 = 32 lanes x 3
+// chunks): LPR lanes per row, 64 / LPR rows per wave, gamma / beta loaded into
+// registers before the row arrives (their latency hides under the row's), no
+// idle lanes in the last chunk (the one-wave-per-row kernel above leaves half
+// of a wave idle for 768 columns).  Two-pass statistics from registers.
+template <int LPR, int CH>
+__global__ __launch_bounds__(256) void layernorm_fit_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ r,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta,
+                                                            uint16_t* __restrict__ y, int rows, float eps) {
+  constexpr int COLS = LPR * 8 * CH;
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / LPR, l = lane % LPR;
+  const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub;
+  float g[CH][8], b[CH][8];
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int c = (k * LPR + l) * 8;
+    const float4 g0 = *reinterpret_cast<const float4*>(gamma + c), g1 = *reinterpret_cast<const float4*>(gamma + c + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(beta + c), b1 = *reinterpret_cast<const float4*>(beta + c + 4);
+    g[k][0] = g0.x; g[k][1] = g0.y; g[k][2] = g0.z; g[k][3] = g0.w;
+    g[k][4] = g1.x; g[k][5] = g1.y; g[k][6] = g1.z; g[k][7] = g1.w;
+    b[k][0] = b0.x; b[k][1] = b0.y; b[k][2] = b0.z; b[k][3] = b0.w;
+    b[k][4] = b1.x; b[k][5] = b1.y; b[k][6] = b1.z; b[k][7] = b1.w;
+  }
+  const bool ok = row < rows;
+  const long base = long(ok ? row : 0) * COLS;
+  float v[CH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    ln_load(x + base, r ? r + base : nullptr, (k * LPR + l) * 8, v[k]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[k][e];
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s * (1.f / COLS);
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < CH; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float d = v[k][e] - mean; ss += d * d; }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  const float inv = rsqrtf(ss * (1.f / COLS) + eps);
+  if (!ok) return;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    float o8[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o8[e] = (v[k][e] - mean) * inv * g[k][e] + b[k][e];
+    *reinterpret_cast<uint4*>(y + base + (k * LPR + l) * 8) = pack8(o8);
+  }
+}
+
 // ---------------------------------------------------------------- embedding + LN
 // One wave per token: y[t] = LN(word[ids[t]] + type[tids[t]] + pos[t % seq]).
 // An id outside its table contributes a zero row (TF's GPU GatherV2 reads zeros
@@ -648,8 +706,28 @@ hipError_t cast_bf16_f32_launch(const uint16_t* x, float* y, int64_t n, hipStrea
   return hipGetLastError();
 }
 
+template <int LPR, int CH>
+hipError_t ln_fit(const uint16_t* x, const uint16_t* r, const float* gamma, const float* beta, uint16_t* y, int rows,
+                  float eps, hipStream_t s) {
+  const int per_block = 4 * (64 / LPR);
+  hipLaunchKernelGGL((layernorm_fit_kernel<LPR, CH>), dim3((rows + per_block - 1) / per_block), dim3(256), 0, s, x, r,
+                     gamma, beta, y, rows, eps);
+  return hipGetLastError();
+}
+
 hipError_t layernorm_launch(const uint16_t* x, const uint16_t* r, const float* gamma, const float* beta,
                             uint16_t* y, int rows, int cols, float eps, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  switch (cols) {
+    case 128: return ln_fit<16, 1>(x, r, gamma, beta, y, rows, eps, s);
+    case 256: return ln_fit<32, 1>(x, r, gamma, beta, y, rows, eps, s);
+    case 384: return ln_fit<16, 3>(x, r, gamma, beta, y, rows, eps, s);
+    case 512: return ln_fit<64, 1>(x, r, gamma, beta, y, rows, eps, s);
+    case 768: return ln_fit<32, 3>(x, r, gamma, beta, y, rows, eps, s);
+    case 1024: return ln_fit<64, 2>(x, r, gamma, beta, y, rows, eps, s);
+    case 2048: return ln_fit<64, 4>(x, r, gamma, beta, y, rows, eps, s);
+    default: break;
+  }
   hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, r, gamma, beta, y, rows, cols,
                      eps);
   return hipGetLastError();

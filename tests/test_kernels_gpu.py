@@ -401,9 +401,11 @@ def test_layernorm_and_embedding():
     assert (e.float().cpu() - ref).abs().max() < 5e-2
 
 
-@pytest.mark.parametrize("cols", [64, 520, 2048, 4104])
+@pytest.mark.parametrize("cols", [64, 520, 2048, 4104, 128, 256, 384, 512, 768, 1024])
 def test_layernorm_register_and_streaming_paths(cols):
-    """Rows up to 2048 columns stay in registers; longer ones stream twice."""
+    """Rows up to 2048 columns stay in registers; longer ones stream twice;
+    exact-fit widths (128 .. 2048) take the lanes-per-row kernel (37 rows: a
+    partial last workgroup)."""
     x = (rnd(37, cols, seed=41) * 3 + 5).to(BF)      # offset mean: the two-pass variance matters
     r = rnd(37, cols, seed=42).to(BF)
     gm, bt = rnd(cols, seed=43), rnd(cols, seed=44)

@@ -102,3 +102,51 @@ def test_resnet_and_bert_coresident_with_hot_reload(paths):
         asyncio.run(scenario())
     finally:
         srv.stop()
+
+
+def test_unloading_a_model_answers_its_in_flight_requests(paths):
+    """Reload to a config WITHOUT the model that has Predicts in flight on the
+    fast path (batched into slots, queued, or still streaming): every call gets
+    an answer -- its result or UNAVAILABLE / NOT_FOUND -- and none waits for its
+    deadline (batcher.cpp Endpoint::close)."""
+    import time
+    import grpc
+    from rust_tensorflow_serving2_amd import native
+    rpath, _bpath = paths
+    so = ServableOptions(device="cuda:0", max_batch_size=8, allowed_batch_sizes=(1, 2, 4, 8))
+    srv = ModelServer(ServerOptions(port=0, host="127.0.0.1",
+                                    model_config=_config(("keep", rpath), ("gone", rpath)),
+                                    device="cuda:0", transport="native", servable=so,
+                                    file_system_poll_wait_seconds=0, batch_timeout_us=2000)).start()
+    try:
+        tr = srv.transports[0]
+        for _ in range(400):
+            if len(tr.stats().get("endpoints", [])) >= 2:
+                break
+            time.sleep(0.05)
+        img = np.random.default_rng(5).random((1, 32, 32, 3), dtype=np.float32)
+        body = native.encode_predict_request(native.spec_tuple("gone", None, None, ""), {"input": img})
+
+        async def scenario():
+            async with grpc.aio.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+                stub = ch.unary_unary("/tensorflow.serving.PredictionService/Predict")
+                calls = [asyncio.ensure_future(stub(body, timeout=20)) for _ in range(96)]
+                await asyncio.sleep(0.01)
+                cl = await TensorflowServing.new().hostname("127.0.0.1").port(srv.port).build()
+                resp = await cl.reload(_config(("keep", rpath)).model_config_list.config[0])
+                assert resp.status.error_code == 0
+                t0 = time.time()
+                codes = []
+                for c in calls:
+                    try:
+                        await c
+                        codes.append("OK")
+                    except grpc.aio.AioRpcError as e:
+                        codes.append(e.code().name)
+                return codes, time.time() - t0
+        codes, waited = asyncio.run(scenario())
+        assert len(codes) == 96 and "DEADLINE_EXCEEDED" not in codes, codes
+        assert set(codes) <= {"OK", "UNAVAILABLE", "NOT_FOUND"}, set(codes)
+        assert waited < 15
+    finally:
+        srv.stop()
