@@ -10,7 +10,7 @@ constexpr int kCGemmCfgBase = 32;
 constexpr int kNumCGemmConfigs = 16;
 // a second id range (after the halo ids): 2-wave and 3-deep variants
 constexpr int kCGemmCfgBase2 = 64;
-constexpr int kNumCGemmConfigs2 = 8;
+constexpr int kNumCGemmConfigs2 = 9;
 inline bool cgemm_cfg_id(int cfg) {
   return (cfg >= kCGemmCfgBase && cfg < kCGemmCfgBase + kNumCGemmConfigs) ||
          (cfg >= kCGemmCfgBase2 && cfg < kCGemmCfgBase2 + kNumCGemmConfigs2);

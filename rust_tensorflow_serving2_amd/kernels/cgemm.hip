@@ -50,8 +50,15 @@ struct CG {
   static constexpr int A_ST = BM * KT, B_ST = BN * KT;            // elements per ring slot
   static constexpr int LDS_MAIN = S * (A_ST + B_ST) * 2;
   static constexpr int CS_LD = BN + 4;
-  static constexpr int LDS_EPI = BM * CS_LD * 4;
+  // the fp32 tile is staged through LDS for the epilogue; a tile whose fp32
+  // image does not fit next to nothing (256 x 192: 196 KB) goes in two row
+  // passes (each wave's rows fall in one pass)
+  static constexpr int LDS_EPI_FULL = BM * CS_LD * 4;
+  static constexpr int PASSES = LDS_EPI_FULL > 160 * 1024 ? 2 : 1;
+  static constexpr int RPP = BM / PASSES;
+  static constexpr int LDS_EPI = RPP * CS_LD * 4;
   static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+  static_assert(RPP % WM == 0, "epilogue passes split the tile at wave-row boundaries");
   static_assert(APW >= 1 && BPW >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "DMA piece split");
   static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
   static_assert(S >= 2 && (S - 2) * PPW < 64, "ring depth / vmcnt range");
@@ -77,11 +84,12 @@ __device__ __forceinline__ void prefetch_residual(const IGemmArgs& p, int m0, in
 // and a rcp, common.h sigm2): fully unrolled over the thread's chunks, residual
 // from the registers prefetched before the K loop.  erf GELU (Keras FFNs): a
 // rolled loop, so the erf expansion is emitted once instead of ITERS x 8 times.
-template <int BM, int BN, int NT, int CS_LD, int ACT>
+template <int BM, int BN, int NT, int CS_LD, int ACT, bool USE_PRE = true>
 __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* Cs, int m0, int n0, int tid,
                                               const uint4 (&rpre)[Epi<BM, BN, NT>::PRE > 0 ? Epi<BM, BN, NT>::PRE : 1],
                                               const float4 b0, const float4 b1) {
   using E = Epi<BM, BN, NT>;
+  constexpr int PRE = USE_PRE ? E::PRE : 0;
   const int M = p.M, N = p.N;
   const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
   constexpr bool cheap = (ACT != kActGeluErf);   // GELU-tanh / tanh are exp + rcp (common.h sigm2)
@@ -94,8 +102,7 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
       if (m >= M || n >= N) continue;
       uint4 rr = make_uint4(0, 0, 0, 0);
       if (p.residual)
-        rr = E::PRE > 0 ? rpre[E::PRE > 0 ? it : 0]
-                        : *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
+        rr = PRE > 0 ? rpre[PRE > 0 ? it : 0] : *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
       epi_chunk<ACT>(p, Cs + row * CS_LD + col, m, n, bv, rr);
     }
   } else {
@@ -311,7 +318,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   };
 
   uint4 rpre[Epi<BM, BN, G::NT>::PRE > 0 ? Epi<BM, BN, G::NT>::PRE : 1];
-  prefetch_residual<BM, BN, G::NT>(p, m0, n0, tid, rpre);
+  if constexpr (G::PASSES == 1) prefetch_residual<BM, BN, G::NT>(p, m0, n0, tid, rpre);
   float4 bias0, bias1;
   prefetch_bias<BM, BN, G::NT>(p, n0, tid, bias0, bias1);
 
@@ -351,47 +358,59 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
   if (dbg & 8) return;
 
   // ---- epilogue: stage the fp32 tile in LDS, then coalesced row chunks
+  // (G::PASSES row passes of G::RPP rows when the whole fp32 tile does not fit)
   float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int RPP = G::RPP;
 #pragma unroll
-  for (int i = 0; i < G::TM; ++i)
+  for (int ps = 0; ps < G::PASSES; ++ps) {
+    if (ps > 0) __syncthreads();    // the previous pass has read Cs
+    if (G::PASSES == 1 || (wm * G::WM) / RPP == ps) {
 #pragma unroll
-    for (int j = 0; j < G::TN; ++j)
+      for (int i = 0; i < G::TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(wm * G::WM + i * 16 + fq * 4 + r) * G::CS_LD + wn * G::WN + j * 16 + fr] = acc[i][j][r];
-  __syncthreads();
-
-  if (p.splits > 1) {
-    // raw (alpha-scaled) partial slab of this K slice; splitk_reduce applies the epilogue
-    const float alpha = p.alpha;
-    float* ws = p.ws + size_t(blockIdx.y) * M * N;
-    constexpr int CPR = BN / 8;
-    const bool v4 = (N % 4 == 0);
-    for (int c = tid; c < BM * CPR; c += G::NT) {
-      const int row = c / CPR, col = (c - row * CPR) * 8;
-      const int m = m0 + row, n = n0 + col;
-      if (m >= M || n >= N) continue;
-      const float* src = Cs + row * G::CS_LD + col;
-      float* dst = ws + size_t(m) * N + n;
-      if (v4 && n + 8 <= N) {
-        float4 a = *reinterpret_cast<const float4*>(src);
-        float4 b = *reinterpret_cast<const float4*>(src + 4);
-        a.x *= alpha; a.y *= alpha; a.z *= alpha; a.w *= alpha;
-        b.x *= alpha; b.y *= alpha; b.z *= alpha; b.w *= alpha;
-        *reinterpret_cast<float4*>(dst) = a;
-        *reinterpret_cast<float4*>(dst + 4) = b;
-      } else {
-        for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = src[e] * alpha;
-      }
+        for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(wm * G::WM - ps * RPP + i * 16 + fq * 4 + r) * G::CS_LD + wn * G::WN + j * 16 + fr] = acc[i][j][r];
     }
-    return;
-  }
-  switch (p.act) {
-    case kActRelu: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActRelu>(p, Cs, m0, n0, tid, rpre, bias0, bias1); break;
-    case kActGeluTanh: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActGeluTanh>(p, Cs, m0, n0, tid, rpre, bias0, bias1); break;
-    case kActGeluErf: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActGeluErf>(p, Cs, m0, n0, tid, rpre, bias0, bias1); break;
-    case kActTanh: epilogue_rows<BM, BN, G::NT, G::CS_LD, kActTanh>(p, Cs, m0, n0, tid, rpre, bias0, bias1); break;
-    default: epilogue_rows<BM, BN, G::NT, G::CS_LD, 0>(p, Cs, m0, n0, tid, rpre, bias0, bias1); break;
+    __syncthreads();
+    const int mp = m0 + ps * RPP;
+
+    if (p.splits > 1) {
+      // raw (alpha-scaled) partial slab of this K slice; splitk_reduce applies the epilogue
+      const float alpha = p.alpha;
+      float* ws = p.ws + size_t(blockIdx.y) * M * N;
+      constexpr int CPR = BN / 8;
+      const bool v4 = (N % 4 == 0);
+      for (int c = tid; c < RPP * CPR; c += G::NT) {
+        const int row = c / CPR, col = (c - row * CPR) * 8;
+        const int m = mp + row, n = n0 + col;
+        if (m >= M || n >= N) continue;
+        const float* src = Cs + row * G::CS_LD + col;
+        float* dst = ws + size_t(m) * N + n;
+        if (v4 && n + 8 <= N) {
+          float4 a = *reinterpret_cast<const float4*>(src);
+          float4 b = *reinterpret_cast<const float4*>(src + 4);
+          a.x *= alpha; a.y *= alpha; a.z *= alpha; a.w *= alpha;
+          b.x *= alpha; b.y *= alpha; b.z *= alpha; b.w *= alpha;
+          *reinterpret_cast<float4*>(dst) = a;
+          *reinterpret_cast<float4*>(dst + 4) = b;
+        } else {
+          for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = src[e] * alpha;
+        }
+      }
+      continue;
+    }
+    constexpr bool P1 = G::PASSES == 1;
+    using RP = uint4[Epi<RPP, BN, G::NT>::PRE > 0 ? Epi<RPP, BN, G::NT>::PRE : 1];
+    const RP& rp = *reinterpret_cast<const RP*>(rpre);   // only read when PASSES == 1 (RPP == BM)
+    switch (p.act) {
+      case kActRelu: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActRelu, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1); break;
+      case kActGeluTanh: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActGeluTanh, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1); break;
+      case kActGeluErf: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActGeluErf, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1); break;
+      case kActTanh: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActTanh, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1); break;
+      default: epilogue_rows<RPP, BN, G::NT, G::CS_LD, 0, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1); break;
+    }
   }
 }
 
@@ -414,9 +433,9 @@ hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
 // S * (BM + BN) * 128 B (or the fp32 epilogue tile if larger).
 constexpr int kAll = kNumCGemmConfigs + kNumCGemmConfigs2;
 constexpr int kBM[kAll] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256, 64, 64, 128, 128, 128, 64,
-                           64, 64, 64, 128, 64, 128, 64, 64};
+                           64, 64, 64, 128, 64, 128, 64, 64, 256};
 constexpr int kBN[kAll] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64, 64, 128, 64, 96, 96, 96,
-                           64, 64, 64, 64, 128, 64, 128, 64};
+                           64, 64, 64, 64, 128, 64, 128, 64, 192};
 
 // config id -> index into the tables (both id ranges)
 int cfg_index(int cfg) {
@@ -458,6 +477,9 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
     case 21: return launch_cfg<128, 64, 2, 1, 3, AM>(a, s);   // 72 KB, wave 64x64
     case 22: return launch_cfg<64, 128, 1, 2, 3, AM>(a, s);   // 72 KB, wave 64x64
     case 23: return launch_cfg<64, 64, 2, 2, 3, AM>(a, s);    // 48 KB, wave 32x32
+    // 8 waves of 64x96 (BERT's 2304 / 3072-wide projections at M = 4096: 192 /
+    // 256 tiles, one per CU); 112 KB ring, epilogue in two 128-row passes
+    case 24: return launch_cfg<256, 192, 4, 2, 2, AM>(a, s);
     default: return hipErrorInvalidValue;
   }
 }

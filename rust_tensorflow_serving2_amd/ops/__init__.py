@@ -98,7 +98,7 @@ CGEMM = {32: (128, 128), 33: (128, 128), 34: (64, 128), 35: (128, 64), 36: (64, 
          37: (256, 128), 38: (128, 256), 39: (128, 128), 40: (64, 256), 41: (256, 64),
          42: (64, 64), 43: (64, 128), 44: (128, 64), 45: (128, 96), 46: (128, 96), 47: (64, 96),
          64: (64, 64), 65: (64, 64), 66: (64, 64), 67: (128, 64), 68: (64, 128), 69: (128, 64), 70: (64, 128),
-         71: (64, 64)}
+         71: (64, 64), 72: (256, 192)}
 TILES.update(CGEMM)
 # halo-tiled 3x3 stride-1 conv (kernels/halo.hip): config id -> (output pixels per tile, BN)
 HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 128), 53: (64, 128), 54: (64, 64),
