@@ -26,6 +26,10 @@ from .manager import AVAILABLE, END, UNLOADING
 from .servable import PREDICT_METHOD
 
 NATIVE_LANES = os.environ.get("TFSERVE_NATIVE_LANES", "1") != "0"
+# CPU servables with batched signatures get the C++ fast path too (Python runs
+# once per batch: cpu_runtime.CpuRunner); TFSERVE_CPU_FAST_PATH=0 keeps them on
+# the per-request Python path
+CPU_FAST_PATH = os.environ.get("TFSERVE_CPU_FAST_PATH", "1") != "0"
 
 log = logging.getLogger("tfserve.native")
 
@@ -214,7 +218,7 @@ class NativeTransport:
         except E.ServingError:
             return
         try:
-            if not servable.options.is_gpu:
+            if not servable.options.is_gpu and not CPU_FAST_PATH:
                 return
             for sig_name, sig in servable.signatures.items():
                 if sig.method_name != PREDICT_METHOD or self._reg_cancelled(name, version):
@@ -225,6 +229,9 @@ class NativeTransport:
                 outs = servable.output_specs(sig_name)
                 if not all(s.shape and s.shape[0] == -1 and all(d >= 0 for d in s.shape[1:]) for s in outs.values()):
                     continue
+                if not servable.options.is_gpu and \
+                        not hasattr(servable.runner(sig_name, sorted(ins), sorted(outs)), "fast_lanes"):
+                    continue      # a CPU signature the batched runner does not take: Python path
                 try:
                     ep = FastEndpoint(self, servable, sig_name, self.batch_timeout_us)
                 except Exception:

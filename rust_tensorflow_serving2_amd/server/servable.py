@@ -207,7 +207,11 @@ class Servable:
         if self.options.is_gpu:
             from .gpu_runtime import GpuRunner
             return GpuRunner(self, in_specs, out_specs, lanes=self.options.lanes)
-        return Runner(self, in_specs, out_specs)
+        r = Runner(self, in_specs, out_specs)
+        from . import cpu_runtime
+        if self.options.lanes > 0 and cpu_runtime.batched(in_specs, out_specs):
+            return cpu_runtime.CpuRunner(r, lanes=min(self.options.lanes, 2))   # batched native fast path
+        return r
 
     def input_specs(self, sig_name: str) -> Dict[str, TensorSpec]:
         return _specs(self.signature(sig_name)[1].inputs)

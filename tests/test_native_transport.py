@@ -137,8 +137,12 @@ def test_native_counters_in_prometheus_metrics(hpt_path):
         srv.stop()
 
 
-def test_trace_dir_records_rpcs(hpt_path, tmp_path):
+def test_trace_dir_records_rpcs(hpt_path, tmp_path, monkeypatch):
+    """Per-RPC trace records of the Python core (the CPU fast path, which
+    batches in C++, is switched off so every call takes the traced path)."""
+    from rust_tensorflow_serving2_amd.server import native_transport
     from rust_tensorflow_serving2_amd.utils import tracing
+    monkeypatch.setattr(native_transport, "CPU_FAST_PATH", False)
     srv = ModelServer(ServerOptions(port=0, host="127.0.0.1", model_name="hpt", model_base_path=hpt_path,
                                     transport="native", file_system_poll_wait_seconds=0,
                                     trace_dir=str(tmp_path / "tr"))).start()
@@ -154,3 +158,42 @@ def test_trace_dir_records_rpcs(hpt_path, tmp_path):
     assert len(rpcs) == 10 and all(r["end_us"] >= r["start_us"] for r in rpcs)
     chrome = tracing.to_chrome(recs)
     assert len(chrome["traceEvents"]) == 10
+
+
+def test_cpu_servable_rides_the_batched_fast_path(hpt_path):
+    """BASELINE config 1 (half_plus_two on CPU): requests are decoded, batched
+    and answered in C++; Python runs the CPU program once per batch
+    (server/cpu_runtime.py).  Results equal the per-request Python path."""
+    import concurrent.futures as cf
+    import grpc
+    from rust_tensorflow_serving2_amd.schema import serving
+    from rust_tensorflow_serving2_amd.utils import tensors as T
+    srv = ModelServer(ServerOptions(port=0, host="127.0.0.1", model_name="hpt", model_base_path=hpt_path,
+                                    transport="native", file_system_poll_wait_seconds=0,
+                                    batch_timeout_us=1000)).start()
+    try:
+        tr = srv.transports[0]
+        import time
+        for _ in range(200):
+            if tr.stats().get("endpoints"):
+                break
+            time.sleep(0.02)
+        assert tr.stats()["endpoints"], "no fast-path endpoint for the CPU servable"
+        xs = [np.array([[float(i)], [float(i) + 0.5]], np.float32) for i in range(64)]
+        bodies = [native.encode_predict_request(native.spec_tuple("hpt", None, None, ""), {"x": x}) for x in xs]
+        with grpc.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+            stub = ch.unary_unary("/tensorflow.serving.PredictionService/Predict")
+            with cf.ThreadPoolExecutor(16) as ex:
+                outs = list(ex.map(lambda b: stub(b, timeout=30), bodies))
+        for x, raw in zip(xs, outs):
+            y = T.tensor_proto_to_numpy(serving.PredictResponse.FromString(raw).outputs["y"])
+            np.testing.assert_allclose(y, x * 0.5 + 2.0, rtol=1e-6)
+        st = tr.srv.stats()
+        assert st["fast_path"] == 64 and st["slow_path"] == 0, st
+        eps = list(tr.stats()["endpoints"].values())
+        assert sum(e["rows"] for e in eps) == 128 and sum(e["batches"] for e in eps) < 64   # batched
+        r = _C.run_loadgen("127.0.0.1", srv.port, "/tensorflow.serving.PredictionService/Predict", bodies[:8],
+                           2000, 32, 2, 2, 60.0)
+        assert r["ok"] == 2000 and r["errors"] == 0
+    finally:
+        srv.stop()

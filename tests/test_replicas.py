@@ -157,8 +157,12 @@ def test_four_replicas_one_connection_and_replica_restart(hpt_path, tmp_path):
     port = _free_port()
     logf = str(tmp_path / "replicas.log")
     stats_dir = str(tmp_path / "stats")
+    # the CPU replicas stand in for GPU replicas whose calls take real service
+    # time: the per-request Python path (not the batched CPU fast path, which
+    # answers half_plus_two in ~0.2 ms and so keeps almost everything local)
+    # gives the load-based router the queueing it reacts to
     env = dict(os.environ, PYTHONPATH=ROOT, TFSERVE_STATS_DIR=stats_dir, TFSERVE_ROUTE_CELLS="16",
-               TFSERVE_ROUTE_MARGIN="2", TFSERVE_SHARE_WAIT_S="2")
+               TFSERVE_ROUTE_MARGIN="2", TFSERVE_SHARE_WAIT_S="2", TFSERVE_CPU_FAST_PATH="0")
     env.pop("WORLD_SIZE", None)
     proc = subprocess.Popen([sys.executable, "-m", "rust_tensorflow_serving2_amd.server", f"--port={port}",
                              "--model_name=a", f"--model_base_path={hpt_path}", "--num_gpus=4", "--device=cpu",
