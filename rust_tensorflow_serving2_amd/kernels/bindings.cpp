@@ -4,6 +4,7 @@
 // beyond the output tensor (so callers can capture them in HIP graphs with
 // pre-allocated outputs via the `out=` forms), and validates shapes on the host
 // before anything touches the GPU.
+#include <cstdlib>
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -40,6 +41,15 @@ hipError_t launch_any(const tfsk::IGemmArgs& a, int a_mode, int64_t cfg, hipStre
   return is_cgemm_cfg(cfg) ? tfsk::cgemm_launch(a, a_mode, int(cfg), st) : tfsk::igemm_launch(a, a_mode, int(cfg), st);
 }
 
+// TFSERVE_SPLITK_FIXUP=1: inside HIP-graph captures, finish split-K in-kernel
+// (no reduce launch).  Off by default: on ResNet-50 it measured neutral (b1
+// 0.391 vs 0.385 ms, b32 0.865 vs 0.873 ms on one box) -- the last slice's
+// slab reads cost about what the reduce launch did.
+bool split_fixup_enabled() {
+  const char* v = std::getenv("TFSERVE_SPLITK_FIXUP");
+  return v && v[0] == '1';
+}
+
 void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, const Tensor& like, hipStream_t st) {
   TORCH_CHECK((cfg >= 0 && cfg < tfsk::kNumIGemmConfigs) || is_cgemm_cfg(cfg) || is_halo_cfg(cfg),
               "bad tile config ", cfg);
@@ -63,8 +73,24 @@ void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, cons
   a.splits = int(splits);
   a.kt_per_split = per;
   a.ws = ws.data_ptr<float>();
+  // inside a HIP-graph capture, cgemm / halo finish split-K in-kernel (the last
+  // slice of each tile reduces): one launch instead of two.  Eager calls keep
+  // the reduce kernel (their counters would need a zeroing launch anyway).
+  a.counters = nullptr;
+  if (split_fixup_enabled() && a.N % 8 == 0 && ((is_cgemm_cfg(cfg) && tfsk::cgemm_fixup_ok(int(cfg))) || is_halo_cfg(cfg))) {
+    tfsk::splitk_counters_prepare(st);
+    long tiles = 0;
+    if (is_halo_cfg(cfg)) {
+      tiles = tfsk::halo_tiles(a, int(cfg));
+    } else {
+      const int bm = tfsk::cgemm_config_bm(int(cfg)), bn = tfsk::cgemm_config_bn(int(cfg));
+      tiles = long((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+    }
+    if (tiles > 0 && tiles < (1L << 24)) a.counters = tfsk::splitk_counters(int(tiles), st);
+  }
   TORCH_CHECK(launch_any(a, a_mode, cfg, st) == hipSuccess, "conv/GEMM (split-K) launch failed");
-  TORCH_CHECK(tfsk::splitk_reduce_launch(a, st) == hipSuccess, "split-K reduce launch failed");
+  if (a.counters == nullptr)
+    TORCH_CHECK(tfsk::splitk_reduce_launch(a, st) == hipSuccess, "split-K reduce launch failed");
 }
 
 void need(const Tensor& t, at::ScalarType st, const char* name) {

@@ -26,6 +26,10 @@ bool cgemm_supported(const IGemmArgs& a, int a_mode);
 int cgemm_config_bm(int cfg);
 int cgemm_config_bn(int cfg);
 hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t stream);
+// the config can finish split-K in-kernel (IGemmArgs::counters)
+bool cgemm_fixup_ok(int cfg);
+// workgroups (= tiles) of a halo launch (its split-K counters)
+long halo_tiles(const IGemmArgs& a, int cfg);
 
 // Halo-tiled 3x3 stride-1 conv (halo.hip): an NHWC bf16 input with C % 64 == 0
 // and the im2col weight layout ([Cout][9 * C]); the workgroup tile is a block

@@ -393,10 +393,45 @@ __global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
           float4 b = *reinterpret_cast<const float4*>(src + 4);
           a.x *= alpha; a.y *= alpha; a.z *= alpha; a.w *= alpha;
           b.x *= alpha; b.y *= alpha; b.z *= alpha; b.w *= alpha;
-          *reinterpret_cast<float4*>(dst) = a;
-          *reinterpret_cast<float4*>(dst + 4) = b;
+          if (p.counters != nullptr) {
+            splitk_store8(dst, a, b);
+          } else {
+            *reinterpret_cast<float4*>(dst) = a;
+            *reinterpret_cast<float4*>(dst + 4) = b;
+          }
         } else {
           for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = src[e] * alpha;
+        }
+      }
+      if constexpr (G::PASSES == 1) {
+        if (p.counters != nullptr) {
+          if (!splitk_arrive(p, blockIdx.x)) return;
+          // the last slice: every slab of the tile summed into Cs, then the epilogue
+          for (int c = tid; c < RPP * CPR; c += G::NT) {
+            const int row = c / CPR, col = (c - row * CPR) * 8;
+            const int m = mp + row, n = n0 + col;
+            if (m >= M || n >= N) continue;
+            float4 lo, hi;
+            splitk_sum8(p, m, n, lo, hi);
+            *reinterpret_cast<float4*>(Cs + row * G::CS_LD + col) = lo;
+            *reinterpret_cast<float4*>(Cs + row * G::CS_LD + col + 4) = hi;
+          }
+          __syncthreads();
+          IGemmArgs q = p;
+          q.splits = 1;
+          q.alpha = 1.f;                      // the slabs carry alpha already
+          float4 qb0, qb1;
+          prefetch_bias<BM, BN, G::NT>(q, n0, tid, qb0, qb1);
+          using RP1 = uint4[Epi<RPP, BN, G::NT>::PRE > 0 ? Epi<RPP, BN, G::NT>::PRE : 1];
+          const RP1& r1 = *reinterpret_cast<const RP1*>(rpre);   // not read (USE_PRE = false)
+          switch (q.act) {
+            case kActRelu: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActRelu, false>(q, Cs, mp, n0, tid, r1, qb0, qb1); break;
+            case kActGeluTanh: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActGeluTanh, false>(q, Cs, mp, n0, tid, r1, qb0, qb1); break;
+            case kActGeluErf: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActGeluErf, false>(q, Cs, mp, n0, tid, r1, qb0, qb1); break;
+            case kActTanh: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActTanh, false>(q, Cs, mp, n0, tid, r1, qb0, qb1); break;
+            default: epilogue_rows<RPP, BN, G::NT, G::CS_LD, 0, false>(q, Cs, mp, n0, tid, r1, qb0, qb1); break;
+          }
+          return;
         }
       }
       continue;
@@ -485,6 +520,12 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
 }
 
 }  // namespace
+
+bool cgemm_fixup_ok(int cfg) {
+  // the in-kernel split-K fixup needs the whole fp32 tile in LDS at once (one pass)
+  const int i = cfg_index(cfg);
+  return size_t(kBM[i]) * (kBN[i] + 4) * 4 <= 160 * 1024;
+}
 
 bool cgemm_supported(const IGemmArgs& a, int a_mode) {
   if (a.K <= 0 || a.K % KT || a.ldb % 8 || a.ldb < a.K) return false;

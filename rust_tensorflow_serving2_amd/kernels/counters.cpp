@@ -1,0 +1,57 @@
+// Split-K arrival counter pool (see launch.h splitk_counters).
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+
+#include "launch.h"
+
+namespace tfsk {
+
+namespace {
+constexpr int kPoolInts = 1 << 20;   // 4 MB per device
+struct Pool {
+  int* base = nullptr;
+  int used = 0;
+};
+std::mutex g_mu;
+std::map<int, Pool> g_pools;
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+}  // namespace
+
+void splitk_counters_prepare(hipStream_t s) {
+  if (capturing(s)) return;     // allocation + memset only outside a capture
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> g(g_mu);
+  Pool& p = g_pools[dev];
+  if (p.base != nullptr) return;
+  void* ptr = nullptr;
+  if (hipMalloc(&ptr, size_t(kPoolInts) * sizeof(int)) != hipSuccess) return;
+  if (hipMemset(ptr, 0, size_t(kPoolInts) * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    hipFree(ptr);
+    return;
+  }
+  p.base = static_cast<int*>(ptr);
+}
+
+int* splitk_counters(int n, hipStream_t s) {
+  if (n <= 0 || !capturing(s)) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_pools.find(dev);
+  if (it == g_pools.end() || it->second.base == nullptr) return nullptr;
+  Pool& p = it->second;
+  const int take = (n + 63) / 64 * 64;
+  if (p.used + take > kPoolInts) return nullptr;
+  int* r = p.base + p.used;
+  p.used += take;
+  return r;
+}
+
+}  // namespace tfsk

@@ -89,6 +89,45 @@ __device__ __forceinline__ void prefetch_bias(const IGemmArgs& p, int n0, int ti
   }
 }
 
+// Split-K without a reduce launch: every slice stores its fp32 slab with
+// agent-scope (write-through) stores, waits for them to complete, and counts
+// its arrival; the slice whose arrival completes tile `t` gets true (the others
+// false), re-zeroes the counter for the next launch and reads the slabs back
+// with agent-scope loads.  No __threadfence: on gfx950 its release writes back
+// the whole L2 and its acquire invalidates it, which made the fixed-up layers
+// slower than a separate reduce launch (MI355X_MICROARCH.md 'handoff-flag':
+// write-through payload + drained vmcnt + flag).
+__device__ __forceinline__ void splitk_store8(float* dst, const float4 a, const float4 b) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) __hip_atomic_store(dst + e, v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool splitk_arrive(const IGemmArgs& p, int t) {
+  __shared__ int s_last;
+  __builtin_amdgcn_s_waitcnt(0);          // this thread's slab stores have completed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(p.counters + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == p.splits - 1;
+    if (s_last) __hip_atomic_store(p.counters + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return s_last;
+}
+
+// Sum of the `splits` slabs for 8 columns at (m, n) (agent-scope loads).
+__device__ __forceinline__ void splitk_sum8(const IGemmArgs& p, int m, int n, float4& lo, float4& hi) {
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const size_t slab = size_t(p.M) * p.N;
+  float* src = p.ws + size_t(m) * p.N + n;
+  for (int s = 0; s < p.splits; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += __hip_atomic_load(src + s * slab + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  lo = make_float4(v[0], v[1], v[2], v[3]);
+  hi = make_float4(v[4], v[5], v[6], v[7]);
+}
+
 // Two floats -> packed bf16 pair (round-to-nearest-even; a plain __bf16 cast
 // compiles to one v_cvt_pk_bf16_f32 on gfx950 and keeps NaNs NaN).
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {

@@ -250,6 +250,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
   };
 
   using E = Epi<BM, BN, G::NT>;
+  IGemmArgs q = p;                      // the epilogue's view (split-K fixup: splits 1, alpha 1)
   if (p.splits > 1) {
     const float alpha = p.alpha;
     float* ws = p.ws + size_t(blockIdx.y) * p.M * p.N;
@@ -265,10 +266,31 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
       a.x *= alpha; a.y *= alpha; a.z *= alpha; a.w *= alpha;
       b.x *= alpha; b.y *= alpha; b.z *= alpha; b.w *= alpha;
       float* dst = ws + size_t(m) * p.N + n;
-      *reinterpret_cast<float4*>(dst) = a;
-      *reinterpret_cast<float4*>(dst + 4) = b;
+      if (p.counters != nullptr) {
+        splitk_store8(dst, a, b);
+      } else {
+        *reinterpret_cast<float4*>(dst) = a;
+        *reinterpret_cast<float4*>(dst + 4) = b;
+      }
     }
-    return;
+    if (p.counters == nullptr || !splitk_arrive(p, blockIdx.x)) return;
+    // the last slice of this tile: every slab summed back into Cs, then the
+    // epilogue below with the bias the split path did not prefetch
+#pragma unroll 1
+    for (int it = 0; it < E::ITERS; ++it) {
+      int row, col;
+      if (!epi_rowcol<BM, BN, G::NT>(tid, it, row, col)) continue;
+      const int m = out_row(row), n = n0 + col;
+      if (m < 0 || n >= p.N) continue;
+      float4 lo, hi;
+      splitk_sum8(p, m, n, lo, hi);
+      *reinterpret_cast<float4*>(Cs + row * G::CS_LD + col) = lo;
+      *reinterpret_cast<float4*>(Cs + row * G::CS_LD + col + 4) = hi;
+    }
+    __syncthreads();
+    q.splits = 1;
+    q.alpha = 1.f;                      // the slabs carry alpha already
+    prefetch_bias<BM, BN, G::NT>(q, n0, tid, bias0, bias1);
   }
   const float bv[8] = {bias0.x, bias0.y, bias0.z, bias0.w, bias1.x, bias1.y, bias1.z, bias1.w};
   auto run = [&](auto act_tag) {
@@ -278,13 +300,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
       int row, col;
       if (!epi_rowcol<BM, BN, G::NT>(tid, it, row, col)) continue;
       const int m = out_row(row), n = n0 + col;
-      if (m < 0 || n >= p.N) continue;
-      const uint4 rr = p.residual ? *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n)
+      if (m < 0 || n >= q.N) continue;
+      const uint4 rr = q.residual ? *reinterpret_cast<const uint4*>(q.residual + size_t(m) * q.ldr + n)
                                   : make_uint4(0, 0, 0, 0);
-      epi_chunk<ACT>(p, Cs + row * G::CS_LD + col, m, n, bv, rr);
+      epi_chunk<ACT>(q, Cs + row * G::CS_LD + col, m, n, bv, rr);
     }
   };
-  switch (p.act) {
+  switch (q.act) {
     case kActRelu: run(std::integral_constant<int, kActRelu>{}); break;
     case kActGeluTanh: run(std::integral_constant<int, kActGeluTanh>{}); break;
     case kActGeluErf: run(std::integral_constant<int, kActGeluErf>{}); break;
@@ -336,8 +358,18 @@ hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
 
 constexpr int kHBM[kNumHaloConfigs] = {256, 128, 128, 64, 256, 64, 64, 128, 256};
 constexpr int kHBN[kNumHaloConfigs] = {64, 128, 64, 64, 128, 128, 64, 64, 64};
+constexpr int kHHR[kNumHaloConfigs] = {320, 192, 192, 128, 320, 128, 128, 192, 320};   // halo rows (HR)
 
 }  // namespace
+
+long halo_tiles(const IGemmArgs& a0, int cfg) {
+  IGemmArgs a = a0;
+  const int c = cfg - kHaloCfgBase;
+  if (c < 0 || c >= kNumHaloConfigs) return 0;
+  if (!pick_block(a.Ho, a.Wo, kHBM[c], kHHR[c], a.TH, a.TW)) return 0;
+  const int nimg = a.M / (a.Ho * a.Wo);
+  return long(nimg) * ((a.Ho + a.TH - 1) / a.TH) * ((a.Wo + a.TW - 1) / a.TW) * ((a.N + kHBN[c] - 1) / kHBN[c]);
+}
 
 bool halo_supported(const IGemmArgs& a) {
   return a.KH == 3 && a.KW == 3 && a.SH == 1 && a.SW == 1 && a.C % KT == 0 && a.K == 9 * a.C && a.ldb >= a.K &&

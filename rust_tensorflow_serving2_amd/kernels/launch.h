@@ -52,7 +52,20 @@ struct IGemmArgs {
   const float* scale2;
   const float* shift2;
   int act2;
+  // split-K without the reduce launch (cgemm / halo, inside HIP graphs): one
+  // arrival counter per tile (zero between launches); the last slice to arrive
+  // sums the slabs and runs the epilogue, then re-zeroes its counter
+  int* counters;
 };
+
+// Per-device pool of zeroed split-K arrival counters for kernels captured into
+// HIP graphs: a capture takes a slice for good (its replays are ordered on its
+// stream, and each tile's last arriver re-zeroes its counter).  nullptr when
+// the stream is not capturing or the pool is exhausted: the caller then uses
+// the separate reduce launch.
+int* splitk_counters(int n, hipStream_t s);
+// Allocates and zeroes this device's pool (no-op while `s` is capturing).
+void splitk_counters_prepare(hipStream_t s);
 
 // kAStem7x7x3: fp32 NHWC input with C == 3 and a 7-wide filter (the ResNet
 // stem) — compile-time geometry for the operand gather.

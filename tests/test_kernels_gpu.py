@@ -553,3 +553,53 @@ def test_maxpool_post_affine():
     ref = torch.relu(ref * sc + sh)
     torch.cuda.synchronize()
     assert (y.float().cpu() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("cfg,splits,shape,post", [
+    (36, 4, (2, 7, 7, 512, 512, 3, 2, (1, 1, 1, 1)), False),      # cgemm im2col, strided
+    (42, 3, (2, 14, 14, 256, 256, 1, 1, (0, 0, 0, 0)), True),     # cgemm dense 1x1, post output
+    (51, 4, (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)), False),      # halo, split over channel chunks
+    (54, 2, (3, 14, 14, 256, 256, 3, 1, (1, 1, 1, 1)), True),     # 9-slot halo, post output
+])
+def test_splitk_in_kernel_fixup_inside_graph(cfg, splits, shape, post, monkeypatch):
+    """Captured in a HIP graph, split-K finishes in-kernel (the last slice of a
+    tile sums the slabs and runs the epilogue; no reduce launch).  Every replay
+    (the tile counters re-zero themselves) equals the eager result, which uses
+    the separate reduce kernel, and the fp32 reference."""
+    monkeypatch.setenv("TFSERVE_SPLITK_FIXUP", "1")
+    n, h, w, cin, cout, k, s, pads = shape
+    x = rnd(n, h, w, cin, seed=61).to(BF)
+    wt = rnd(k, k, cin, cout, scale=1 / math.sqrt(k * k * cin), seed=62).to(BF).float()
+    b = rnd(cout, scale=0.1, seed=63)
+    ho = (h + pads[0] + pads[1] - k) // s + 1
+    wo = (w + pads[2] + pads[3] - k) // s + 1
+    res = rnd(n, ho, wo, cout, seed=64).to(BF)
+    kw = {}
+    sc, sh = rnd(cout, seed=65).to(DEV), rnd(cout, seed=66).to(DEV)
+    xd, wd, bd, rd = x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV)
+
+    def call(out, out2):
+        extra = dict(post_scale=sc, post_shift=sh, post_act=ACT["relu"], out2=out2) if post else {}
+        return hip().conv2d(xd, wd, bd, rd, k, k, s, s, *pads, act=ACT["relu"], cfg=cfg, out=out, splits=splits,
+                            **extra)
+    eager = torch.empty(n, ho, wo, cout, device=DEV, dtype=BF)
+    eager2 = torch.empty_like(eager)
+    call(eager, eager2 if post else None)
+    torch.cuda.synchronize()
+    ref = ref_conv(x, wt, b, s, pads, res, "relu")
+    assert (eager.float().cpu() - ref).abs().max() < 3e-2 * max(1.0, ref.abs().max().item())
+    out = torch.empty_like(eager)
+    out2 = torch.empty_like(eager)
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            call(out, out2 if post else None)
+    for _ in range(3):
+        out.zero_()
+        out2.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager), (out.float() - eager.float()).abs().max()
+        if post:
+            assert torch.equal(out2, eager2)
