@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--c1-requests", type=int, default=200,
                     help="after the timed window: batch-1 round trips at concurrency 1 over one connection "
                          "(reported as p50_c1_ms; 0 = skip)")
-    ap.add_argument("--ref-client-requests", type=int, default=2000,
+    ap.add_argument("--ref-client-requests", type=int, default=6000,
                     help="after the timed window: rank 0 drives this many Predicts over 2 HTTP/2 connections "
                          "(the reference client's channel pattern, src/lib.rs:132-138) while every rank serves; "
                          "reported as ref_client_rps + the share each GPU served (per-stream routing; 0 = skip)")
@@ -255,7 +255,9 @@ def main():
             dist.barrier()
         s0 = served()
         if rank == 0:
-            lg2 = _C.LoadGen("127.0.0.1", server.port, PREDICT, bodies, min(conc, 128), 2, 1)
+            # two connections, each driven by its own thread (a tonic channel's
+            # connection task runs on one runtime thread at a time)
+            lg2 = _C.LoadGen("127.0.0.1", server.port, PREDICT, bodies, min(conc, 128), 2, 2)
             lg2.run(max(64, args.ref_client_requests // 10), 120.0)
             s0 = served()
             r2 = lg2.run(args.ref_client_requests, 300.0)
