@@ -56,6 +56,29 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_kernel(const uint16_t* __res
     float m[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+    if (KH == 3 && KW == 3) {
+      // the ResNet stem pool: all nine 16-B loads issued before any max (the
+      // generic loop below has run-time trip counts, so its loads went out one
+      // at a time, each paying the full latency); out-of-range taps load a
+      // clamped in-range address and are masked
+      uint4 v[9];
+      bool ok[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int hi = ho * SH - PT + t / 3, wi = wo * SW - PL + t % 3;
+        ok[t] = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+        const int hc = min(max(hi, 0), H - 1), wc = min(max(wi, 0), W - 1);
+        v[t] = *reinterpret_cast<const uint4*>(x + ((long(n) * H + hc) * W + wc) * long(C) + c8 * 8);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (!ok[t]) continue;
+        float f[8];
+        unpack8(v[t], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
+      }
+    } else
     for (int kh = 0; kh < KH; ++kh) {
       const int hi = ho * SH - PT + kh;
       if ((unsigned)hi >= (unsigned)H) continue;
