@@ -1,0 +1,47 @@
+"""hipBLASLt (torch._addmm_activation: bias + ReLU epilogue) vs our tuned cgemm on
+the ResNet-50 1x1 convs without a residual, timed like the serving graph runs
+them: captured in a HIP graph, rotating over 8 operand copies (L2-cold).
+
+    python scripts/blaslt_vs_cgemm.py
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from rust_tensorflow_serving2_amd.ops import ACT, candidates, hip  # noqa: E402
+from scripts.conv_sweep import time_graph  # noqa: E402
+
+BF = torch.bfloat16
+SHAPES = {  # name: (M, N, K) at b32
+    "s1_64_64": (100352, 64, 64), "s1_256_64": (100352, 64, 256), "s2_256_128_56": (100352, 128, 256),
+    "s2_512_128": (25088, 128, 512), "s3_512_256_28": (25088, 256, 512), "s3_1024_256": (6272, 256, 1024),
+    "s4_1024_512_14": (6272, 512, 1024), "s4_2048_512": (1568, 512, 2048),
+    "b1_s3_1024_256": (196, 256, 1024), "b1_s4_2048_512": (49, 512, 2048),
+}
+
+
+def main():
+    for name, (M, N, K) in SHAPES.items():
+        xs = [torch.randn(M, K, device="cuda").to(BF) for _ in range(8)]
+        ws = [(torch.randn(N, K, device="cuda") * 0.05).to(BF) for _ in range(8)]
+        b = torch.zeros(N, device="cuda", dtype=BF)
+        bf = torch.zeros(N, device="cuda")
+        outs = [torch.empty(M, N, device="cuda", dtype=BF) for _ in range(8)]
+        t_lt = time_graph(lambda i: torch._addmm_activation(b, xs[i % 8], ws[i % 8].t(), use_gelu=False))
+        best = (1e9, None)
+        for cfg, sp in candidates(M, N, K, True, True):
+            try:
+                t = time_graph(lambda i, cfg=cfg, sp=sp: hip().linear(xs[i % 8], ws[i % 8], bf, None, ACT["relu"], cfg,
+                                                                       False, 1.0, outs[i % 8], sp))
+            except RuntimeError:
+                continue
+            best = min(best, (t, (cfg, sp)))
+        print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "hipblaslt_us": round(t_lt, 2),
+                          "cgemm_us": round(best[0], 2), "cgemm_cfg": best[1]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
