@@ -227,6 +227,19 @@ def record_tuned_keys():
         _REC.keys = prev
 
 
+def graph_tune_params(bucket: int) -> dict:
+    """graph_tune knobs (env overrides for experiments): TFSERVE_GRAPH_TUNE_TOP,
+    _RATIO, _MIN_US."""
+    out = {}
+    if os.environ.get("TFSERVE_GRAPH_TUNE_TOP"):
+        out["top"] = int(os.environ["TFSERVE_GRAPH_TUNE_TOP"])
+    if os.environ.get("TFSERVE_GRAPH_TUNE_RATIO"):
+        out["ratio"] = float(os.environ["TFSERVE_GRAPH_TUNE_RATIO"])
+    if os.environ.get("TFSERVE_GRAPH_TUNE_MIN_US"):
+        out["min_ms"] = float(os.environ["TFSERVE_GRAPH_TUNE_MIN_US"]) / 1e3
+    return out
+
+
 def graph_tune(keys: Dict[Tuple, int], time_fn: Callable[[], float], top: int = 4, ratio: float = 1.35,
                min_ms: float = 0.012) -> Dict[Tuple, Tuple[int, int]]:
     """Re-pick tile configs by timing the WHOLE program (``time_fn`` captures

@@ -199,7 +199,7 @@ class GpuRunner:
         lane.stream.synchronize()
         self._ensure_host_out(lane, outs)
         if keys and self.servable.options.graph_autotune and ops.AUTOTUNE:
-            changed = ops.graph_tune(keys, lambda: self._replay_ms(lane, ins))
+            changed = ops.graph_tune(keys, lambda: self._replay_ms(lane, ins), **ops.graph_tune_params(b))
             if changed:
                 log.info("graph autotune %s bucket=%d: %s", self.servable.name, b, changed)
         if src is not None and keys:
