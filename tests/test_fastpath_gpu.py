@@ -239,7 +239,14 @@ def test_request_logging_on_the_gpu_fast_path(tmp_path):
         sent = dict(zip(bodies, outs))
         for pl in recs:
             req = pl.predict_log.request.SerializeToString()
-            assert req in sent and pl.predict_log.response.SerializeToString() == sent[req]
+            if req not in sent:
+                same = [b for b in sent if len(b) == len(req)]
+                diffs = [next(i for i, (x, y) in enumerate(zip(b, req)) if x != y) for b in same]
+                raise AssertionError(f"logged request ({len(req)} B) matches no sent body; first differing "
+                                     f"offsets vs the {len(same)} same-length bodies: {diffs}")
+            # compare as messages: map entries (the outputs) have no canonical wire order, and
+            # the re-serialised log copy need not list them in the order the server sent them
+            assert pl.predict_log.response == serving.PredictResponse.FromString(sent[req])
             assert pl.log_metadata.model_spec.name == "resnet" and pl.log_metadata.model_spec.version.value == 1
         assert lg.stats()["dropped"] == 0
     finally:
