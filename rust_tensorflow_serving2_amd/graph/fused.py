@@ -11,7 +11,8 @@ a single consumer and is not fetched):
   directly (ingest cast fused into the operand loads).
 * ``MatMul -> [BiasAdd] -> [Add(residual)] -> [Relu|Tanh|GELU]`` => ``_FusedMatMul``
   (fp32 output when it feeds a Softmax/ArgMax head or is fetched).
-* ``Mean(NHWC, axes=[1,2])`` => ``_GlobalAvgPool``;  ``MaxPool`` => ``_MaxPool``.
+* ``Mean(NHWC, axes=[1,2])`` => ``_GlobalAvgPool``;  ``MaxPool`` => ``_MaxPool``;
+  the ResNet stem ``_FusedConv2D(7x7/2, RGB) -> _MaxPool(3x3/2)`` => ``_StemPool``.
 * ``Softmax(x)`` + ``ArgMax(x, -1)`` on the same logits => ``_SoftmaxArgMax``.
 * BERT: decomposed LayerNorm => ``_LayerNorm``; tanh/erf GELU subgraphs => act
   of the producing ``_FusedMatMul``; Q/K/V projections + attention core =>
@@ -470,6 +471,40 @@ class ClassifierHead:
 
 O.OPS["_ClassifierHead"] = _impl_op
 
+
+class StemPool:
+    """``_FusedConv2D(7x7/2, RGB) -> _MaxPool(3x3/2)`` (the ResNet stem) as ONE
+    kernel (``hip().stem_pool``, kernels/stem.hip): the fp32 request is read
+    directly, the conv output stays in LDS and only the pooled map is written
+    (three launches and two passes over the 112x112x64 conv output before)."""
+
+    def __init__(self, conv: FusedConv, pool: MaxPool):
+        self.conv, self.pool = conv, pool
+        self.use_hip = conv.use_hip and conv.c4
+
+    def __call__(self, ctx, node, ins):
+        x = O.to_torch(ins[0])
+        conv, pool = self.conv, self.pool
+        if not (self.use_hip and x.is_cuda and x.dim() == 4):
+            return pool(ctx, node, conv(ctx, node, [x]))
+        from ..ops import ACT, hip
+        pt, pb, pl, pr = conv.pads_for(x.shape[1], x.shape[2])
+        hc = (x.shape[1] + pt + pb - conv.kh) // conv.sh + 1
+        wc = (x.shape[2] + pl + pr - conv.kw) // conv.sw + 1
+        if pool.padding == "SAME":
+            (ppt, ppb), (ppl, ppr) = O.tf_same_pads(hc, 3, 2), O.tf_same_pads(wc, 3, 2)
+        else:
+            ppt = ppb = ppl = ppr = 0
+        kw = {}
+        if pool.post is not None:
+            sc, sh, act = pool.post
+            kw = dict(post_scale=sc, post_shift=sh, post_act=ACT[act])
+        return [hip().stem_pool(x.float().contiguous(), conv.w, conv.b, pt, pb, pl, pr, ACT[conv.act],
+                                ppt, ppb, ppl, ppr, **kw)]
+
+
+O.OPS["_StemPool"] = _impl_op
+
 _PASSTHROUGH = ("Identity", "Squeeze", "Reshape")
 
 
@@ -514,6 +549,36 @@ def fuse_classifier_head(g, order, fed, fetch_refs, device, opts):
         sm.ctrl = _merge_ctrl(chain + [sm])
         for n in chain:
             del g.nodes[n.name]
+        c.refresh()
+
+
+def fuse_stem_pool(g, order, fed, fetch_refs, device, opts):
+    """``_MaxPool(3x3/2)(_FusedConv2D(7x7/2, C <= 4 channels, 16..64 outputs))``
+    -> ``_StemPool`` when the conv has no residual / post output and feeds only
+    the pool, and the pool writes a single output."""
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    for name in order:
+        p = g.nodes.get(name)
+        if p is None or p.op != "_MaxPool" or not p.inputs or p.inputs[0][1] != 0:
+            continue
+        pool = p.attrs["_impl"]
+        if (pool.kh, pool.kw, pool.sh, pool.sw) != (3, 3, 2, 2) or pool.post_mode == "dual":
+            continue
+        cn = g.nodes.get(p.inputs[0][0])
+        if cn is None or cn.op != "_FusedConv2D" or len(cn.inputs) != 1 or c.only_consumer(cn.name) is not p:
+            continue
+        conv = cn.attrs["_impl"]
+        if not isinstance(conv, FusedConv) or (conv.kh, conv.kw, conv.sh, conv.sw) != (7, 7, 2, 2) or \
+                conv.cin > 4 or conv.cout % 16 or not 16 <= conv.cout <= 64 or conv.post is not None or \
+                conv.act not in ("none", "relu"):
+            continue
+        if c.use_hip and not conv.c4:
+            continue
+        p.op = "_StemPool"
+        p.inputs = [cn.inputs[0]]
+        p.ctrl = _merge_ctrl([cn, p])
+        p.attrs = {"_impl": StemPool(conv, pool)}
+        del g.nodes[cn.name]
         c.refresh()
 
 
@@ -836,4 +901,4 @@ def fuse_post_activation(g, order, fed, fetch_refs, device, opts):
 def default_passes(options=None):
     from .patterns import bert_passes
     return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_dual_conv, fuse_post_activation,
-                                                                 fuse_matmul, fuse_classifier_head]
+                                                                 fuse_stem_pool, fuse_matmul, fuse_classifier_head]

@@ -73,9 +73,9 @@ void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, cons
   a.splits = int(splits);
   a.kt_per_split = per;
   a.ws = ws.data_ptr<float>();
-  // inside a HIP-graph capture, cgemm / halo finish split-K in-kernel (the last
-  // slice of each tile reduces): one launch instead of two.  Eager calls keep
-  // the reduce kernel (their counters would need a zeroing launch anyway).
+  // cgemm / halo finish split-K in-kernel (the last slice of each tile
+  // reduces): one launch instead of two.  Eager launches (autotuning) use the
+  // fixup too, so the tuner times the split-K candidates as the graph runs them.
   a.counters = nullptr;
   if (split_fixup_enabled() && a.N % 8 == 0 && ((is_cgemm_cfg(cfg) && tfsk::cgemm_fixup_ok(int(cfg))) || is_halo_cfg(cfg))) {
     tfsk::splitk_counters_prepare(st);
@@ -298,6 +298,45 @@ Tensor maxpool(const Tensor& x, int64_t KH, int64_t KW, int64_t SH, int64_t SW, 
   }
   check(tfsk::maxpool_nhwc_launch(bf16p(x), bf16p_mut(y), N, H, W, C, KH, KW, SH, SW, PT, PL, Ho, Wo,
                                   cur_stream(x), sc, sh, int(post_act)), "maxpool");
+  return y;
+}
+
+// ResNet stem: conv 7x7/2 (+bias, act) -> max pool 3x3/2 (+post) in one kernel
+// (stem.hip).  x: fp32 NHWC request with C <= 4; w: [cout][ldw] bf16 in the
+// padded-RGBA order of the c4 stem ([kh][8 taps][4 ch]).
+Tensor stem_pool(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t PT, int64_t PB, int64_t PL, int64_t PR,
+                 int64_t act, int64_t PPT, int64_t PPB, int64_t PPL, int64_t PPR,
+                 const c10::optional<Tensor>& post_scale, const c10::optional<Tensor>& post_shift, int64_t post_act) {
+  need(x, at::kFloat, "x");
+  need(w, at::kBFloat16, "w");
+  need(bias, at::kFloat, "bias");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) >= 1 && x.size(3) <= 4, "stem_pool: x must be NHWC with C <= 4");
+  TORCH_CHECK(w.dim() == 2 && w.size(0) % 16 == 0 && w.size(0) >= 16 && w.size(0) <= 64 && w.size(1) >= 224 &&
+              w.size(1) % 8 == 0, "stem_pool: w must be [cout in 16..64 step 16][>= 224, % 8]");
+  TORCH_CHECK(bias.numel() == w.size(0), "stem_pool: bias must have cout entries");
+  TORCH_CHECK(PT >= 0 && PB >= 0 && PL >= 0 && PR >= 0 && PPT >= 0 && PPT <= 2 && PPL >= 0 && PPL <= 2 &&
+              PPB >= 0 && PPR >= 0, "stem_pool: bad padding");
+  TORCH_CHECK(w.device() == x.device() && bias.device() == x.device(), "stem_pool: tensors on different devices");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), cout = w.size(0);
+  const int Hc = (H + PT + PB - 7) / 2 + 1, Wc = (W + PL + PR - 7) / 2 + 1;
+  TORCH_CHECK(Hc >= 1 && Wc >= 1, "stem_pool: input smaller than the filter");
+  const int Hp = (Hc + PPT + PPB - 3) / 2 + 1, Wp = (Wc + PPL + PPR - 3) / 2 + 1;
+  TORCH_CHECK(Hp >= 1 && Wp >= 1, "stem_pool: conv output smaller than the pool window");
+  Tensor y = torch::empty({N, Hp, Wp, cout}, x.options().dtype(at::kBFloat16));
+  const float* sc = nullptr;
+  const float* sh = nullptr;
+  if (post_scale.has_value()) {
+    TORCH_CHECK(post_shift.has_value(), "post_scale needs post_shift");
+    need(*post_scale, at::kFloat, "post_scale");
+    need(*post_shift, at::kFloat, "post_shift");
+    TORCH_CHECK(post_scale->numel() == cout && post_shift->numel() == cout, "post scale / shift must have cout entries");
+    sc = post_scale->data_ptr<float>();
+    sh = post_shift->data_ptr<float>();
+  }
+  check(tfsk::stem_pool_launch(x.data_ptr<float>(), bf16p(w), int(w.size(1)), bias.data_ptr<float>(), bf16p_mut(y), N,
+                               H, W, C, cout, int(PT), int(PL), Hc, Wc, int(PPT), int(PPL), Hp, Wp, int(act), sc, sh,
+                               int(post_act), cur_stream(x)), "stem_pool");
   return y;
 }
 
@@ -535,6 +574,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear", &linear,"x @ w^T (+bias +residual +act)", py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("residual") = py::none(), py::arg("act") = 0, py::arg("cfg") = 0, py::arg("out_f32") = false,
         py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("splits") = 1);
+  m.def("stem_pool", &stem_pool, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pt"), py::arg("pb"),
+        py::arg("pl"), py::arg("pr"), py::arg("act"), py::arg("ppt"), py::arg("ppb"), py::arg("ppl"), py::arg("ppr"),
+        py::arg("post_scale") = py::none(), py::arg("post_shift") = py::none(), py::arg("post_act") = 0);
   m.def("maxpool", &maxpool, py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
         py::arg("pt"), py::arg("pb"), py::arg("pl"), py::arg("pr"), py::arg("out") = py::none(),
         py::arg("post_scale") = py::none(), py::arg("post_shift") = py::none(), py::arg("post_act") = 0);

@@ -10,9 +10,17 @@ namespace tfsk {
 
 namespace {
 constexpr int kPoolInts = 1 << 20;   // 4 MB per device
+// [0, kCapInts): permanent slices for launches captured into HIP graphs (a
+// graph node keeps its counters for the graph's lifetime); [kCapInts,
+// kPoolInts): a ring for eager launches (autotuning, warm-up), reused
+// cyclically.  Counters return to zero when a tile's last slice arrives, so a
+// ring slice is free again once the launch that took it has finished -- which
+// the ring's length (thousands of launches) leaves ample time for.
+constexpr int kCapInts = 3 << 18;
 struct Pool {
   int* base = nullptr;
   int used = 0;
+  int ring = kCapInts;
 };
 std::mutex g_mu;
 std::map<int, Pool> g_pools;
@@ -40,7 +48,8 @@ void splitk_counters_prepare(hipStream_t s) {
 }
 
 int* splitk_counters(int n, hipStream_t s) {
-  if (n <= 0 || !capturing(s)) return nullptr;
+  if (n <= 0) return nullptr;
+  const bool cap = capturing(s);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> g(g_mu);
@@ -48,7 +57,14 @@ int* splitk_counters(int n, hipStream_t s) {
   if (it == g_pools.end() || it->second.base == nullptr) return nullptr;
   Pool& p = it->second;
   const int take = (n + 63) / 64 * 64;
-  if (p.used + take > kPoolInts) return nullptr;
+  if (!cap) {
+    if (take > (kPoolInts - kCapInts) / 8) return nullptr;
+    if (p.ring + take > kPoolInts) p.ring = kCapInts;
+    int* r = p.base + p.ring;
+    p.ring += take;
+    return r;
+  }
+  if (p.used + take > kCapInts) return nullptr;
   int* r = p.base + p.used;
   p.used += take;
   return r;

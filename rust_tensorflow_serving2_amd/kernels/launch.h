@@ -58,11 +58,11 @@ struct IGemmArgs {
   int* counters;
 };
 
-// Per-device pool of zeroed split-K arrival counters for kernels captured into
-// HIP graphs: a capture takes a slice for good (its replays are ordered on its
-// stream, and each tile's last arriver re-zeroes its counter).  nullptr when
-// the stream is not capturing or the pool is exhausted: the caller then uses
-// the separate reduce launch.
+// Per-device pool of zeroed split-K arrival counters: a launch captured into a
+// HIP graph takes a slice for good (its replays are ordered on its stream, and
+// each tile's last arriver re-zeroes its counter); an eager launch takes the
+// next slice of a ring.  nullptr when the pool is missing or exhausted: the
+// caller then uses the separate reduce launch.
 int* splitk_counters(int n, hipStream_t s);
 // Allocates and zeroes this device's pool (no-op while `s` is capturing).
 void splitk_counters_prepare(hipStream_t s);
@@ -95,6 +95,13 @@ int igemm_config_stages(int cfg);
 int igemm_config_bk(int cfg);
 hipError_t igemm_launch(const IGemmArgs& args, int a_mode, int cfg, hipStream_t stream);
 
+// Fused ResNet stem (stem.hip): fp32 [N][H][W][C<=4] -> 7x7/2 conv (weights
+// [cout][ldw] bf16, k = kh*32 + kw*4 + c, cout in {16,32,48,64}) + bias + act
+// -> 3x3/2 max pool (+ optional scale/shift/act after the max) -> bf16
+// [N][Hp][Wp][cout].  pt/pl: conv padding; ppt/ppl: pool padding.
+hipError_t stem_pool_launch(const float* x, const uint16_t* w, int ldw, const float* bias, uint16_t* y, int N, int H,
+                            int W, int C, int cout, int pt, int pl, int Hc, int Wc, int ppt, int ppl, int Hp, int Wp,
+                            int act, const float* pscale, const float* pshift, int pact, hipStream_t s);
 // NHWC bf16 max-pool (TF SAME/VALID padding given explicitly).  With `scale`
 // (and `shift`): y = act(max * scale[c] + shift[c]) — a folded inference
 // BatchNorm (+ ReLU when act == 1) applied after the pooling.

@@ -1,0 +1,278 @@
+// ResNet stem in ONE kernel: fp32 RGB request -> 7x7/2 conv (+folded BN, act)
+// -> 3x3/2 max pool (+ optional folded BN/act after the max, ResNet v2).
+//
+// The unfused path ran three launches and moved the 112x112x64 conv output
+// through memory twice (b32: ingest 12.4 us + stem cgemm 34.6 us + maxpool
+// 17.7 us, profiles/round2/r50_b32_replay_head_halo9.txt).  Here a workgroup
+// owns a 4 x 8 tile of POOLED outputs: it computes the 9 x 17 conv pixels
+// under that tile's pooling windows (1.2x recompute of the shared border),
+// keeps them in LDS, and writes only the pooled tile.
+//
+//   * input patch: the 23 x 40 fp32 pixels under those conv windows, read
+//     straight from the request tensor (out-of-image -> 0, the conv's zero
+//     padding), cast to bf16 and padded to 4 channels in LDS (8 B / pixel);
+//   * the K order is [kh][kw (7 -> 8, tap 7 has zero weight)][4 ch], so one
+//     32-deep MFMA k-step is one filter row and a lane's 8 k-values are two
+//     horizontally adjacent pixels: one 16-B LDS read per A fragment;
+//   * weights (<= 64 x 224 bf16) live in registers for the workgroup's whole
+//     life: the grid is persistent (<= 2 workgroups per CU), each workgroup
+//     walks a contiguous run of tiles and prefetches the next tile's patch
+//     into registers while its MFMAs run;
+//   * waves split the 10 row groups of 16 conv pixels (3/3/2/2) and each
+//     computes all output channels, so a patch fragment is read from LDS once
+//     per use by 1-4 MFMAs;
+//   * C = W x patch^T: a lane's accumulator is 4 consecutive channels of one
+//     pixel, stored to LDS packed (v_cvt_pk_bf16_f32) as order-preserving
+//     int16 keys, so the 3x3 max runs as packed v_pk_max_i16 (the first
+//     version's per-value conversions / stores made it VALU-issue bound:
+//     62 us at b32);
+//   * conv pixels outside the conv's output range are stored as -inf, so the
+//     pooling max ignores them (TF SAME/VALID pooling semantics).
+//
+// The op replaces _FusedConv2D(7x7/2, C <= 4) -> _MaxPool(3x3/2) in the graph
+// (graph/fused.py fuse_stem_pool); the model is the one the reference serves
+// (/root/reference/serving/fetch.sh:7, resnet_v2_fp32_savedmodel_NHWC) and the
+// request tensor is the one its client sends (src/lib.rs:229-257).
+#include "common.h"
+#include "launch.h"
+
+namespace tfsk {
+namespace {
+
+constexpr int kTPY = 4, kTPX = 8;                   // pooled tile
+constexpr int kCR = 2 * kTPY + 1, kCC = 2 * kTPX + 1;  // conv pixels under it: 9 x 17
+constexpr int kNPix = kCR * kCC;                    // 153
+constexpr int kNRG = (kNPix + 15) / 16;             // 10 row groups of 16
+constexpr int kIR = 2 * (kCR - 1) + 7;              // 23 input rows
+constexpr int kIC = 2 * (kCC - 1) + 8;              // 40 input cols (tap 7 is padding)
+constexpr int kPatch = kIR * kIC;                   // 920 pixels
+constexpr int kSlots = (kPatch + 255) / 256;        // 4 per thread
+constexpr int kKSteps = 7;                          // filter rows
+
+struct StemArgs {
+  const float* x;       // [N][H][W][C] fp32
+  const uint16_t* w;    // [Cout][ldw] bf16, k = kh*32 + kw*4 + c
+  const float* bias;    // [Cout]
+  uint16_t* y;          // [N][Hp][Wp][Cout] bf16
+  const float* pscale;  // optional [Cout] (after the max)
+  const float* pshift;
+  int N, H, W, C, ldw;
+  int pt, pl, Hc, Wc;   // conv padding (top / left) and output size
+  int ppt, ppl, Hp, Wp; // pool padding (top / left) and output size
+  int tiles_y, tiles_x, tiles;
+  float lo, plo;        // activation as a floor: 0 (ReLU) or -inf (none)
+};
+
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(2))) short s16x2;
+
+// two f32 -> packed bf16 (v_cvt_pk_bf16_f32, round-to-nearest-even)
+__device__ __forceinline__ uint32_t cvt2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+// order-preserving bf16 <-> int16 key (self-inverse): negative values get
+// their magnitude bits flipped, so a signed 16-bit max is the float max and
+// the pool runs on packed v_pk_max_i16 (two channels per instruction)
+__device__ __forceinline__ uint32_t okey(uint32_t u) {
+  const s16x2 v = __builtin_bit_cast(s16x2, u);
+  return __builtin_bit_cast(uint32_t, v ^ ((v >> 15) & (s16x2){0x7fff, 0x7fff}));
+}
+__device__ __forceinline__ uint32_t kmax(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, a),
+                                                                __builtin_bit_cast(s16x2, b)));
+}
+
+template <int NCG>
+__global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
+  constexpr int COUT = NCG * 16;
+  constexpr int CS = COUT + 8;                      // conv tile row stride (halves), 16-B aligned rows
+  __shared__ uint2 patch[kPatch];
+  __shared__ __attribute__((aligned(16))) uint16_t ctile[kNRG * 16 * CS];   // rows >= 153: scratch
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar branches)
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // ---- this workgroup's run of tiles (XCD-aware: neighbouring runs share an L2)
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int t_begin = int(long(wg) * p.tiles / gridDim.x);
+  const int t_end = int(long(wg + 1) * p.tiles / gridDim.x);
+  if (t_begin >= t_end) return;
+
+  // ---- weights (MFMA A operand: rows = output channels) and bias in registers
+  // for the whole run.  C = W x patch^T, so a lane's accumulator holds 4
+  // CONSECUTIVE channels of one conv pixel: one packed 8-B LDS store each.
+  bf16x8 wf[kKSteps][NCG];
+  float4 bias[NCG];
+#pragma unroll
+  for (int j = 0; j < NCG; ++j) {
+    const uint16_t* wr = p.w + long(j * 16 + fr) * p.ldw + fq * 8;
+#pragma unroll
+    for (int kh = 0; kh < kKSteps; ++kh) wf[kh][j] = *reinterpret_cast<const bf16x8*>(wr + kh * 32);
+    bias[j] = *reinterpret_cast<const float4*>(p.bias + j * 16 + fq * 4);
+  }
+
+  // ---- this lane's conv pixel in each of the wave's row groups (B operand
+  // columns); pixels past 153 clamp their reads and store to scratch rows
+  constexpr int kRGW = (kNRG + 3) / 4;              // row groups per wave (max)
+  int aoff[kRGW], pcy[kRGW], pcx[kRGW];
+#pragma unroll
+  for (int i = 0; i < kRGW; ++i) {
+    const int px = min((wid + 4 * i) * 16 + fr, kNPix - 1);
+    pcy[i] = px / kCC;
+    pcx[i] = px - pcy[i] * kCC;
+    aoff[i] = 2 * pcy[i] * kIC + 2 * pcx[i] + 2 * fq;
+  }
+
+  float pf[kSlots][4];
+  auto load_patch = [&](int t) {
+    const int n = t / (p.tiles_y * p.tiles_x);
+    const int rem = t - n * p.tiles_y * p.tiles_x;
+    const int ty = rem / p.tiles_x, tx = rem - ty * p.tiles_x;
+    const int iy0 = 2 * (2 * ty * kTPY - p.ppt) - p.pt;
+    const int ix0 = 2 * (2 * tx * kTPX - p.ppl) - p.pl;
+    const float* xn = p.x + long(n) * p.H * p.W * p.C;
+    // branch-free: every load reads a clamped in-image address, then masks
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+      const int q = tid + s * 256;
+      const int r = q / kIC, c = q - r * kIC;
+      const int gy = iy0 + r, gx = ix0 + c;
+      const bool ok = q < kPatch && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W;
+      const int gyc = min(max(gy, 0), p.H - 1), gxc = min(max(gx, 0), p.W - 1);
+      const float* src = xn + (long(gyc) * p.W + gxc) * p.C;
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch) {
+        const float v = src[min(ch, p.C - 1)];
+        pf[s][ch] = ok && ch < p.C ? v : 0.f;
+      }
+    }
+  };
+
+  load_patch(t_begin);
+  for (int t = t_begin; t < t_end; ++t) {
+    // ---- stage the prefetched patch (the previous tile's MFMA reads ended at
+    // its post-epilogue barrier)
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+      const int q = tid + s * 256;
+      if (q < kPatch) patch[q] = make_uint2(cvt2(pf[s][0], pf[s][1]), cvt2(pf[s][2], pf[s][3]));
+    }
+    __syncthreads();
+    if (t + 1 < t_end) load_patch(t + 1);           // in flight during the MFMAs
+
+    // ---- conv: 7 k-steps x (2-3 row groups) x NCG channel groups
+    f32x4 acc[kRGW][NCG];
+#pragma unroll
+    for (int i = 0; i < kRGW; ++i)
+#pragma unroll
+      for (int j = 0; j < NCG; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* pb = reinterpret_cast<const char*>(patch);
+#pragma unroll
+    for (int kh = 0; kh < kKSteps; ++kh) {
+#pragma unroll
+      for (int i = 0; i < kRGW; ++i) {
+        if (wid + 4 * i >= kNRG) continue;          // wave-uniform
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(pb + size_t(aoff[i] + kh * kIC) * 8);
+#pragma unroll
+        for (int j = 0; j < NCG; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kh][j], a, acc[i][j], 0, 0, 0);
+      }
+    }
+
+    // ---- epilogue -> LDS conv tile as order keys (bias, act; outside the
+    // conv output: -inf)
+    const int n = t / (p.tiles_y * p.tiles_x);
+    const int rem = t - n * p.tiles_y * p.tiles_x;
+    const int ty = rem / p.tiles_x, tx = rem - ty * p.tiles_x;
+    const int cy0 = 2 * ty * kTPY - p.ppt, cx0 = 2 * tx * kTPX - p.ppl;
+#pragma unroll
+    for (int i = 0; i < kRGW; ++i) {
+      if (wid + 4 * i >= kNRG) continue;
+      const int px = (wid + 4 * i) * 16 + fr;
+      const bool in = (unsigned)(cy0 + pcy[i]) < (unsigned)p.Hc && (unsigned)(cx0 + pcx[i]) < (unsigned)p.Wc;
+#pragma unroll
+      for (int j = 0; j < NCG; ++j) {
+        float v[4];
+        const float b[4] = {bias[j].x, bias[j].y, bias[j].z, bias[j].w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = in ? fmaxf(acc[i][j][r] + b[r], p.lo) : -INFINITY;
+        *reinterpret_cast<uint2*>(ctile + px * CS + j * 16 + fq * 4) =
+            make_uint2(okey(cvt2(v[0], v[1])), okey(cvt2(v[2], v[3])));
+      }
+    }
+    __syncthreads();
+
+    // ---- 3x3/2 max over the conv tile -> pooled tile (16 B = 8 channels per item)
+    constexpr int C8 = COUT / 8;
+    for (int idx = tid; idx < kTPY * kTPX * C8; idx += 256) {
+      const int q = idx / C8, c8 = idx - q * C8;
+      const int qy = q / kTPX, qx = q - qy * kTPX;
+      const int py = ty * kTPY + qy, px = tx * kTPX + qx;
+      if (py >= p.Hp || px >= p.Wp) continue;
+      const uint16_t* c0 = ctile + (2 * qy * kCC + 2 * qx) * CS + c8 * 8;
+      uint4 m = *reinterpret_cast<const uint4*>(c0);
+#pragma unroll
+      for (int tap = 1; tap < 9; ++tap) {
+        const uint4 v = *reinterpret_cast<const uint4*>(c0 + ((tap / 3) * kCC + tap % 3) * CS);
+        m = make_uint4(kmax(m.x, v.x), kmax(m.y, v.y), kmax(m.z, v.z), kmax(m.w, v.w));
+      }
+      uint32_t o[4] = {okey(m.x), okey(m.y), okey(m.z), okey(m.w)};
+      if (p.pscale) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = c8 * 8 + 2 * e;
+          const float lo = fmaxf(__uint_as_float(o[e] << 16) * p.pscale[c] + p.pshift[c], p.plo);
+          const float hi = fmaxf(__uint_as_float(o[e] & 0xffff0000u) * p.pscale[c + 1] + p.pshift[c + 1], p.plo);
+          o[e] = cvt2(lo, hi);
+        }
+      }
+      *reinterpret_cast<uint4*>(p.y + ((long(n) * p.Hp + py) * p.Wp + px) * COUT + c8 * 8) =
+          make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    // the next iteration's barrier (after its patch store) orders these ctile
+    // reads before its epilogue's writes
+  }
+}
+
+int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;   // benign race: every writer stores the same value
+  }
+  return cached[dev];
+}
+
+}  // namespace
+
+hipError_t stem_pool_launch(const float* x, const uint16_t* w, int ldw, const float* bias, uint16_t* y, int N, int H,
+                            int W, int C, int cout, int pt, int pl, int Hc, int Wc, int ppt, int ppl, int Hp, int Wp,
+                            int act, const float* pscale, const float* pshift, int pact, hipStream_t s) {
+  if (N <= 0 || Hp <= 0 || Wp <= 0) return hipSuccess;
+  if (C < 1 || C > 4 || cout % 16 || cout < 16 || cout > 64 || ldw < kKSteps * 32 || ldw % 8 ||
+      (pscale == nullptr) != (pshift == nullptr) || ppt < 0 || ppl < 0 || pt < 0 || pl < 0)
+    return hipErrorInvalidValue;
+  if (Hc <= 0 || Wc <= 0 || ppt > 2 || ppl > 2) return hipErrorInvalidValue;
+  if ((act != kActNone && act != kActRelu) || (pact != kActNone && pact != kActRelu)) return hipErrorInvalidValue;
+  StemArgs a{x, w, bias, y, pscale, pshift, N, H, W, C, ldw, pt, pl, Hc, Wc, ppt, ppl, Hp, Wp, 0, 0, 0,
+             act == kActRelu ? 0.f : -INFINITY, pact == kActRelu ? 0.f : -INFINITY};
+  a.tiles_y = (Hp + kTPY - 1) / kTPY;
+  a.tiles_x = (Wp + kTPX - 1) / kTPX;
+  const long tiles = long(N) * a.tiles_y * a.tiles_x;
+  if (tiles > (1L << 30)) return hipErrorInvalidValue;
+  a.tiles = int(tiles);
+  const int grid = int(tiles < 2L * cu_count() ? tiles : 2L * cu_count());
+  switch (cout / 16) {
+    case 1: hipLaunchKernelGGL(stem_pool_kernel<1>, dim3(grid), dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(stem_pool_kernel<2>, dim3(grid), dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(stem_pool_kernel<3>, dim3(grid), dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(stem_pool_kernel<4>, dim3(grid), dim3(256), 0, s, a); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace tfsk

@@ -603,3 +603,49 @@ def test_splitk_in_kernel_fixup_inside_graph(cfg, splits, shape, post, monkeypat
         assert torch.equal(out, eager), (out.float() - eager.float()).abs().max()
         if post:
             assert torch.equal(out2, eager2)
+
+
+# ResNet stem fused with its max pool (stem.hip): fp32 RGB in, pooled bf16 out.
+# (n, h, w, C, cout, conv pads (t, b, l, r), pool pads (t, b, l, r), act, post)
+STEM_CASES = [
+    (2, 224, 224, 3, 64, (3, 3, 3, 3), (0, 1, 0, 1), "relu", False),   # ResNet-50 v1.5 stem (Pad 3 + VALID, SAME pool)
+    (1, 224, 224, 3, 64, (3, 3, 3, 3), (0, 1, 0, 1), "none", True),    # v2: pool carries block 1's pre-activation
+    (3, 160, 160, 3, 16, (3, 3, 3, 3), (0, 1, 0, 1), "relu", False),
+    (2, 37, 53, 3, 32, (2, 3, 2, 3), (0, 1, 1, 1), "relu", False),     # odd sizes, partial tiles
+    (1, 41, 29, 1, 48, (0, 0, 0, 0), (0, 0, 0, 0), "none", False),     # VALID conv + VALID pool, 1 channel
+    (2, 64, 64, 4, 64, (3, 3, 3, 3), (1, 1, 1, 1), "relu", True),      # RGBA, symmetric pool padding
+]
+
+
+@pytest.mark.parametrize("n,h,w,c,cout,cp,pp,act,post", STEM_CASES)
+def test_stem_pool_fused_kernel(n, h, w, c, cout, cp, pp, act, post):
+    x = torch.rand(n, h, w, c, generator=torch.Generator().manual_seed(h * w + cout))
+    wt = rnd(cout, 7, 7, c, scale=0.05, seed=cout + c)
+    w4 = torch.zeros(cout, 8, 8, 4)
+    w4[:, :7, :7, :c] = wt
+    wk = w4.reshape(cout, 256).to(BF)
+    b = rnd(cout, scale=0.1, seed=7)
+    kw = {}
+    if post:
+        sc, sh = rnd(cout, seed=8) * 0.5, rnd(cout, seed=9) * 0.2
+        kw = dict(post_scale=sc.to(DEV), post_shift=sh.to(DEV), post_act=ACT["relu"])
+    y = hip().stem_pool(x.to(DEV), wk.to(DEV), b.to(DEV), *cp, ACT[act], *pp, **kw)
+    # reference: bf16-rounded operands, fp32 conv, conv output rounded to bf16
+    # (as the unfused path stores it), -inf-padded max pool
+    xr = x.to(BF).float().permute(0, 3, 1, 2)
+    wr = wk.float().reshape(cout, 8, 8, 4)[:, :7, :7, :c].permute(0, 3, 1, 2)
+    pt, pb, pl, pr = cp
+    conv = F.conv2d(F.pad(xr, [pl, pr, pt, pb]), wr, stride=2) + b.view(1, -1, 1, 1)
+    if act == "relu":
+        conv = torch.relu(conv)
+    conv = conv.to(BF).float()
+    qt, qb, ql, qr = pp
+    ref = F.max_pool2d(F.pad(conv, [ql, qr, qt, qb], value=float("-inf")), 3, 2).permute(0, 2, 3, 1)
+    if post:
+        ref = torch.relu(ref * sc + sh).to(BF).float()
+    torch.cuda.synchronize()
+    assert y.shape == ref.shape and y.dtype == BF
+    err = (y.float().cpu() - ref).abs()
+    assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
+    # most outputs agree exactly: only bf16 rounding ties of the conv values can differ
+    assert (err == 0).float().mean().item() > 0.9

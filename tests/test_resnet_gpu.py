@@ -58,8 +58,10 @@ def test_resnet50_gpu_matches_cpu(resnet50):
     hist = runner.program.op_histogram()
     # 53 convs: 4 stage-entry (expand conv + projection shortcut) pairs run as
     # one K-concatenated dual-source GEMM each
+    # the stem conv runs inside the fused stem + max-pool kernel
     assert hist.get("_FusedDualConv") == 4 and "Conv2D" not in hist
-    assert hist.get("_FusedConv2D") + 2 * hist["_FusedDualConv"] == 53
+    assert hist.get("_StemPool") == 1 and "_MaxPool" not in hist
+    assert hist.get("_FusedConv2D") + 2 * hist["_FusedDualConv"] + hist["_StemPool"] == 53
 
 
 @pytest.fixture(scope="module")
@@ -87,7 +89,8 @@ def test_resnet50_v2_gpu_fully_fused_matches_cpu(resnet50_v2):
     hist = runner.program.op_histogram()
     for op in ("FusedBatchNormV3", "Relu", "Mul", "Conv2D", "AddV2"):
         assert op not in hist, hist
-    assert hist.get("_FusedConv2D") + 2 * hist.get("_FusedDualConv", 0) == 53
+    assert hist.get("_StemPool") == 1 and "_MaxPool" not in hist
+    assert hist.get("_FusedConv2D") + 2 * hist.get("_FusedDualConv", 0) + hist["_StemPool"] == 53
 
 
 def test_smoke():
