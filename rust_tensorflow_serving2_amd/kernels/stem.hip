@@ -203,11 +203,14 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
     }
     __syncthreads();
 
-    // ---- 3x3/2 max over the conv tile -> pooled tile (16 B = 8 channels per item)
+    // ---- 3x3/2 max over the conv tile -> pooled tile (16 B = 8 channels per
+    // item).  Pooled column fastest across lanes: neighbouring lanes read conv
+    // pixels 2 apart (288 B = bank offset 8 for COUT 64), so 8 lanes x 16 B
+    // cover all 64 banks; channel-chunk-fastest order had 2-way conflicts
+    // (SQ_LDS_BANK_CONFLICT 2.1M cycles per launch at b32)
     constexpr int C8 = COUT / 8;
     for (int idx = tid; idx < kTPY * kTPX * C8; idx += 256) {
-      const int q = idx / C8, c8 = idx - q * C8;
-      const int qy = q / kTPX, qx = q - qy * kTPX;
+      const int qx = idx % kTPX, c8 = (idx / kTPX) % C8, qy = idx / (kTPX * C8);
       const int py = ty * kTPY + qy, px = tx * kTPX + qx;
       if (py >= p.Hp || px >= p.Wp) continue;
       const uint16_t* c0 = ctile + (2 * qy * kCC + 2 * qx) * CS + c8 * 8;
