@@ -478,6 +478,8 @@ class StemPool:
     directly, the conv output stays in LDS and only the pooled map is written
     (three launches and two passes over the 112x112x64 conv output before)."""
 
+    children = ("conv", "pool")        # weight_refs (graph/placement.py) walks these
+
     def __init__(self, conv: FusedConv, pool: MaxPool):
         self.conv, self.pool = conv, pool
         self.use_hip = conv.use_hip and conv.c4

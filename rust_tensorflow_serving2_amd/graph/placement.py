@@ -71,14 +71,19 @@ def weight_refs(program) -> List[Tuple[Ref, torch.Tensor]]:
     dev = program.device
     out = []
     seen = set()
-    for fn, node, _ins, _outs in program.steps:
-        impl = node.attrs.get("_impl")
+
+    def visit(impl):
         if impl is None or id(impl) in seen:
-            continue
+            return
         seen.add(id(impl))
         for k, i, t in _tensor_attrs(impl):
             if t.device.type == dev.type and t.numel() > 0:
                 out.append(((impl, k, i), t))
+        for child in getattr(impl, "children", ()):   # fused ops built from other fused ops
+            visit(getattr(impl, child))
+
+    for fn, node, _ins, _outs in program.steps:
+        visit(node.attrs.get("_impl"))
     for pos, (slot, v) in enumerate(program.const_slots):
         if isinstance(v, torch.Tensor) and v.device.type == dev.type and v.numel() > 0 and \
                 (v.is_floating_point() or v.is_meta or dev.type != "cpu"):

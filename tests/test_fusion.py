@@ -76,8 +76,15 @@ def test_resnet_stem_conv_and_pool_become_one_op(models_dir, version):
     b = fused.run("serving_default", {"input": x}, ["classes", "probabilities"])
     np.testing.assert_allclose(a["probabilities"], b["probabilities"], atol=1e-5)
     np.testing.assert_array_equal(a["classes"], b["classes"])
-    hist = fused.runner("serving_default", ["input"], ["classes", "probabilities"]).program.op_histogram()
+    prog = fused.runner("serving_default", ["input"], ["classes", "probabilities"]).program
+    hist = prog.op_histogram()
     assert hist["_StemPool"] == 1 and "_MaxPool" not in hist, hist
+    # the replicated-weights packer (graph/placement.py) must see the stem conv
+    # nested inside the fused op, or a follower replica would keep its own copy
+    from rust_tensorflow_serving2_amd.graph.placement import weight_refs
+    stem = next(n.attrs["_impl"] for _f, n, _i, _o in prog.steps if n.op == "_StemPool")
+    held = {id(ref[0]) for ref, _t in weight_refs(prog)}
+    assert id(stem.conv) in held
 
 
 def test_bert_fusion_exact(tiny_bert):
