@@ -558,6 +558,9 @@ def fuse_stem_pool(g, order, fed, fetch_refs, device, opts):
     """``_MaxPool(3x3/2)(_FusedConv2D(7x7/2, C <= 4 channels, 16..64 outputs))``
     -> ``_StemPool`` when the conv has no residual / post output and feeds only
     the pool, and the pool writes a single output."""
+    import os
+    if os.environ.get("TFSERVE_STEM_POOL", "1") == "0":       # A/B switch
+        return
     c = _Ctx(g, order, fed, fetch_refs, device, opts)
     for name in order:
         p = g.nodes.get(name)
