@@ -75,18 +75,30 @@ __device__ __forceinline__ bool epi_rowcol(int tid, int it, int& row, int& col) 
   return E::EXACT || (tid < E::NTE && row < BM);
 }
 
+// 16 B at byte offset `voff` of a buffer resource as float4 (an offset past the
+// buffer's records -- kOOB, or any offset of a 0-record resource -- reads zeros)
+__device__ __forceinline__ float4 buffer_f4(__amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
 // This thread's 8 bias values (its epilogue column is fixed), loaded before the
-// K loop so the latency of the load hides under it.
+// K loop so the latency of the load hides under it.  Branch-free buffer loads:
+// a guarded `if (ok) b = *p` became a conditional block whose register moves
+// waited (vmcnt(0)) for the load -- and for every residual prefetch issued
+// before it -- ahead of the first operand DMA, i.e. one full memory round trip
+// per workgroup before its K loop could start (seen in the gfx950 ISA).
 template <int BM, int BN, int NT>
 __device__ __forceinline__ void prefetch_bias(const IGemmArgs& p, int n0, int tid, float4& b0, float4& b1) {
   int row0, col0;
   epi_rowcol<BM, BN, NT>(tid, 0, row0, col0);   // col0 < BN for every thread
   const int n = n0 + col0;
-  b0 = b1 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (p.bias && p.splits <= 1 && p.N % 8 == 0 && n + 8 <= p.N) {
-    b0 = *reinterpret_cast<const float4*>(p.bias + n);
-    b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
-  }
+  const bool use = p.bias && p.splits <= 1 && p.N % 8 == 0;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.bias), 0, use ? p.N * 4 : 0, 0x00020000);
+  const uint32_t voff = n + 8 <= p.N ? uint32_t(n) * 4u : kOOB;
+  b0 = buffer_f4(rs, voff);
+  b1 = buffer_f4(rs, voff + 16u);
 }
 
 // Split-K without a reduce launch: every slice stores its fp32 slab with

@@ -467,13 +467,34 @@ __global__ __launch_bounds__(256) void layernorm_fit_kernel(const uint16_t* __re
   }
   const bool ok = row < rows;
   const long base = long(ok ? row : 0) * COLS;
+  // every row load (x chunks and residual chunks) in flight at once: the
+  // residual goes through a buffer resource (0 records when there is none ->
+  // zeros), because `if (r) load` compiled to per-chunk conditional blocks that
+  // each waited for their load -- 2 x CH serial memory round trips per row
+  uint4 xv[CH];
+  u32x4 rv[CH];
+  const __amdgpu_buffer_rsrc_t rsR = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(r), 0, r ? int(long(rows) * COLS * 2) : 0, 0x00020000);
+#pragma unroll
+  for (int k = 0; k < CH; ++k) xv[k] = *reinterpret_cast<const uint4*>(x + base + (k * LPR + l) * 8);
+#pragma unroll
+  for (int k = 0; k < CH; ++k)
+    rv[k] = __builtin_amdgcn_raw_buffer_load_b128(rsR, uint32_t(base + (k * LPR + l) * 8) * 2u, 0, 0);
+  // keep the gamma/beta loads above ahead of the row math (the scheduler sank
+  // them below the reduction: one more serial round trip before the stores)
+  __builtin_amdgcn_sched_barrier(0);
   float v[CH][8];
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
-    ln_load(x + base, r ? r + base : nullptr, (k * LPR + l) * 8, v[k]);
+    float rf[8];
+    unpack8(xv[k], v[k]);
+    unpack8(make_uint4(rv[k].x, rv[k].y, rv[k].z, rv[k].w), rf);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) s += v[k][e];
+    for (int e = 0; e < 8; ++e) {
+      v[k][e] += rf[e];
+      s += v[k][e];
+    }
   }
 #pragma unroll
   for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -486,13 +507,14 @@ __global__ __launch_bounds__(256) void layernorm_fit_kernel(const uint16_t* __re
 #pragma unroll
   for (int o = LPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
   const float inv = rsqrtf(ss * (1.f / COLS) + eps);
-  if (!ok) return;
+  // no early return for rows past the end: with one, the gamma/beta loads
+  // were sunk below it and issued only after the row reduction
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     float o8[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o8[e] = (v[k][e] - mean) * inv * g[k][e] + b[k][e];
-    *reinterpret_cast<uint4*>(y + base + (k * LPR + l) * 8) = pack8(o8);
+    if (ok) *reinterpret_cast<uint4*>(y + base + (k * LPR + l) * 8) = pack8(o8);
   }
 }
 
@@ -733,6 +755,11 @@ template <int LPR, int CH>
 hipError_t ln_fit(const uint16_t* x, const uint16_t* r, const float* gamma, const float* beta, uint16_t* y, int rows,
                   float eps, hipStream_t s) {
   const int per_block = 4 * (64 / LPR);
+  if (long(rows) * LPR * 8 * CH * 2 >= 0x7fffffffL) {   // residual buffer offsets are 32-bit
+    hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, r, gamma, beta, y, rows,
+                       LPR * 8 * CH, eps);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((layernorm_fit_kernel<LPR, CH>), dim3((rows + per_block - 1) / per_block), dim3(256), 0, s, x, r,
                      gamma, beta, y, rows, eps);
   return hipGetLastError();

@@ -125,6 +125,15 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
     aoff[i] = 2 * pcy[i] * kIC + 2 * pcx[i] + 2 * fq;
   }
 
+  // request tensor as a buffer resource: an out-of-image pixel or a channel
+  // >= C reads through an out-of-range offset and gets the conv's zero padding
+  // from the hardware.  (The first version loaded through plain pointers and
+  // selected afterwards; hipcc turned that into per-slot conditional blocks
+  // that waited for their loads on the spot, so the "prefetch" of the next
+  // tile's patch was four serial memory round trips per tile: ~8 us per tile.)
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.x), 0, int(long(p.N) * p.H * p.W * p.C * 4), 0x00020000);
+  constexpr uint32_t kOff = 0x80000000u;
   float pf[kSlots][4];
   auto load_patch = [&](int t) {
     const int n = t / (p.tiles_y * p.tiles_x);
@@ -132,20 +141,17 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
     const int ty = rem / p.tiles_x, tx = rem - ty * p.tiles_x;
     const int iy0 = 2 * (2 * ty * kTPY - p.ppt) - p.pt;
     const int ix0 = 2 * (2 * tx * kTPX - p.ppl) - p.pl;
-    const float* xn = p.x + long(n) * p.H * p.W * p.C;
-    // branch-free: every load reads a clamped in-image address, then masks
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
       const int q = tid + s * 256;
       const int r = q / kIC, c = q - r * kIC;
       const int gy = iy0 + r, gx = ix0 + c;
       const bool ok = q < kPatch && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W;
-      const int gyc = min(max(gy, 0), p.H - 1), gxc = min(max(gx, 0), p.W - 1);
-      const float* src = xn + (long(gyc) * p.W + gxc) * p.C;
+      const uint32_t pix = uint32_t(((n * p.H + gy) * p.W + gx) * p.C) * 4u;
 #pragma unroll
       for (int ch = 0; ch < 4; ++ch) {
-        const float v = src[min(ch, p.C - 1)];
-        pf[s][ch] = ok && ch < p.C ? v : 0.f;
+        const uint32_t voff = ok && ch < p.C ? pix + uint32_t(ch) * 4u : kOff;
+        pf[s][ch] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsX, voff, 0, 0));
       }
     }
   };
@@ -267,6 +273,7 @@ hipError_t stem_pool_launch(const float* x, const uint16_t* w, int ldw, const fl
   a.tiles_x = (Wp + kTPX - 1) / kTPX;
   const long tiles = long(N) * a.tiles_y * a.tiles_x;
   if (tiles > (1L << 30)) return hipErrorInvalidValue;
+  if (long(N) * H * W * C * 4 >= 0x7fffffffL) return hipErrorInvalidValue;   // 32-bit buffer offsets
   a.tiles = int(tiles);
   const int grid = int(tiles < 2L * cu_count() ? tiles : 2L * cu_count());
   switch (cout / 16) {
