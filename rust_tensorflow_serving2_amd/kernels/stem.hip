@@ -61,6 +61,7 @@ struct StemArgs {
   int ppt, ppl, Hp, Wp; // pool padding (top / left) and output size
   int tiles_y, tiles_x, tiles;
   float lo, plo;        // activation as a floor: 0 (ReLU) or -inf (none)
+  int dbg;              // profiling ablations (TFSK_STEM_DBG; 0 in production)
 };
 
 typedef __attribute__((ext_vector_type(2))) float f32x2;
@@ -130,11 +131,14 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
   // from the hardware.  (The first version loaded through plain pointers and
   // selected afterwards; hipcc turned that into per-slot conditional blocks
   // that waited for their loads on the spot, so the "prefetch" of the next
-  // tile's patch was four serial memory round trips per tile: ~8 us per tile.)
+  // tile's patch was serial memory round trips: b32 47.5 -> 38.5 us in graph
+  // replay with this form.  Ablations after the change, b32 eager 35.5 us:
+  // without the loads 30.1, the MFMAs 26.5, the pool 31.6, the conv-tile
+  // stores 30.0, all four 12.6 -- profiles/round2/stem_ablate.log)
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(p.x), 0, int(long(p.N) * p.H * p.W * p.C * 4), 0x00020000);
   constexpr uint32_t kOff = 0x80000000u;
-  float pf[kSlots][4];
+  float pf[kSlots][4] = {};
   auto load_patch = [&](int t) {
     const int n = t / (p.tiles_y * p.tiles_x);
     const int rem = t - n * p.tiles_y * p.tiles_x;
@@ -156,7 +160,10 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
     }
   };
 
-  load_patch(t_begin);
+  // ablations (timing only, results are garbage): bit 0 skips the patch
+  // loads, bit 1 the MFMAs, bit 2 the pool phase, bit 3 the conv-tile stores
+  const int dbg = p.dbg;
+  if (!(dbg & 1)) load_patch(t_begin);
   for (int t = t_begin; t < t_end; ++t) {
     // ---- stage the prefetched patch (the previous tile's MFMA reads ended at
     // its post-epilogue barrier)
@@ -166,7 +173,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
       if (q < kPatch) patch[q] = make_uint2(cvt2(pf[s][0], pf[s][1]), cvt2(pf[s][2], pf[s][3]));
     }
     __syncthreads();
-    if (t + 1 < t_end) load_patch(t + 1);           // in flight during the MFMAs
+    if (t + 1 < t_end && !(dbg & 1)) load_patch(t + 1);   // in flight during the MFMAs
 
     // ---- conv: 7 k-steps x (2-3 row groups) x NCG channel groups
     f32x4 acc[kRGW][NCG];
@@ -179,7 +186,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
     for (int kh = 0; kh < kKSteps; ++kh) {
 #pragma unroll
       for (int i = 0; i < kRGW; ++i) {
-        if (wid + 4 * i >= kNRG) continue;          // wave-uniform
+        if (wid + 4 * i >= kNRG || (dbg & 2)) continue;   // wave-uniform
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(pb + size_t(aoff[i] + kh * kIC) * 8);
 #pragma unroll
         for (int j = 0; j < NCG; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kh][j], a, acc[i][j], 0, 0, 0);
@@ -194,7 +201,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
     const int cy0 = 2 * ty * kTPY - p.ppt, cx0 = 2 * tx * kTPX - p.ppl;
 #pragma unroll
     for (int i = 0; i < kRGW; ++i) {
-      if (wid + 4 * i >= kNRG) continue;
+      if (wid + 4 * i >= kNRG || (dbg & 8)) continue;
       const int px = (wid + 4 * i) * 16 + fr;
       const bool in = (unsigned)(cy0 + pcy[i]) < (unsigned)p.Hc && (unsigned)(cx0 + pcx[i]) < (unsigned)p.Wc;
 #pragma unroll
@@ -215,7 +222,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
     // cover all 64 banks; channel-chunk-fastest order had 2-way conflicts
     // (SQ_LDS_BANK_CONFLICT 2.1M cycles per launch at b32)
     constexpr int C8 = COUT / 8;
-    for (int idx = tid; idx < kTPY * kTPX * C8; idx += 256) {
+    for (int idx = tid; idx < kTPY * kTPX * C8 && !(dbg & 4); idx += 256) {
       const int qx = idx % kTPX, c8 = (idx / kTPX) % C8, qy = idx / (kTPX * C8);
       const int py = ty * kTPY + qy, px = tx * kTPX + qx;
       if (py >= p.Hp || px >= p.Wp) continue;
@@ -268,7 +275,12 @@ hipError_t stem_pool_launch(const float* x, const uint16_t* w, int ldw, const fl
   if (Hc <= 0 || Wc <= 0 || ppt > 2 || ppl > 2) return hipErrorInvalidValue;
   if ((act != kActNone && act != kActRelu) || (pact != kActNone && pact != kActRelu)) return hipErrorInvalidValue;
   StemArgs a{x, w, bias, y, pscale, pshift, N, H, W, C, ldw, pt, pl, Hc, Wc, ppt, ppl, Hp, Wp, 0, 0, 0,
-             act == kActRelu ? 0.f : -INFINITY, pact == kActRelu ? 0.f : -INFINITY};
+             act == kActRelu ? 0.f : -INFINITY, pact == kActRelu ? 0.f : -INFINITY, 0};
+  static const int dbg = [] {
+    const char* e = getenv("TFSK_STEM_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = dbg;
   a.tiles_y = (Hp + kTPY - 1) / kTPY;
   a.tiles_x = (Wp + kTPX - 1) / kTPX;
   const long tiles = long(N) * a.tiles_y * a.tiles_x;
