@@ -174,11 +174,20 @@ __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restr
   float v[kSmPer];
   float mx = -INFINITY;
   int arg = 0x7fffffff;
+  // every load of the register tile issued before any compare: unconditional
+  // loads of clamped columns, masked afterwards (`if (c < cols) x = load(c)`
+  // compiled to one conditional block per k that waited for its loads, i.e.
+  // kSmPer serial memory round trips per row)
 #pragma unroll
   for (int k = 0; k < kSmPer; ++k) {
     const int c = k * 256 + tid;
-    float x = -INFINITY;
-    if (c < cols) x = load(c);
+    v[k] = load(c < cols ? c : cols - 1);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < kSmPer; ++k) {
+    const int c = k * 256 + tid;
+    const float x = c < cols ? v[k] : -INFINITY;
     v[k] = x;
     if (c < cols && (x > mx || (x == mx && c < arg))) { mx = x; arg = c; }
   }

@@ -9,6 +9,7 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 timeout -k 10 120 python -u scripts/stem_bench.py --batch 32 > gpurun_out/${TAG}_stem.log 2>&1 &&
 timeout -k 10 120 python -u scripts/stem_bench.py --batch 1 >> gpurun_out/${TAG}_stem.log 2>&1 &&
 timeout -k 10 300 python -u scripts/bench_engine.py --model resnet50 --batch 1 32 > gpurun_out/${TAG}_engine.log 2>&1 &&
+timeout -k 10 300 python -u scripts/bench_engine.py --model bert-base --batch 32 >> gpurun_out/${TAG}_engine.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_kt -o run -- python scripts/bench_engine.py --model resnet50 --batch 32 --iters 20 > /tmp/kt.log 2>&1 &&
 python scripts/replay_kernels.py $(find /tmp/prof_kt -name '*.db' | head -1) --first stem_pool --list > gpurun_out/${TAG}_replay_b32.txt
 rc=$?
