@@ -254,7 +254,21 @@ __global__ __launch_bounds__(256) void gap_rows_kernel(const uint16_t* __restric
   const int tid = threadIdx.x, cg = tid & 7, hs = tid >> 3;
   float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint16_t* p = x + long(m) * HW * K + k0 + cg * 8;
-  for (int hw = hs; hw < HW; hw += 32) {
+  // the first two positions of this lane group (all of them for HW <= 64,
+  // e.g. ResNet's 7x7) load together from clamped rows, masked afterwards: the
+  // rolled loop issued one load per trip and waited for it (2 serial round trips)
+  {
+    const uint4 v0 = *reinterpret_cast<const uint4*>(p + long(min(hs, HW - 1)) * K);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(p + long(min(hs + 32, HW - 1)) * K);
+    __builtin_amdgcn_sched_barrier(0);
+    float f0[8], f1[8];
+    unpack8(v0, f0);
+    unpack8(v1, f1);
+    const bool in0 = hs < HW, in1 = hs + 32 < HW;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s8[e] = (in0 ? f0[e] : 0.f) + (in1 ? f1[e] : 0.f);
+  }
+  for (int hw = hs + 64; hw < HW; hw += 32) {
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(p + long(hw) * K), f);
 #pragma unroll
@@ -550,32 +564,44 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ i
   const int tt = tids ? tids[t] : -1;
   const bool tok = tt >= 0 && tt < ntypes;
   const int p = t % seq;
+  // every table row chunk (word, type, position) and gamma/beta in flight at
+  // once: buffer loads whose out-of-range offsets read zeros stand in for the
+  // `if (c < hidden) { if (wok) ... }` blocks, which waited for each load in
+  // turn (an absent table is a 0-record descriptor)
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(word), 0, vocab * hidden * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsT = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(type), 0, type ? ntypes * hidden * 2 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsP =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(pos), 0, pos ? seq * hidden * 2 : 0, 0x00020000);
+  u32x4 rw[kEmbChunks], rt[kEmbChunks], rp[kEmbChunks];
+  float4 gl[kEmbChunks][2], bl[kEmbChunks][2];
+#pragma unroll
+  for (int k = 0; k < kEmbChunks; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    const bool in = c < hidden;
+    rw[k] = __builtin_amdgcn_raw_buffer_load_b128(rsW, in && wok ? uint32_t(id * hidden + c) * 2u : 0x80000000u, 0, 0);
+    rt[k] = __builtin_amdgcn_raw_buffer_load_b128(rsT, in && tok ? uint32_t(tt * hidden + c) * 2u : 0x80000000u, 0, 0);
+    rp[k] = __builtin_amdgcn_raw_buffer_load_b128(rsP, in ? uint32_t(p * hidden + c) * 2u : 0x80000000u, 0, 0);
+    const int cc = in ? c : 0;
+    gl[k][0] = *reinterpret_cast<const float4*>(gamma + cc);
+    gl[k][1] = *reinterpret_cast<const float4*>(gamma + cc + 4);
+    bl[k][0] = *reinterpret_cast<const float4*>(beta + cc);
+    bl[k][1] = *reinterpret_cast<const float4*>(beta + cc + 4);
+  }
+  __builtin_amdgcn_sched_barrier(0);
   float v[kEmbChunks][8];
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < kEmbChunks; ++k) {
-    const int c = (k * 64 + lane) * 8;
+    float a[8], b[8], d[8];
+    unpack8(make_uint4(rw[k].x, rw[k].y, rw[k].z, rw[k].w), a);
+    unpack8(make_uint4(rt[k].x, rt[k].y, rt[k].z, rt[k].w), b);
+    unpack8(make_uint4(rp[k].x, rp[k].y, rp[k].z, rp[k].w), d);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[k][e] = 0.f;
-    if (c < hidden) {
-      float a[8];
-      if (wok) {
-        unpack8(*reinterpret_cast<const uint4*>(word + long(id) * hidden + c), a);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[k][e] += a[e];
-      }
-      if (tok) {
-        unpack8(*reinterpret_cast<const uint4*>(type + long(tt) * hidden + c), a);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[k][e] += a[e];
-      }
-      if (pos) {
-        unpack8(*reinterpret_cast<const uint4*>(pos + long(p) * hidden + c), a);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[k][e] += a[e];
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s += v[k][e];
+    for (int e = 0; e < 8; ++e) {
+      v[k][e] = a[e] + b[e] + d[e];   // zeros past `hidden`
+      s += v[k][e];
     }
   }
   const float mean = wave_sum(s) / hidden;
@@ -591,8 +617,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ i
   for (int k = 0; k < kEmbChunks; ++k) {
     const int c = (k * 64 + lane) * 8;
     if (c < hidden) {
-      const float4 g0 = *reinterpret_cast<const float4*>(gamma + c), g1 = *reinterpret_cast<const float4*>(gamma + c + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(beta + c), b1 = *reinterpret_cast<const float4*>(beta + c + 4);
+      const float4 g0 = gl[k][0], g1 = gl[k][1], b0 = bl[k][0], b1 = bl[k][1];
       const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
       const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
       float o[8];
@@ -796,6 +821,10 @@ hipError_t embed_ln_launch(const int* ids, const int* type_ids, const uint16_t* 
                            const uint16_t* type, const float* gamma, const float* beta, uint16_t* y, int tokens,
                            int seq, int hidden, int vocab, int ntypes, float eps, hipStream_t s) {
   if (hidden % 8 || hidden > 64 * 8 * kEmbChunks || seq <= 0) return hipErrorInvalidValue;
+  // 32-bit buffer offsets into the tables
+  if (long(vocab) * hidden * 2 >= 0x7fffffffL || long(ntypes) * hidden * 2 >= 0x7fffffffL ||
+      long(seq) * hidden * 2 >= 0x7fffffffL)
+    return hipErrorInvalidValue;
   hipLaunchKernelGGL(embed_ln_kernel, dim3((tokens + 3) / 4), dim3(256), 0, s, ids, type_ids, word, pos, type,
                      gamma, beta, y, tokens, seq, hidden, vocab, ntypes, eps);
   return hipGetLastError();
