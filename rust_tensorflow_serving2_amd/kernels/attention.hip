@@ -55,34 +55,29 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   const long row_stride = 3L * H * D;
   const uint16_t* base = qkv + long(b) * S * row_stride;
 
-  // ---- stage K (row-major, XOR-swizzled 16-B chunks)
-  for (int c = tid; c < S * 8; c += NTH) {
-    const int key = c >> 3, ch = c & 7;
-    const uint4 kv = *reinterpret_cast<const uint4*>(base + long(key) * row_stride + H * D + h * D + ch * 8);
-    *reinterpret_cast<uint4*>(Ks + key * D + ((ch ^ (key & 7)) * 8)) = kv;
+  // ---- every staging load (K chunks, this thread's 8x8 V block, Q fragments)
+  // issued before the first LDS store: the rolled K loop loaded and stored one
+  // chunk per trip, i.e. S * 8 / NTH serial memory round trips before the
+  // MFMAs could start (seen in the gfx950 ISA)
+  static_assert((S * 8) % NTH == 0 && S <= NTH, "staging split");
+  constexpr int KIT = S * 8 / NTH;
+  uint4 kv[KIT];
+#pragma unroll
+  for (int i = 0; i < KIT; ++i) {
+    const int c = tid + i * NTH, key = c >> 3, ch = c & 7;
+    kv[i] = *reinterpret_cast<const uint4*>(base + long(key) * row_stride + H * D + h * D + ch * 8);
   }
-  // ---- stage V transposed: an 8-key x 8-dim block per step, transposed in
+  // V transposed: an 8-key x 8-dim block per thread (threads >= S idle; their
+  // loads read a clamped in-range block and are dropped), transposed in
   // registers (8 x 16-B loads in, 8 x 16-B LDS stores out)
-  for (int blk = tid; blk < (S / 8) * 8; blk += NTH) {
-    const int kg = blk >> 3, ch = blk & 7;
-    uint32_t w[8][4];
+  const int vblk = tid < S ? tid : S - 1;
+  const int kg = vblk >> 3, vch = vblk & 7;
+  uint32_t w[8][4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint4 v = *reinterpret_cast<const uint4*>(base + long(kg * 8 + k) * row_stride + 2 * H * D + h * D +
-                                                      ch * 8);
-      w[k][0] = v.x; w[k][1] = v.y; w[k][2] = v.z; w[k][3] = v.w;
-    }
-#pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      uint32_t o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t lo = (d & 1) ? (w[2 * j][d >> 1] >> 16) : (w[2 * j][d >> 1] & 0xffffu);
-        const uint32_t hi = (d & 1) ? (w[2 * j + 1][d >> 1] & 0xffff0000u) : (w[2 * j + 1][d >> 1] << 16);
-        o[j] = lo | hi;
-      }
-      *reinterpret_cast<uint4*>(Vt + (ch * 8 + d) * VT_LD + kg * 8) = make_uint4(o[0], o[1], o[2], o[3]);
-    }
+  for (int k = 0; k < 8; ++k) {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + long(kg * 8 + k) * row_stride + 2 * H * D + h * D +
+                                                    vch * 8);
+    w[k][0] = v.x; w[k][1] = v.y; w[k][2] = v.z; w[k][3] = v.w;
   }
   // ---- Q fragments straight from global (A operand: row = fr, k = 8*fq + j)
   const int q0 = qb * QB + wid * 16;
@@ -90,6 +85,41 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
     qf[kk] = *reinterpret_cast<const bf16x8*>(base + long(q0 + fr) * row_stride + h * D + kk * 32 + fq * 8);
+  // the [B,1,1,S] key mask (BERT's adder, mask_qstride == 0) of this lane's
+  // key columns, loaded with the operands instead of after the QK^T MFMAs (a
+  // 0-record descriptor when the mask is per query row or absent: zeros)
+  const bool key_mask = mask_bias != nullptr && mask_qstride == 0;
+  const __amdgpu_buffer_rsrc_t rsM = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(key_mask ? mask_bias + long(b) * mask_bstride : mask_bias), 0, key_mask ? S * 4 : 0,
+      0x00020000);
+  float mbk[S / 16];
+#pragma unroll
+  for (int nt = 0; nt < S / 16; ++nt)
+    mbk[nt] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsM, uint32_t(nt * 16 + fr) * 4u, 0, 0));
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < KIT; ++i) {
+    const int c = tid + i * NTH, key = c >> 3, ch = c & 7;
+    *reinterpret_cast<uint4*>(Ks + key * D + ((ch ^ (key & 7)) * 8)) = kv[i];
+  }
+  // (no `if (tid < S)` around the stores: the compiler sank the V loads into
+  // any such block; idle threads store into the rows' 16-B padding columns
+  // [S, S + 8), which no P.V read touches)
+  uint4 vt8[8];
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = (d & 1) ? (w[2 * j][d >> 1] >> 16) : (w[2 * j][d >> 1] & 0xffffu);
+      const uint32_t hi = (d & 1) ? (w[2 * j + 1][d >> 1] & 0xffff0000u) : (w[2 * j + 1][d >> 1] << 16);
+      o[j] = lo | hi;
+    }
+    vt8[d] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  const int vcol = tid < S ? kg * 8 : S;
+#pragma unroll
+  for (int d = 0; d < 8; ++d) *reinterpret_cast<uint4*>(Vt + (vch * 8 + d) * VT_LD + vcol) = vt8[d];
   __syncthreads();
 
   // ---- scores
@@ -109,11 +139,11 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   // ---- softmax (rows fq*4 + r, columns nt*16 + fr)
   float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   const float* mrow = mask_bias ? mask_bias + long(b) * mask_bstride + long(q0 + fq * 4) * mask_qstride : nullptr;
-  if (mrow && mask_qstride == 0) {
-    // key mask shared by every query row (BERT's [B,1,1,S] adder): one load per key tile
+  if (key_mask) {
+    // key mask shared by every query row (BERT's [B,1,1,S] adder): prefetched above
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const float mb = mrow[nt * 16 + fr];
+      const float mb = mbk[nt];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float v = s[nt][r] * scale + mb;
