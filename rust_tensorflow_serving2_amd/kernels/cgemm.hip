@@ -119,8 +119,16 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
   }
 }
 
+// Waves per SIMD the register allocation must leave room for: the 4-wave
+// 32-KB tiles (64x64, 2 slots) fit 5 workgroups per CU by LDS, i.e. 5 waves
+// per SIMD, which needs <= 102 VGPRs (unconstrained they took 128: 4 per CU)
+template <int BM, int BN, int WGM, int WGN, int S>
+constexpr int cg_waves_per_eu() {
+  return (WGM * WGN == 4 && CG<BM, BN, WGM, WGN, S>::LDS <= 32 * 1024) ? 5 : 1;
+}
+
 template <int BM, int BN, int WGM, int WGN, int S, int AM>
-__global__ __launch_bounds__(64 * WGM * WGN) void cgemm_kernel(IGemmArgs p) {
+__global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, S>())) void cgemm_kernel(IGemmArgs p) {
   using G = CG<BM, BN, WGM, WGN, S>;
   constexpr bool IM2COL = (AM == 1), DUAL = (AM == 2), STEM = (AM == 3);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
