@@ -25,6 +25,23 @@ steps are untimed; then exactly K steps are timed between barriers with
 ``torch.cuda.synchronize()`` on both sides; the max time over ranks is used
 and ``value`` = total RPCs of all ranks / that time (weak scaling: fixed work
 per GPU).  Extra fields report p50/p99 latency.
+
+Launch.  ``--gpus N`` with N > 1 and no ``WORLD_SIZE`` in the environment
+makes this process a launcher: it starts N child ranks (fresh subprocesses,
+never an exec; the launcher itself makes no HIP call) with the torchrun
+variables set, forwards rank 0's JSON line and exits with the worst child exit
+code.  Under torchrun ``--gpus`` must equal ``WORLD_SIZE``.
+
+Placement.  Every rank pins itself (before any thread exists) to a disjoint set
+of CPUs on its GPU's NUMA node (``parallel/topology.py``): its IO threads,
+lanes, pinned batch slots and load generator stay next to its GPU.
+
+Diagnostics (always on).  Over a diagnostic window -- the pre-warm + warmup
+traffic, >= 1 s, long enough to be meaningful when the timed window is only a
+few ms -- each rank reports CPU cores per thread group, IO-thread us per
+request and its GPU's ``gpu_busy_percent`` (sampled every 10 ms through the
+timed window too); rank 0's JSON carries all ranks' figures under
+``diagnostics``.
 """
 from __future__ import annotations
 
@@ -80,42 +97,95 @@ def parse():
                          "(the reference client's channel pattern, src/lib.rs:132-138) while every rank serves; "
                          "reported as ref_client_rps + the share each GPU served (per-stream routing; 0 = skip)")
     ap.add_argument("--cpu-report", action="store_true",
-                    help="add per-thread-group CPU seconds of the timed window (from /proc) to the JSON")
+                    help="(always on now; kept for old command lines) per-thread-group CPU of the windows")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = CPU servables + gloo (multi-rank launcher tests without a GPU)")
+    ap.add_argument("--no-pin", action="store_true", help="do not pin ranks to their GPU's NUMA-node CPUs")
     return ap.parse_args()
 
 
-def thread_cpu() -> dict:
-    """{thread name: cpu seconds} of this process (utime+stime from /proc)."""
-    tick = os.sysconf("SC_CLK_TCK")
-    out = {}
-    base = f"/proc/{os.getpid()}/task"
-    for tid in os.listdir(base):
-        try:
-            with open(f"{base}/{tid}/comm") as f:
-                name = f.read().strip()
-            with open(f"{base}/{tid}/stat") as f:
-                fields = f.read().rsplit(")", 1)[1].split()
-            out[name] = out.get(name, 0.0) + (int(fields[11]) + int(fields[12])) / tick
-        except (FileNotFoundError, ProcessLookupError, IndexError):
-            continue
-    return out
+def launch_ranks(args) -> int:
+    """``--gpus N`` without torchrun: N child ranks, one per GPU."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                r = p.poll()
+                if r is None:
+                    continue
+                live.remove(p)
+                if r != 0:
+                    rc = rc or (r if r > 0 else 128 - r)
+                    for q in live:          # one rank failed: the collective cannot finish
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        rc = 130
+    finally:
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    return rc
 
 
 def main():
     args = parse()
+    if args.device == "cpu":
+        args.c1_requests = min(args.c1_requests, 20)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (one rank per GPU)")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+
+    # pin before torch / HIP / our server create any thread: every thread of
+    # this rank (IO, lanes, load generator) inherits the mask
+    from rust_tensorflow_serving2_amd.parallel import topology
+    placement = topology.plan(local_world)[local]
+    pinned = False if args.no_pin else topology.pin(placement.cpus)
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    on_gpu = args.device == "cuda"
     # TFSERVE_BENCH_BACKEND=gloo rehearses the multi-rank flow with fewer GPUs than
     # ranks (ranks share devices round-robin); the real run uses nccl (= RCCL)
-    backend = os.environ.get("TFSERVE_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    backend = os.environ.get("TFSERVE_BENCH_BACKEND", "nccl" if on_gpu else "gloo")
+    if on_gpu:
+        if backend != "nccl":
+            local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+
+    def dev_sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+    coll_dev = device if backend == "nccl" else "cpu"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
@@ -207,37 +277,52 @@ def main():
             loadgen.stop(10.0)
             raise SystemExit(f"{what} errors: {res['errors']} {res['first_error']}")
 
+    def io_stats():
+        return server.transports[0].stats() if args.transport == "native" else None
+
+    def diag(c0, c1, io0, io1, ru0, ru1, secs):
+        d = topology.cpu_by_group(c0, c1, secs)
+        d["process_total"] = round((ru1.user + ru1.system - ru0.user - ru0.system) / max(secs, 1e-9), 2)
+        if io0 is not None and io1 is not None:
+            nreq = max(1, io1["requests"] - io0["requests"])
+            for k in ("io_s_recv", "io_s_h2", "io_s_dispatch", "io_s_send"):
+                d[k.replace("io_s_", "io_us_per_req_")] = round((io1[k] - io0[k]) / nreq * 1e6, 1)
+            d["requests"] = io1["requests"] - io0["requests"]
+            b = sum(e.get("batches", 0) for e in io1.get("endpoints", {}).values()) - \
+                sum(e.get("batches", 0) for e in io0.get("endpoints", {}).values())
+            rows = sum(e.get("rows", 0) for e in io1.get("endpoints", {}).values()) - \
+                sum(e.get("rows", 0) for e in io0.get("endpoints", {}).values())
+            d["batches"] = b
+            d["avg_batch"] = round(rows / b, 2) if b else None
+            r0, r1 = io0.get("router"), io1.get("router")
+            if r0 and r1:
+                d["router"] = {k: r1[k] - r0[k] for k in ("forwarded", "streamed", "ingested", "returned",
+                                                          "reclaimed", "lost", "no_cell", "rerun")
+                               if k in r1 and k in r0}
+        return d
+
+    gpu_info = topology.gpus()
+    busy = topology.BusySampler(gpu_info[local].bdf if on_gpu and local < len(gpu_info) else "").start()
+    dc0, dio0, dru0, dt0 = topology.thread_cpu(), io_stats(), os.times(), time.perf_counter()
     t_pre = time.perf_counter()
     while time.perf_counter() - t_pre < args.prewarm_s:
         check(loadgen.window(64 * per_step, 600.0), "pre-warm")
     check(loadgen.window(max(per_step, args.warmup * per_step), 600.0), "warmup")
+    dsecs = time.perf_counter() - dt0
+    diag_window = diag(dc0, topology.thread_cpu(), dio0, io_stats(), dru0, os.times(), dsecs)
+    diag_window["window_s"] = round(dsecs, 3)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    cpu0 = thread_cpu() if args.cpu_report else None
-    io0 = server.transports[0].stats() if args.cpu_report and args.transport == "native" else None
-    ru0 = os.times()
+    dev_sync()
+    cpu0, io0, ru0 = topology.thread_cpu(), io_stats(), os.times()
     t0 = time.perf_counter()
     r = loadgen.window(args.steps * per_step, 600.0)
-    torch.cuda.synchronize()
+    dev_sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    cpu_report = None
-    if cpu0 is not None:
-        cpu1 = thread_cpu()
-        groups = {}
-        for k, v in cpu1.items():
-            g = k.rstrip("0123456789")
-            groups[g] = groups.get(g, 0.0) + v - cpu0.get(k, 0.0)
-        cpu_report = {k: round(v / elapsed, 2) for k, v in sorted(groups.items(), key=lambda x: -x[1]) if v > 0.01}
-        ru1 = os.times()
-        cpu_report["process_total"] = round((ru1.user + ru1.system - ru0.user - ru0.system) / elapsed, 2)
-        if io0 is not None:
-            io1 = server.transports[0].stats()
-            nreq = max(1, io1["requests"] - io0["requests"])
-            for k in ("io_s_recv", "io_s_h2", "io_s_dispatch", "io_s_send"):
-                cpu_report[k.replace("io_s_", "io_us_per_req_")] = round((io1[k] - io0[k]) / nreq * 1e6, 1)
+    cpu_report = diag(cpu0, topology.thread_cpu(), io0, io_stats(), ru0, os.times(), elapsed)
+    gpu_busy = busy.stop()
     loadgen.stop(30.0)
     check(r, "timed window")
 
@@ -245,6 +330,7 @@ def main():
     # two channels) on rank 0's port while every rank serves; the router
     # spreads its streams over the GPUs
     ref = None
+    my_ref_diag = None
     if args.ref_client_requests > 0 and args.transport == "native":
         srvc = server.transports[0].srv
 
@@ -254,19 +340,22 @@ def main():
         if world > 1:
             dist.barrier()
         s0 = served()
+        rc0, rio0, rru0, rt0 = topology.thread_cpu(), io_stats(), os.times(), time.perf_counter()
         if rank == 0:
             # two connections, each driven by its own thread (a tonic channel's
             # connection task runs on one runtime thread at a time)
             lg2 = _C.LoadGen("127.0.0.1", server.port, PREDICT, bodies, min(conc, 128), 2, 2)
             lg2.run(max(64, args.ref_client_requests // 10), 120.0)
             s0 = served()
+            rc0, rio0, rru0, rt0 = topology.thread_cpu(), io_stats(), os.times(), time.perf_counter()
             r2 = lg2.run(args.ref_client_requests, 300.0)
             ref = {"ok": r2["ok"], "errors": r2["errors"], "elapsed_s": r2["elapsed_s"]}
             del lg2
         if world > 1:
             dist.barrier()
-        share = torch.tensor([float(served() - s0)], dtype=torch.float64,
-                             device=device if backend == "nccl" else "cpu")
+        my_ref_diag = diag(rc0, topology.thread_cpu(), rio0, io_stats(), rru0, os.times(),
+                           time.perf_counter() - rt0)
+        share = torch.tensor([float(served() - s0)], dtype=torch.float64, device=coll_dev)
         if world > 1:
             parts = [torch.zeros_like(share) for _ in range(world)]
             dist.all_gather(parts, share)
@@ -294,13 +383,20 @@ def main():
         np.save(os.environ["TFSERVE_BENCH_DUMP"], lat)      # completion-order latencies (diagnostics)
     mine = torch.tensor([elapsed, float(r["ok"]), float(r["errors"]), np.percentile(lat, 50) if lat.size else 0,
                          np.percentile(lat, 99) if lat.size else 0, p50_c1 or 0.0], dtype=torch.float64,
-                        device=device if backend == "nccl" else "cpu")
+                        device=coll_dev)
+    my_diag = {"placement": dict(placement.as_dict(), pinned=pinned,
+                                 bdf=gpu_info[local].bdf if local < len(gpu_info) else None),
+               "gpu_busy_pct": gpu_busy, "timed": cpu_report, "prewarm": diag_window,
+               "ref_client": my_ref_diag}
     if world > 1:
         allv = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allv, mine)
         allv = torch.stack(allv).cpu().numpy()
+        all_diag = [None] * world
+        dist.all_gather_object(all_diag, my_diag)
     else:
         allv = mine.cpu().numpy()[None]
+        all_diag = [my_diag]
     stats = server.transports[0].stats() if args.transport == "native" else {}
     if rank == 0:
         t_max = float(allv[:, 0].max())
@@ -317,7 +413,8 @@ def main():
         out = {
             "metric": metric, "value": round(value, 1), "unit": "Predict RPCs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * t_max / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if on_gpu else "fp32 (cpu test mode)",
             "data": data,
             "config": {"model": model_label,
                        "global_batch": args.batch * world,
@@ -332,6 +429,8 @@ def main():
             "p50_c1_ms": round(float(np.median(allv[:, 5])), 3) if allv.shape[1] > 5 and allv[0, 5] > 0 else None,
             "load_s": round(t_load, 2), "prewarm_s": args.prewarm_s,
             "cpu_cores_by_thread": cpu_report,
+            "gpu_busy_pct": [d["gpu_busy_pct"] for d in all_diag],
+            "diagnostics": all_diag,
             "fast_path_share": round(stats.get("fast_path", 0) / max(1, stats.get("requests", 1)), 3) if stats else None,
         }
         if ref is not None:

@@ -23,6 +23,9 @@ constexpr uint64_t kMagic = 0x7466735f726f7574ULL;   // "tfs_rout"
 constexpr int kMaxRanks = 64;
 constexpr size_t kMethodCap = 256, kErrCap = 256;
 enum CellState : uint32_t { kFree = 0, kWriting = 1, kReady = 2, kTaken = 3, kDone = 4 };
+// CellHdr::status of a DONE cell whose answer did not fit the cell's response
+// area: the origin runs the call itself (its message is still in the cell)
+constexpr int32_t kRerunLocally = -1;
 
 struct alignas(64) SegHdr {
   uint64_t magic;
@@ -107,6 +110,26 @@ struct Router::Pending {
   int cell;
   std::unique_ptr<Call> call;
 };
+
+// A call given up on (its peer looked dead while running it) whose cell the
+// peer may still mark DONE later -- a stalled heartbeat, not a dead process.
+// Nobody else frees such a cell, so the origin keeps the token and frees it.
+struct Router::Tomb {
+  int peer;
+  std::shared_ptr<RouterSeg> seg;
+  int cell;
+  uint64_t token;
+};
+
+namespace {
+// The message of a forwarded call, rebuilt as a local call (gRPC frame prefix + message)
+void take_message(Call& c, const RouterSeg& s, int cell) {
+  c.body.assign(5, '\0');
+  c.body.append(reinterpret_cast<const char*>(s.msg(cell)), s.cell(cell)->msg_len);
+  c.off = 5;
+  c.routed = true;
+}
+}  // namespace
 
 // A streamed Predict whose payload goes from the socket into a peer's cell.
 struct RemoteStream final : StreamRes {
@@ -349,11 +372,12 @@ void Router::respond_remote(const Call& c, int status, const std::string& msg, c
   RouterSeg& s = *self_;
   CellHdr* ch = s.cell(int(c.cell));
   if (status == 0 && body.size() > s.hdr()->resp_cap) {
-    status = 13;   // INTERNAL
-    const std::string m = "response of " + std::to_string(body.size()) + " bytes exceeds the cross-replica cell";
-    ch->err_len = uint32_t(std::min(m.size(), kErrCap));
-    memcpy(s.err(int(c.cell)), m.data(), ch->err_len);
+    // the answer does not fit the cell: the origin runs the call itself, so a
+    // routed call succeeds exactly when the same call served locally would
+    status = kRerunLocally;
+    ch->err_len = 0;
     ch->resp_len = 0;
+    stats.too_large++;
   } else {
     ch->err_len = uint32_t(std::min(msg.size(), kErrCap));
     memcpy(s.err(int(c.cell)), msg.data(), ch->err_len);
@@ -414,6 +438,15 @@ void Router::reap(bool check_peers) {
       CellHdr* ch = s.cell(pd.cell);
       const uint32_t st = ch->state.load(std::memory_order_acquire);
       if (st == kDone) {
+        if (ch->status == kRerunLocally) {
+          std::unique_ptr<Call> c = std::move(pd.call);
+          take_message(*c, s, pd.cell);
+          ch->state.store(kFree, std::memory_order_release);
+          rerun.push_back(std::move(c));
+          stats.rerun++;
+          it = pending_.erase(it);
+          continue;
+        }
         Ans a;
         a.call = std::move(pd.call);
         a.status = ch->status;
@@ -427,14 +460,14 @@ void Router::reap(bool check_peers) {
       const bool dead = check_peers && (!peers_[pd.peer]->alive || peers_[pd.peer]->seg != pd.seg);
       if (dead) {
         uint32_t expect = kReady;
-        if (ch->state.compare_exchange_strong(expect, kFree)) {
-          // never taken: run it here (the message is still in the old mapping)
+        // READY -> TAKEN (not FREE) while the message is copied out: a replica
+        // that still thinks the peer alive must not claim the cell meanwhile
+        if (ch->state.compare_exchange_strong(expect, kTaken)) {
           std::unique_ptr<Call> c = std::move(pd.call);
-          c->body.assign(5, '\0');
-          c->body.append(reinterpret_cast<const char*>(s.msg(pd.cell)), ch->msg_len);
-          c->off = 5;
-          c->routed = true;
+          take_message(*c, s, pd.cell);
+          ch->state.store(kFree, std::memory_order_release);
           rerun.push_back(std::move(c));
+          stats.reclaimed++;
         } else {
           Ans a;
           a.call = std::move(pd.call);
@@ -442,8 +475,29 @@ void Router::reap(bool check_peers) {
           a.msg = "replica " + std::to_string(pd.peer) + " failed while serving the request";
           answers.push_back(std::move(a));
           stats.lost++;
+          tombs_.push_back(Tomb{pd.peer, pd.seg, pd.cell, ch->token});
         }
         it = pending_.erase(it);
+        continue;
+      }
+      ++it;
+    }
+    // abandoned calls: free the cell if the peer finishes after all; forget it
+    // once the peer's process is gone or replaced (its ring goes with it)
+    for (auto it = tombs_.begin(); it != tombs_.end();) {
+      CellHdr* ch = it->seg->cell(it->cell);
+      if (ch->token != it->token) {
+        it = tombs_.erase(it);
+        continue;
+      }
+      if (ch->state.load(std::memory_order_acquire) == kDone) {
+        ch->state.store(kFree, std::memory_order_release);
+        stats.tomb_freed++;
+        it = tombs_.erase(it);
+        continue;
+      }
+      if (check_peers && (peers_[it->peer]->seg != it->seg || !pid_alive(it->seg->hdr()->pid))) {
+        it = tombs_.erase(it);
         continue;
       }
       ++it;
@@ -453,10 +507,7 @@ void Router::reap(bool check_peers) {
     stats.returned++;
     srv_->respond(*a.call, a.status, std::move(a.msg), std::move(a.body));
   }
-  for (auto& c : rerun) {
-    stats.reclaimed++;
-    srv_->dispatch(std::move(c));
-  }
+  for (auto& c : rerun) srv_->dispatch(std::move(c));
 }
 
 // (mu_ held) map peers' current generations, refresh liveness

@@ -19,14 +19,17 @@
 //   * p's router thread takes READY cells and dispatches them as local calls
 //     (fast path or Python) whose body is the cell itself; the answer is
 //     written back into the cell (DONE) and the origin's doorbell rung; the
-//     origin's router thread answers the original HTTP/2 stream.
+//     origin's router thread answers the original HTTP/2 stream.  An answer
+//     larger than the cell's response area is sent back as "run it yourself"
+//     and the origin serves the call locally from the message still in the cell.
 //   * Load = calls a replica has accepted and not answered yet (an atomic in
 //     its header).  A call goes remote only when a live peer's load is lower
 //     than the local one by more than `margin`: balanced replicas (many
 //     connections, the benchmark) keep their own traffic.
 //   * Liveness: the owner's pid and a heartbeat its router thread advances.
 //     A peer that dies leaves its calls: cells it had not taken yet are
-//     re-dispatched locally, taken ones are answered UNAVAILABLE; a restarted
+//     re-dispatched locally, taken ones are answered UNAVAILABLE (and their
+//     cells freed should the peer, only stalled, finish them later); a restarted
 //     replica gets a new generation (a directory segment maps rank ->
 //     generation) and peers re-map it.
 #pragma once
@@ -53,6 +56,9 @@ struct RouterStats {
   std::atomic<uint64_t> reclaimed{0};   // forwarded calls re-run locally (the peer died before taking them)
   std::atomic<uint64_t> lost{0};        // forwarded calls answered UNAVAILABLE (the peer died while running them)
   std::atomic<uint64_t> no_cell{0};     // routing wanted a peer whose ring was full
+  std::atomic<uint64_t> rerun{0};       // forwarded calls re-run here: the answer did not fit the cell
+  std::atomic<uint64_t> too_large{0};   // peers' calls whose answer did not fit their cell (sent back)
+  std::atomic<uint64_t> tomb_freed{0};  // cells of given-up calls freed when the peer finished late
 };
 
 class Router : public RemoteSink {
@@ -77,6 +83,7 @@ class Router : public RemoteSink {
 
   struct Pending;
   struct Peer;
+  struct Tomb;
 
  private:
   friend struct RemoteStream;
@@ -100,6 +107,7 @@ class Router : public RemoteSink {
   std::mutex mu_;                                 // peers_ + pending_
   std::vector<std::unique_ptr<Peer>> peers_;
   std::map<uint64_t, std::unique_ptr<Pending>> pending_;
+  std::vector<Tomb> tombs_;
   uint64_t next_token_ = 1;
   std::atomic<bool> running_{false};
   std::thread th_;

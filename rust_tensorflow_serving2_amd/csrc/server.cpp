@@ -383,6 +383,14 @@ struct PyServer {
   std::unique_ptr<FastPath> fast;
   std::mutex lmu;
   std::vector<std::unique_ptr<NativeLane>> lanes;
+  // Explicit teardown (also when stop_router()/stop() were never called, e.g.
+  // an exception during start-up): the router's thread dispatches into srv
+  // and answers its pending calls through srv, so it stops while srv is alive;
+  // member order alone would destroy srv first.
+  ~PyServer() {
+    if (router) router->stop();
+    if (srv) srv->stop();
+  }
   // join (and drop) the lanes of an endpoint that has been closed
   void join_lanes(int ep_id) {
     std::vector<std::unique_ptr<NativeLane>> done;
@@ -599,6 +607,7 @@ void register_server(py::module_& m) {
         d["forwarded"] = st.forwarded.load(); d["streamed"] = st.streamed.load();
         d["ingested"] = st.ingested.load(); d["returned"] = st.returned.load();
         d["reclaimed"] = st.reclaimed.load(); d["lost"] = st.lost.load(); d["no_cell"] = st.no_cell.load();
+        d["rerun"] = st.rerun.load(); d["too_large"] = st.too_large.load(); d["tomb_freed"] = st.tomb_freed.load();
         d["peers_alive"] = s.router->peers_alive();
         d["loads"] = s.router->loads();
         d["rank"] = s.router->rank();

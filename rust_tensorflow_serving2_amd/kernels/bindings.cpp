@@ -73,9 +73,11 @@ void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, cons
   a.splits = int(splits);
   a.kt_per_split = per;
   a.ws = ws.data_ptr<float>();
-  // cgemm / halo finish split-K in-kernel (the last slice of each tile
-  // reduces): one launch instead of two.  Eager launches (autotuning) use the
-  // fixup too, so the tuner times the split-K candidates as the graph runs them.
+  // With TFSERVE_SPLITK_FIXUP=1 (opt-in, see split_fixup_enabled) cgemm /
+  // halo finish split-K in-kernel (the last slice of each tile reduces): one
+  // launch instead of two; eager launches (autotuning) then use the fixup too,
+  // so the tuner times the split-K candidates as the graph runs them.
+  // Otherwise, or when no counters are left, a separate reduce launch.
   a.counters = nullptr;
   if (split_fixup_enabled() && a.N % 8 == 0 && ((is_cgemm_cfg(cfg) && tfsk::cgemm_fixup_ok(int(cfg))) || is_halo_cfg(cfg))) {
     tfsk::splitk_counters_prepare(st);

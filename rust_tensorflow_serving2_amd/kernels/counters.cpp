@@ -1,6 +1,7 @@
 // Split-K arrival counter pool (see launch.h splitk_counters).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <map>
 #include <mutex>
 
@@ -10,12 +11,17 @@ namespace tfsk {
 
 namespace {
 constexpr int kPoolInts = 1 << 20;   // 4 MB per device
+// Only used with TFSERVE_SPLITK_FIXUP=1 (opt-in; the default split-K path
+// reduces in a second launch and needs no counters).
 // [0, kCapInts): permanent slices for launches captured into HIP graphs (a
-// graph node keeps its counters for the graph's lifetime); [kCapInts,
-// kPoolInts): a ring for eager launches (autotuning, warm-up), reused
-// cyclically.  Counters return to zero when a tile's last slice arrives, so a
-// ring slice is free again once the launch that took it has finished -- which
-// the ring's length (thousands of launches) leaves ample time for.
+// graph node keeps its counters for the graph's lifetime; slices are never
+// returned, so repeated captures -- tuning candidates, reloads, more buckets
+// or lanes -- use the 768K ints up, after which launches fall back to the
+// reduce launch, logged once); [kCapInts, kPoolInts): a ring for eager
+// launches (autotuning, warm-up), reused cyclically.  A maximal take (32K
+// ints) wraps the 256K-int ring after 8 launches; reuse is still safe because
+// eager launches are stream-ordered and counters return to zero when a
+// tile's last slice arrives, before the next launch on the stream starts.
 constexpr int kCapInts = 3 << 18;
 struct Pool {
   int* base = nullptr;
@@ -64,7 +70,15 @@ int* splitk_counters(int n, hipStream_t s) {
     p.ring += take;
     return r;
   }
-  if (p.used + take > kCapInts) return nullptr;
+  if (p.used + take > kCapInts) {
+    static bool warned = false;
+    if (!warned) {
+      warned = true;
+      fprintf(stderr, "[tfserve] split-K counter pool for captured graphs is used up; "
+                      "further captures reduce split-K in a separate launch\n");
+    }
+    return nullptr;
+  }
   int* r = p.base + p.used;
   p.used += take;
   return r;

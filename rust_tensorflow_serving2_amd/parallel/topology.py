@@ -1,0 +1,334 @@
+"""Host topology for one-process-per-GPU serving: which CPUs sit next to which GPU.
+
+Every replica's data plane (HTTP/2 IO threads, the batcher, the native lanes
+and -- in the benchmark -- the load generator) moves ~602 KB per request
+through host memory (socket buffer -> pinned batch slot -> SDMA).  On a
+two-socket 8-GPU node a replica whose threads and pinned slots land on the far
+socket pays every one of those bytes across the socket link, so each rank is
+pinned to CPUs of its own GPU's NUMA node ("the data plane next
+to its GPU"; the reference runs one container, ``serving/rundocker.sh:15``).
+
+Nothing here touches the HIP runtime (the launcher and the supervisor must
+never initialise a device).  Sources, all sysfs:
+
+* ``/sys/class/kfd/kfd/topology/nodes/*/properties``: GPU agents in HIP device
+  order (nodes with ``simd_count > 0`` sorted by node id, narrowed by
+  ``ROCR_VISIBLE_DEVICES`` / ``HIP_VISIBLE_DEVICES``), their PCI
+  ``location_id`` (bus << 8 | dev << 3 | fn) and ``domain``;
+* ``/sys/bus/pci/devices/<bdf>/numa_node`` (falls back to the KFD io-link to a
+  CPU node when the firmware reports -1);
+* ``/sys/devices/system/node/node*/cpulist``;
+* ``/sys/bus/pci/devices/<bdf>/gpu_busy_percent`` for the busy sampler.
+
+``root`` re-bases every path (tests build a fake sysfs tree).
+"""
+from __future__ import annotations
+
+import os
+import threading
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+
+@dataclass
+class GpuInfo:
+    index: int                 # HIP device index in this process
+    kfd_node: int
+    bdf: str                   # PCI address "dddd:bb:dd.f" ("" if unknown)
+    numa_node: int             # -1 if unknown
+
+
+@dataclass
+class Placement:
+    rank: int
+    gpu: int
+    numa_node: int
+    cpus: List[int] = field(default_factory=list)
+
+    def as_dict(self) -> dict:
+        return {"rank": self.rank, "gpu": self.gpu, "numa_node": self.numa_node, "cpus": compress(self.cpus)}
+
+
+def _read(path: str) -> Optional[str]:
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def parse_cpulist(s: str) -> List[int]:
+    """"0-3,8,10-11" -> [0, 1, 2, 3, 8, 10, 11]."""
+    out: List[int] = []
+    for part in (s or "").split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-", 1)
+            out.extend(range(int(a), int(b) + 1))
+        else:
+            out.append(int(part))
+    return sorted(set(out))
+
+
+def compress(cpus: Sequence[int]) -> str:
+    """[0, 1, 2, 3, 8] -> "0-3,8"."""
+    cpus = sorted(set(cpus))
+    parts, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        parts.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(parts)
+
+
+def _props(path: str) -> Dict[str, str]:
+    txt = _read(path)
+    if txt is None:
+        return {}
+    out = {}
+    for line in txt.splitlines():
+        f = line.split()
+        if len(f) >= 2:
+            out[f[0]] = f[1]
+    return out
+
+
+def _visible(n: int) -> List[int]:
+    """Indices (into the KFD GPU list) this process sees, in HIP order."""
+    idx = list(range(n))
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if not v or not v.strip():      # unset or empty: no narrowing
+            continue
+        try:
+            sel = [int(x) for x in v.split(",") if x.strip() != ""]
+        except ValueError:          # UUID form: keep the order we have
+            continue
+        idx = [idx[i] for i in sel if 0 <= i < len(idx)]
+    return idx
+
+
+def gpus(root: str = "/") -> List[GpuInfo]:
+    """Visible GPUs in HIP device order (empty when there is no KFD)."""
+    base = os.path.join(root, "sys/class/kfd/kfd/topology/nodes")
+    try:
+        nodes = sorted(int(x) for x in os.listdir(base) if x.isdigit())
+    except OSError:
+        return []
+    gpu_nodes, cpu_nodes = [], []
+    for nd in nodes:
+        p = _props(os.path.join(base, str(nd), "properties"))
+        if int(p.get("simd_count", "0")) > 0:
+            gpu_nodes.append((nd, p))
+        elif int(p.get("cpu_cores_count", "0")) > 0:
+            cpu_nodes.append(nd)
+    out = []
+    for i, k in enumerate(_visible(len(gpu_nodes))):
+        nd, p = gpu_nodes[k]
+        loc = int(p.get("location_id", "0"))
+        dom = int(p.get("domain", "0"))
+        bdf = f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 0x7:x}" if loc else ""
+        numa = -1
+        if bdf:
+            v = _read(os.path.join(root, "sys/bus/pci/devices", bdf, "numa_node"))
+            if v is not None and v.lstrip("-").isdigit():
+                numa = int(v)
+        if numa < 0:
+            # KFD io-link from the GPU to its CPU node (CPU KFD nodes are the
+            # NUMA nodes, in order)
+            lbase = os.path.join(base, str(nd), "io_links")
+            try:
+                for ln in sorted(os.listdir(lbase)):
+                    to = int(_props(os.path.join(lbase, ln, "properties")).get("node_to", "-1"))
+                    if to in cpu_nodes:
+                        numa = cpu_nodes.index(to)
+                        break
+            except OSError:
+                pass
+        out.append(GpuInfo(index=i, kfd_node=nd, bdf=bdf, numa_node=numa))
+    return out
+
+
+def numa_cpus(root: str = "/") -> Dict[int, List[int]]:
+    base = os.path.join(root, "sys/devices/system/node")
+    out: Dict[int, List[int]] = {}
+    try:
+        names = os.listdir(base)
+    except OSError:
+        return out
+    for n in names:
+        if n.startswith("node") and n[4:].isdigit():
+            c = _read(os.path.join(base, n, "cpulist"))
+            if c:
+                out[int(n[4:])] = parse_cpulist(c)
+    return out
+
+
+def _core_order(cpus: List[int], root: str) -> List[int]:
+    first = {}
+    for c in cpus:
+        sib = _read(os.path.join(root, f"sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list"))
+        first[c] = min(parse_cpulist(sib)) if sib else c
+    return sorted(cpus, key=lambda c: (first[c], c))
+
+
+def plan(nranks: int, allowed: Optional[Sequence[int]] = None, root: str = "/",
+         gpu_of_rank: Optional[Sequence[int]] = None) -> List[Placement]:
+    """Disjoint CPU sets for ``nranks`` replicas, each from its GPU's NUMA node.
+
+    The CPUs this process may use (``allowed``, default its affinity mask) are
+    grouped by NUMA node; each node's CPUs are split evenly over the ranks whose
+    GPU hangs off it.  Ranks with an unknown node (or more ranks than GPUs, the
+    shared-GPU rehearsal) draw from what is left, so every rank gets a
+    non-empty set whenever ``len(allowed) >= nranks``."""
+    allowed = sorted(set(allowed if allowed is not None else os.sched_getaffinity(0)))
+    info = gpus(root)
+    if gpu_of_rank is None:
+        gpu_of_rank = [r % len(info) if info else r for r in range(nranks)]
+    nodes = numa_cpus(root)
+    node_of_cpu = {c: n for n, cs in nodes.items() for c in cs}
+    free_by_node: Dict[int, List[int]] = {}
+    for c in allowed:
+        free_by_node.setdefault(node_of_cpu.get(c, -1), []).append(c)
+    # SMT siblings adjacent, so an even split hands out whole physical cores
+    # (Linux numbers a core's second thread cpu+ncores: a plain slice of the
+    # node's list would put two ranks on the two threads of one core)
+    for nd in free_by_node:
+        free_by_node[nd] = _core_order(free_by_node[nd], root)
+    out = [Placement(rank=r, gpu=int(g), numa_node=(info[g].numa_node if g < len(info) else -1))
+           for r, g in enumerate(gpu_of_rank)]
+    # ranks per node (known node and that node has allowed CPUs)
+    by_node: Dict[int, List[Placement]] = {}
+    for p in out:
+        if p.numa_node in free_by_node:
+            by_node.setdefault(p.numa_node, []).append(p)
+    for nd, ps in by_node.items():
+        cs = free_by_node[nd]
+        share = len(cs) // len(ps)
+        if share == 0:
+            continue
+        for i, p in enumerate(ps):
+            p.cpus = cs[i * share:(i + 1) * share]
+        free_by_node[nd] = cs[len(ps) * share:]
+    rest = [p for p in out if not p.cpus]
+    if rest:
+        pool = [c for cs in free_by_node.values() for c in cs]
+        if len(pool) < len(rest):          # too few left over: share the whole allowed set
+            pool = allowed
+        share = max(1, len(pool) // len(rest))
+        for i, p in enumerate(rest):
+            p.cpus = pool[(i * share) % len(pool):(i * share) % len(pool) + share] or list(pool)
+            if p.numa_node < 0 and p.cpus:
+                p.numa_node = node_of_cpu.get(p.cpus[0], -1)
+    return out
+
+
+def pin(cpus: Sequence[int]) -> bool:
+    """Restrict this process (threads created afterwards inherit it)."""
+    if not cpus:
+        return False
+    try:
+        os.sched_setaffinity(0, set(cpus))
+        return True
+    except (OSError, ValueError):
+        return False
+
+
+def busy_path(bdf: str, root: str = "/") -> Optional[str]:
+    if not bdf:
+        return None
+    p = os.path.join(root, "sys/bus/pci/devices", bdf, "gpu_busy_percent")
+    return p if os.path.exists(p) else None
+
+
+class BusySampler:
+    """Samples a GPU's ``gpu_busy_percent`` (the amdgpu driver's activity
+    counter, the same source rocm-smi reads) on a background thread."""
+
+    def __init__(self, bdf: str, period_s: float = 0.01, root: str = "/"):
+        self.path = busy_path(bdf, root)
+        self.period_s = period_s
+        self.samples: List[float] = []
+        self._stop = threading.Event()
+        self._th: Optional[threading.Thread] = None
+
+    def start(self) -> "BusySampler":
+        if self.path is not None:
+            self._th = threading.Thread(target=self._run, name="tfs-busy", daemon=True)
+            self._th.start()
+        return self
+
+    def _run(self):
+        while not self._stop.wait(self.period_s):
+            v = _read(self.path)
+            if v is not None and v.isdigit():
+                self.samples.append(float(v))
+
+    def stop(self) -> Optional[dict]:
+        self._stop.set()
+        if self._th is not None:
+            self._th.join(timeout=2)
+        if not self.samples:
+            return None
+        s = self.samples
+        return {"mean": round(sum(s) / len(s), 1), "max": max(s), "samples": len(s)}
+
+
+def cpu_quota() -> Optional[float]:
+    """cgroup-v2 CPU quota in cores (None when unlimited / unknown)."""
+    v = _read("/sys/fs/cgroup/cpu.max")
+    if not v:
+        return None
+    q, _, per = v.partition(" ")
+    if q == "max":
+        return None
+    try:
+        return int(q) / int(per or 100000)
+    except ValueError:
+        return None
+
+
+def thread_cpu(pid: Optional[int] = None) -> Dict[str, float]:
+    """{thread name: CPU seconds} of a process: on-CPU nanoseconds from
+    ``schedstat`` (tick-based utime+stime from ``stat`` when schedstats are
+    off; ticks are 10 ms, too coarse for a few-ms window)."""
+    tick = os.sysconf("SC_CLK_TCK")
+    out: Dict[str, float] = {}
+    base = f"/proc/{pid or os.getpid()}/task"
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"{base}/{tid}/comm") as f:
+                name = f.read().strip()
+            v = None
+            try:
+                with open(f"{base}/{tid}/schedstat") as f:
+                    v = int(f.read().split()[0]) / 1e9
+            except (OSError, ValueError, IndexError):
+                pass
+            if v is None:
+                with open(f"{base}/{tid}/stat") as f:
+                    fields = f.read().rsplit(")", 1)[1].split()
+                v = (int(fields[11]) + int(fields[12])) / tick
+            out[name] = out.get(name, 0.0) + v
+        except (FileNotFoundError, ProcessLookupError, IndexError, ValueError):
+            continue
+    return out
+
+
+def cpu_by_group(before: Dict[str, float], after: Dict[str, float], elapsed: float) -> Dict[str, float]:
+    """Cores used per thread group (thread names without trailing digits)."""
+    groups: Dict[str, float] = {}
+    for k, v in after.items():
+        g = k.rstrip("0123456789")
+        groups[g] = groups.get(g, 0.0) + v - before.get(k, 0.0)
+    return {k: round(v / max(elapsed, 1e-9), 2) for k, v in sorted(groups.items(), key=lambda x: -x[1])
+            if v > 0.01}
+

@@ -1,0 +1,137 @@
+"""bench.py as the driver invokes it: ``--gpus N`` launches N ranks by itself,
+pins each to its GPU's NUMA-node CPUs and reports per-rank diagnostics.
+
+CPU mode (``--device cpu``: CPU servables + gloo) so it runs without a GPU;
+the GPU path differs only in the device and the nccl backend."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from rust_tensorflow_serving2_amd.parallel import topology
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _json_line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus2_self_launch_cpu(tmp_path):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["TMPDIR"] = str(tmp_path)
+    cmd = [sys.executable, BENCH, "--gpus", "2", "--device", "cpu", "--model", "tiny", "--image-size", "32",
+           "--steps", "4", "--warmup", "1", "--prewarm-s", "0.2", "--ref-client-requests", "64",
+           "--c1-requests", "10", "--io-threads", "2", "--client-threads", "1", "--connections", "2",
+           "--lanes", "2"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = _json_line(p.stdout)
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["errors"] == 0 and out["value"] > 0
+    diags = out["diagnostics"]
+    assert [d["placement"]["rank"] for d in diags] == [0, 1]
+    # both ranks served their own load generator's traffic in the timed window
+    assert all(d["timed"]["requests"] > 0 for d in diags), diags
+    assert all(d["prewarm"]["window_s"] > 0 for d in diags)
+    # disjoint CPU sets when there are enough CPUs for both
+    if len(os.sched_getaffinity(0)) >= 2:
+        a, b = (set(topology.parse_cpulist(d["placement"]["cpus"])) for d in diags)
+        assert a and b and not (a & b)
+        assert all(d["placement"]["pinned"] for d in diags)
+    assert out["ref_client_errors"] == 0
+
+
+def test_bench_rejects_gpus_world_mismatch(tmp_path):
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "cpu"], env=env, capture_output=True,
+                       text=True, timeout=120, cwd=str(tmp_path))
+    assert p.returncode != 0
+    assert "WORLD_SIZE" in p.stderr
+
+
+def _fake_sysfs(root, gpus_numa, cpus_per_node=8, smt=True):
+    """KFD topology with CPU nodes then GPU nodes, PCI numa_node, NUMA cpulists
+    and SMT siblings (cpu c and c + ncores)."""
+    nnodes = max(gpus_numa) + 1
+    ncores = nnodes * cpus_per_node
+    kfd = root / "sys/class/kfd/kfd/topology/nodes"
+    for n in range(nnodes):
+        d = kfd / str(n)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count {cpus_per_node}\nsimd_count 0\n")
+    for i, numa in enumerate(gpus_numa):
+        d = kfd / str(nnodes + i)
+        d.mkdir(parents=True)
+        bus = 0x10 * (i + 1)
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
+        pci = root / f"sys/bus/pci/devices/0000:{bus:02x}:00.0"
+        pci.mkdir(parents=True)
+        (pci / "numa_node").write_text(f"{numa}\n")
+        (pci / "gpu_busy_percent").write_text("42\n")
+    for n in range(nnodes):
+        d = root / f"sys/devices/system/node/node{n}"
+        d.mkdir(parents=True)
+        lo = n * cpus_per_node
+        lst = f"{lo}-{lo + cpus_per_node - 1}"
+        if smt:
+            lst += f",{ncores + lo}-{ncores + lo + cpus_per_node - 1}"
+        (d / "cpulist").write_text(lst + "\n")
+    for c in range(ncores):
+        for t in ([c, c + ncores] if smt else [c]):
+            d = root / f"sys/devices/system/cpu/cpu{t}/topology"
+            d.mkdir(parents=True, exist_ok=True)
+            (d / "thread_siblings_list").write_text(f"{c},{c + ncores}\n" if smt else f"{c}\n")
+    return list(range(2 * ncores if smt else ncores))
+
+
+def test_topology_plan_numa_local_whole_cores(tmp_path, monkeypatch):
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    # 8 GPUs, 4 per socket, 2 sockets x 8 cores x 2 threads
+    allowed = _fake_sysfs(tmp_path, [0, 0, 0, 0, 1, 1, 1, 1])
+    info = topology.gpus(str(tmp_path))
+    assert [g.numa_node for g in info] == [0, 0, 0, 0, 1, 1, 1, 1]
+    assert info[0].bdf == "0000:10:00.0"
+    pl = topology.plan(8, allowed=allowed, root=str(tmp_path))
+    node_cpus = topology.numa_cpus(str(tmp_path))
+    seen = set()
+    for p in pl:
+        assert len(p.cpus) == 4
+        assert set(p.cpus) <= set(node_cpus[p.numa_node])        # local socket
+        cores = {c % 16 for c in p.cpus}
+        assert len(cores) == 2                                     # two whole cores (both SMT threads)
+        assert not (seen & set(p.cpus))
+        seen |= set(p.cpus)
+    # a restricted affinity mask (the 1-GPU box share) is respected
+    pl = topology.plan(2, allowed=[0, 1, 16, 17], root=str(tmp_path))
+    assert sorted(c for p in pl for c in p.cpus) == [0, 1, 16, 17]
+    assert pl[0].cpus == [0, 16] and pl[1].cpus == [1, 17]
+
+
+def test_topology_visible_devices_and_rehearsal(tmp_path, monkeypatch):
+    allowed = _fake_sysfs(tmp_path, [0, 1], cpus_per_node=4, smt=False)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "1")
+    info = topology.gpus(str(tmp_path))
+    assert len(info) == 1 and info[0].numa_node == 1 and info[0].index == 0
+    # 4 ranks sharing the one visible GPU (gloo rehearsal): disjoint slices of its node
+    pl = topology.plan(4, allowed=allowed, root=str(tmp_path))
+    assert all(p.gpu == 0 and p.numa_node == 1 for p in pl)
+    assert sorted(c for p in pl for c in p.cpus) == [4, 5, 6, 7]
+    s = topology.BusySampler(info[0].bdf, period_s=0.005, root=str(tmp_path)).start()
+    import time
+    time.sleep(0.05)
+    r = s.stop()
+    assert r and r["mean"] == 42.0
+
+
+def test_cpulist_roundtrip():
+    assert topology.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert topology.compress([0, 1, 2, 3, 8, 10, 11]) == "0-3,8,10-11"

@@ -40,8 +40,9 @@ def _cleanup(group):
 class Replica:
     """A front end whose 'slow path' answers with its own name after `delay`."""
 
-    def __init__(self, name, group, rank, world, delay=0.0, hold=None, **router):
+    def __init__(self, name, group, rank, world, delay=0.0, hold=None, pad=0, **router):
         self.name = name
+        self.pad = pad                   # answer padding (bytes)
         self.srv = _C.Http2Server("127.0.0.1", 0, 2)
         self.srv.enable_router(group, rank, world, **router)
         self.delay = delay
@@ -62,7 +63,7 @@ class Replica:
                 self.hold.wait()
             time.sleep(self.delay)
             self.served += 1
-            self.srv.respond(c, 0, "", self.name.encode() + c.body[:16])
+            self.srv.respond(c, 0, "", self.name.encode() + c.body[:16] + b"\0" * self.pad)
 
     def close(self):
         self.stop.set()
@@ -233,6 +234,39 @@ def test_dead_peer_calls_reclaimed_or_failed():
         assert "RB" not in codes
         assert codes.count("UNAVAILABLE") == st["lost"] and st["lost"] >= 1, (codes, st)
         assert codes.count("RA") == 64 - st["lost"]
+        # RB was only stalled: when it finishes the given-up calls late, RA
+        # frees their cells (nobody else would; the ring would shrink for good)
+        hold.set()
+        t0 = time.time()
+        while a.srv.router_stats()["tomb_freed"] < st["lost"] and time.time() - t0 < 10:
+            time.sleep(0.05)
+        assert a.srv.router_stats()["tomb_freed"] == st["lost"]
+    finally:
+        a.close()
+        b.close()
+        _cleanup(g)
+
+
+def test_oversized_answer_reruns_locally():
+    """An answer larger than the peer's cell (e.g. BERT's [1,128,768] f32
+    sequence output vs a 256 KB cell) is sent back as "run it yourself": the
+    origin serves the call from the message still in the cell, so a call that
+    succeeds locally also succeeds when it was routed."""
+    g = _group()
+    a = Replica("RA", g, 0, 2, delay=0.004, ncells=16, resp_cap=4096)
+    b = Replica("RB", g, 1, 2, pad=8192, ncells=16, resp_cap=4096)
+    try:
+        assert _wait_peers([a, b], 1)
+        with grpc.insecure_channel(f"127.0.0.1:{a.srv.port}") as ch:
+            stub = ch.unary_unary(PREDICT)
+            with cf.ThreadPoolExecutor(24) as ex:
+                futs = [ex.submit(stub, b"payload-%04d" % i, timeout=30) for i in range(200)]
+                for i, f in enumerate(futs):
+                    r = f.result()                               # every call succeeds
+                    assert r[:2] == b"RA" and r[2:18] == (b"payload-%04d" % i)[:16]
+        sa, sb = a.srv.router_stats(), b.srv.router_stats()
+        assert sa["forwarded"] > 0, sa
+        assert sa["rerun"] == sa["forwarded"] == sb["too_large"], (sa, sb)
     finally:
         a.close()
         b.close()
