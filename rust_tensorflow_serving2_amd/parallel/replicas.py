@@ -26,10 +26,12 @@ Topology (MI355X-first, SURVEY.md §2.4 "DP replicas", §7.2 step 6):
   (``csrc/router.h``; group name in ``TFSERVE_ROUTE_GROUP``).
 * Fault isolation: :func:`launch` is a supervisor.  It hosts the control
   store itself (no replica's death takes the store down), restarts only a
-  replica that died (a fresh child process that loads from disk, not through
-  the collective, and applies the group's current config), and marks the
-  weight-broadcast group broken so the survivors load from disk too.  Config
-  reloads wait only for replicas whose heartbeat is fresh.
+  replica that died (a fresh child process that reads the models the group
+  already holds from disk and applies the group's current config), and bumps
+  the weight-broadcast generation (``tfs/gen``): the live replicas and the
+  replacement form a new group at the leader's next load, so later loads are
+  broadcast on every GPU again (parallel/weights.py).  Config reloads wait
+  only for replicas whose heartbeat is fresh.
 """
 from __future__ import annotations
 
@@ -263,8 +265,9 @@ def launch(argv: Sequence[str], nproc: int, module: str = "rust_tensorflow_servi
                 procs[i] = None
                 if stopping or r == 0:
                     continue
-                # the weight-broadcast group lost a member: everyone loads from disk from now on
-                store.set("tfs/group_broken", "1")
+                # the weight-broadcast group lost a member: a new generation, whose
+                # group (live ranks + the replacement) forms at the leader's next event
+                store.add("tfs/gen", 1)
                 if restarts[i] >= max_restarts:
                     log.error("replica %d (pid %d) exited with %d; restart budget spent", i, p.pid, r)
                     rc = rc or r

@@ -27,19 +27,33 @@ broadcast unit".
 Collective ordering.  Each rank's model manager decides *when* to load on its
 own (file-system polling, reload RPCs arriving on any rank), but collectives
 must be issued in the same order everywhere.  So only the leader initiates:
-it publishes ``(seq, kind, ...)`` events to the control store and runs the
-collective; every follower has ONE event thread that consumes leader events
-strictly in ``seq`` order, joins each collective and parks the result until
-the local manager / compiler asks for it.  If a replica dies the supervisor
-marks the group broken (``tfs/group_broken``) and every rank loads and
-compiles from disk from then on.  The reference has no multi-GPU path at all
-(one TF Serving container, ``serving/rundocker.sh:15``).
+it publishes ``(seq, kind, ..., generation)`` events to the control store and
+runs the collective; every follower has ONE event thread that consumes leader
+events strictly in ``seq`` order, joins each collective and parks the result
+until the local manager / compiler asks for it.
+
+Generations.  The broadcast group is re-formed after a replica restart
+instead of being given up: the supervisor bumps ``tfs/gen`` when it restarts a
+replica (parallel/replicas.py), and the next event the leader publishes carries
+the new generation.  Every live rank -- the replacement included -- then
+builds a fresh process group on the store prefix ``tfs/pg/g<gen>`` (a
+standalone ``ProcessGroupNCCL`` / ``ProcessGroupGloo``: the dead process is no
+member of it) before it joins that event's collective, so later loads are
+broadcast again on every GPU.  A replacement skips events of older generations
+(their groups ran without it) and reads the models the group loaded before it
+existed from disk.  While a replica is down (its heartbeat stale) the leader
+loads from disk and says so in the model's marker, so no rank waits for a
+collective that could not complete.  The reference has no multi-GPU path at all
+(SURVEY.md §2.4-2.5: one TF Serving container, ``serving/rundocker.sh:15``);
+the supersede-on-reload contract this keeps fast on every GPU is
+``model_service.proto:19-21``.
 """
 from __future__ import annotations
 
 import json
 import logging
 import os
+import pickle
 import threading
 import time
 from concurrent.futures import Future
@@ -95,14 +109,13 @@ def _sync(device: torch.device):
         torch.cuda.synchronize(device)
 
 
-def broadcast_meta(path: Optional[str], root: int, group, device: torch.device) -> sm.SavedModelBundle:
+def broadcast_meta(path: Optional[str], root: int, comm: "_Comm") -> sm.SavedModelBundle:
     """Collective: the root loads ``path``; followers get a meta bundle (float
     variables shape-only, small non-float ones by value).  A load failure on
     the root is broadcast as an error so followers never wait for it."""
-    rank = dist.get_rank(group)
-    meta = [None]
+    meta = None
     b = None
-    if rank == root:
+    if comm.rank == root:
         try:
             b = sm.load(path)
             names = sorted(b.bundle.keys()) if b.bundle is not None else []
@@ -112,15 +125,13 @@ def broadcast_meta(path: Optional[str], root: int, group, device: torch.device) 
                 entries.append((n, dt, list(b.bundle.shape(n))))
                 if dt not in _META_DT:
                     small[n] = np.asarray(b.bundle[n])
-            meta[0] = ("ok", b.meta_graph.SerializeToString(), entries, list(b.tags), small)
+            meta = ("ok", b.meta_graph.SerializeToString(), entries, list(b.tags), small)
         except Exception as e:    # propagated to every rank
-            meta[0] = ("error", f"{type(e).__name__}: {e}", None, None, None)
-    dist.broadcast_object_list(meta, src=root, group=group,
-                               device=device if device.type == "cuda" else None)
-    status, mg_bytes, entries, tags, small = meta[0]
+            meta = ("error", f"{type(e).__name__}: {e}", None, None, None)
+    status, mg_bytes, entries, tags, small = comm.bcast_obj(meta, root)
     if status != "ok":
         raise LoadError(mg_bytes)
-    if rank == root:
+    if comm.rank == root:
         return b
     arrays, dtypes = {}, {}
     for n, dt, shape in entries:
@@ -130,24 +141,22 @@ def broadcast_meta(path: Optional[str], root: int, group, device: torch.device) 
     return sm.SavedModelBundle(path or "", mg, MemoryBundle(arrays, dtypes), tags)
 
 
-def broadcast_blob(blob: Optional[torch.Tensor], manifest, root: int, group, device: torch.device,
+def broadcast_blob(blob: Optional[torch.Tensor], manifest, root: int, comm: "_Comm",
                    stats: Optional[dict] = None) -> Tuple[torch.Tensor, list]:
     """Collective: the root's packed program weights -> every rank's device."""
-    rank = dist.get_rank(group)
-    meta = [manifest if rank == root else None]
-    dist.broadcast_object_list(meta, src=root, group=group, device=device if device.type == "cuda" else None)
-    manifest = meta[0]
-    if rank != root:
+    manifest = comm.bcast_obj(manifest if comm.rank == root else None, root)
+    device = comm.device
+    if comm.rank != root:
         blob = torch.empty(placement.blob_bytes(manifest), dtype=torch.uint8, device=device)
     _sync(device)
     t0 = time.perf_counter()
-    if device.type == "cuda" and dist.get_backend(group) == "gloo":
+    if device.type == "cuda" and comm.backend == "gloo":
         host = blob.cpu()                      # gloo rehearsal of the device path: staged through the host
-        dist.broadcast(host, src=root, group=group)
-        if rank != root:
+        comm.bcast_tensor(host, root)
+        if comm.rank != root:
             blob.copy_(host)
     else:
-        dist.broadcast(blob, src=root, group=group)
+        comm.bcast_tensor(blob, root)          # RCCL: device to device over xGMI
     _sync(device)
     if stats is not None:
         stats["broadcast_s"] = stats.get("broadcast_s", 0.0) + time.perf_counter() - t0
@@ -156,44 +165,114 @@ def broadcast_blob(blob: Optional[torch.Tensor], manifest, root: int, group, dev
     return blob, manifest
 
 
+class _Comm:
+    """One generation's process group: the whole world, rank numbers as in
+    the replica group.  Generation 0 may be the default group
+    (``init_process_group``); later ones are standalone groups on a fresh
+    store prefix."""
+
+    def __init__(self, pg, rank: int, world: int, backend: str, device: torch.device, gen: int):
+        self.pg, self.rank, self.world, self.backend, self.device, self.gen = pg, rank, world, backend, device, gen
+
+    @classmethod
+    def form(cls, store, gen: int, rank: int, world: int, backend: str, device: torch.device,
+             timeout_s: float) -> "_Comm":
+        from datetime import timedelta
+        ps = dist.PrefixStore(f"tfs/pg/g{gen}", store)
+        if backend == "nccl":
+            pg = dist.ProcessGroupNCCL(ps, rank, world, timedelta(seconds=timeout_s))
+        else:
+            pg = dist.ProcessGroupGloo(ps, rank, world, timedelta(seconds=timeout_s))
+        return cls(pg, rank, world, backend, device, gen)
+
+    def _dev(self):
+        return self.device if self.backend == "nccl" else torch.device("cpu")
+
+    def bcast_tensor(self, t: torch.Tensor, root: int) -> None:
+        opts = dist.BroadcastOptions()
+        opts.rootRank = root
+        opts.rootTensor = 0
+        self.pg.broadcast([t], opts).wait()
+
+    def bcast_obj(self, obj, root: int):
+        """Pickled object from ``root`` (our own control messages only: meta
+        graphs, shapes, manifests; never a file's bytes)."""
+        dev = self._dev()
+        if self.rank == root:
+            data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+            n = torch.tensor([len(data)], dtype=torch.int64, device=dev)
+        else:
+            n = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.bcast_tensor(n, root)
+        size = int(n.item())
+        if self.rank == root:
+            buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+        else:
+            buf = torch.empty(size, dtype=torch.uint8, device=dev)
+        self.bcast_tensor(buf, root)
+        if self.rank == root:
+            return obj
+        return pickle.loads(buf.cpu().numpy().tobytes())
+
+
+GEN_KEY = "tfs/gen"
+
+
 class ReplicatedWeightSource:
     """Leader-ordered weight replication for every replica (see module doc).
 
-    ``store`` is a ``torch.distributed.Store`` shared by the replicas;
-    ``group`` the process group the broadcasts run on (nccl/RCCL for GPUs,
-    gloo for CPU replicas)."""
+    ``store`` is a ``torch.distributed.Store`` shared by the replicas.  The
+    generation-0 group is ``group`` (default: the default process group when
+    one is initialised); a replica started after a restart has none and forms
+    the group of the current generation with the others at the next event.
+    ``rank`` / ``world`` default to the default group's."""
 
     def __init__(self, store, group=None, device: Optional[torch.device] = None, leader: int = 0,
                  load_timeout: float = 900.0, prefix: str = "tfs/wev", tuned_timeout: float = 600.0,
-                 program_timeout: float = 120.0, share: Optional[bool] = None):
+                 program_timeout: float = 120.0, share: Optional[bool] = None, rank: Optional[int] = None,
+                 world: Optional[int] = None, restarted: bool = False, pg_timeout_s: float = 300.0,
+                 dead_after_s: float = 3.0):
         self.store = store
-        self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
+        if rank is None or world is None:
+            rank, world = dist.get_rank(group), dist.get_world_size(group)
+        self.rank = int(rank)
+        self.world = int(world)
         self.leader = leader
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
                 else torch.device("cpu")
         self.device = device
+        self.backend = "nccl" if device.type == "cuda" else "gloo"
         # GPU replicas share the leader's compiled device weights; CPU replicas
-        # (tests, control-plane-only deployments) just read the disk each
-        # unless asked to rehearse the protocol (share=True)
+        # (tests, control-plane-only deployments) read the disk each unless
+        # asked to rehearse the protocol (share=True / TFSERVE_SHARE_WEIGHTS=1)
         if share is None:
-            share = device.type == "cuda" and os.environ.get("TFSERVE_SHARE_WEIGHTS", "1") != "0"
+            share = os.environ.get("TFSERVE_SHARE_WEIGHTS", "1" if device.type == "cuda" else "0") != "0"
         self.share = bool(share)
         self.load_timeout = load_timeout
         self.tuned_timeout = tuned_timeout
         self.program_timeout = program_timeout
+        self.pg_timeout_s = pg_timeout_s
+        self.dead_after_s = dead_after_s
         self.announce_wait_s = float(os.environ.get("TFSERVE_SHARE_WAIT_S", "20"))
         self.prefix = prefix
-        self.stats: dict = {}
+        self.stats: dict = {"gen": 0, "regroups": 0, "disk_loads": 0}
         self._lock = threading.Lock()           # leader: one collective at a time, seq order
-        self._seq = 0
         self._pending: Dict[Tuple, Future] = {}
         self._parked: Dict[Tuple, Tuple[float, object]] = {}
         self._stop = threading.Event()
         self._thread = None
         self._disk: set = set()                  # (name, version) loaded from disk: compiled locally
+        self._old_comms: list = []               # superseded groups (never destroyed under a peer's feet)
+        # generation this process started in: events of older generations ran
+        # in groups it was never part of
+        self.min_gen = self._current_gen()
+        self.comm: Optional[_Comm] = None
+        if not restarted and self.min_gen == 0 and dist.is_initialized():
+            pg = group if group is not None else dist.distributed_c10d._get_default_group()
+            self.comm = _Comm(pg, self.rank, self.world, self.backend, device, 0)
+        # followers consume events from the one after the newest at start-up
+        self._first_seq = int(self.store.add(f"{prefix}/seq", 0)) + 1 if restarted else 1
         if self.rank != leader and self.share:
             self._thread = threading.Thread(target=self._follow, name="tfs-wev", daemon=True)
             self._thread.start()
@@ -202,23 +281,72 @@ class ReplicatedWeightSource:
     def is_leader(self) -> bool:
         return self.rank == self.leader
 
-    def group_broken(self) -> bool:
-        """A replica died (the supervisor says so): the collective can no
-        longer complete, every rank loads from disk from now on."""
+    @property
+    def gen(self) -> int:
+        return self.comm.gen if self.comm is not None else -1
+
+    # ------------------------------------------------------------ generations / liveness
+    def _current_gen(self) -> int:
         try:
-            return self.store.check(["tfs/group_broken"])
+            return int(self.store.add(GEN_KEY, 0))
         except Exception:
-            return True
+            return -1
+
+    def _alive(self, rank: int) -> bool:
+        """Heartbeat of ``rank`` (parallel/replicas.py ReplicaControl); ranks
+        without one (no control plane, e.g. the benchmark) count as alive."""
+        key = f"tfs/hb/{rank}"
+        try:
+            if not self.store.check([key]):
+                return True
+            return time.time() - float(self.store.get(key).decode()) < self.dead_after_s
+        except Exception:
+            return False
+
+    def _all_alive(self) -> bool:
+        return all(self._alive(r) for r in range(self.world) if r != self.rank)
+
+    def _ensure_comm(self, gen: int) -> _Comm:
+        """The process group of generation ``gen`` (formed on first use: every
+        rank of the generation constructs it at the same event)."""
+        if self.comm is not None and self.comm.gen == gen:
+            return self.comm
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        comm = _Comm.form(self.store, gen, self.rank, self.world, self.backend, self.device, self.pg_timeout_s)
+        if self.comm is not None:
+            self._old_comms.append(self.comm)
+        self.comm = comm
+        self.stats["gen"] = gen
+        self.stats["regroups"] = self.stats.get("regroups", 0) + 1
+        log.info("rank %d: weight-broadcast group of generation %d formed", self.rank, gen)
+        return comm
+
+    def group_broken(self) -> bool:
+        """(compatibility) the leader is down: waiting for its broadcast is pointless."""
+        return not self._alive(self.leader)
 
     # ------------------------------------------------------------ events
+    def _marker_key(self, name: str, version: int) -> str:
+        return f"{self.prefix}/loaded/{name}/{int(version)}"
+
+    def _marker(self, name: str, version: int) -> Optional[dict]:
+        k = self._marker_key(name, version)
+        try:
+            if not self.store.check([k]):
+                return None
+            return json.loads(self.store.get(k).decode())
+        except Exception:
+            return None
+
     def _publish(self, event):
-        self._seq += 1
-        self.store.set(f"{self.prefix}/{self._seq}", json.dumps(event))
+        seq = int(self.store.add(f"{self.prefix}/seq", 1))
+        self.store.set(f"{self.prefix}/{seq}", json.dumps(event))
 
     def _follow(self):
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
-        seq = 1
+        seq = self._first_seq
         while not self._stop.is_set():
             key = f"{self.prefix}/{seq}"
             if not self.store.check([key]):     # non-blocking poll (lets close() end the thread)
@@ -226,15 +354,19 @@ class ReplicatedWeightSource:
                 continue
             ev = json.loads(self.store.get(key).decode())
             seq += 1
+            gen = int(ev[-1])
+            if gen < self.min_gen:
+                continue                          # a collective of a group this process never joined
+            k = tuple(ev[:4]) if ev[0] == "prog" else tuple(ev[:3])
             try:
+                comm = self._ensure_comm(gen)
                 if ev[0] == "load":
-                    res = broadcast_meta(None, self.leader, self.group, self.device)
+                    res = broadcast_meta(None, self.leader, comm)
                 else:
-                    res = broadcast_blob(None, None, self.leader, self.group, self.device, self.stats)
+                    res = broadcast_blob(None, None, self.leader, comm, self.stats)
                 err = None
             except Exception as e:
                 res, err = None, e
-            k = tuple(ev[:4]) if ev[0] == "prog" else tuple(ev[:3])
             self._deliver(k, res, err)
 
     def _deliver(self, k, res, err):
@@ -254,7 +386,8 @@ class ReplicatedWeightSource:
         for k in [k for k, (t, _) in self._parked.items() if now - t > ttl]:
             del self._parked[k]
 
-    def _await(self, k, what: str, fallback, timeout: Optional[float] = None, fallback_on_timeout: bool = False):
+    def _await(self, k, what: str, fallback, timeout: Optional[float] = None, fallback_on_timeout: bool = False,
+               disk_marker: Optional[Tuple[str, int]] = None):
         """A follower's parked / pending leader result for ``k``."""
         with self._lock:
             parked = self._parked.pop(k, None)
@@ -271,56 +404,76 @@ class ReplicatedWeightSource:
             try:
                 return fut.result(timeout=0.5)
             except FutureTimeout:
-                if self.group_broken() or time.time() > deadline:
+                leader_down = self.group_broken()
+                m = self._marker(*disk_marker) if disk_marker else None
+                skipped = m is not None and m.get("mode") == "disk"
+                if leader_down or skipped or time.time() > deadline:
                     with self._lock:
                         self._pending.pop(k, None)
-                    if self.group_broken() or fallback_on_timeout:   # the leader may be the replica that died
+                    if leader_down or skipped or fallback_on_timeout:
                         return fallback()
                     raise LoadError(f"timed out waiting for the leader rank to broadcast {what}")
 
+    def _disk_load(self, key, path):
+        self.stats["disk_loads"] = self.stats.get("disk_loads", 0) + 1
+        self._disk.add(key)
+        return sm.load(path)
+
     # ------------------------------------------------------------ API: load
     def load(self, name: str, version: int, path: str):
+        key = (name, int(version))
         if not self.share:
-            self._disk.add((name, int(version)))
+            self._disk.add(key)
             return sm.load(path)
-        if self.group_broken():
-            self.stats["disk_loads"] = self.stats.get("disk_loads", 0) + 1
-            self._disk.add((name, int(version)))
-            return sm.load(path)
-        self._disk.discard((name, int(version)))
+        self._disk.discard(key)
         if self.is_leader:
             with self._lock:
-                self._publish(["load", name, int(version), path])
-                return broadcast_meta(path, self.leader, self.group, self.device)
-
-        def disk():
-            self._disk.add((name, int(version)))
-            return sm.load(path)
-        return self._await(("load", name, int(version)), f"{name} version {version}", disk)
+                gen = self._current_gen()
+                if gen < 0 or not self._all_alive():
+                    # a replica is down (being restarted): no collective can complete
+                    self.store.set(self._marker_key(name, version), json.dumps({"gen": gen, "mode": "disk"}))
+                    return self._disk_load(key, path)
+                self.store.set(self._marker_key(name, version), json.dumps({"gen": gen, "mode": "bcast"}))
+                # publish first: forming a new generation's group is itself a
+                # rendezvous the followers join when they see this event
+                self._publish(["load", name, int(version), path, gen])
+                comm = self._ensure_comm(gen)
+                return broadcast_meta(path, self.leader, comm)
+        m = self._marker(name, version)
+        if m is not None and (m.get("mode") == "disk" or int(m.get("gen", 0)) < self.min_gen):
+            # the leader broadcast it before this process existed, or not at all
+            return self._disk_load(key, path)
+        b = self._await(("load", name, int(version)), f"{name} version {version}",
+                        lambda: self._disk_load(key, path), disk_marker=(name, int(version)))
+        if key not in self._disk:
+            self.stats["bcast_loads"] = self.stats.get("bcast_loads", 0) + 1
+        return b
 
     # ------------------------------------------------------------ API: compiled programs
     def share_program(self, name: str, version: int, key: str, program, recompile=None) -> None:
         """After compiling ``program`` for runner ``key`` of (name, version):
         the leader packs + broadcasts its device weights, a follower binds its
         program to the received blob (``recompile()`` builds the program from
-        disk instead when the group broke meanwhile; the caller's program is
-        then replaced by the return value through ``program.__dict__``)."""
+        disk instead when the leader does not share it; the caller's program
+        is then replaced by the return value through ``program.__dict__``)."""
         k = ("prog", name, int(version), key)
         if not self.share or (name, int(version)) in self._disk:
             return                                   # compiled from real weights: nothing to bind
         if self.is_leader:
-            if self.group_broken():
-                return
             with self._lock:
+                gen = self._current_gen()
+                if gen < 0 or not self._all_alive():
+                    return
                 self.store.set(self._announce_key(name, version, key), "1")
-                self._publish(["prog", name, int(version), key])
+                self._publish(["prog", name, int(version), key, gen])
+                comm = self._ensure_comm(gen)
                 blob, man = placement.export_weights(program)
-                broadcast_blob(blob, man, self.leader, self.group, self.device, self.stats)
+                broadcast_blob(blob, man, self.leader, comm, self.stats)
             return
 
         def rebuild():
             if recompile is None:
-                raise LoadError("the weight-broadcast group broke before this program's weights arrived")
+                raise LoadError("the leader did not broadcast this program's weights")
             return ("recompiled", recompile())
         # a runner the leader does not build (one only this replica's traffic
         # asked for) is compiled from disk: wait for the leader to announce it
@@ -360,12 +513,12 @@ class ReplicatedWeightSource:
 
     def publish_tuned(self, name: str, version: int, key: str, bucket: int, table: Dict[str, list]) -> None:
         """Leader: the tile configs its capture of ``bucket`` settled on."""
-        if self.share and self.is_leader and not self.group_broken():
+        if self.share and self.is_leader:
             self.store.set(self.tuned_key(name, version, key, bucket), json.dumps(table))
 
     def wait_tuned(self, name: str, version: int, key: str, bucket: int) -> Optional[Dict[str, list]]:
         """Follower: the leader's tile configs for ``bucket`` (None after the
-        timeout or when the group broke: the caller tunes for itself)."""
+        timeout or when the leader is down: the caller tunes for itself)."""
         if not self.share or self.is_leader or (name, int(version)) in self._disk:
             return None
         sk = self.tuned_key(name, version, key, bucket)

@@ -119,11 +119,14 @@ def make_server(args, rank: int = 0, world: int = 1):
             from datetime import timedelta
             host, sport = store_addr.rsplit(":", 1)
             store = dist.TCPStore(host, int(sport), is_master=False, timeout=timedelta(seconds=120))
+        from datetime import timedelta
         if restarts == 0:
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 backend = "nccl" if dev.type == "cuda" else "gloo"
                 kw = {"device_id": dev} if dev.type == "cuda" else {}
+                # bounded: a collective whose peer died must fail, not hang the replica
+                kw["timeout"] = timedelta(seconds=300)
                 if store is not None:
                     dist.init_process_group(backend, store=dist.PrefixStore("tfs/pg", store), rank=rank,
                                             world_size=world, **kw)
@@ -131,9 +134,12 @@ def make_server(args, rank: int = 0, world: int = 1):
                     dist.init_process_group(backend, **kw)
             if store is None:
                 store = dist.distributed_c10d._get_default_store()
-            weight_source = ReplicatedWeightSource(store, device=dev)
-        # a replacement replica (restarted by the supervisor) is not a member of
-        # the weight-broadcast group: it loads from disk
+        # a replacement replica (restarted by the supervisor) joins the group of
+        # the current generation at the leader's next load; the models the group
+        # already holds it reads from disk
+        if store is not None:
+            weight_source = ReplicatedWeightSource(store, device=dev, rank=rank, world=world,
+                                                   restarted=restarts > 0)
         replicas = ReplicaControl(store, rank, world, restarted=restarts > 0)
         router = (os.environ.get("TFSERVE_ROUTE_GROUP") or f"p{os.environ.get('MASTER_PORT', '0')}", rank, world)
     sopts = ServableOptions(device=device, hip_graphs=args.hip_graphs, warmup=args.enable_model_warmup,
@@ -165,6 +171,10 @@ def _write_stats(server, stats_dir: str, rank: int):
             d["requests"] = st["requests"]
             d["router"] = rs
             d["served"] = st["requests"] - rs.get("forwarded", 0)   # answered by this replica's device
+    ws = getattr(server.opts, "weight_source", None)
+    if ws is not None:
+        d["weights"] = {k: v for k, v in ws.stats.items() if isinstance(v, (int, float))}
+        d["weights"]["gen"] = ws.gen
     os.makedirs(stats_dir, exist_ok=True)
     path = os.path.join(stats_dir, f"replica{rank}.{os.getpid()}.json")
     with open(path + ".tmp", "w") as f:

@@ -16,7 +16,9 @@
 from __future__ import annotations
 
 import logging
+import os
 import threading
+import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -199,7 +201,18 @@ class GpuRunner:
         lane.stream.synchronize()
         self._ensure_host_out(lane, outs)
         if keys and self.servable.options.graph_autotune and ops.AUTOTUNE:
-            changed = ops.graph_tune(keys, lambda: self._replay_ms(lane, ins), **ops.graph_tune_params(b))
+            conc = self.tune_concurrency(b)
+            if conc > 1:
+                # the serving regime of the largest bucket: `conc` lanes replay
+                # batches at once, so tiles are picked for aggregate throughput
+                # (per-batch time of concurrent replays), where small-LDS tiles
+                # that co-reside with other lanes' kernels can beat the tiles
+                # that are fastest alone
+                params = dict(top=6, ratio=2.0)
+                params.update(ops.graph_tune_params(b))
+                changed = ops.graph_tune(keys, lambda: self._replay_ms_concurrent(ins, conc), **params)
+            else:
+                changed = ops.graph_tune(keys, lambda: self._replay_ms(lane, ins), **ops.graph_tune_params(b))
             if changed:
                 log.info("graph autotune %s bucket=%d: %s", self.servable.name, b, changed)
         if src is not None and keys:
@@ -240,6 +253,46 @@ class GpuRunner:
                 e.synchronize()
                 best = min(best, s.elapsed_time(e) / iters)
         del graph
+        return best
+
+    def tune_concurrency(self, b: int) -> int:
+        """Concurrent batches the graph tuner times for bucket ``b``: the fast
+        path's lane count for the largest bucket (a full server runs that many
+        batches at once), 1 (latency) for the smaller ones.
+        ``TFSERVE_GRAPH_TUNE_CONC`` overrides (0/1 = isolated replays)."""
+        env = os.environ.get("TFSERVE_GRAPH_TUNE_CONC")
+        if env is not None:
+            return max(1, min(int(env), len(self.lanes)))
+        if b != self.buckets[-1]:
+            return 1
+        return max(1, min(4, len(self.lanes) - 1))
+
+    def _replay_ms_concurrent(self, ins: List[torch.Tensor], k: int, reps: int = 3, iters: int = 4) -> float:
+        """Per-batch ms of ``k`` copies of the program (current tile picks)
+        replayed at once on ``k`` lanes' streams: the throughput regime of a
+        loaded server (best of ``reps`` rounds of ``iters`` replays per stream;
+        the graphs are dropped)."""
+        streams = [l.stream for l in self.lanes[:k]]
+        graphs = []
+        for st in streams:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st, capture_error_mode="thread_local"):
+                self._finish(self.program.run(ins))
+            graphs.append(g)
+        for g, st in zip(graphs, streams):
+            with torch.cuda.stream(st):
+                g.replay()
+        torch.cuda.synchronize(self.device)
+        best = float("inf")
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                for g, st in zip(graphs, streams):
+                    with torch.cuda.stream(st):
+                        g.replay()
+            torch.cuda.synchronize(self.device)
+            best = min(best, (time.perf_counter() - t0) * 1e3 / (iters * k))
+        del graphs
         return best
 
     def _launch(self, lane: _Lane, n: int) -> int:

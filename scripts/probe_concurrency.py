@@ -1,0 +1,72 @@
+"""ResNet-50 b32 engine throughput with K batches in flight at once (the
+serving regime: each fast-path lane replays its own HIP graph on its own
+stream).  Prints per-batch ms for K = 1..lanes and the tile picks.
+
+TFSERVE_GRAPH_TUNE_CONC=1 reproduces the isolated-replay tuner."""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert-base"])
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--lanes", type=int, default=4)
+    ap.add_argument("--iters", type=int, default=40)
+    args = ap.parse_args()
+    from rust_tensorflow_serving2_amd import ops
+    from rust_tensorflow_serving2_amd.models import bert, resnet
+    from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
+    path = os.path.join(tempfile.mkdtemp(), "1")
+    opts = ServableOptions(device="cuda:0", max_batch_size=args.batch, allowed_batch_sizes=(args.batch,),
+                           lanes=args.lanes)
+    if args.model == "bert-base":
+        bert.export(path, seed=0)
+        s = Servable("bert", 1, path, opts)
+        r = s.runner("serving_default", ["input_ids", "input_mask", "segment_ids"], ["pooled_output", "probabilities"])
+    else:
+        resnet.export(path)
+        s = Servable("resnet", 1, path, opts)
+        r = s.runner("serving_default", ["input"], ["classes", "probabilities"])
+    t0 = time.perf_counter()
+    for i in r.fast_lanes():
+        r.lane_host_pointers(i)
+    t_cap = time.perf_counter() - t0
+    b = args.batch
+    lanes = [r.lanes[i] for i in r.fast_lanes()]
+    res = {"model": args.model, "batch": b, "capture_s": round(t_cap, 2),
+           "tune_conc": r.tune_concurrency(b)}
+    for k in range(1, len(lanes) + 1):
+        gs = [(l.graphs[b], l.stream) for l in lanes[:k]]
+        for g, st in gs:
+            with torch.cuda.stream(st):
+                g.replay()
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(3):
+            t = time.perf_counter()
+            for _ in range(args.iters):
+                for g, st in gs:
+                    with torch.cuda.stream(st):
+                        g.replay()
+            torch.cuda.synchronize()
+            best = min(best, (time.perf_counter() - t) * 1e3 / (args.iters * k))
+        res[f"ms_per_batch_k{k}"] = round(best, 4)
+    picks = {}
+    for key, v in ops.tuned_table().items():
+        picks[repr(key)[:90]] = list(v)
+    res["picks"] = picks
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

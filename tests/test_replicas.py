@@ -239,3 +239,91 @@ def test_four_replicas_one_connection_and_replica_restart(hpt_path, tmp_path):
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, 9)
             proc.wait()
+
+
+def test_restart_reforms_weight_broadcast_group(tiny_resnet_path, tmp_path):
+    """Three CPU replicas sharing weights through the leader's broadcast
+    (gloo; TFSERVE_SHARE_WEIGHTS=1 rehearses the GPU path).  `kill -9` of a
+    follower: the supervisor restarts it and bumps the group's generation.
+    A reload to a new version is then broadcast again -- every follower, the
+    replacement included, forms the generation-1 group and receives the new
+    version from the leader (no disk read on the survivor) -- instead of every
+    later load on every rank going to disk (model_service.proto:19-21)."""
+    import json
+    import shutil
+    import signal as sig
+    from rust_tensorflow_serving2_amd.client import TensorflowServing
+    from rust_tensorflow_serving2_amd.schema import serving
+    base = str(tmp_path / "r")
+    shutil.copytree(os.path.join(tiny_resnet_path, "1"), os.path.join(base, "1"))
+    port = _free_port()
+    logf = str(tmp_path / "replicas.log")
+    stats_dir = str(tmp_path / "stats")
+    env = dict(os.environ, PYTHONPATH=ROOT, TFSERVE_STATS_DIR=stats_dir, TFSERVE_SHARE_WEIGHTS="1",
+               TFSERVE_SHARE_WAIT_S="5")
+    env.pop("WORLD_SIZE", None)
+    proc = subprocess.Popen([sys.executable, "-m", "rust_tensorflow_serving2_amd.server", f"--port={port}",
+                             "--model_name=r", f"--model_base_path={base}", "--num_gpus=3", "--device=cpu",
+                             "--host=127.0.0.1", "--file_system_poll_wait_seconds=0", "--log_level=WARNING",
+                             "--io_threads=1"],
+                            env=env, stdout=open(logf, "w"), stderr=subprocess.STDOUT, text=True,
+                            start_new_session=True)
+
+    def ready_count():
+        return open(logf).read().count("ready:")
+
+    x = np.random.default_rng(0).random((1, 32, 32, 3), dtype=np.float32)
+
+    async def predict(version=None):
+        c = await TensorflowServing.new().hostname("127.0.0.1").port(port).build()
+        from rust_tensorflow_serving2_amd.client import ModelDescription
+        return await c.predict_tensors(ModelDescription("r", version) if version else "r", {"input": x})
+
+    try:
+        deadline = time.time() + 240
+        while time.time() < deadline and proc.poll() is None and ready_count() < 3:
+            time.sleep(0.2)
+        assert ready_count() == 3, open(logf).read()[-3000:]
+        p1 = asyncio.run(predict())["probabilities"]
+        time.sleep(1.0)
+        st = _stats(stats_dir)
+        gen0 = {r: s["weights"] for (r, _p), s in st.items()}
+        assert gen0[1]["gen"] == 0 and gen0[2]["gen"] == 0 and gen0[2]["disk_loads"] == 0, gen0
+
+        victim = 1
+        vpid = next(p for (r, p) in st if r == victim)
+        os.kill(vpid, sig.SIGKILL)
+        deadline = time.time() + 240
+        while time.time() < deadline and ready_count() < 4:
+            time.sleep(0.2)
+        assert ready_count() == 4, open(logf).read()[-3000:]
+        time.sleep(1.5)                                   # the replacement's heartbeat is fresh
+
+        # a new version, loaded by a reload (supersedes the config)
+        shutil.copytree(os.path.join(base, "1"), os.path.join(base, "2"))
+
+        async def reload():
+            c = await TensorflowServing.new().hostname("127.0.0.1").port(port).build()
+            return await c.reload([serving.ModelConfig(name="r", base_path=base, model_platform="tensorflow")])
+        resp = asyncio.run(reload())
+        assert resp.status.error_code == 0, resp.status.error_message
+        for _ in range(6):
+            np.testing.assert_allclose(asyncio.run(predict(2))["probabilities"], p1, rtol=1e-5, atol=1e-6)
+        time.sleep(1.0)
+        st2 = _stats(stats_dir)
+        now = {r: s for (r, p), s in st2.items() if p != vpid}
+        surv, repl = now[2]["weights"], now[victim]["weights"]
+        assert now[victim]["restarts"] == 1
+        # the survivor: regrouped at generation 1 and got version 2 over the broadcast
+        assert surv["gen"] == 1 and surv["disk_loads"] == 0 and surv["bcast_loads"] >= 2, surv
+        # the replacement: version 1 from disk (before it existed), version 2 over the broadcast
+        assert repl["gen"] == 1 and repl["disk_loads"] == 1 and repl["bcast_loads"] >= 1, repl
+        assert now[0]["weights"]["gen"] == 1
+        assert proc.poll() is None
+    finally:
+        os.killpg(proc.pid, 15)
+        try:
+            proc.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, 9)
+            proc.wait()

@@ -31,7 +31,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, backend, port, path, out_q):
+def _worker(rank, world, backend, port, path, out_q, regroup=False):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from rust_tensorflow_serving2_amd import ops
@@ -54,6 +54,20 @@ def _worker(rank, world, backend, port, path, out_q):
         res = {"probs": out["probabilities"], "classes": out["classes"], "h2d": placement.H2D_BYTES - h2d0,
                "bound": ws.stats.get("bound_bytes", 0), "bcast": ws.stats.get("broadcast_bytes", 0),
                "tuned_here": len(ops._TUNE_TIMES), "remote": len(ops._REMOTE)}
+        if regroup:
+            # a replica restart bumps the generation: the next load forms a
+            # standalone ProcessGroupNCCL on a fresh store prefix and broadcasts
+            # through it (parallel/weights.py _Comm.form)
+            store = dist.distributed_c10d._get_default_store()
+            store.add("tfs/gen", 1)
+            b0 = res["bcast"]
+            b2 = ws.load("resnet", 2, path)
+            s2 = Servable("resnet", 2, path, ServableOptions(device="cuda:0", max_batch_size=4,
+                                                              allowed_batch_sizes=(4,)), b2, weight_source=ws)
+            out2 = s2.run("serving_default", {"input": x}, ["classes", "probabilities"])
+            res.update(gen=ws.gen, regroups=ws.stats.get("regroups", 0),
+                       bcast2=ws.stats.get("broadcast_bytes", 0) - b0, probs2=out2["probabilities"],
+                       pg=type(ws.comm.pg).__name__)
         ws.close()
         dist.barrier()
         dist.destroy_process_group()
@@ -63,11 +77,11 @@ def _worker(rank, world, backend, port, path, out_q):
         out_q.put((rank, {"error": f"{e}\n{traceback.format_exc()}"}))
 
 
-def _run(world, backend, path):
+def _run(world, backend, path, regroup=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, backend, port, path, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, backend, port, path, q, regroup)) for r in range(world)]
     for p in ps:
         p.start()
     out = dict(q.get(timeout=300) for _ in ps)
@@ -91,6 +105,18 @@ def test_rccl_world1_leader_path(r50):
     r = out[0]
     assert r["bcast"] > 20e6                       # ResNet-50's packed bf16 program weights went through RCCL
     np.testing.assert_allclose(r["probs"].sum(1), 1.0, atol=1e-4)
+
+
+def test_rccl_regroup_after_restart_world1(r50):
+    """Single-device stand-in for the post-restart regroup (RCCL refuses two
+    ranks on one GPU): after the generation bump the next load runs through a
+    freshly formed standalone ProcessGroupNCCL -- the device-side broadcast
+    call a live replica and its replacement make on a real 8-GPU node."""
+    out = _run(1, "nccl", r50, regroup=True)
+    r = out[0]
+    assert r["gen"] == 1 and r["regroups"] >= 1 and r["pg"] == "ProcessGroupNCCL"
+    assert r["bcast2"] > 20e6                     # version 2's weights went through the generation-1 group
+    np.testing.assert_array_equal(r["probs"], r["probs2"])
 
 
 def test_follower_binds_leader_blob_without_host_copies(r50):
