@@ -84,10 +84,15 @@ def parse():
     ap.add_argument("--batch-timeout-us", type=int, default=2000)
     ap.add_argument("--distinct-requests", type=int, default=64, help="distinct pre-encoded request bodies")
     ap.add_argument("--lanes", type=int, default=4, help="GPU lanes (batch slots in flight) per rank")
-    ap.add_argument("--model", default="resnet50", choices=["resnet50", "resnet50-v2", "tiny", "bert-base"],
+    ap.add_argument("--model", default="resnet50",
+                    choices=["resnet50", "resnet50-v2", "tiny", "bert-base", "multi"],
                     help="resnet50 = headline config (v1.5); resnet50-v2 = the pre-activation ResNet the reference "
                          "serves (serving/fetch.sh:7); bert-base = BASELINE config 3 (seq 128); "
-                         "tiny = same 224x224x3 payload, negligible compute (transport ceiling probe)")
+                         "tiny = same 224x224x3 payload, negligible compute (transport ceiling probe); "
+                         "multi = BASELINE config 5: ResNet-50 + BERT-base co-resident, BERT dropped and "
+                         "re-added by HandleReloadConfigRequest under ResNet load (scripts/bench_multi.py)")
+    ap.add_argument("--reload-cycles", type=int, default=3, help="--model multi: BERT drop/re-add cycles")
+    ap.add_argument("--bert-requests", type=int, default=2000, help="--model multi: BERT calls per phase")
     ap.add_argument("--seq-len", type=int, default=128)
     ap.add_argument("--c1-requests", type=int, default=200,
                     help="after the timed window: batch-1 round trips at concurrency 1 over one connection "
@@ -193,6 +198,14 @@ def main():
         else:
             dist.init_process_group(backend)
     logging.basicConfig(level=logging.WARNING)
+    if args.model == "multi":
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import bench_multi
+        bench_multi.run(args, rank, world, device, on_gpu, dist, topology, placement, pinned)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     from rust_tensorflow_serving2_amd import _C, native
     from rust_tensorflow_serving2_amd.models import resnet

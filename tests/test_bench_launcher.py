@@ -135,3 +135,24 @@ def test_topology_visible_devices_and_rehearsal(tmp_path, monkeypatch):
 def test_cpulist_roundtrip():
     assert topology.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
     assert topology.compress([0, 1, 2, 3, 8, 10, 11]) == "0-3,8,10-11"
+
+
+@pytest.mark.timeout(300)
+def test_bench_multi_model_reload_cpu(tmp_path):
+    """--model multi (BASELINE config 5) in CPU mode: ResNet traffic keeps
+    flowing with zero errors while BERT is dropped and re-added by
+    HandleReloadConfigRequest; reload-to-AVAILABLE times are reported."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["TMPDIR"] = str(tmp_path)
+    cmd = [sys.executable, BENCH, "--model", "multi", "--device", "cpu", "--image-size", "32", "--seq-len", "16",
+           "--batch", "8", "--reload-cycles", "2", "--bert-requests", "32", "--prewarm-s", "0.2",
+           "--io-threads", "2", "--client-threads", "1", "--connections", "2", "--lanes", "2", "--concurrency", "16"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = _json_line(p.stdout)
+    assert out["errors"] == 0 and out["value"] > 0 and out["bert_rps"] > 0
+    assert len(out["reload_to_available_s"]) == 2 and all(t > 0 for t in out["reload_to_available_s"])
+    r0 = out["per_rank"][0]
+    assert r0["resnet_calls_during_reload"] > 0          # ResNet served while BERT reloaded
+    # after the drop BERT was gone or on its way out (UNLOADING 40 / END 50), never AVAILABLE (30)
+    assert all(30 not in c["bert_states_after_drop"] for c in r0["cycles"])
