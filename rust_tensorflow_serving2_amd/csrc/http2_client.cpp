@@ -44,6 +44,12 @@ struct Shared {
   std::atomic<bool> continuous{false};
   std::atomic<bool> stopping{false};
   Clock::time_point deadline;
+  // a window() waiting for completion number `target`: the worker that
+  // completes it wakes the waiter (no polling thread burning a core of the
+  // CPU share the server and the generator run in)
+  std::atomic<uint64_t> target{~uint64_t(0)};
+  std::mutex wmu;
+  std::condition_variable wcv;
 };
 
 // One completion in continuous mode: (sequence number, latency, ok)
@@ -166,8 +172,16 @@ int on_close(nghttp2_session* s, int32_t sid, uint32_t err, void* ud) {
   *c->bytes_recv += r->bytes;
   const bool good = err == 0 && r->http_status == 200 && r->grpc_status == 0;
   if (c->sh->continuous.load(std::memory_order_relaxed)) {
-    std::lock_guard<std::mutex> g(*c->done_mu);
-    c->done->push_back(Done{c->sh->finished.fetch_add(1), us, good});
+    uint64_t seq;
+    {
+      std::lock_guard<std::mutex> g(*c->done_mu);
+      seq = c->sh->finished.fetch_add(1);
+      c->done->push_back(Done{seq, us, good});
+    }
+    if (seq + 1 == c->sh->target.load(std::memory_order_acquire)) {
+      std::lock_guard<std::mutex> g(c->sh->wmu);
+      c->sh->wcv.notify_all();
+    }
   }
   if (good) {
     (*c->ok)++;
@@ -529,7 +543,12 @@ LoadGenResult LoadGen::window(uint64_t n, double timeout_s) {
                   w->done.end());
   }
   // the window ends at the completion with sequence number s0 + n - 1
+  sh->target.store(s0 + n, std::memory_order_release);
   for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(sh->wmu);
+      sh->wcv.wait_for(lk, std::chrono::milliseconds(2), [&] { return sh->finished.load() >= s0 + n; });
+    }
     if (sh->finished.load() >= s0 + n) break;
     if (Clock::now() > deadline) {
       res.first_error = "load generator window timed out";
@@ -543,8 +562,8 @@ LoadGenResult LoadGen::window(uint64_t n, double timeout_s) {
       res.first_error = "every connection was lost";
       break;
     }
-    std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
+  sh->target.store(~uint64_t(0), std::memory_order_release);
   res.elapsed_s = std::chrono::duration<double>(Clock::now() - t0).count();
   for (auto& w : workers_) {
     std::lock_guard<std::mutex> g(w->done_mu);

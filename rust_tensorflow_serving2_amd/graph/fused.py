@@ -309,20 +309,67 @@ class FusedMatMul:
             return [y if self.out_f32 or not x.is_cuda else y.to(BF16)]
         from ..ops import ACT, hip, tuned_config
         H = hip()
-        x = _to_bf16(x).contiguous()
+        x = _to_bf16(x)
+        if not (x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0 and res is None):
+            # (a row-strided 2-D view -- BERT's pooler reading each sequence's
+            # first token out of [B, S, H] -- is read in place: no copy kernel)
+            x = x.contiguous()
         if res is not None:
             res = _to_bf16(res).contiguous()
-        M = x.numel() // self.k
+        M = x.shape[0] if x.dim() == 2 else x.numel() // self.k
         padded = self.np != self.n and res is None and x.dim() == 2
         n = self.np if padded else self.n
         w, b = (self.w, self.b) if padded or self.np == self.n else (self.w[:self.n], self.b[:self.n])
         shape = list(x.shape[:-1]) + [n]
         out = torch.empty(shape, device=x.device, dtype=torch.float32 if self.out_f32 else BF16)
-        key = ("mm", M, n, self.k, res is not None, self.out_f32, self.act)
+        key = ("mm", M, n, self.k, res is not None, self.out_f32, self.act) + \
+            ((x.stride(0),) if not x.is_contiguous() else ())
         run = lambda c, s: H.linear(x, w, b, res, ACT[self.act], c, self.out_f32, 1.0, out, s)  # noqa
         cfg, splits = tuned_config(key, M, n, run, self.k, True, self.k % 64 == 0)
         y = run(cfg, splits)
         return [y[:, :self.n] if padded else y]
+
+
+class DenseSoftmax:
+    """softmax(x @ W + b) over a few classes (BERT's classifier: 2 labels):
+    one kernel (misc.hip dense_softmax_kernel) from the fp32 pooled rows,
+    instead of cast + a GEMM launch with mostly empty tiles + torch softmax."""
+    children = ("mm",)          # placement.weight_refs: the classifier weights live in mm
+
+    def __init__(self, mm: "FusedMatMul"):
+        self.mm = mm
+
+    def __call__(self, ctx, node, ins):
+        x = O.to_torch(ins[0])
+        mm = self.mm
+        if mm.use_hip and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.is_contiguous() and \
+                mm.k % 4 == 0:
+            from ..ops import hip
+            return [hip().dense_softmax(x, mm.w, mm.b, mm.n)]
+        y = mm(ctx, node, [x])[0]
+        return [torch.softmax(y.float(), dim=-1)]
+
+
+def fuse_dense_softmax(g, order, fed, fetch_refs, device, opts):
+    """Softmax(_FusedMatMul(x)) with <= 16 classes, no activation / residual and
+    the logits used by nothing else -> _DenseSoftmax(x)."""
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    for name in order:
+        sm = g.nodes.get(name)
+        if sm is None or sm.op != "Softmax" or len(sm.inputs) != 1:
+            continue
+        mm = g.nodes.get(sm.inputs[0][0])
+        if mm is None or mm.op != "_FusedMatMul" or sm.inputs[0][1] != 0 or len(mm.inputs) != 1:
+            continue
+        impl = mm.attrs.get("_impl")
+        if impl is None or impl.n > 16 or impl.act != "none" or c.only_consumer(mm.name) is not sm:
+            continue
+        sm.op = "_DenseSoftmax"
+        sm.inputs = [mm.inputs[0]]
+        sm.ctrl = _merge_ctrl([mm, sm])
+        sm.attrs = {"_impl": DenseSoftmax(impl)}
+        del g.nodes[mm.name]
+        c.refresh()
 
 
 def _with_post(impl, y: torch.Tensor) -> list:
@@ -363,7 +410,7 @@ def _impl_op(ctx, node, ins):
 
 
 for _op in ("_FusedConv2D", "_FusedDualConv", "_FusedMatMul", "_GlobalAvgPool", "_MaxPool", "_SoftmaxArgMax", "_LayerNorm",
-            "_FusedQKV", "_Attention", "_EmbeddingLN", "_KeyMaskAdder"):
+            "_FusedQKV", "_Attention", "_EmbeddingLN", "_KeyMaskAdder", "_DenseSoftmax"):
     O.OPS[_op] = _impl_op
 
 
@@ -906,4 +953,5 @@ def fuse_post_activation(g, order, fed, fetch_refs, device, opts):
 def default_passes(options=None):
     from .patterns import bert_passes
     return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_dual_conv, fuse_post_activation,
-                                                                 fuse_stem_pool, fuse_matmul, fuse_classifier_head]
+                                                                 fuse_stem_pool, fuse_matmul, fuse_classifier_head,
+                                                                 fuse_dense_softmax]

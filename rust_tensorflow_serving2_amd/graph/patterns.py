@@ -571,6 +571,9 @@ class KeyMaskAdderOp:
         x = O.to_torch(ins[0])
         if x.dim() != 3 or x.shape[1] != 1:
             raise O.Unsupported("key mask must be [B, 1, S]")
+        if x.is_cuda and x.dtype in (torch.int32, torch.float32):
+            from ..ops import hip
+            return [hip().key_mask_adder(x.contiguous(), self.one, self.scale).unsqueeze(1)]   # one launch
         return [(x.float() * -self.scale).add_(self.one * self.scale).unsqueeze(1)]
 
 

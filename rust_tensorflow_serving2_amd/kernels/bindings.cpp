@@ -243,11 +243,21 @@ Tensor conv2d_dual(const Tensor& h, const Tensor& x, const Tensor& w, const c10:
 Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
               const c10::optional<Tensor>& residual, int64_t act, int64_t cfg, bool out_f32, double alpha,
               const c10::optional<Tensor>& out, int64_t splits) {
-  need(x, at::kBFloat16, "x");
+  // x: contiguous, or a row-strided 2-D view (x[r][k] at r * lda + k; e.g.
+  // BERT's pooler reads every sequence's first token straight from [B, S, H])
+  const bool strided = !x.is_contiguous();
+  if (strided) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 &&
+                    x.stride(0) >= x.size(1) && x.stride(0) % 8 == 0,
+                "x must be contiguous or a row-strided 2-D bf16 view");
+  } else {
+    need(x, at::kBFloat16, "x");
+  }
   need(w, at::kBFloat16, "w");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int K = x.size(-1);
   const int M = x.numel() / K;
+  const int lda = strided ? int(x.stride(0)) : K;
   const int N = w.size(0), ldb = w.size(1);
   TORCH_CHECK(ldb >= K && K % 8 == 0 && ldb % 8 == 0, "linear: K must be a multiple of 8 and fit in w");
   auto sizes = x.sizes().vec();
@@ -257,10 +267,10 @@ Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   TORCH_CHECK(y.numel() == int64_t(M) * N, "out has the wrong size");
   tfsk::IGemmArgs a{};
   a.a = x.data_ptr(); a.b = bf16p(w);
-  a.a_bytes = x.numel() * 2;
+  a.a_bytes = M > 0 ? (int64_t(M - 1) * lda + K) * 2 : 0;
   a.b_bytes = w.numel() * 2;
   TORCH_CHECK(a.a_bytes < 0x7ffffff0LL && a.b_bytes < 0x7ffffff0LL, "linear operands must be < 2 GiB");
-  a.M = M; a.N = N; a.K = K; a.lda = K; a.ldb = ldb;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb;
   if (bias.has_value()) {
     need(*bias, at::kFloat, "bias");
     TORCH_CHECK(bias->numel() == N, "bias size");
@@ -275,6 +285,37 @@ Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   a.act = act; a.out = y.data_ptr(); a.ldc = N; a.out_f32 = out_f32; a.alpha = float(alpha);
   run_igemm(a, tfsk::kADense, cfg, splits, x, cur_stream(x));
   return y;
+}
+
+Tensor dense_softmax(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, int64_t n) {
+  need(x, at::kFloat, "x");
+  need(w, at::kBFloat16, "w");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) >= x.size(1) && w.size(0) >= n && n >= 1 && n <= 16,
+              "dense_softmax: x [B, K] f32, w [>= n, >= K] bf16, 1 <= n <= 16");
+  TORCH_CHECK(x.size(1) % 4 == 0 && w.size(1) % 4 == 0, "dense_softmax: K % 4 == 0");
+  const float* b = nullptr;
+  if (bias.has_value()) {
+    need(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() >= n, "bias size");
+    b = bias->data_ptr<float>();
+  }
+  Tensor probs = torch::empty({x.size(0), n}, x.options());
+  TORCH_CHECK(tfsk::dense_softmax_launch(x.data_ptr<float>(), int(x.size(1)), bf16p(w), int(w.size(1)), b,
+                                         probs.data_ptr<float>(), int(x.size(0)), int(n), int(x.size(1)),
+                                         cur_stream(x)) == hipSuccess, "dense_softmax launch failed");
+  return probs;
+}
+
+Tensor key_mask_adder(const Tensor& m, double one, double scale) {
+  TORCH_CHECK(m.is_cuda() && m.is_contiguous() && (m.scalar_type() == at::kInt || m.scalar_type() == at::kFloat),
+              "key mask must be a contiguous int32 / f32 GPU tensor");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(m.device());
+  Tensor out = torch::empty(m.sizes(), m.options().dtype(at::kFloat));
+  TORCH_CHECK(tfsk::key_mask_adder_launch(m.data_ptr(), m.scalar_type() == at::kInt, float(one), float(scale),
+                                          out.data_ptr<float>(), m.numel(), cur_stream(m)) == hipSuccess,
+              "key_mask_adder launch failed");
+  return out;
 }
 
 Tensor maxpool(const Tensor& x, int64_t KH, int64_t KW, int64_t SH, int64_t SW, int64_t PT, int64_t PB,
@@ -587,6 +628,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w"), py::arg("bias"), py::arg("n"));
   m.def("softmax_argmax", &softmax_argmax, py::arg("logits"), py::arg("want_probs") = true,
         py::arg("want_classes") = true, py::arg("probs_out") = py::none(), py::arg("classes_out") = py::none());
+  m.def("dense_softmax", &dense_softmax, "softmax(x @ w[:n]^T + bias[:n]) for n <= 16 labels (x f32)",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("n"));
+  m.def("key_mask_adder", &key_mask_adder, "(one - m) * scale as f32", py::arg("m"), py::arg("one"),
+        py::arg("scale"));
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("out") = py::none());
   m.def("ingest_c4", &ingest_c4, "fp32 NHWC (C<=4) -> bf16 NHWC C=4", py::arg("x"), py::arg("out") = py::none());
   m.def("ingest_c4_padded", &ingest_c4_padded, "fp32 NHWC (C<=4) -> zero-bordered bf16 RGBA [N][Hp][Wp][4]",

@@ -121,6 +121,12 @@ hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const fl
                                   float* probs, int64_t* classes, int M, int HW, int K, int Np, int N,
                                   hipStream_t s);
 size_t classifier_head_ws_floats(int M, int K, int Np);
+// BERT head: probs[r] = softmax(x[r] @ w^T + bias) over N <= 16 labels (x fp32)
+hipError_t dense_softmax_launch(const float* x, int ldx, const uint16_t* w, int ldw, const float* bias,
+                                float* probs, int rows, int N, int K, hipStream_t s);
+// (one - m) * scale over a key mask (int32 when is_int, else f32) -> f32
+hipError_t key_mask_adder_launch(const void* m, int is_int, float one, float scale, float* out, int64_t n,
+                                 hipStream_t s);
 hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, int64_t* classes,
                                  int rows, int cols, long ld, hipStream_t stream);
 // fp32 -> bf16 cast (vectorized).

@@ -376,6 +376,69 @@ __global__ void cast_bf16_f32_kernel(const uint16_t* __restrict__ x, float* __re
     y[i] = bf16_to_f32(x[i]);
 }
 
+// ---------------------------------------------------------------- BERT head
+// Classifier + softmax over a few labels (BERT's num_labels = 2): one
+// workgroup per row; each thread accumulates its k-slice of every label's dot
+// product from the fp32 pooled row (vectorised float4 / 4-bf16 loads), a
+// wave-shuffle + LDS reduction combines them, one lane applies the softmax.
+// Replaces cast + a mostly-empty GEMM tile + torch's softmax (3 launches).
+constexpr int kDsMaxN = 16;
+
+__global__ __launch_bounds__(256) void dense_softmax_kernel(const float* __restrict__ x, int ldx,
+                                                            const uint16_t* __restrict__ w, int ldw,
+                                                            const float* __restrict__ bias, float* __restrict__ probs,
+                                                            int N, int K) {
+  __shared__ float red[4][kDsMaxN];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* xr = x + size_t(row) * ldx;
+  float acc[kDsMaxN];
+#pragma unroll
+  for (int n = 0; n < kDsMaxN; ++n) acc[n] = 0.f;
+  for (int k = tid * 4; k < K; k += 256 * 4) {        // K % 4 == 0 (host check)
+    const float4 xv = *reinterpret_cast<const float4*>(xr + k);
+#pragma unroll
+    for (int n = 0; n < kDsMaxN; ++n) {
+      if (n < N) {
+        const uint2 wv4 = *reinterpret_cast<const uint2*>(w + size_t(n) * ldw + k);
+        acc[n] += xv.x * bf16_to_f32(uint16_t(wv4.x & 0xffff)) + xv.y * bf16_to_f32(uint16_t(wv4.x >> 16)) +
+                  xv.z * bf16_to_f32(uint16_t(wv4.y & 0xffff)) + xv.w * bf16_to_f32(uint16_t(wv4.y >> 16));
+      }
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < kDsMaxN; ++n) {
+    float v = acc[n];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[wv][n] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float logit[kDsMaxN], mx = -INFINITY;
+    for (int n = 0; n < N; ++n) {
+      logit[n] = red[0][n] + red[1][n] + red[2][n] + red[3][n] + (bias ? bias[n] : 0.f);
+      mx = fmaxf(mx, logit[n]);
+    }
+    float sum = 0.f;
+    for (int n = 0; n < N; ++n) {
+      logit[n] = __expf(logit[n] - mx);
+      sum += logit[n];
+    }
+    const float inv = 1.f / sum;
+    for (int n = 0; n < N; ++n) probs[size_t(row) * N + n] = logit[n] * inv;
+  }
+}
+
+// BERT attention adder from a key mask X [B, 1, S] (int32 or f32):
+// (one - X) * scale, one launch instead of cast + mul + add.
+__global__ void key_mask_adder_kernel(const void* __restrict__ m, int is_int, float one, float scale,
+                                      float* __restrict__ out, long n) {
+  for (long i = blockIdx.x * long(blockDim.x) + threadIdx.x; i < n; i += long(gridDim.x) * blockDim.x) {
+    const float v = is_int ? float(static_cast<const int*>(m)[i]) : static_cast<const float*>(m)[i];
+    out[i] = (one - v) * scale;
+  }
+}
+
 // ---------------------------------------------------------------- LayerNorm
 // One wave per row, y = LN(x + r). Rows up to 64 * 8 * kLnChunks columns are
 // read once into registers (16-B loads), statistics are two-pass from the
@@ -777,6 +840,22 @@ hipError_t ingest_c4_pad_launch(const float* x, uint16_t* y, int N, int H, int W
   const dim3 grid(unsigned((Wp + 255) / 256), unsigned(rows < 65535 ? rows : 65535));
   hipLaunchKernelGGL(ingest_c4_pad_kernel, grid, dim3(256), 0, s, x, reinterpret_cast<uint2*>(y), N, H, W, C, Hp,
                      Wp, pt, pl);
+  return hipGetLastError();
+}
+
+hipError_t dense_softmax_launch(const float* x, int ldx, const uint16_t* w, int ldw, const float* bias,
+                                float* probs, int rows, int N, int K, hipStream_t s) {
+  if (N < 1 || N > kDsMaxN || K % 4 || ldx % 4 || ldw % 4) return hipErrorInvalidValue;
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(dense_softmax_kernel, dim3(rows), dim3(256), 0, s, x, ldx, w, ldw, bias, probs, N, K);
+  return hipGetLastError();
+}
+
+hipError_t key_mask_adder_launch(const void* m, int is_int, float one, float scale, float* out, int64_t n,
+                                 hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(key_mask_adder_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, m, is_int, one, scale, out,
+                     long(n));
   return hipGetLastError();
 }
 

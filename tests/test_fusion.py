@@ -105,7 +105,9 @@ def test_bert_fusion_exact(tiny_bert):
     # embedding gathers + adds + LN -> one op; the [B,S,S] mask adder chain -> one [B,1,1,S] op
     assert hist["_EmbeddingLN"] == 1 and hist["_KeyMaskAdder"] == 1
     assert "GatherV2" not in hist and "ExpandDims" not in hist and "Cast" not in hist
-    assert hist["_FusedMatMul"] == 8 and "MatMul" not in hist and "BatchMatMulV2" not in hist
+    # (the 2-label classifier + softmax is one _DenseSoftmax op)
+    assert hist["_FusedMatMul"] == 7 and hist["_DenseSoftmax"] == 1 and "Softmax" not in hist
+    assert "MatMul" not in hist and "BatchMatMulV2" not in hist
     assert "Rsqrt" not in hist and "Pow" not in hist and "Tanh" not in hist
 
 

@@ -649,3 +649,37 @@ def test_stem_pool_fused_kernel(n, h, w, c, cout, cp, pp, act, post):
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
     # most outputs agree exactly: only bf16 rounding ties of the conv values can differ
     assert (err == 0).float().mean().item() > 0.9
+
+
+@pytest.mark.parametrize("cfg", [3, 36, 42])
+def test_linear_row_strided_input(cfg):
+    """BERT's pooler: rows are every sequence's first token of [B, S, H],
+    read in place (lda = S * H) -- no gather copy."""
+    B, S, H = 32, 16, 768
+    seq = rnd(B, S, H, seed=21).to(BF).to(DEV)
+    x = seq[:, 0, :]                                   # [B, H], stride (S*H, 1)
+    assert not x.is_contiguous()
+    w = rnd(H, H, scale=1 / math.sqrt(H), seed=22).to(BF)
+    b = rnd(H, scale=0.1, seed=23)
+    y = hip().linear(x, w.to(DEV), b.to(DEV), None, ACT["tanh"], cfg, True)
+    ref = torch.tanh(seq[:, 0, :].float().cpu() @ w.float().t() + b)
+    assert (y.cpu() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("b,n,k", [(32, 2, 768), (5, 3, 1024), (1, 16, 64)])
+def test_dense_softmax_matches_fp32(b, n, k):
+    x = rnd(b, k, seed=31).to(DEV)
+    w = rnd(n + 3, k, scale=1 / math.sqrt(k), seed=32).to(BF)          # padded rows are ignored
+    bias = rnd(n + 3, scale=0.5, seed=33)
+    p = hip().dense_softmax(x, w.to(DEV), bias.to(DEV), n)
+    ref = torch.softmax(x.cpu() @ w[:n].float().t() + bias[:n], -1)
+    assert p.shape == (b, n)
+    assert (p.cpu() - ref).abs().max().item() < 1e-5
+
+
+def test_key_mask_adder_matches_fp32():
+    m = torch.randint(0, 2, (7, 1, 33), dtype=torch.int32)
+    out = hip().key_mask_adder(m.to(DEV), 1.0, -10000.0)
+    torch.testing.assert_close(out.cpu(), (1.0 - m.float()) * -10000.0)
+    mf = torch.rand(3, 1, 9)
+    torch.testing.assert_close(hip().key_mask_adder(mf.to(DEV), 1.0, 2.5).cpu(), (1.0 - mf) * 2.5)
