@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <pthread.h>
+#include <sys/prctl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -222,6 +223,7 @@ class NativeLane {
       rx.push("tfs.issue");   // H2D + graph launch + D2H enqueued on the lane stream
     }
     int e = 0;
+    const auto t_issue = Clock::now();
     if (eager_) {
       // every row was already queued on the copy stream as it arrived
       e = rt.event_record(copied_, copy_stream_);
@@ -244,26 +246,38 @@ class NativeLane {
       rx.pop();
       rx.push("tfs.gpu_wait");
     }
-    if (!e) e = wait(rt, done, deadline_from(Clock::now()));
+    const size_t bi = size_t(b - buckets_.data());
+    if (!e) e = wait(rt, done, t_issue, deadline_from(Clock::now()), ema_us_[bi]);
+    if (!e) {
+      const double us = std::chrono::duration<double, std::micro>(Clock::now() - t_issue).count();
+      ema_us_[bi] = ema_us_[bi] <= 0 ? us : 0.8 * ema_us_[bi] + 0.2 * us;
+    }
     if (rx.on()) {
       rx.pop();
       rx.pop();
     }
     return e;
   }
-  // Poll the batch's completion event: a short yield phase, then 40 us naps.
-  // (hipEventSynchronize busy-waits a core per lane for the whole ~1 ms batch;
-  // the IO threads need those cores.)  Gives up after `deadline` (a hung
-  // kernel or wedged stream): returns kLaneHung.
-  static int wait(HipRt& rt, void* ev, Clock::time_point deadline) {
+  // Wait for the batch's completion event without burning a core (a
+  // hipEventSynchronize spin would take one per lane from the IO threads):
+  // ONE nap for most of this bucket's expected issue->done time (a running
+  // average), then polls every ~8 us.  The lane thread runs with 1-us timer
+  // slack, so a nap ends when asked (the default 50-us slack made each 40-us
+  // nap ~90 us, which a batch-1 request paid in full).  Gives up after
+  // `deadline` (a hung kernel or wedged stream): returns kLaneHung.
+  static int wait(HipRt& rt, void* ev, Clock::time_point t_issue, Clock::time_point deadline, double expect_us) {
+    if (expect_us > 60.0) {
+      const auto wake = t_issue + std::chrono::microseconds(int64_t(0.75 * expect_us));
+      if (Clock::now() < wake && rt.event_query(ev) == kHipErrorNotReady) std::this_thread::sleep_until(wake);
+    }
     for (int i = 0;; ++i) {
       const int e = rt.event_query(ev);
       if (e != kHipErrorNotReady) return e;
-      if (i < 16) {
+      if (i < 8) {
         std::this_thread::yield();
       } else {
         if ((i & 63) == 0 && Clock::now() > deadline) return kLaneHung;
-        std::this_thread::sleep_for(std::chrono::microseconds(40));
+        std::this_thread::sleep_for(std::chrono::microseconds(8));
       }
     }
   }
@@ -286,6 +300,8 @@ class NativeLane {
   }
   void run() {
     pthread_setname_np(pthread_self(), "tfs-nlane");
+    prctl(PR_SET_TIMERSLACK, 1000UL);     // 1-us timer slack for the completion naps (wait())
+    ema_us_.assign(buckets_.size(), 0.0);
     HipRt& rt = hip_rt();
     rt.set_device(device_);
     void* done = nullptr;
@@ -371,6 +387,7 @@ class NativeLane {
   int fault_hang_ = -1;
   int timeout_floor_ms_ = 10000;
   double mean_ms_ = 0.0;
+  std::vector<double> ema_us_;     // per bucket: running issue -> done time (wait()'s first nap)
   uint64_t seen_ = 0;
   std::thread th_;
 };

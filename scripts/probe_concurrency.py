@@ -61,6 +61,43 @@ def main():
             torch.cuda.synchronize()
             best = min(best, (time.perf_counter() - t) * 1e3 / (args.iters * k))
         res[f"ms_per_batch_k{k}"] = round(best, 4)
+    # the serving lane's full GPU-side cycle: H2D of the live rows (SDMA),
+    # graph replay, D2H of the outputs -- k lanes at once
+    for k in range(1, len(lanes) + 1):
+        sel = lanes[:k]
+        def cycle(l):
+            with torch.cuda.stream(l.stream):
+                for h, d in zip(l.host_in, l.static_in[b]):
+                    d[:b].copy_(h[:b], non_blocking=True)
+                l.graphs[b].replay()
+                for so, ho in zip(l.static_out[b], l.host_out):
+                    ho[:b].copy_(so[:b], non_blocking=True)
+        for l in sel:
+            cycle(l)
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(3):
+            t = time.perf_counter()
+            for _ in range(args.iters):
+                for l in sel:
+                    cycle(l)
+            torch.cuda.synchronize()
+            best = min(best, (time.perf_counter() - t) * 1e3 / (args.iters * k))
+        res[f"ms_per_batch_with_copies_k{k}"] = round(best, 4)
+    # H2D alone (SDMA): bytes of one batch's inputs per lane, k lanes at once
+    nbytes = sum(h[:b].numel() * h.element_size() for h in lanes[0].host_in)
+    for k in range(1, len(lanes) + 1):
+        sel = lanes[:k]
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.iters):
+            for l in sel:
+                with torch.cuda.stream(l.stream):
+                    for h, d in zip(l.host_in, l.static_in[b]):
+                        d[:b].copy_(h[:b], non_blocking=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        res[f"h2d_GBps_k{k}"] = round(nbytes * args.iters * k / dt / 1e9, 2)
     picks = {}
     for key, v in ops.tuned_table().items():
         picks[repr(key)[:90]] = list(v)
