@@ -327,7 +327,7 @@ def main():
     if world > 1:
         dist.barrier()
     dev_sync()
-    cpu0, io0, ru0 = topology.thread_cpu(), io_stats(), os.times()
+    cpu0, io0, ru0, tid0 = topology.thread_cpu(), io_stats(), os.times(), topology.thread_cpu_by_tid()
     t0 = time.perf_counter()
     r = loadgen.window(args.steps * per_step, 600.0)
     dev_sync()
@@ -335,6 +335,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     cpu_report = diag(cpu0, topology.thread_cpu(), io0, io_stats(), ru0, os.times(), elapsed)
+    cpu_report["top_threads"] = topology.top_threads(tid0, topology.thread_cpu_by_tid(), elapsed)
     gpu_busy = busy.stop()
     loadgen.stop(30.0)
     check(r, "timed window")

@@ -61,6 +61,56 @@ _REC = threading.local()
 _REMOTE: Dict[str, Tuple[int, int]] = {}
 
 
+def _table_schema() -> str:
+    """Identity of the tile-config tables a cached pick refers to."""
+    import hashlib
+    return hashlib.sha1(repr(sorted(TILES.items())).encode()).hexdigest()[:12]
+
+
+TUNED_CACHE = os.environ.get("TFSERVE_TUNED_CACHE",
+                             os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_mi355x.json"))
+
+
+def load_tuned_cache(path: Optional[str] = None) -> int:
+    """Install tile picks measured earlier on this GPU model (a committed
+    table, like a library's performance database): keys found there are
+    neither autotuned nor graph-tuned at capture.  The table is keyed by the
+    exact launch shape and only used when its config-table schema and device
+    (gfx arch, CU count) match this process.  Returns the entries installed."""
+    import json
+    path = path or TUNED_CACHE
+    if not path or path == "0" or not os.path.exists(path):
+        return 0
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return 0
+    if doc.get("schema") != _table_schema():
+        return 0
+    if torch.cuda.is_available():
+        p = torch.cuda.get_device_properties(torch.cuda.current_device())
+        if doc.get("arch") != getattr(p, "gcnArchName", "").split(":")[0] or \
+                int(doc.get("cus", -1)) != p.multi_processor_count:
+            return 0
+    install_remote_tuned(doc.get("picks", {}))
+    return len(doc.get("picks", {}))
+
+
+def save_tuned_cache(path: str, keys=None) -> int:
+    """Write the current picks (all, or ``keys``) in load_tuned_cache's format."""
+    import json
+    p = torch.cuda.get_device_properties(torch.cuda.current_device())
+    with _TUNE_LOCK:
+        picks = {repr(k): list(v) for k, v in _TUNED.items() if keys is None or k in keys}
+    doc = {"schema": _table_schema(), "arch": getattr(p, "gcnArchName", "").split(":")[0],
+           "cus": p.multi_processor_count, "picks": picks}
+    with open(path + ".tmp", "w") as f:
+        json.dump(doc, f, indent=0, sort_keys=True)
+    os.replace(path + ".tmp", path)
+    return len(picks)
+
+
 def install_remote_tuned(table: Dict[str, list]) -> None:
     with _TUNE_LOCK:
         for k, v in table.items():
@@ -159,6 +209,19 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
     return out
 
 
+_CACHE_STATE = {"loaded": False, "entries": 0}
+_CACHE_LOCK = threading.Lock()
+
+
+def _ensure_cache() -> None:
+    if not _CACHE_STATE["loaded"]:
+        with _CACHE_LOCK:
+            if not _CACHE_STATE["loaded"]:
+                _CACHE_STATE["loaded"] = True
+                if AUTOTUNE:
+                    _CACHE_STATE["entries"] = load_tuned_cache()
+
+
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
                  dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
                  halo: bool = False) -> Tuple[int, int]:
@@ -168,6 +231,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
     rec = getattr(_REC, "keys", None)
     if rec is not None:
         rec[key] = rec.get(key, 0) + 1
+    _ensure_cache()
     hit = _TUNED.get(key)
     if hit is not None:
         return hit

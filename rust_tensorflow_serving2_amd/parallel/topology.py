@@ -27,7 +27,7 @@ from __future__ import annotations
 import os
 import threading
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 
 @dataclass
@@ -290,6 +290,37 @@ def cpu_quota() -> Optional[float]:
         return int(q) / int(per or 100000)
     except ValueError:
         return None
+
+
+def thread_cpu_by_tid(pid: Optional[int] = None) -> Dict[int, Tuple[str, float]]:
+    """{tid: (thread name, CPU seconds)} (schedstat ns, like thread_cpu)."""
+    out: Dict[int, Tuple[str, float]] = {}
+    base = f"/proc/{pid or os.getpid()}/task"
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"{base}/{tid}/comm") as f:
+                name = f.read().strip()
+            with open(f"{base}/{tid}/schedstat") as f:
+                out[int(tid)] = (name, int(f.read().split()[0]) / 1e9)
+        except (OSError, ValueError, IndexError):
+            continue
+    return out
+
+
+def top_threads(before: Dict[int, Tuple[str, float]], after: Dict[int, Tuple[str, float]], elapsed: float,
+                n: int = 6) -> List[list]:
+    """The ``n`` busiest threads of a window: [name, tid, cores, is_main_thread]."""
+    rows = []
+    for tid, (name, v) in after.items():
+        d = v - before.get(tid, (name, 0.0))[1]
+        if d > 0:
+            rows.append([name, tid, round(d / max(elapsed, 1e-9), 2), tid == os.getpid()])
+    rows.sort(key=lambda r: -r[2])
+    return rows[:n]
 
 
 def thread_cpu(pid: Optional[int] = None) -> Dict[str, float]:

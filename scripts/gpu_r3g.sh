@@ -1,0 +1,15 @@
+#!/bin/bash
+# fabric traffic per ResNet-50 b32 forward (two PMC passes) + per-step kernel map + bench
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/r3g
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d /tmp/prof_f -o run -- python scripts/bench_engine.py --model resnet50 --batch 32 --iters 3 --graph-tune 0 > gpurun_out/r3g/pmc_f_run.log 2>&1 &&
+python scripts/pmc_summary.py /tmp/prof_f --replay stem > gpurun_out/r3g/pmc_fetch_r50_b32.txt 2>&1 &&
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE -d /tmp/prof_w -o run -- python scripts/bench_engine.py --model resnet50 --batch 32 --iters 3 --graph-tune 0 > gpurun_out/r3g/pmc_w_run.log 2>&1 &&
+python scripts/pmc_summary.py /tmp/prof_w --replay stem > gpurun_out/r3g/pmc_write_r50_b32.txt 2>&1 &&
+timeout -k 10 300 python scripts/prof_program_ops.py --model resnet50 --batch 32 > gpurun_out/r3g/ops_r50.log 2>&1 &&
+timeout -k 10 300 python scripts/prof_program_ops.py --model bert-base --batch 32 > gpurun_out/r3g/ops_bert.log 2>&1 &&
+timeout -k 10 300 python bench.py --gpus 1 --steps 300 --warmup 30 > gpurun_out/r3g/bench1.log 2>&1
+rc=$?
+rm -rf /tmp/prof_f /tmp/prof_w
+exit $rc

@@ -56,6 +56,22 @@ def main():
     if len(idx) < 2:
         raise SystemExit(f"need two dispatches of {a.replay!r}, found {len(idx)}")
     rep = rows[idx[-2]:idx[-1]]
+    sq = {"GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"}
+    extra = sorted({n for _k, d in rep for n in d} - sq)
+    if extra:
+        # memory counters: per dispatch, MB (FETCH_SIZE / WRITE_SIZE are KB in rocprofv3) and totals
+        print(f"{'#':>3} {'kernel':60s} {'kcycles':>9} " + " ".join(f"{n:>14}" for n in extra))
+        tot = defaultdict(float)
+        cyc_t = 0.0
+        for i, (k, d) in enumerate(rep):
+            cyc = d.get("GRBM_GUI_ACTIVE", 0.0) / 8
+            cyc_t += cyc
+            for n in extra:
+                tot[n] += d.get(n, 0.0)
+            print(f"{i:3d} {_short(k):60s} {cyc / 1e3:9.1f} " + " ".join(f"{d.get(n, 0.0):14.1f}" for n in extra))
+        print(f"replay: {len(rep)} dispatches, {cyc_t / 1e3:.1f} kcycles; totals: " +
+              ", ".join(f"{n}={tot[n]:.1f}" for n in extra))
+        return
     tot_busy = tot_cyc = 0.0
     print(f"{'#':>3} {'kernel':60s} {'kcycles':>9} {'mfma%':>6} {'wait%':>6} {'active%':>7}")
     for i, (k, d) in enumerate(rep):

@@ -22,12 +22,16 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--save-tuned", default="", help="write the tile picks (ops.save_tuned_cache format) here")
+    ap.add_argument("--buckets", type=int, nargs="*", default=None,
+                    help="capture these batch buckets too (all tuned; only --batch is timed)")
     args = ap.parse_args()
     from rust_tensorflow_serving2_amd import ops
     from rust_tensorflow_serving2_amd.models import bert, resnet
     from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
     path = os.path.join(tempfile.mkdtemp(), "1")
-    opts = ServableOptions(device="cuda:0", max_batch_size=args.batch, allowed_batch_sizes=(args.batch,),
+    opts = ServableOptions(device="cuda:0", max_batch_size=args.batch,
+                           allowed_batch_sizes=tuple(sorted(set(args.buckets or []) | {args.batch})),
                            lanes=args.lanes)
     if args.model == "bert-base":
         bert.export(path, seed=0)
@@ -102,6 +106,8 @@ def main():
     for key, v in ops.tuned_table().items():
         picks[repr(key)[:90]] = list(v)
     res["picks"] = picks
+    if args.save_tuned:
+        res["saved_tuned"] = ops.save_tuned_cache(args.save_tuned)
     print(json.dumps(res), flush=True)
 
 

@@ -146,3 +146,19 @@ def test_gelu_erf_form_matches():
     p1 = compile_program(from_graph_def(g.graph), ["x:0"], [out + ":0"], passes=default_passes())
     assert p1.op_histogram() == {"_FusedMatMul": 1}
     torch.testing.assert_close(p0.run([xs])[0], p1.run([xs])[0], atol=1e-5, rtol=1e-5)
+
+
+def test_tuned_cache_roundtrip(tmp_path, monkeypatch):
+    """A committed tile-pick table is installed only when its schema matches
+    (stale config ids are never launched)."""
+    import json
+    from rust_tensorflow_serving2_amd import ops
+    monkeypatch.setattr(ops, "_REMOTE", {})
+    p = tmp_path / "t.json"
+    key = ("mm", 32, 768, 768, False, True, "tanh")
+    p.write_text(json.dumps({"schema": ops._table_schema(), "arch": "gfx950", "cus": 256,
+                             "picks": {repr(key): [42, 1]}}))
+    assert ops.load_tuned_cache(str(p)) == 1 and ops._REMOTE[repr(key)] == (42, 1)
+    monkeypatch.setattr(ops, "_REMOTE", {})
+    p.write_text(json.dumps({"schema": "stale", "picks": {repr(key): [42, 1]}}))
+    assert ops.load_tuned_cache(str(p)) == 0 and not ops._REMOTE
