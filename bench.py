@@ -99,8 +99,9 @@ def parse():
                          "(reported as p50_c1_ms; 0 = skip)")
     ap.add_argument("--ref-client-requests", type=int, default=6000,
                     help="after the timed window: rank 0 drives this many Predicts over 2 HTTP/2 connections "
-                         "(the reference client's channel pattern, src/lib.rs:132-138) while every rank serves; "
-                         "reported as ref_client_rps + the share each GPU served (per-stream routing; 0 = skip)")
+                         "(the reference client's channel pattern, src/lib.rs:132-138) with min(concurrency, 128) "
+                         "x N calls in flight while every rank serves; reported as ref_client_rps + the share each "
+                         "GPU served (per-stream routing; 0 = skip)")
     ap.add_argument("--cpu-report", action="store_true",
                     help="(always on now; kept for old command lines) per-thread-group CPU of the windows")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -358,7 +359,9 @@ def main():
         if rank == 0:
             # two connections, each driven by its own thread (a tonic channel's
             # connection task runs on one runtime thread at a time)
-            lg2 = _C.LoadGen("127.0.0.1", server.port, PREDICT, bodies, min(conc, 128), 2, 2)
+            # enough calls in flight to feed every GPU's batch pipeline (the
+            # router keeps them on rank 0 until its own pipeline is full)
+            lg2 = _C.LoadGen("127.0.0.1", server.port, PREDICT, bodies, min(conc, 128) * world, 2, 2)
             lg2.run(max(64, args.ref_client_requests // 10), 120.0)
             s0 = served()
             rc0, rio0, rru0, rt0 = topology.thread_cpu(), io_stats(), os.times(), time.perf_counter()
@@ -379,7 +382,7 @@ def main():
         if ref is not None:
             tot = max(1.0, sum(share_v))
             ref = {"ref_client_rps": round(ref["ok"] / max(ref["elapsed_s"], 1e-9), 1),
-                   "ref_client_errors": ref["errors"],
+                   "ref_client_errors": ref["errors"], "ref_client_in_flight": min(conc, 128) * world,
                    "ref_client_gpu_share": [round(v / tot, 3) for v in share_v]}
 
     # latency mode: one client, one connection, one call in flight (the

@@ -255,6 +255,7 @@ void Router::stop() {
 int Router::pick(size_t msg_len) {
   if (msg_len > req_cap_ || world_ < 2) return -1;
   const int64_t mine = self_->hdr()->load.load(std::memory_order_relaxed);
+  if (mine < local_cap_.load(std::memory_order_relaxed)) return -1;
   int best = -1;
   int64_t best_load = mine - margin_;
   std::lock_guard<std::mutex> g(mu_);

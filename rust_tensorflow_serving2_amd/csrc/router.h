@@ -23,9 +23,12 @@
 //     larger than the cell's response area is sent back as "run it yourself"
 //     and the origin serves the call locally from the message still in the cell.
 //   * Load = calls a replica has accepted and not answered yet (an atomic in
-//     its header).  A call goes remote only when a live peer's load is lower
-//     than the local one by more than `margin`: balanced replicas (many
-//     connections, the benchmark) keep their own traffic.
+//     its header).  A call goes remote only when the local load has reached
+//     `local_cap` (the local GPU's batch pipeline is full: lanes x max batch)
+//     and a live peer's load is lower than the local one by more than
+//     `margin`: balanced replicas (many connections, the benchmark) keep their
+//     own traffic, and a client with fewer calls in flight than one GPU can
+//     batch is served at full batch size instead of in fragments on every GPU.
 //   * Liveness: the owner's pid and a heartbeat its router thread advances.
 //     A peer that dies leaves its calls: cells it had not taken yet are
 //     re-dispatched locally, taken ones are answered UNAVAILABLE (and their
@@ -77,6 +80,11 @@ class Router : public RemoteSink {
   std::atomic<int64_t>* load_word();
   void respond_remote(const Call& c, int status, const std::string& msg, const std::string& body) override;
   int rank() const { return rank_; }
+  // Keep calls local while this replica has fewer than `cap` outstanding: a
+  // GPU replica's batches fill (and its HIP graphs run at full batch size)
+  // before any call spills to a peer; 0 = route on load difference alone.
+  void set_local_cap(int64_t cap) { local_cap_.store(cap, std::memory_order_relaxed); }
+  int64_t local_cap() const { return local_cap_.load(std::memory_order_relaxed); }
   int peers_alive();
   std::vector<int64_t> loads();
   RouterStats stats;
@@ -110,6 +118,7 @@ class Router : public RemoteSink {
   std::vector<Tomb> tombs_;
   uint64_t next_token_ = 1;
   std::atomic<bool> running_{false};
+  std::atomic<int64_t> local_cap_{0};
   std::thread th_;
 };
 

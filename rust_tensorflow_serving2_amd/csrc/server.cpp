@@ -613,6 +613,9 @@ void register_server(py::module_& m) {
         s.router->start();
       }, py::arg("group"), py::arg("rank"), py::arg("world"), py::arg("ncells") = 64,
          py::arg("req_cap") = size_t(1) << 20, py::arg("resp_cap") = size_t(64) << 10, py::arg("margin") = 8)
+      .def("set_router_local_cap", [](PyServer& s, int64_t cap) {
+        if (s.router) s.router->set_local_cap(cap);
+      })
       .def("stop_router", [](PyServer& s) {
         py::gil_scoped_release nogil;
         if (s.router) s.router->stop();
@@ -625,6 +628,7 @@ void register_server(py::module_& m) {
         d["ingested"] = st.ingested.load(); d["returned"] = st.returned.load();
         d["reclaimed"] = st.reclaimed.load(); d["lost"] = st.lost.load(); d["no_cell"] = st.no_cell.load();
         d["rerun"] = st.rerun.load(); d["too_large"] = st.too_large.load(); d["tomb_freed"] = st.tomb_freed.load();
+        d["local_cap"] = s.router->local_cap();
         d["peers_alive"] = s.router->peers_alive();
         d["loads"] = s.router->loads();
         d["rank"] = s.router->rank();

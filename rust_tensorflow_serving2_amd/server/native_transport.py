@@ -90,6 +90,7 @@ class FastEndpoint:
                                   name=f"tfs-gpu-{servable.name}-{lane_idx}")
             th.start()
             self.workers.append(th)
+        transport.pipeline_rows(self.id, self.max_rows * len(lanes))
 
     def _work(self, lane_idx: int):
         _C.set_thread_name(f"tfs-lane{lane_idx}")
@@ -122,6 +123,7 @@ class FastEndpoint:
         try:
             if self.id >= 0:
                 self.t.srv.remove_endpoint(self.id)
+                self.t.pipeline_rows(self.id, None)
             for th in self.workers:
                 th.join(timeout=5)
         finally:
@@ -136,6 +138,9 @@ class NativeTransport:
         self.core = core
         self.srv = _C.Http2Server(host, port, io_threads, max_message)
         self.port = self.srv.port
+        self._router = router is not None
+        self._cap_lock = threading.Lock()
+        self._pipe_rows: dict = {}
         if router is not None:
             # (group, rank, world): per-stream routing over shared memory rings
             # (csrc/router.h); sizes from the environment for unusual models
@@ -326,6 +331,21 @@ class NativeTransport:
             self.core.manager.listeners.remove(self._on_state)
         except ValueError:
             pass
+
+    def pipeline_rows(self, ep_id: int, rows: Optional[int]) -> None:
+        """A fast endpoint's batch pipeline (lanes x max batch): the router keeps
+        calls local until that many are outstanding (TFSERVE_ROUTE_LOCAL_CAP
+        overrides; 0 = route on load difference alone)."""
+        if not self._router:
+            return
+        with self._cap_lock:
+            if rows is None:
+                self._pipe_rows.pop(ep_id, None)
+            else:
+                self._pipe_rows[ep_id] = rows
+            env = os.environ.get("TFSERVE_ROUTE_LOCAL_CAP")
+            cap = int(env) if env is not None else max(self._pipe_rows.values(), default=0)
+        self.srv.set_router_local_cap(cap)
 
     def prometheus_lines(self):
         """C++ front-end and fast-path counters in Prometheus text form."""

@@ -271,3 +271,30 @@ def test_oversized_answer_reruns_locally():
         a.close()
         b.close()
         _cleanup(g)
+
+
+def test_local_cap_keeps_calls_until_the_pipeline_is_full():
+    """Below the local cap (a GPU replica's lanes x max batch) every call stays
+    local -- batches fill instead of fragmenting over the GPUs; above it the
+    surplus spills to the least-loaded peer."""
+    g = _group()
+    reps = [Replica(f"R{i}", g, i, 2, delay=0.004) for i in range(2)]
+    try:
+        assert _wait_peers(reps, 1)
+        reps[0].srv.set_router_local_cap(64)
+        assert reps[0].srv.router_stats()["local_cap"] == 64
+        with grpc.insecure_channel(f"127.0.0.1:{reps[0].srv.port}") as ch:
+            stub = ch.unary_unary(PREDICT)
+            with cf.ThreadPoolExecutor(24) as ex:           # <= 24 in flight < cap: all local
+                got = [f.result()[:2] for f in [ex.submit(stub, b"x", timeout=30) for _ in range(200)]]
+        assert set(got) == {b"R0"} and reps[0].srv.router_stats()["forwarded"] == 0
+        reps[0].srv.set_router_local_cap(8)
+        with grpc.insecure_channel(f"127.0.0.1:{reps[0].srv.port}") as ch:
+            stub = ch.unary_unary(PREDICT)
+            with cf.ThreadPoolExecutor(48) as ex:           # well above the cap: the surplus spills
+                got = [f.result()[:2] for f in [ex.submit(stub, b"x", timeout=30) for _ in range(400)]]
+        assert got.count(b"R1") > 0 and reps[0].srv.router_stats()["forwarded"] == got.count(b"R1")
+    finally:
+        for r in reps:
+            r.close()
+        _cleanup(g)
