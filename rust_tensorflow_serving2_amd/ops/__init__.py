@@ -166,8 +166,20 @@ def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
     return s
 
 
+_LN_OK: Dict[int, bool] = {}
+
+
+def _ln_ok(cfg: int) -> bool:
+    if cfg not in _LN_OK:
+        try:
+            _LN_OK[cfg] = bool(hip().cgemm_ln_ok(cfg))
+        except (KernelsUnavailable, AttributeError):
+            _LN_OK[cfg] = False
+    return _LN_OK[cfg]
+
+
 def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-               halo: bool = False):
+               halo: bool = False, no_split: bool = False, n_multiple: bool = False):
     """(tile config, split-K) pairs worth timing for an M x N x K problem
     (``dma``: the operand mode uses the direct-to-LDS path, so the deeper
     DMA-ring configs apply; ``aligned64``: K and the conv channels are
@@ -201,9 +213,13 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
             continue   # mostly-empty tiles
         if bn % 64 and N % bn:
             continue   # 96-wide tiles: only where they divide N (BERT's 768 / 2304 / 3072)
+        if n_multiple and N % bn:
+            continue   # per-tile row statistics need whole tiles along N (LayerNorm folding)
+        if no_split and cgemm_only and not _ln_ok(cfg):
+            continue   # (the LayerNorm-fold GEMMs: only configs with that epilogue compiled in)
         tiles = -(-M // bm) * -(-N // bn)
         for s in (1, 2, 4, 8, 16):
-            if s > 1 and (nk // s < 2 or tiles >= 1024 or tiles * s > 4096):
+            if s > 1 and (no_split or nk // s < 2 or tiles >= 1024 or tiles * s > 4096):
                 continue
             out.append((cfg, s))
     return out
@@ -224,7 +240,7 @@ def _ensure_cache() -> None:
 
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
                  dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-                 halo: bool = False) -> Tuple[int, int]:
+                 halo: bool = False, no_split: bool = False, n_multiple: bool = False) -> Tuple[int, int]:
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
     heuristic is used)."""
@@ -242,8 +258,8 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
             _GRAPH_TUNED.add(key)          # the leader already graph-tuned it
         return remote
     if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
-        c = 42 if cgemm_only else heuristic_config(M, N)
-        return c, heuristic_splits(M, N, K, c)
+        c = (36 if no_split else 42) if cgemm_only else heuristic_config(M, N)
+        return c, 1 if no_split else heuristic_splits(M, N, K, c)
     with _TUNE_LOCK:
         hit = _TUNED.get(key)
         if hit is not None:
@@ -251,7 +267,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
         best, best_t = None, float("inf")
         times = []
         flush = _flush_buffer()
-        for c, s in candidates(M, N, K, dma, aligned64, cgemm_only, halo):
+        for c, s in candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, n_multiple):
             launch(c, s)   # warm (also sets the kernel's LDS attribute)
             samples = []
             for _rep in range(5):
