@@ -157,7 +157,8 @@ int Endpoint::offer(std::unique_ptr<Call>& call, PredictRequestView& req) {
 void Endpoint::copy_rows(int slot, int r0, int n, const std::vector<const uint8_t*>& src) {
   Slot& s = slots_[slot];
   for (size_t i = 0; i < inputs.size(); ++i)
-    std::memcpy(s.in_base[i] + size_t(r0) * inputs[i].row_bytes, src[i], size_t(n) * inputs[i].row_bytes);
+    ingest_rows(s.in_base[i] + size_t(r0) * inputs[i].slot_bytes(), src[i], size_t(n) * inputs[i].row_bytes,
+                inputs[i].conv);
   std::lock_guard<std::mutex> g(mu_);
   s.copied += n;
   s.ready.emplace_back(r0, n);
@@ -208,6 +209,9 @@ std::shared_ptr<StreamRes> Endpoint::reserve_stream(const std::shared_ptr<Endpoi
   // the same acceptance rules as offer(), on the header alone
   if (inputs.size() != 1) return nullptr;
   const TensorSpecC& in = inputs[0];
+  // a logged request is recorded from its bytes as received: with a converting
+  // row those are gone, so logged endpoints buffer such requests instead
+  if (in.conv && logging()) return nullptr;
   if (pi.alias != in.alias || pi.dtype != in.dtype || pi.shape.size() != in.row_shape.size() + 1) return nullptr;
   for (size_t d = 0; d < in.row_shape.size(); ++d)
     if (pi.shape[d + 1] != in.row_shape[d]) return nullptr;
@@ -236,8 +240,9 @@ std::shared_ptr<StreamRes> Endpoint::reserve_stream(const std::shared_ptr<Endpoi
   r->slot = slot;
   r->idx = int(s.reqs.size()) - 1;
   r->n = n;
-  r->dst = s.in_base[0] + size_t(r0) * in.row_bytes;
+  r->dst = s.in_base[0] + size_t(r0) * in.slot_bytes();
   r->len = pi.payload_len;
+  r->conv = in.conv;
   return r;
 }
 
@@ -364,7 +369,9 @@ void Endpoint::complete(int slot, Server& srv) {
       // the request message as received: a streamed one is its header bytes +
       // the payload sitting in this slot's row (not yet reused)
       if (p.sres) {
-        if (p.call->head.size() > 5)
+        // (a converted row no longer holds the request's fp32 bytes: such a
+        // stream is not reserved while logging is on, see reserve_stream)
+        if (p.call->head.size() > 5 && !p.sres->conv)
           log->submit_predict(spec, p.call->head.substr(5),
                               std::string(reinterpret_cast<const char*>(p.sres->dst), p.sres->len), body);
       } else {

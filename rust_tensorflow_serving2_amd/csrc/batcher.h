@@ -33,7 +33,12 @@ struct TensorSpecC {
   int dtype = 0;
   std::vector<int64_t> row_shape;
   size_t row_elems = 1;
-  size_t row_bytes = 0;
+  size_t row_bytes = 0;    // one row on the wire
+  // the row in a batch slot: the wire bytes (conv 0) or, for an fp32 input the
+  // device program takes as bf16, the values converted while they are copied
+  // in (conv 1, csrc/ingest.h: half the bytes)
+  int conv = 0;
+  size_t slot_bytes() const { return conv == 1 ? row_elems * 2 : row_bytes; }
 };
 
 class Endpoint;

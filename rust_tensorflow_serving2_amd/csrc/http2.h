@@ -10,6 +10,7 @@
 // path (batcher.h) or to a queue drained by Python control-plane threads.
 // Responses from any thread are posted to the owning IO thread (eventfd).
 #pragma once
+#include "ingest.h"
 #include <atomic>
 #include <cstring>
 #include <chrono>
@@ -84,7 +85,13 @@ struct StreamRes {
   std::atomic<int> state{0};     // 0 streaming, 1 committed, 2 abandoned (by either side)
   std::atomic<int> writers{0};   // IO thread inside write(); the batcher waits for 0 before reusing the row
   uint8_t* dst = nullptr;
-  size_t len = 0, got = 0;
+  size_t len = 0, got = 0;       // payload (wire) bytes expected / arrived
+  // ingest conversion: 1 = the wire's fp32 values land in the row as bf16
+  // (csrc/ingest.h), so the row holds len / 2 bytes and a float split across
+  // two chunks waits in `carry`
+  int conv = 0;
+  int ncarry = 0;
+  uint8_t carry[4] = {0, 0, 0, 0};
   virtual ~StreamRes() = default;
   // Every payload byte arrived and the message ended: hand over the call.
   virtual void commit(std::unique_ptr<Call> call) = 0;
@@ -98,11 +105,32 @@ struct StreamRes {
   bool write(const uint8_t* p, size_t n) {
     writers.fetch_add(1);
     const bool live = state.load() == 0;
-    // p == dst + got: the IO thread already recv()'d these bytes into the row
-    if (live && p != dst + got) std::memcpy(dst + got, p, n);
+    if (live) {
+      if (conv) {
+        write_converted(p, n);
+      } else if (p != dst + got) {   // p == dst + got: recv()'d straight into the row
+        std::memcpy(dst + got, p, n);
+      }
+    }
     writers.fetch_sub(1);
     got += n;
     return live;
+  }
+
+ private:
+  void write_converted(const uint8_t* p, size_t n) {
+    uint16_t* out = reinterpret_cast<uint16_t*>(dst) + (got - size_t(ncarry)) / 4;   // values completed so far
+    size_t i = 0;
+    if (ncarry) {
+      while (ncarry < 4 && i < n) carry[ncarry++] = p[i++];
+      if (ncarry < 4) return;
+      ingest_f32_to_bf16(out++, carry, 1);
+      ncarry = 0;
+    }
+    const size_t nv = (n - i) / 4;
+    ingest_f32_to_bf16(out, p + i, nv);
+    i += nv * 4;
+    while (i < n) carry[ncarry++] = p[i++];
   }
 };
 

@@ -580,7 +580,7 @@ class IoThread {
       if (st && st->mode == kStreamMode && !st->overflow && st->sres) {
         StreamRes* r = st->sres.get();
         const size_t room = r->len - r->got;
-        if (room) {
+        if (room && !r->conv) {   // (a converting row takes its bytes through write())
           r->writers.fetch_add(1);
           if (r->state.load() == 0) {
             held = r;

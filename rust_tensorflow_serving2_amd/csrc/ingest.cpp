@@ -1,0 +1,66 @@
+// fp32 -> bf16 ingest conversion (see ingest.h).  AVX-512 BF16 when the CPU
+// has it (one vcvtne2ps2bf16 per 32 values), scalar round-to-nearest-even
+// otherwise.  Both give the same bits for every input: NaNs stay NaN and
+// fp32 denormals (|x| < 1.2e-38, which vcvtne2ps2bf16 reads as zero) become
+// signed zeros in the scalar path too.
+#include "ingest.h"
+
+#include <cstring>
+#include <immintrin.h>
+
+namespace tfs {
+
+namespace {
+
+inline uint16_t bf16_rne(uint32_t u) {
+  if ((u & 0x7fffffffu) > 0x7f800000u) return uint16_t((u >> 16) | 0x40u);   // quiet NaN
+  if ((u & 0x7f800000u) == 0) return uint16_t((u >> 16) & 0x8000u);         // denormal -> signed zero
+  return uint16_t((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+void convert_scalar(uint16_t* dst, const uint8_t* src, size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t u;
+    std::memcpy(&u, src + 4 * i, 4);
+    dst[i] = bf16_rne(u);
+  }
+}
+
+__attribute__((target("avx512f,avx512bf16,avx512vl")))
+void convert_avx512(uint16_t* dst, const uint8_t* src, size_t n) {
+  size_t i = 0;
+  for (; i + 32 <= n; i += 32) {
+    const __m512 a = _mm512_loadu_ps(reinterpret_cast<const float*>(src + 4 * i));
+    const __m512 b = _mm512_loadu_ps(reinterpret_cast<const float*>(src + 4 * i + 64));
+    // (b, a): the low 16 lanes of the result come from the second operand
+    const __m512bh r = _mm512_cvtne2ps_pbh(b, a);
+    _mm512_storeu_si512(reinterpret_cast<void*>(dst + i), reinterpret_cast<__m512i>(r));
+  }
+  if (i < n) convert_scalar(dst + i, src + 4 * i, n - i);
+}
+
+using ConvFn = void (*)(uint16_t*, const uint8_t*, size_t);
+
+ConvFn pick() {
+  __builtin_cpu_init();
+  if (__builtin_cpu_supports("avx512bf16") && __builtin_cpu_supports("avx512vl")) return convert_avx512;
+  return convert_scalar;
+}
+
+const ConvFn g_conv = pick();
+
+}  // namespace
+
+void ingest_f32_to_bf16(uint16_t* dst, const uint8_t* src, size_t n) {
+  if (n) g_conv(dst, src, n);
+}
+
+void ingest_rows(uint8_t* dst, const uint8_t* src, size_t wire_bytes, int conv) {
+  if (conv == 1) {
+    ingest_f32_to_bf16(reinterpret_cast<uint16_t*>(dst), src, wire_bytes / 4);
+  } else {
+    std::memcpy(dst, src, wire_bytes);
+  }
+}
+
+}  // namespace tfs

@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "ingest.h"
 #include "sstable.h"
 #include "wire.h"
 
@@ -192,6 +193,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dims"), py::arg("lut"),
         "PredictRequest of one DT_FLOAT float_val tensor from u8 pixels mapped through a 256-entry table");
 
+  m.def("ingest_f32_to_bf16", [](py::bytes b) {
+    const std::string in = b;
+    std::string out(in.size() / 4 * 2, '\0');
+    {
+      py::gil_scoped_release nogil;
+      tfs::ingest_f32_to_bf16(reinterpret_cast<uint16_t*>(&out[0]), reinterpret_cast<const uint8_t*>(in.data()),
+                              in.size() / 4);
+    }
+    return py::bytes(out);
+  }, py::arg("f32_bytes"), "fp32 bytes -> bf16 bytes (the fast path's ingest conversion, csrc/ingest.h)");
   m.def("set_thread_name", [](const std::string& name) {
     // OS-level thread name (<= 15 chars), visible in /proc/<pid>/task/*/comm
     pthread_setname_np(pthread_self(), name.substr(0, 15).c_str());

@@ -444,6 +444,16 @@ std::vector<TensorSpecC> specs_from(const py::list& l) {
     const int esz = dtype_size(s.dtype);
     if (esz == 0) throw std::invalid_argument("fast path: unsupported dtype for " + s.alias);
     s.row_bytes = s.row_elems * size_t(esz);
+    // optional 4th field: the dtype of the batch-slot rows (DT_BFLOAT16 for an
+    // fp32 input converted on ingest)
+    if (t.size() > 3 && !t[3].is_none()) {
+      const int slot_dt = t[3].cast<int>();
+      if (slot_dt == DT_BFLOAT16 && s.dtype == DT_FLOAT) {
+        s.conv = 1;
+      } else if (slot_dt != s.dtype) {
+        throw std::invalid_argument("fast path: unsupported slot dtype for " + s.alias);
+      }
+    }
     out.push_back(std::move(s));
   }
   std::sort(out.begin(), out.end(), [](const TensorSpecC& a, const TensorSpecC& b) { return a.alias < b.alias; });

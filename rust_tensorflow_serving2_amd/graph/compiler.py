@@ -119,6 +119,20 @@ class Program:
                     vals[s] = o
         return [vals[s] for s in self.fetch_slots]
 
+    def feed_accepts_bf16(self, i: int) -> bool:
+        """Whether feed ``i`` may be given as bf16 instead of fp32: every step
+        that reads it is a fused op that rounds that operand to bf16 itself
+        (``accepts_bf16_input``), and the feed is not fetched."""
+        slot = self.feed_slots[i]
+        if slot in self.fetch_slots:
+            return False
+        users = [(node, list(ins).index(slot)) for _fn, node, ins, _o in self.steps if slot in ins]
+        for node, pos in users:
+            impl = node.attrs.get("_impl")
+            if impl is None or not getattr(impl, "accepts_bf16_input", lambda _p: False)(pos):
+                return False
+        return bool(users)
+
     def op_histogram(self) -> Dict[str, int]:
         h: Dict[str, int] = {}
         for _fn, node, _i, _o in self.steps:

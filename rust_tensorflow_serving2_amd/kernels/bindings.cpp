@@ -431,12 +431,14 @@ Tensor maxpool(const Tensor& x, int64_t KH, int64_t KW, int64_t SH, int64_t SW, 
 }
 
 // ResNet stem: conv 7x7/2 (+bias, act) -> max pool 3x3/2 (+post) in one kernel
-// (stem.hip).  x: fp32 NHWC request with C <= 4; w: [cout][ldw] bf16 in the
-// padded-RGBA order of the c4 stem ([kh][8 taps][4 ch]).
+// (stem.hip).  x: fp32 NHWC request with C <= 4 (or that request converted to
+// bf16 on ingest, csrc/ingest.h); w: [cout][ldw] bf16 in the padded-RGBA order
+// of the c4 stem ([kh][8 taps][4 ch]).
 Tensor stem_pool(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t PT, int64_t PB, int64_t PL, int64_t PR,
                  int64_t act, int64_t PPT, int64_t PPB, int64_t PPL, int64_t PPR,
                  const c10::optional<Tensor>& post_scale, const c10::optional<Tensor>& post_shift, int64_t post_act) {
-  need(x, at::kFloat, "x");
+  const bool xb16 = x.scalar_type() == at::kBFloat16;
+  need(x, xb16 ? at::kBFloat16 : at::kFloat, "x");
   need(w, at::kBFloat16, "w");
   need(bias, at::kFloat, "bias");
   TORCH_CHECK(x.dim() == 4 && x.size(3) >= 1 && x.size(3) <= 4, "stem_pool: x must be NHWC with C <= 4");
@@ -463,7 +465,7 @@ Tensor stem_pool(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t P
     sc = post_scale->data_ptr<float>();
     sh = post_shift->data_ptr<float>();
   }
-  check(tfsk::stem_pool_launch(x.data_ptr<float>(), bf16p(w), int(w.size(1)), bias.data_ptr<float>(), bf16p_mut(y), N,
+  check(tfsk::stem_pool_launch(x.data_ptr(), xb16, bf16p(w), int(w.size(1)), bias.data_ptr<float>(), bf16p_mut(y), N,
                                H, W, C, cout, int(PT), int(PL), Hc, Wc, int(PPT), int(PPL), Hp, Wp, int(act), sc, sh,
                                int(post_act), cur_stream(x)), "stem_pool");
   return y;

@@ -121,9 +121,10 @@ hipError_t igemm_launch(const IGemmArgs& args, int a_mode, int cfg, hipStream_t 
 // [cout][ldw] bf16, k = kh*32 + kw*4 + c, cout in {16,32,48,64}) + bias + act
 // -> 3x3/2 max pool (+ optional scale/shift/act after the max) -> bf16
 // [N][Hp][Wp][cout].  pt/pl: conv padding; ppt/ppl: pool padding.
-hipError_t stem_pool_launch(const float* x, const uint16_t* w, int ldw, const float* bias, uint16_t* y, int N, int H,
-                            int W, int C, int cout, int pt, int pl, int Hc, int Wc, int ppt, int ppl, int Hp, int Wp,
-                            int act, const float* pscale, const float* pshift, int pact, hipStream_t s);
+hipError_t stem_pool_launch(const void* x, bool x_bf16, const uint16_t* w, int ldw, const float* bias, uint16_t* y,
+                            int N, int H, int W, int C, int cout, int pt, int pl, int Hc, int Wc, int ppt, int ppl,
+                            int Hp, int Wp, int act, const float* pscale, const float* pshift, int pact,
+                            hipStream_t s);
 // NHWC bf16 max-pool (TF SAME/VALID padding given explicitly).  With `scale`
 // (and `shift`): y = act(max * scale[c] + shift[c]) — a folded inference
 // BatchNorm (+ ReLU when act == 1) applied after the pooling.

@@ -50,7 +50,7 @@ constexpr int kSlots = (kPatch + 255) / 256;        // 4 per thread
 constexpr int kKSteps = 7;                          // filter rows
 
 struct StemArgs {
-  const float* x;       // [N][H][W][C] fp32
+  const void* x;        // [N][H][W][C] fp32, or bf16 (XB16: converted on ingest, csrc/ingest.h)
   const uint16_t* w;    // [Cout][ldw] bf16, k = kh*32 + kw*4 + c
   const float* bias;    // [Cout]
   uint16_t* y;          // [N][Hp][Wp][Cout] bf16
@@ -84,7 +84,7 @@ __device__ __forceinline__ uint32_t kmax(uint32_t a, uint32_t b) {
                                                                 __builtin_bit_cast(s16x2, b)));
 }
 
-template <int NCG>
+template <int NCG, bool XB16>
 __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
   constexpr int COUT = NCG * 16;
   constexpr int CS = COUT + 8;                      // conv tile row stride (halves), 16-B aligned rows
@@ -135,8 +135,11 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
   // replay with this form.  Ablations after the change, b32 eager 35.5 us:
   // without the loads 30.1, the MFMAs 26.5, the pool 31.6, the conv-tile
   // stores 30.0, all four 12.6 -- profiles/round2/stem_ablate.log)
+  // (a bf16 request -- rounded on ingest exactly as cvt2 rounds below -- is
+  // read as 16-bit values and widened: the staged patch is the same bits)
+  constexpr uint32_t kEsz = XB16 ? 2u : 4u;
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.x), 0, int(long(p.N) * p.H * p.W * p.C * 4), 0x00020000);
+      const_cast<void*>(p.x), 0, int(long(p.N) * p.H * p.W * p.C * kEsz), 0x00020000);
   constexpr uint32_t kOff = 0x80000000u;
   float pf[kSlots][4] = {};
   auto load_patch = [&](int t) {
@@ -151,11 +154,14 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
       const int r = q / kIC, c = q - r * kIC;
       const int gy = iy0 + r, gx = ix0 + c;
       const bool ok = q < kPatch && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W;
-      const uint32_t pix = uint32_t(((n * p.H + gy) * p.W + gx) * p.C) * 4u;
+      const uint32_t pix = uint32_t(((n * p.H + gy) * p.W + gx) * p.C) * kEsz;
 #pragma unroll
       for (int ch = 0; ch < 4; ++ch) {
-        const uint32_t voff = ok && ch < p.C ? pix + uint32_t(ch) * 4u : kOff;
-        pf[s][ch] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsX, voff, 0, 0));
+        const uint32_t voff = ok && ch < p.C ? pix + uint32_t(ch) * kEsz : kOff;
+        if constexpr (XB16)
+          pf[s][ch] = __uint_as_float(uint32_t(__builtin_amdgcn_raw_buffer_load_b16(rsX, voff, 0, 0)) << 16);
+        else
+          pf[s][ch] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsX, voff, 0, 0));
       }
     }
   };
@@ -265,9 +271,10 @@ int cu_count() {
 
 }  // namespace
 
-hipError_t stem_pool_launch(const float* x, const uint16_t* w, int ldw, const float* bias, uint16_t* y, int N, int H,
-                            int W, int C, int cout, int pt, int pl, int Hc, int Wc, int ppt, int ppl, int Hp, int Wp,
-                            int act, const float* pscale, const float* pshift, int pact, hipStream_t s) {
+hipError_t stem_pool_launch(const void* x, bool x_bf16, const uint16_t* w, int ldw, const float* bias, uint16_t* y,
+                            int N, int H, int W, int C, int cout, int pt, int pl, int Hc, int Wc, int ppt, int ppl,
+                            int Hp, int Wp, int act, const float* pscale, const float* pshift, int pact,
+                            hipStream_t s) {
   if (N <= 0 || Hp <= 0 || Wp <= 0) return hipSuccess;
   if (C < 1 || C > 4 || cout % 16 || cout < 16 || cout > 64 || ldw < kKSteps * 32 || ldw % 8 ||
       (pscale == nullptr) != (pshift == nullptr) || ppt < 0 || ppl < 0 || pt < 0 || pl < 0)
@@ -285,14 +292,23 @@ hipError_t stem_pool_launch(const float* x, const uint16_t* w, int ldw, const fl
   a.tiles_x = (Wp + kTPX - 1) / kTPX;
   const long tiles = long(N) * a.tiles_y * a.tiles_x;
   if (tiles > (1L << 30)) return hipErrorInvalidValue;
-  if (long(N) * H * W * C * 4 >= 0x7fffffffL) return hipErrorInvalidValue;   // 32-bit buffer offsets
+  if (long(N) * H * W * C * (x_bf16 ? 2 : 4) >= 0x7fffffffL) return hipErrorInvalidValue;   // 32-bit buffer offsets
   a.tiles = int(tiles);
   const int grid = int(tiles < 2L * cu_count() ? tiles : 2L * cu_count());
-  switch (cout / 16) {
-    case 1: hipLaunchKernelGGL(stem_pool_kernel<1>, dim3(grid), dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(stem_pool_kernel<2>, dim3(grid), dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(stem_pool_kernel<3>, dim3(grid), dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(stem_pool_kernel<4>, dim3(grid), dim3(256), 0, s, a); break;
+  if (x_bf16) {
+    switch (cout / 16) {
+      case 1: hipLaunchKernelGGL((stem_pool_kernel<1, true>), dim3(grid), dim3(256), 0, s, a); break;
+      case 2: hipLaunchKernelGGL((stem_pool_kernel<2, true>), dim3(grid), dim3(256), 0, s, a); break;
+      case 3: hipLaunchKernelGGL((stem_pool_kernel<3, true>), dim3(grid), dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL((stem_pool_kernel<4, true>), dim3(grid), dim3(256), 0, s, a); break;
+    }
+  } else {
+    switch (cout / 16) {
+      case 1: hipLaunchKernelGGL((stem_pool_kernel<1, false>), dim3(grid), dim3(256), 0, s, a); break;
+      case 2: hipLaunchKernelGGL((stem_pool_kernel<2, false>), dim3(grid), dim3(256), 0, s, a); break;
+      case 3: hipLaunchKernelGGL((stem_pool_kernel<3, false>), dim3(grid), dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL((stem_pool_kernel<4, false>), dim3(grid), dim3(256), 0, s, a); break;
+    }
   }
   return hipGetLastError();
 }

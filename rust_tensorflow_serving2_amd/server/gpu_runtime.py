@@ -35,6 +35,13 @@ log = logging.getLogger("tfserve.gpu")
 # another thread is capturing or warming up a servable can deadlock the two.
 CAPTURE_LOCK = threading.RLock()
 
+# Buckets of one lane capture into one shared graph memory pool (largest bucket
+# first, so the smaller ones fit in its freed activation blocks).  Safe because
+# a lane never replays two of its graphs at once (one stream, one batch at a
+# time) and a bucket's outputs are only read (D2H) right after its own replay.
+# TFSERVE_SHARED_GRAPH_POOL=0 (read when a lane is created) gives every graph
+# a private pool.
+
 
 def buckets_for(max_batch: int, allowed: Sequence[int] = ()) -> List[int]:
     if allowed:
@@ -70,6 +77,11 @@ class _Lane:
         # arrive (native lanes' eager H2D), before the batch size is known
         self.dev_in: List[torch.Tensor] = []
         self.done = torch.cuda.Event()
+        # one HIP-graph memory pool for every bucket of the lane: a lane replays
+        # one bucket at a time on its one stream, so the buckets' activations
+        # can share blocks (only the captured outputs stay reserved per bucket)
+        self.pool = None
+        self.share_pool = os.environ.get("TFSERVE_SHARED_GRAPH_POOL", "1") != "0"
 
 
 class GpuRunner:
@@ -98,17 +110,26 @@ class GpuRunner:
         # the Python lane locks: the Python run() path then only uses the rest
         # (one spare lane is always kept for it)
         self.claimed: set = set()
+        # fp32 inputs the program reads as bf16 anyway (the ResNet stem) are
+        # staged as bf16: converted on ingest (csrc/ingest.h) or by the H2D
+        # staging copy, half the pinned / PCIe / device bytes
+        self.slot_dtypes = [T.DT_BFLOAT16 if self._bf16_feed(i, s) else s.dtype for i, s in enumerate(in_specs)]
         if self.batched:
             with torch.cuda.device(self.device):
                 self.lanes = [_Lane(self.device) for _ in range(max(1, lanes) + 1)]
                 for lane in self.lanes:
                     self._alloc_host(lane)
 
+    def _bf16_feed(self, i: int, spec) -> bool:
+        if os.environ.get("TFSERVE_BF16_INGEST", "1") == "0" or spec.dtype != T.DT_FLOAT:
+            return False
+        return self.program.feed_accepts_bf16(i)
+
     # ------------------------------------------------------------ buffers
     def _alloc_host(self, lane: _Lane):
         bmax = self.buckets[-1]
-        for s in self.in_specs:
-            lane.host_in.append(torch.zeros([bmax] + list(s.shape[1:]), dtype=_torch_dtype(s.dtype),
+        for s, dt in zip(self.in_specs, self.slot_dtypes):
+            lane.host_in.append(torch.zeros([bmax] + list(s.shape[1:]), dtype=_torch_dtype(dt),
                                             pin_memory=True))
         self._out_shapes: Optional[List[Tuple[int, ...]]] = None
 
@@ -184,8 +205,8 @@ class GpuRunner:
         dev = self.device
         if not lane.dev_in:
             bmax = self.buckets[-1]
-            lane.dev_in = [torch.zeros([bmax] + list(s.shape[1:]), dtype=_torch_dtype(s.dtype), device=dev)
-                           for s in self.in_specs]
+            lane.dev_in = [torch.zeros([bmax] + list(s.shape[1:]), dtype=_torch_dtype(dt), device=dev)
+                           for s, dt in zip(self.in_specs, self.slot_dtypes)]
         ins = [t[:b] for t in lane.dev_in]
         from .. import ops
         src = getattr(self.servable, "weight_source", None)
@@ -222,7 +243,9 @@ class GpuRunner:
         # blit kernels that read host memory over PCIe from the CUs) and move only
         # the n live rows of a batch, not the whole bucket
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=lane.stream, capture_error_mode="thread_local"):
+        if lane.pool is None and lane.share_pool:
+            lane.pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(graph, pool=lane.pool, stream=lane.stream, capture_error_mode="thread_local"):
             outs = self._finish(self.program.run(ins))
         # replay once now: a graph's first launch uploads it to the device
         # (milliseconds), which must not land on the first live batch of a

@@ -64,7 +64,9 @@ class FastEndpoint:
         out_aliases = sorted(out_specs)
         self.runner = servable.runner(sig_name, in_aliases, out_aliases)
         self.max_rows = self.runner.buckets[-1]
-        ins = [(a, in_specs[a].dtype, list(in_specs[a].shape[1:])) for a in in_aliases]
+        # 4th field: the batch-slot row dtype (bf16 for an fp32 input converted on ingest)
+        slot_dt = getattr(self.runner, "slot_dtypes", None) or [in_specs[a].dtype for a in in_aliases]
+        ins = [(a, in_specs[a].dtype, list(in_specs[a].shape[1:]), dt) for a, dt in zip(in_aliases, slot_dt)]
         outs = [(a, out_specs[a].dtype, list(out_specs[a].shape[1:])) for a in out_aliases]
         self.id = srv.add_endpoint(servable.name, servable.version, sig_name, ins, outs, self.max_rows, timeout_us)
         srv.set_idle_dispatch(self.id, transport.idle_dispatch)

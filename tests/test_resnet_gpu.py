@@ -96,3 +96,68 @@ def test_resnet50_v2_gpu_fully_fused_matches_cpu(resnet50_v2):
 def test_smoke():
     from rust_tensorflow_serving2_amd.smoke import run_smoke
     run_smoke()
+
+
+def _pool_bytes(pool_ids):
+    """Device bytes reserved by the given graph memory pools (allocator snapshot)."""
+    snap = torch.cuda.memory._snapshot()
+    return sum(seg["total_size"] for seg in snap["segments"] if tuple(seg.get("segment_pool_id", ())) in pool_ids)
+
+
+def test_lane_buckets_share_one_graph_pool(resnet50, monkeypatch):
+    """Every bucket graph of a lane captures into one memory pool (the lane
+    replays one bucket at a time): far less device memory than a private pool
+    per bucket, and replays in any bucket order give the same outputs."""
+    import gc
+    from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
+    x = torch.from_numpy(np.random.default_rng(5).random((32, 224, 224, 3), dtype=np.float32))
+    used = {}
+    for share in ("0", "1"):
+        monkeypatch.setenv("TFSERVE_SHARED_GRAPH_POOL", share)
+        s = Servable("resnet", 1, resnet50, ServableOptions(
+            device="cuda:0", max_batch_size=32, allowed_batch_sizes=(1, 2, 4, 8, 16, 32), lanes=1))
+        r = s.runner("serving_default", ["input"], ["classes", "probabilities"])
+        r.lane_host_pointers(0)
+        lane = r.lanes[0]
+        torch.cuda.synchronize()
+        pools = {tuple(g.pool()) for g in lane.graphs.values()}
+        assert len(pools) == (1 if share == "1" else len(lane.graphs))
+        used[share] = _pool_bytes(pools)
+        lane.dev_in[0].copy_(x.to(lane.dev_in[0].device))
+        probs = {}
+        for b in (32, 1, 16, 2, 32, 8, 4, 1, 16):
+            with torch.cuda.stream(lane.stream):
+                lane.graphs[b].replay()
+            lane.stream.synchronize()
+            probs.setdefault(b, []).append(lane.static_out[b][1][:b].float().cpu().clone())
+        for b, ps in probs.items():
+            for p in ps[1:]:
+                assert torch.equal(p, ps[0]), b
+            # buckets may pick different tiles / split-K -> fp32 summation order differs
+            torch.testing.assert_close(ps[0], probs[32][0][:b], atol=2e-4, rtol=0)
+        del s, r, lane
+        gc.collect()
+        torch.cuda.empty_cache()
+    assert used["1"] > 0 and used["1"] < 0.7 * used["0"], used
+
+
+def test_bf16_ingest_is_bit_identical_to_fp32_feed(resnet50, monkeypatch):
+    """The stem rounds its fp32 input to bf16 itself, so the runner stages the
+    request as bf16 (half the pinned / PCIe / device bytes) and the outputs are
+    the same bits as feeding fp32 (same tile picks: autotuning off)."""
+    from rust_tensorflow_serving2_amd import ops
+    from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
+    from rust_tensorflow_serving2_amd.utils import tensors as T
+    monkeypatch.setattr(ops, "AUTOTUNE", False)
+    x = np.random.default_rng(9).random((4, 224, 224, 3), dtype=np.float32) * 255.0
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("TFSERVE_BF16_INGEST", mode)
+        s = Servable("resnet", 1, resnet50, ServableOptions(device="cuda:0", max_batch_size=4,
+                                                              allowed_batch_sizes=(4,), graph_autotune=False))
+        r = s.runner("serving_default", ["input"], ["classes", "probabilities"])
+        assert r.slot_dtypes == [T.DT_BFLOAT16 if mode == "1" else T.DT_FLOAT]
+        assert r.lanes[0].host_in[0].dtype == (torch.bfloat16 if mode == "1" else torch.float32)
+        outs[mode] = r.run([x])
+    np.testing.assert_array_equal(outs["0"][0], outs["1"][0])
+    np.testing.assert_array_equal(outs["0"][1], outs["1"][1])

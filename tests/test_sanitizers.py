@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "rust_tensorflow_serving2_amd", "csrc")
 
 
-SRCS = ("wire.cpp", "sstable.cpp", "batcher.cpp", "http2_server.cpp", "router.cpp", "request_log.cpp")
+SRCS = ("wire.cpp", "sstable.cpp", "batcher.cpp", "http2_server.cpp", "router.cpp", "request_log.cpp", "ingest.cpp")
 
 
 def _build_driver(tmp_path, name, flags, cxx=None):
