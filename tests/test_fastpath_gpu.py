@@ -195,11 +195,14 @@ def test_native_lane_device_failure_reloads_servable(tmp_path, monkeypatch):
         srv.stop()
 
 
-def test_request_logging_on_the_gpu_fast_path(tmp_path):
+@pytest.mark.parametrize("ingest", ["bf16", "fp32"])
+def test_request_logging_on_the_gpu_fast_path(tmp_path, monkeypatch, ingest):
     """logging_config sampling_rate=1.0 on a GPU model: every Predict served by
     the native fast path (streamed 300 KB images included) is read back as a
     valid PredictionLog TFRecord holding the request as sent and the response
-    as received."""
+    as received.  With bf16 ingest a row no longer holds the request's fp32
+    bytes, so a logged endpoint buffers those requests instead of streaming."""
+    monkeypatch.setenv("TFSERVE_BF16_INGEST", "1" if ingest == "bf16" else "0")
     from rust_tensorflow_serving2_amd.models import resnet
     from rust_tensorflow_serving2_amd.utils.request_log import read_tfrecords
     import time
@@ -231,7 +234,8 @@ def test_request_logging_on_the_gpu_fast_path(tmp_path):
                 return await asyncio.gather(*[stub(b) for b in bodies])
         outs = asyncio.run(go())
         st = tr.srv.stats()
-        assert st["fast_path"] == 12 and st["streamed"] >= 1 and st["slow_path"] == 0, st
+        assert st["fast_path"] == 12 and st["slow_path"] == 0, st
+        assert (st["streamed"] == 0) if ingest == "bf16" else (st["streamed"] >= 1), st
         lg = srv.request_logs.get("resnet")
         lg.flush()
         recs = [serving.PredictionLog.FromString(r) for r in read_tfrecords(lg.path)]
