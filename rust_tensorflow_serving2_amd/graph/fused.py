@@ -602,6 +602,42 @@ class StemPool:
 
 O.OPS["_StemPool"] = _impl_op
 
+# (K1, N1, N2) shapes kernels/chain.hip is built for (ResNet-50 stages 1-2)
+CHAIN_SHAPES = {(64, 256, 64), (64, 256, 128), (128, 512, 128), (128, 512, 256)}
+
+
+class ChainConv:
+    """A bottleneck's expand 1x1 conv (+ shortcut, act) and the NEXT
+    bottleneck's reduce 1x1 conv (+ act), which reads exactly its output, as
+    one kernel (``hip().conv_chain``, kernels/chain.hip): outputs
+    ``[y1, y2]``; y1 (the block output, also the next shortcut) is written
+    once and never read back by the reduce.  SURVEY.md S8 fused conv epilogues;
+    the request path is the reference client's ResNet Predict
+    (/root/reference/src/lib.rs:229-257)."""
+
+    children = ("a", "b")
+
+    def __init__(self, a: FusedConv, b: FusedConv):
+        self.a, self.b = a, b
+        self.use_hip = a.use_hip and b.use_hip
+        self.name = a.name
+
+    def __call__(self, ctx, node, ins):
+        x = O.to_torch(ins[0])
+        res = O.to_torch(ins[1]) if len(ins) > 1 else None
+        a, b = self.a, self.b
+        if self.use_hip and x.is_cuda and x.dim() == 4 and x.shape[-1] == a.cin:
+            from ..ops import ACT, hip
+            y1, y2 = hip().conv_chain(_to_bf16(x).contiguous(), a.w, a.b,
+                                      None if res is None else _to_bf16(res).contiguous(), ACT[a.act],
+                                      b.w, b.b, ACT[b.act])
+            return [y1, y2]
+        y1 = a(ctx, node, ins)[0]
+        return [y1, b(ctx, node, [y1])[0]]
+
+
+O.OPS["_ChainConv"] = _impl_op
+
 _PASSTHROUGH = ("Identity", "Squeeze", "Reshape")
 
 
@@ -998,8 +1034,55 @@ def fuse_post_activation(g, order, fed, fetch_refs, device, opts):
         c.refresh()
 
 
+def _chainable_1x1(impl) -> bool:
+    return (isinstance(impl, FusedConv) and impl.kh == 1 and impl.kw == 1 and impl.sh == 1 and impl.sw == 1 and
+            not impl.c4 and impl.post is None and impl.act in ("relu", "none") and
+            (impl.padding != "EXPLICIT" or not any(impl.pads)))
+
+
+def fuse_conv_chain(g, order, fed, fetch_refs, device, opts):
+    """``_FusedConv2D`` A (1x1 expand, optional residual) whose output feeds a
+    ``_FusedConv2D`` B (1x1 reduce, no residual) -> ``_ChainConv`` with outputs
+    ``[A, B]`` when (A.cin, A.cout, B.cout) is a kernel shape; A's other
+    consumers (the next shortcut) keep reading output 0.  GPU programs only
+    (``TFSERVE_CONV_CHAIN=0`` disables it, ``force`` applies it on CPU too:
+    the op then runs both reference convs)."""
+    import os
+    mode = os.environ.get("TFSERVE_CONV_CHAIN", "1")
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    if mode == "0" or (not c.use_hip and mode != "force"):
+        return
+    for name in order:
+        p = g.nodes.get(name)
+        if p is None or p.op != "_FusedConv2D" or name in c.fetch_nodes:
+            continue
+        a = p.attrs["_impl"]
+        if not _chainable_1x1(a):
+            continue
+        cons = c.cons.get(name, [])
+        if any(i != 0 for _c, _p, i in cons):
+            continue
+        bs = [g.nodes[cn] for cn, pos, _i in cons
+              if pos == 0 and g.nodes[cn].op == "_FusedConv2D" and len(g.nodes[cn].inputs) == 1 and
+              cn not in c.fetch_nodes and _chainable_1x1(g.nodes[cn].attrs["_impl"])]
+        if len(bs) != 1:
+            continue
+        bnode = bs[0]
+        b = bnode.attrs["_impl"]
+        if b.cin != a.cout or (a.cin, a.cout, b.cout) not in CHAIN_SHAPES:
+            continue
+        chain = ChainConv(a, b)
+        p.op = "_ChainConv"
+        p.attrs = {"_impl": chain}
+        for cn, pos, _i in c.cons.get(bnode.name, []):
+            g.nodes[cn].inputs[pos] = (name, 1)
+        p.ctrl = _merge_ctrl([p, bnode])
+        del g.nodes[bnode.name]
+        c.refresh()
+
+
 def default_passes(options=None):
     from .patterns import bert_passes, late_passes
     return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_dual_conv, fuse_post_activation,
                                                                  fuse_stem_pool, fuse_matmul, fuse_classifier_head,
-                                                                 fuse_dense_softmax] + late_passes()
+                                                                 fuse_dense_softmax, fuse_conv_chain] + late_passes()

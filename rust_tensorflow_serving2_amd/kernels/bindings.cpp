@@ -471,6 +471,42 @@ Tensor stem_pool(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t P
   return y;
 }
 
+// A bottleneck's expand 1x1 (+ shortcut, act) and the next bottleneck's
+// reduce 1x1 (+ act) as one kernel (chain.hip): returns (y1, y2), NHWC bf16.
+std::vector<Tensor> conv_chain(const Tensor& x, const Tensor& w1, const Tensor& b1,
+                               const c10::optional<Tensor>& residual, int64_t act1, const Tensor& w2,
+                               const Tensor& b2, int64_t act2) {
+  need(x, at::kBFloat16, "x");
+  need(w1, at::kBFloat16, "w1");
+  need(w2, at::kBFloat16, "w2");
+  need(b1, at::kFloat, "b1");
+  need(b2, at::kFloat, "b2");
+  TORCH_CHECK(x.dim() == 4, "conv_chain: x must be NHWC");
+  const int K1 = x.size(3), N1 = w1.size(0), N2 = w2.size(0);
+  TORCH_CHECK(w1.dim() == 2 && w2.dim() == 2 && w1.size(1) >= K1 && w2.size(1) >= N1 && w1.size(1) % 8 == 0 &&
+                  w2.size(1) % 8 == 0, "conv_chain: w1 [N1][>= K1], w2 [N2][>= N1]");
+  TORCH_CHECK(tfsk::conv_chain_supported(K1, N1, N2), "conv_chain: unsupported shape K1=", K1, " N1=", N1, " N2=", N2);
+  TORCH_CHECK(b1.numel() == N1 && b2.numel() == N2, "conv_chain: bias sizes");
+  TORCH_CHECK(w1.device() == x.device() && w2.device() == x.device() && b1.device() == x.device() &&
+                  b2.device() == x.device(), "conv_chain: tensors on different devices");
+  const uint16_t* rp = nullptr;
+  if (residual.has_value()) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->dim() == 4 && residual->size(0) == x.size(0) && residual->size(1) == x.size(1) &&
+                    residual->size(2) == x.size(2) && residual->size(3) == N1, "conv_chain: residual [n][h][w][N1]");
+    rp = bf16p(*residual);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int M = x.size(0) * x.size(1) * x.size(2);
+  Tensor y1 = torch::empty({x.size(0), x.size(1), x.size(2), N1}, x.options());
+  Tensor y2 = torch::empty({x.size(0), x.size(1), x.size(2), N2}, x.options());
+  check(tfsk::conv_chain_launch(bf16p(x), bf16p(w1), int(w1.size(1)), b1.data_ptr<float>(), rp, bf16p_mut(y1),
+                                bf16p(w2), int(w2.size(1)), b2.data_ptr<float>(), bf16p_mut(y2), M, K1, N1, N2,
+                                int(act1), int(act2), cur_stream(x)),
+        "conv_chain");
+  return {y1, y2};
+}
+
 Tensor global_avgpool(const Tensor& x, const c10::optional<Tensor>& out) {
   need(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "global_avgpool: NHWC with C % 8 == 0");
@@ -697,6 +733,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none(), py::arg("out_f32") = false, py::arg("splits") = 1,
         py::arg("post_scale") = py::none(), py::arg("post_shift") = py::none(), py::arg("post_act") = 0,
         py::arg("out2") = py::none(), py::arg("post_only") = false);
+  m.def("conv_chain", &conv_chain, "expand 1x1 (+residual, act) -> next reduce 1x1 (+act) in one kernel",
+        py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("residual"), py::arg("act1"), py::arg("w2"),
+        py::arg("b2"), py::arg("act2"));
+  m.def("conv_chain_supported", [](int64_t k1, int64_t n1, int64_t n2) {
+    return tfsk::conv_chain_supported(int(k1), int(n1), int(n2));
+  });
   m.def("conv2d_dual", &conv2d_dual, "act(conv1x1(h) + conv1x1_stride(x) + bias) as one K-concatenated GEMM",
         py::arg("h"), py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"), py::arg("sw"), py::arg("act") = 0,
         py::arg("cfg") = 36, py::arg("out") = py::none(), py::arg("splits") = 1,

@@ -47,8 +47,12 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// Barrier without the vmcnt(0) drain __syncthreads' fence would add.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
+// Barrier without a vmcnt(0) drain: waits for this wave's own LDS reads
+// (lgkmcnt(0)) and then meets the other waves.  The lgkmcnt wait matters: the
+// compiler may leave the previous step's ds_reads in flight (their MFMAs sunk
+// below the barrier), and the DMA issued right after the barrier refills that
+// very ring slot -- found as run-to-run differences of chain.hip's output.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---- epilogue over the fp32 tile staged in LDS (8-column row chunks, NT threads)
 // NTE = the threads that take part: a multiple of the chunks per row, so a

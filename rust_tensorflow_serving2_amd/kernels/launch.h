@@ -125,6 +125,12 @@ hipError_t stem_pool_launch(const void* x, bool x_bf16, const uint16_t* w, int l
                             int N, int H, int W, int C, int cout, int pt, int pl, int Hc, int Wc, int ppt, int ppl,
                             int Hp, int Wp, int act, const float* pscale, const float* pshift, int pact,
                             hipStream_t s);
+// Two chained 1x1 convs in one launch (chain.hip): y1 = act1(x w1^T + b1 + res),
+// y2 = act2(y1 w2^T + b2); (K1, N1, N2) in conv_chain_supported().
+bool conv_chain_supported(int K1, int N1, int N2);
+hipError_t conv_chain_launch(const uint16_t* x, const uint16_t* w1, int ldw1, const float* b1, const uint16_t* res,
+                             uint16_t* y1, const uint16_t* w2, int ldw2, const float* b2, uint16_t* y2, int M, int K1,
+                             int N1, int N2, int act1, int act2, hipStream_t s);
 // NHWC bf16 max-pool (TF SAME/VALID padding given explicitly).  With `scale`
 // (and `shift`): y = act(max * scale[c] + shift[c]) — a folded inference
 // BatchNorm (+ ReLU when act == 1) applied after the pooling.

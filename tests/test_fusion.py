@@ -162,3 +162,26 @@ def test_tuned_cache_roundtrip(tmp_path, monkeypatch):
     monkeypatch.setattr(ops, "_REMOTE", {})
     p.write_text(json.dumps({"schema": "stale", "picks": {repr(key): [42, 1]}}))
     assert ops.load_tuned_cache(str(p)) == 0 and not ops._REMOTE
+
+
+def test_conv_chain_pass_pairs_expand_with_next_reduce(models_dir, monkeypatch):
+    """ResNet-50 stage-1/2 widths: every 1x1 expand whose output feeds the next
+    block's 1x1 reduce becomes one _ChainConv with outputs [expand, reduce]
+    (7 pairs on CPU; on the GPU the two projecting blocks' expands are dual
+    convs first, leaving 5); the fused program still equals the unfused
+    interpreter."""
+    from rust_tensorflow_serving2_amd.models import resnet
+    monkeypatch.setenv("TFSERVE_CONV_CHAIN", "force")     # the pass is GPU-only by default
+    path = os.path.join(str(models_dir), "chain_resnet", "1")
+    resnet.export(path, blocks=(3, 4, 1, 1), width=64, num_classes=10, image_size=32, seed=5)
+    ref, fused = _pair(path)
+    x = np.random.default_rng(2).random((2, 32, 32, 3), dtype=np.float32)
+    a = ref.run("serving_default", {"input": x}, ["classes", "probabilities"])
+    b = fused.run("serving_default", {"input": x}, ["classes", "probabilities"])
+    np.testing.assert_allclose(a["probabilities"], b["probabilities"], atol=1e-5)
+    np.testing.assert_array_equal(a["classes"], b["classes"])
+    hist = fused.runner("serving_default", ["input"], ["classes", "probabilities"]).program.op_histogram()
+    assert hist["_ChainConv"] == 7 - hist.get("_FusedDualConv", 0), hist
+    convs = 3 * 9 + 4                                     # 9 blocks x 3 + 4 projections (the stem is in _StemPool)
+    assert hist["_StemPool"] == 1
+    assert hist["_FusedConv2D"] + 2 * hist["_ChainConv"] + 2 * hist.get("_FusedDualConv", 0) == convs, hist

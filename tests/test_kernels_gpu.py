@@ -738,3 +738,59 @@ def test_linear_ln_fold_modes_match_fp32(cfg, bn):
 
 def F_gelu(x):
     return F.gelu(x, approximate="tanh")
+
+
+@pytest.mark.parametrize("k1,n1,n2", [(64, 256, 64), (64, 256, 128), (128, 512, 128), (128, 512, 256)])
+@pytest.mark.parametrize("m,with_res,act1,act2", [(4 * 56 * 56, True, "relu", "relu"), (77, False, "none", "relu"),
+                                                   (130, True, "relu", "none")])
+def test_conv_chain_matches_fp32(k1, n1, n2, m, with_res, act1, act2):
+    """expand 1x1 (+residual, act) -> next reduce 1x1 (+act) in one kernel vs
+    fp32 torch; y2 is checked against the reference applied to the kernel's own
+    bf16 y1 (what the separate reduce conv would read).  Row counts that are
+    not a multiple of the 64-row tile included."""
+    x = rnd(m, k1, seed=61).to(BF)
+    w1 = rnd(n1, k1, scale=1 / math.sqrt(k1), seed=62).to(BF)
+    b1 = rnd(n1, scale=0.1, seed=63)
+    res = rnd(m, n1, seed=64).to(BF) if with_res else None
+    w2 = rnd(n2, n1, scale=1 / math.sqrt(n1), seed=65).to(BF)
+    b2 = rnd(n2, scale=0.1, seed=66)
+    x4 = x.reshape(1, 1, m, k1)
+    y1, y2 = hip().conv_chain(x4.to(DEV), w1.to(DEV), b1.to(DEV),
+                              None if res is None else res.reshape(1, 1, m, n1).to(DEV), ACT[act1],
+                              w2.to(DEV), b2.to(DEV), ACT[act2])
+    assert y1.shape == (1, 1, m, n1) and y2.shape == (1, 1, m, n2)
+    ref1 = x.float() @ w1.float().t() + b1 + (res.float() if res is not None else 0)
+    ref1 = torch.relu(ref1) if act1 == "relu" else ref1
+    y1c = y1.reshape(m, n1).float().cpu()
+    assert (y1c - ref1).abs().max().item() < 2e-2 * max(1.0, ref1.abs().max().item())
+    ref2 = y1c @ w2.float().t() + b2
+    ref2 = torch.relu(ref2) if act2 == "relu" else ref2
+    y2c = y2.reshape(m, n2).float().cpu()
+    assert (y2c - ref2).abs().max().item() < 1e-2 * max(1.0, ref2.abs().max().item())
+
+
+def test_conv_chain_is_deterministic():
+    """Two launches on the same operands give the same bits (ResNet stage-1 b32 size)."""
+    m, k1, n1, n2 = 32 * 56 * 56, 64, 256, 64
+    x = rnd(1, 1, m, k1, seed=71).to(BF).to(DEV)
+    w1 = rnd(n1, k1, scale=1 / 8, seed=72).to(BF).to(DEV)
+    w2 = rnd(n2, n1, scale=1 / 16, seed=73).to(BF).to(DEV)
+    b1, b2 = rnd(n1, seed=74).to(DEV), rnd(n2, seed=75).to(DEV)
+    res = rnd(1, 1, m, n1, seed=76).to(BF).to(DEV)
+    outs = [hip().conv_chain(x, w1, b1, res, ACT["relu"], w2, b2, ACT["relu"]) for _ in range(4)]
+    for y1, y2 in outs[1:]:
+        assert torch.equal(y1, outs[0][0]) and torch.equal(y2, outs[0][1])
+
+
+@pytest.mark.parametrize("cfg", HALO_CFGS)
+def test_halo_conv_is_deterministic(cfg):
+    """Repeated launches give the same bits (the ring refill after each barrier
+    must not race the previous step's LDS reads)."""
+    n, h, w, cin, cout = 32, 56, 56, 64, 64
+    x = rnd(n, h, w, cin, seed=81).to(BF).to(DEV)
+    wt = rnd(3, 3, cin, cout, scale=1 / 24, seed=82).to(BF).float()
+    b = rnd(cout, scale=0.1, seed=83).to(DEV)
+    wp = pack_w(wt)
+    ys = [hip().conv2d(x, wp, b, None, 3, 3, 1, 1, 1, 1, 1, 1, act=ACT["relu"], cfg=cfg) for _ in range(4)]
+    for y in ys[1:]:
+        assert torch.equal(y, ys[0])

@@ -61,7 +61,9 @@ def test_resnet50_gpu_matches_cpu(resnet50):
     # the stem conv runs inside the fused stem + max-pool kernel
     assert hist.get("_FusedDualConv") == 4 and "Conv2D" not in hist
     assert hist.get("_StemPool") == 1 and "_MaxPool" not in hist
-    assert hist.get("_FusedConv2D") + 2 * hist["_FusedDualConv"] + hist["_StemPool"] == 53
+    # 5 expand -> next-reduce pairs of stages 1-2 run as one chained kernel each
+    assert hist.get("_ChainConv") == 5
+    assert hist.get("_FusedConv2D") + 2 * hist["_FusedDualConv"] + 2 * hist["_ChainConv"] + hist["_StemPool"] == 53
 
 
 @pytest.fixture(scope="module")
@@ -90,7 +92,8 @@ def test_resnet50_v2_gpu_fully_fused_matches_cpu(resnet50_v2):
     for op in ("FusedBatchNormV3", "Relu", "Mul", "Conv2D", "AddV2"):
         assert op not in hist, hist
     assert hist.get("_StemPool") == 1 and "_MaxPool" not in hist
-    assert hist.get("_FusedConv2D") + 2 * hist.get("_FusedDualConv", 0) + hist["_StemPool"] == 53
+    assert hist.get("_FusedConv2D") + 2 * hist.get("_FusedDualConv", 0) + 2 * hist.get("_ChainConv", 0) + \
+        hist["_StemPool"] == 53
 
 
 def test_smoke():
