@@ -602,8 +602,13 @@ class StemPool:
 
 O.OPS["_StemPool"] = _impl_op
 
-# (K1, N1, N2) shapes kernels/chain.hip is built for (ResNet-50 stages 1-2)
-CHAIN_SHAPES = {(64, 256, 64), (64, 256, 128), (128, 512, 128), (128, 512, 256)}
+# (K1, N1, N2) shapes kernels/chain.hip is built for (ResNet-50 stages 1-2).
+# Stage 2's (N1 = 512) pairs measured no faster chained than as two launches
+# (each workgroup re-reads 256-384 KB of weights for 64 rows, one workgroup per
+# CU: profiles/round3/conv_chain.md), so by default only the stage-1 shapes are
+# chained; TFSERVE_CONV_CHAIN_SHAPES=all enables every kernel shape.
+CHAIN_SHAPES_ALL = {(64, 256, 64), (64, 256, 128), (128, 512, 128), (128, 512, 256)}
+CHAIN_SHAPES_DEFAULT = {(64, 256, 64), (64, 256, 128)}
 
 
 class ChainConv:
@@ -1049,6 +1054,7 @@ def fuse_conv_chain(g, order, fed, fetch_refs, device, opts):
     the op then runs both reference convs)."""
     import os
     mode = os.environ.get("TFSERVE_CONV_CHAIN", "1")
+    shapes = CHAIN_SHAPES_ALL if os.environ.get("TFSERVE_CONV_CHAIN_SHAPES") == "all" else CHAIN_SHAPES_DEFAULT
     c = _Ctx(g, order, fed, fetch_refs, device, opts)
     if mode == "0" or (not c.use_hip and mode != "force"):
         return
@@ -1069,7 +1075,7 @@ def fuse_conv_chain(g, order, fed, fetch_refs, device, opts):
             continue
         bnode = bs[0]
         b = bnode.attrs["_impl"]
-        if b.cin != a.cout or (a.cin, a.cout, b.cout) not in CHAIN_SHAPES:
+        if b.cin != a.cout or (a.cin, a.cout, b.cout) not in shapes:
             continue
         chain = ChainConv(a, b)
         p.op = "_ChainConv"

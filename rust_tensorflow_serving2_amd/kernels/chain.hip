@@ -20,7 +20,7 @@
 //   * phase 2: each wave stages its accumulators 16 rows x 64 columns at a time
 //     through a private fp32 LDS slab (no workgroup barrier), applies bias +
 //     residual + act, stores Y1 with 16-B row chunks and writes the same bf16
-//     chunk into the LDS chain tile; the first W2 ring slots are in flight;
+//     chunk into the LDS chain tile;
 //   * phase 3: Y1(LDS) x W2(ring) on a 2 x 2 wave grid, then the Y2 epilogue
 //     through the same per-wave slab.
 // Y2 is computed from the bf16 Y1 values, exactly what the separate reduce
@@ -57,8 +57,10 @@ struct CH {
   static constexpr int STG = 4 * 16 * kStgLd * 4;              // one 16-row slab per wave
   static constexpr int S2 = N2 <= 128 ? 3 : 2;                 // W2 ring depth
   static constexpr int W2_SLOT = N2 * KT * 2;
-  static constexpr int RING_OFF = CHAIN + STG;
-  static constexpr int P23 = RING_OFF + S2 * W2_SLOT;
+  // the W2 ring and the per-wave epilogue slabs share one region (the ring is
+  // idle during both epilogues): 80 KB for the stage-1 shapes = 2 workgroups per CU
+  static constexpr int RING_OFF = CHAIN;
+  static constexpr int P23 = CHAIN + (STG > S2 * W2_SLOT ? STG : S2 * W2_SLOT);
   static constexpr int LDS = P1 > P23 ? P1 : P23;
   static constexpr int WN1 = N1 / 4, TN1 = WN1 / 16, U1 = WN1 / 64;   // GEMM1: wave = 64 rows x WN1
   static constexpr int WN2 = N2 / 2, TN2 = WN2 / 16;                  // GEMM2: wave = 32 rows x WN2
@@ -166,7 +168,6 @@ __global__ __launch_bounds__(256, 1) void conv_chain_kernel(ChainArgs p) {
   }
   __syncthreads();   // every wave is done with the phase-1 images
 
-  // ---- W2 ring prologue (lands while epilogue 1 runs)
   auto issue_w2 = [&](int kt2, int slot) {
 #pragma unroll
     for (int j = 0; j < G::W2PW; ++j) {
@@ -177,9 +178,6 @@ __global__ __launch_bounds__(256, 1) void conv_chain_kernel(ChainArgs p) {
                                                16, v, 0, 0, 0);
     }
   };
-#pragma unroll
-  for (int s = 0; s < G::S2 - 1; ++s)
-    if (s < G::KT2) issue_w2(s, s);
 
   // ---- epilogue 1 through this wave's fp32 slab
   float* stg = reinterpret_cast<float*>(smem + G::CHAIN) + wid * 16 * kStgLd;
@@ -234,6 +232,11 @@ __global__ __launch_bounds__(256, 1) void conv_chain_kernel(ChainArgs p) {
   const uint32_t rb0 = uint32_t(((wn2 * G::WN2 + fr) * KT + ((fq ^ (fr & 7)) * 8)) * 2);
   const uint32_t rb1 = uint32_t(((wn2 * G::WN2 + fr) * KT + (((4 + fq) ^ (fr & 7)) * 8)) * 2);
   constexpr int S = G::S2;
+  // ---- W2 ring prologue, once every wave is done with its slab (same region)
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < G::S2 - 1; ++s)
+    if (s < G::KT2) issue_w2(s, s);
   // the ring prologue landed and the Y1 stores are drained (a workgroup-scope
   // __syncthreads waits for LDS only, and stores may complete out of order
   // with the DMAs), every wave's chain-tile writes are visible: from here on
@@ -271,7 +274,8 @@ __global__ __launch_bounds__(256, 1) void conv_chain_kernel(ChainArgs p) {
     }
   }
 
-  // ---- epilogue 2 (the slab region is disjoint from the ring and the chain tile)
+  // ---- epilogue 2 (its slabs overlay the ring: every wave is done reading it)
+  __syncthreads();
   constexpr int CPR2 = G::UW2 / 8;                  // chunks per slab row (4 or 8)
   constexpr int IT2 = 16 * CPR2 / 64;               // items per lane (1 or 2)
 #pragma unroll

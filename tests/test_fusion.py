@@ -172,6 +172,7 @@ def test_conv_chain_pass_pairs_expand_with_next_reduce(models_dir, monkeypatch):
     interpreter."""
     from rust_tensorflow_serving2_amd.models import resnet
     monkeypatch.setenv("TFSERVE_CONV_CHAIN", "force")     # the pass is GPU-only by default
+    monkeypatch.setenv("TFSERVE_CONV_CHAIN_SHAPES", "all")
     path = os.path.join(str(models_dir), "chain_resnet", "1")
     resnet.export(path, blocks=(3, 4, 1, 1), width=64, num_classes=10, image_size=32, seed=5)
     ref, fused = _pair(path)
