@@ -135,13 +135,20 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
   // replay with this form.  Ablations after the change, b32 eager 35.5 us:
   // without the loads 30.1, the MFMAs 26.5, the pool 31.6, the conv-tile
   // stores 30.0, all four 12.6 -- profiles/round2/stem_ablate.log)
-  // (a bf16 request -- rounded on ingest exactly as cvt2 rounds below -- is
-  // read as 16-bit values and widened: the staged patch is the same bits)
+  // A bf16 request (rounded on ingest exactly as cvt2 rounds below) is read
+  // as the two aligned dwords covering the pixel's channels -- 2 loads per
+  // pixel instead of one per channel -- and its bf16 halves are staged as
+  // they are: the same patch bits as the fp32 path.  (The record count is
+  // rounded up to whole dwords: the last pixel's second dword may run 2 B past
+  // the tensor, inside its 512-B allocation granule.)
   constexpr uint32_t kEsz = XB16 ? 2u : 4u;
+  const long xbytes = long(p.N) * p.H * p.W * p.C * kEsz;
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(p.x), 0, int(long(p.N) * p.H * p.W * p.C * kEsz), 0x00020000);
+      const_cast<void*>(p.x), 0, int(XB16 ? (xbytes + 3) & ~3L : xbytes), 0x00020000);
   constexpr uint32_t kOff = 0x80000000u;
-  float pf[kSlots][4] = {};
+  float pf[XB16 ? 1 : kSlots][4] = {};
+  uint32_t pv[XB16 ? kSlots : 1][2] = {};
+  uint32_t podd[XB16 ? kSlots : 1] = {};
   auto load_patch = [&](int t) {
     const int n = t / (p.tiles_y * p.tiles_x);
     const int rem = t - n * p.tiles_y * p.tiles_x;
@@ -154,14 +161,19 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
       const int r = q / kIC, c = q - r * kIC;
       const int gy = iy0 + r, gx = ix0 + c;
       const bool ok = q < kPatch && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W;
-      const uint32_t pix = uint32_t(((n * p.H + gy) * p.W + gx) * p.C) * kEsz;
+      if constexpr (XB16) {
+        const uint32_t e0 = uint32_t(((n * p.H + gy) * p.W + gx) * p.C);
+        const uint32_t base = (e0 & ~1u) * 2u;
+        pv[s][0] = __builtin_amdgcn_raw_buffer_load_b32(rsX, ok ? base : kOff, 0, 0);
+        pv[s][1] = __builtin_amdgcn_raw_buffer_load_b32(rsX, ok ? base + 4u : kOff, 0, 0);
+        podd[s] = e0 & 1u;
+      } else {
+        const uint32_t pix = uint32_t(((n * p.H + gy) * p.W + gx) * p.C) * kEsz;
 #pragma unroll
-      for (int ch = 0; ch < 4; ++ch) {
-        const uint32_t voff = ok && ch < p.C ? pix + uint32_t(ch) * kEsz : kOff;
-        if constexpr (XB16)
-          pf[s][ch] = __uint_as_float(uint32_t(__builtin_amdgcn_raw_buffer_load_b16(rsX, voff, 0, 0)) << 16);
-        else
+        for (int ch = 0; ch < 4; ++ch) {
+          const uint32_t voff = ok && ch < p.C ? pix + uint32_t(ch) * kEsz : kOff;
           pf[s][ch] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsX, voff, 0, 0));
+        }
       }
     }
   };
@@ -176,7 +188,15 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
       const int q = tid + s * 256;
-      if (q < kPatch) patch[q] = make_uint2(cvt2(pf[s][0], pf[s][1]), cvt2(pf[s][2], pf[s][3]));
+      if constexpr (XB16) {
+        // halves h0..h3 cover elements (e0 & ~1) .. +3: channels start at h[odd]
+        const uint64_t v = (uint64_t(pv[s][1]) << 32) | pv[s][0];
+        uint64_t c4 = v >> (16 * podd[s]);
+        c4 &= p.C >= 4 ? ~0ull : (1ull << (16 * p.C)) - 1ull;      // channels >= C are zero
+        if (q < kPatch) patch[q] = make_uint2(uint32_t(c4), uint32_t(c4 >> 32));
+      } else {
+        if (q < kPatch) patch[q] = make_uint2(cvt2(pf[s][0], pf[s][1]), cvt2(pf[s][2], pf[s][3]));
+      }
     }
     __syncthreads();
     if (t + 1 < t_end && !(dbg & 1)) load_patch(t + 1);   // in flight during the MFMAs

@@ -794,3 +794,17 @@ def test_halo_conv_is_deterministic(cfg):
     ys = [hip().conv2d(x, wp, b, None, 3, 3, 1, 1, 1, 1, 1, 1, act=ACT["relu"], cfg=cfg) for _ in range(4)]
     for y in ys[1:]:
         assert torch.equal(y, ys[0])
+
+
+@pytest.mark.parametrize("n,h,w,c", [(2, 224, 224, 3), (1, 33, 35, 3), (1, 17, 19, 1), (1, 21, 23, 4)])
+def test_stem_pool_bf16_input_is_bit_identical(n, h, w, c):
+    """The stem reading a request converted to bf16 on ingest (two dword loads
+    per pixel, either parity, the tensor's last pixel included) gives exactly
+    the output of reading the fp32 request."""
+    x = rnd(n, h, w, c, seed=91) * 100.0
+    wt = rnd(64, 224, scale=0.05, seed=92).to(BF).to(DEV)
+    b = rnd(64, scale=0.1, seed=93).to(DEV)
+    args = (wt, b, 3, 3, 3, 3, ACT["relu"], 1, 1, 1, 1)
+    y32 = hip().stem_pool(x.to(DEV), *args)
+    y16 = hip().stem_pool(x.to(BF).to(DEV), *args)
+    assert torch.equal(y32, y16)
