@@ -99,6 +99,7 @@ class Program:
         self.graph = graph
         self.order = order
         self._ctx = O.Ctx(device)
+        self.free_after = plan_release(steps, n_slots, feed_slots, fetch_slots, const_slots)
 
     def run(self, feeds: Sequence) -> List:
         vals: List = [None] * self.n_slots
@@ -107,7 +108,7 @@ class Program:
         for slot, v in zip(self.feed_slots, feeds):
             vals[slot] = v
         ctx = self._ctx
-        for fn, node, in_slots, out_slots in self.steps:
+        for (fn, node, in_slots, out_slots), dead in zip(self.steps, self.free_after):
             try:
                 outs = fn(ctx, node, [vals[s] for s in in_slots])
             except (O.OpError, O.Unsupported):
@@ -117,7 +118,23 @@ class Program:
             for s, o in zip(out_slots, outs):
                 if s >= 0:
                     vals[s] = o
+            # activation memory plan: drop every value whose last reader was
+            # this step, so the allocator (and a HIP-graph capture's pool)
+            # reuses its block for later steps -- peak-live instead of the sum
+            # of all activations per captured graph
+            for s in dead:
+                vals[s] = None
         return [vals[s] for s in self.fetch_slots]
+
+    def activation_plan(self) -> Dict[str, int]:
+        """Values alive at once: peak under the release plan vs all computed."""
+        produced = sum(1 for _f, _n, _i, outs in self.steps for s in outs if s >= 0)
+        live, peak = 0, 0
+        for (_f, _n, _i, outs), dead in zip(self.steps, self.free_after):
+            live += sum(1 for s in outs if s >= 0)
+            peak = max(peak, live)
+            live -= len(dead)
+        return {"values": produced, "peak_live_values": peak}
 
     def feed_accepts_bf16(self, i: int) -> bool:
         """Whether feed ``i`` may be given as bf16 instead of fp32: every step
@@ -138,6 +155,26 @@ class Program:
         for _fn, node, _i, _o in self.steps:
             h[node.op] = h.get(node.op, 0) + 1
         return h
+
+
+def plan_release(steps, n_slots: int, feed_slots, fetch_slots, const_slots) -> List[List[int]]:
+    """Per step, the value slots whose last use it is (liveness over the linear
+    step list): computed values that are not fetched, plus outputs nobody reads
+    (dropped right after their producer).  Feeds and constants belong to the
+    caller / the program and are never released."""
+    keep = set(fetch_slots) | set(feed_slots) | {s for s, _v in const_slots}
+    last: Dict[int, int] = {}
+    for i, (_fn, _node, ins, outs) in enumerate(steps):
+        for s in outs:
+            if s >= 0:
+                last.setdefault(s, i)
+        for s in ins:
+            last[s] = i
+    free: List[List[int]] = [[] for _ in steps]
+    for s, i in last.items():
+        if s not in keep:
+            free[i].append(s)
+    return free
 
 
 def _fold(g: Graph, order: List[str], fed: Set[str]) -> None:

@@ -186,3 +186,24 @@ def test_conv_chain_pass_pairs_expand_with_next_reduce(models_dir, monkeypatch):
     convs = 3 * 9 + 4                                     # 9 blocks x 3 + 4 projections (the stem is in _StemPool)
     assert hist["_StemPool"] == 1
     assert hist["_FusedConv2D"] + 2 * hist["_ChainConv"] + 2 * hist.get("_FusedDualConv", 0) == convs, hist
+
+
+def test_activation_release_plan(tiny_resnet_path):
+    """The program drops each value after its last reader (compile-time
+    liveness): results are unchanged and far fewer values are alive at once."""
+    from rust_tensorflow_serving2_amd.graph.compiler import plan_release
+    fused = Servable("m", 1, os.path.join(tiny_resnet_path, "1"), ServableOptions(device="cpu", fuse=True))
+    prog = fused.runner("serving_default", ["input"], ["classes", "probabilities"]).program
+    plan = prog.activation_plan()
+    assert plan["peak_live_values"] <= 4 < plan["values"], plan
+    # no fetched, fed or constant slot is ever released
+    keep = set(prog.fetch_slots) | set(prog.feed_slots) | {s for s, _v in prog.const_slots}
+    assert not keep & {s for dead in prog.free_after for s in dead}
+    x = np.random.default_rng(3).random((2, 32, 32, 3), dtype=np.float32)
+    import torch
+    a = [t.clone() if hasattr(t, "clone") else t for t in prog.run([torch.from_numpy(x)])]
+    prog.free_after = [[] for _ in prog.steps]            # keep everything: the old behaviour
+    b = prog.run([torch.from_numpy(x)])
+    for u, v in zip(a, b):
+        np.testing.assert_array_equal(np.asarray(u), np.asarray(v))
+    assert plan_release([], 0, [], [], []) == []
