@@ -150,10 +150,14 @@ class Program:
                 return False
         return bool(users)
 
-    def op_histogram(self) -> Dict[str, int]:
+    def op_histogram(self, flat: bool = False) -> Dict[str, int]:
+        """Steps per op; ``flat``: count the member ops of block ops (``_FlowBlock``)
+        instead of the blocks."""
         h: Dict[str, int] = {}
         for _fn, node, _i, _o in self.steps:
-            h[node.op] = h.get(node.op, 0) + 1
+            subs = getattr(node.attrs.get("_impl"), "subs", None) if flat else None
+            for op in ([sub[1].op for sub in subs] if subs else [node.op]):
+                h[op] = h.get(op, 0) + 1
         return h
 
 

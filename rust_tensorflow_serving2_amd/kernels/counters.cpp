@@ -10,19 +10,19 @@
 namespace tfsk {
 
 namespace {
-constexpr int kPoolInts = 1 << 20;   // 4 MB per device
-// Only used with TFSERVE_SPLITK_FIXUP=1 (opt-in; the default split-K path
-// reduces in a second launch and needs no counters).
+constexpr int kPoolInts = 1 << 22;   // 16 MB per device
+// Used by the split-K fixup (TFSERVE_SPLITK_FIXUP=1, opt-in) and by the
+// control words of captured flow launches (flow.hip, kernels/flow.h).
 // [0, kCapInts): permanent slices for launches captured into HIP graphs (a
 // graph node keeps its counters for the graph's lifetime; slices are never
 // returned, so repeated captures -- tuning candidates, reloads, more buckets
-// or lanes -- use the 768K ints up, after which launches fall back to the
+// or lanes -- use the 3.75M ints up, after which launches fall back to the
 // reduce launch, logged once); [kCapInts, kPoolInts): a ring for eager
 // launches (autotuning, warm-up), reused cyclically.  A maximal take (32K
 // ints) wraps the 256K-int ring after 8 launches; reuse is still safe because
 // eager launches are stream-ordered and counters return to zero when a
 // tile's last slice arrives, before the next launch on the stream starts.
-constexpr int kCapInts = 3 << 18;
+constexpr int kCapInts = 15 << 18;
 struct Pool {
   int* base = nullptr;
   int used = 0;

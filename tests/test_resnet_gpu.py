@@ -55,7 +55,7 @@ def test_resnet50_gpu_matches_cpu(resnet50):
     # bucket 4 vs bucket 8 may pick different tile/split-K configs -> fp32 summation order differs
     np.testing.assert_allclose(g2["probabilities"], g["probabilities"][:3], atol=2e-4)
     runner = next(iter(gpu._runners.values()))
-    hist = runner.program.op_histogram()
+    hist = runner.program.op_histogram(flat=True)
     # 53 convs: 4 stage-entry (expand conv + projection shortcut) pairs run as
     # one K-concatenated dual-source GEMM each
     # the stem conv runs inside the fused stem + max-pool kernel
@@ -88,7 +88,7 @@ def test_resnet50_v2_gpu_fully_fused_matches_cpu(resnet50_v2):
     np.testing.assert_allclose(g["probabilities"].sum(1), 1.0, atol=1e-4)
     _check_logits_and_classes(g, c)
     runner = next(iter(gpu._runners.values()))
-    hist = runner.program.op_histogram()
+    hist = runner.program.op_histogram(flat=True)
     for op in ("FusedBatchNormV3", "Relu", "Mul", "Conv2D", "AddV2"):
         assert op not in hist, hist
     assert hist.get("_StemPool") == 1 and "_MaxPool" not in hist
