@@ -47,7 +47,8 @@ _ALIGN = 256
 
 
 def max_batch() -> int:
-    """Largest batch that runs as one persistent launch (TFSERVE_FLOW_MAX_BATCH)."""
+    """Largest batch that runs as one persistent launch (TFSERVE_FLOW_MAX_BATCH;
+    larger batches run the block's member ops one by one)."""
     return int(os.environ.get("TFSERVE_FLOW_MAX_BATCH", "4"))
 
 
@@ -80,7 +81,8 @@ def pick_splits(tiles: int, nk: int, target: int) -> Tuple[int, int]:
     """(splits, k-tiles per split): K-slices until the layer has ~``target``
     tasks, keeping at least two k-tiles per slice."""
     s = 1
-    while s < 16 and tiles * s * 2 <= target and nk // (s * 2) >= 2:
+    cap = int(os.environ.get("TFSERVE_FLOW_MAX_SPLITS", "1"))
+    while s < cap and tiles * s * 2 <= target and nk // (s * 2) >= 2:
         s *= 2
     per = -(-nk // s)
     return -(-nk // per), per
@@ -251,9 +253,10 @@ class FlowBlock:
             if hit is None:
                 props = torch.cuda.get_device_properties(x.device)
                 cus = int(getattr(props, "multi_processor_count", 256))
-                hit = self.build_table(tuple(x.shape), target_tasks=cus)
+                target = int(os.environ.get("TFSERVE_FLOW_TARGET", str(cus)))
+                hit = self.build_table(tuple(x.shape), target_tasks=target)
                 hit["table_dev"] = torch.from_numpy(hit["table"]).to(x.device)
-                mult = float(os.environ.get("TFSERVE_FLOW_GRID_MULT", "2"))
+                mult = float(os.environ.get("TFSERVE_FLOW_GRID_MULT", "1"))
                 hit["grid"] = max(1, min(hit["ntasks"], int(cus * mult)))
                 last = next(s for s in hit["steps"] if s["out"] == self.exit_id)
                 hit["out_shape"] = (int(x.shape[0]), last["Ho"], last["Wo"], last["N"])
@@ -262,7 +265,7 @@ class FlowBlock:
 
     def enabled_for(self, x) -> bool:
         return (self.use_hip and isinstance(x, torch.Tensor) and x.is_cuda and x.dim() == 4 and
-                x.dtype == BF16 and x.shape[0] <= max_batch() and os.environ.get("TFSERVE_FLOW", "1") != "0")
+                x.dtype == BF16 and x.shape[0] <= max_batch())
 
     def run_flow(self, x, ctrl: Optional[torch.Tensor] = None):
         """One persistent launch.  ``ctrl``: zeroed int32 control words (the
@@ -328,9 +331,13 @@ def _region(g, c: _Ctx, names: List[str]):
 
 def fuse_flow(g, order, fed, fetch_refs, device, opts):
     """Maximal runs of flow-capable fused convs (consecutive in program order,
-    one input, one output) -> ``_FlowBlock`` (GPU programs; TFSERVE_FLOW=0
-    disables it, ``force`` builds it on CPU too, where it runs sequentially)."""
-    mode = os.environ.get("TFSERVE_FLOW", "1")
+    one input, one output) -> ``_FlowBlock``.  Opt-in (TFSERVE_FLOW=1 on GPU
+    programs; ``force`` builds it on CPU too, where it runs sequentially): on
+    MI355X the one-launch chain measured slower than the HIP-graph launch
+    chain it replaces at every batch (b1 0.417 vs 0.387 ms at its best knobs,
+    profiles/round3/flow.md), so the default program keeps the per-layer
+    kernels."""
+    mode = os.environ.get("TFSERVE_FLOW", "0")
     c = _Ctx(g, order, fed, fetch_refs, device, opts)
     if mode == "0" or (not c.use_hip and mode != "force"):
         return

@@ -68,14 +68,14 @@ __device__ __forceinline__ char* ref_ptr(int64_t r, char* arena, const char* ent
 
 // lane 0 only: wait until the wrapping counter *p has reached `target`
 // (false on timeout)
-__device__ __forceinline__ bool wait_count(int* p, uint32_t target) {
+__device__ __forceinline__ bool wait_count(int* p, uint32_t target, bool spin) {
   auto reached = [&] {
     return int(uint32_t(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - target) >= 0;
   };
   if (reached()) return true;
   const uint64_t t0 = wall_clock64();
   for (;;) {
-    __builtin_amdgcn_s_sleep(2);
+    if (!spin) __builtin_amdgcn_s_sleep(2);
     if (reached()) return true;
     if (wall_clock64() - t0 > kWaitTicks) return false;
   }
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(NT) void flow_kernel(const char* __restrict__ table
         dep_rows(P, rels[d], m0, m1, lo, hi);
         hi = min(hi, Q.ntm - 1);
         const uint32_t target = (epoch + 1u) * uint32_t(Q.ntn);
-        for (int b = lo; b <= hi; ++b) ok = wait_count(ctrl + Q.rctr + b * kFlowRowStride, target) && ok;
+        for (int b = lo; b <= hi; ++b) ok = wait_count(ctrl + Q.rctr + b * kFlowRowStride, target, dbg & 4) && ok;
       }
       if (!ok) __hip_atomic_store(ctrl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!(dbg & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(NT) void flow_kernel(const char* __restrict__ table
 }  // namespace
 
 // timing ablations (TFSERVE_FLOW_DBG, results are wrong with them): bit 0 skips
-// the acquire fence, bit 1 the dependency waits
+// the acquire fence, bit 1 the dependency waits; bit 2 polls without s_sleep
 int dbg_flags() {
   static const int v = [] {
     const char* e = getenv("TFSERVE_FLOW_DBG");

@@ -25,8 +25,21 @@ def r50_path(tmp_path_factory):
 
 @pytest.fixture(scope="module")
 def r50_gpu(r50_path):
+    """The flow pass is opt-in (TFSERVE_FLOW=1); K-slices on, so the in-kernel
+    split-K path is exercised too."""
     from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
-    return Servable("resnet", 1, r50_path, ServableOptions(device="cuda:0", max_batch_size=4))
+    old = {k: os.environ.get(k) for k in ("TFSERVE_FLOW", "TFSERVE_FLOW_MAX_SPLITS")}
+    os.environ.update(TFSERVE_FLOW="1", TFSERVE_FLOW_MAX_SPLITS="16")
+    try:
+        s = Servable("resnet", 1, r50_path, ServableOptions(device="cuda:0", max_batch_size=4))
+        s.runner("serving_default", ["input"], ["classes", "probabilities"])
+        yield s
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def _program(servable):
@@ -101,6 +114,7 @@ def test_flow_served_model_matches_cpu(r50_gpu, r50_path):
 def test_flow_disabled_runs_layer_kernels(r50_path, monkeypatch):
     """TFSERVE_FLOW_MAX_BATCH=0: the block runs its member ops one by one."""
     from rust_tensorflow_serving2_amd.graph import flow
+    monkeypatch.setenv("TFSERVE_FLOW", "1")
     monkeypatch.setenv("TFSERVE_FLOW_MAX_BATCH", "0")
     assert flow.max_batch() == 0
     from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions

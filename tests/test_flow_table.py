@@ -140,7 +140,8 @@ def _w(impl):
 
 
 @pytest.mark.parametrize("batch,target", [(1, 256), (2, 256), (3, 64)])
-def test_flow_table_interpreter_matches_fp32(batch, target):
+def test_flow_table_interpreter_matches_fp32(batch, target, monkeypatch):
+    monkeypatch.setenv("TFSERVE_FLOW_MAX_SPLITS", "16")
     block, ref, impls = _chain()
     x = torch.rand(batch, 12, 12, 64)
     tab = block.build_table(tuple(x.shape), target_tasks=target)
@@ -156,7 +157,9 @@ def test_flow_table_interpreter_matches_fp32(batch, target):
     torch.testing.assert_close(y.reshape(want.shape), want, rtol=1e-4, atol=1e-4)
 
 
-def test_pick_splits():
+def test_pick_splits(monkeypatch):
+    assert flow.pick_splits(16, 32, 256) == (1, 32)          # default: no K-slices (measured fastest)
+    monkeypatch.setenv("TFSERVE_FLOW_MAX_SPLITS", "16")
     assert flow.pick_splits(300, 64, 256) == (1, 64)
     assert flow.pick_splits(16, 32, 256) == (16, 2)
     assert flow.pick_splits(16, 3, 256) == (1, 3)
