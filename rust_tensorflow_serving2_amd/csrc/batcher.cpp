@@ -281,6 +281,37 @@ void Endpoint::abandon_stalled_locked(Slot& s) {
   }
 }
 
+int Endpoint::poll_slot_locked(int slot, Clock::time_point now, Clock::time_point& wake) {
+  Slot& s = slots_[slot];
+  if (s.state == kReady && s.reserved > 0 && s.copied == s.reserved) {
+    s.state = kRunning;
+    ++running_;
+    st_.batches++;
+    st_.rows += s.reserved;
+    return s.reserved;
+  }
+  if (s.state == kReady && s.reserved > 0) {
+    // rows still streaming in: give a stalled sender kStreamStall, then run without it
+    const auto stall = s.first + std::chrono::microseconds(timeout_us) + kStreamStall;
+    if (now >= stall) {
+      abandon_stalled_locked(s);
+      return -1;
+    }
+    wake = std::min(wake, stall);
+    return 0;
+  }
+  if (s.state == kOpen && s.reserved > 0) {
+    const auto due = s.first + std::chrono::microseconds(timeout_us);
+    if (now >= due || (idle_dispatch_ && running_ == 0 && s.copied == s.reserved)) {
+      s.state = kReady;
+      if (open_ == slot) open_ = -1;
+      return -1;
+    }
+    wake = std::min(wake, due);
+  }
+  return 0;
+}
+
 int Endpoint::acquire(int slot, int timeout_ms, std::vector<std::pair<int, int>>* ranges) {
   std::unique_lock<std::mutex> lk(mu_);
   if (slot < 0 || slot >= int(slots_.size())) return -1;
@@ -294,37 +325,47 @@ int Endpoint::acquire(int slot, int timeout_ms, std::vector<std::pair<int, int>>
       // hand the rows over now unless this already completes the batch
       if (!(s.state == kReady && s.reserved > 0 && s.copied == s.reserved)) return 0;
     }
-    if (s.state == kReady && s.reserved > 0 && s.copied == s.reserved) {
-      s.state = kRunning;
-      ++running_;
-      st_.batches++;
-      st_.rows += s.reserved;
-      return s.reserved;
-    }
-    if (s.state == kReady && s.reserved > 0) {
-      // rows still streaming in: give a stalled sender kStreamStall, then run without it
-      const auto stall = s.first + std::chrono::microseconds(timeout_us) + kStreamStall;
-      if (now >= stall) {
-        abandon_stalled_locked(s);
-        continue;
-      }
-      if (now >= deadline) return 0;
-      s.cv->wait_until(lk, std::min(stall, deadline));
-      continue;
-    }
-    if (s.state == kOpen && s.reserved > 0) {
-      const auto due = s.first + std::chrono::microseconds(timeout_us);
-      if (now >= due || (idle_dispatch_ && running_ == 0 && s.copied == s.reserved)) {
-        s.state = kReady;
-        if (open_ == slot) open_ = -1;
-        continue;
-      }
-      if (now >= deadline) return 0;
-      s.cv->wait_until(lk, std::min(due, deadline));
-      continue;
-    }
+    auto wake = deadline;
+    const int r = poll_slot_locked(slot, now, wake);
+    if (r > 0) return r;
+    if (r < 0) continue;
     if (now >= deadline) return 0;
-    s.cv->wait_until(lk, deadline);
+    s.cv->wait_until(lk, wake);
+  }
+  return -1;
+}
+
+void Endpoint::pair_slots(int a, int b) {
+  std::lock_guard<std::mutex> g(mu_);
+  const int N = int(slots_.size());
+  if (a < 0 || b < 0 || a >= N || b >= N || a == b) return;
+  slots_[b].cv = slots_[a].cv;
+}
+
+int Endpoint::acquire_any(int a, int b, int timeout_ms, int* which) {
+  std::unique_lock<std::mutex> lk(mu_);
+  const int N = int(slots_.size());
+  if (a < 0 || b < 0 || a >= N || b >= N) return -1;
+  const auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (!closed_) {
+    const auto now = Clock::now();
+    // the batch that opened first goes first (FIFO across the two slots)
+    const bool b_first = slots_[b].state != kFree && slots_[b].reserved > 0 &&
+                         (slots_[a].state == kFree || slots_[a].reserved == 0 || slots_[b].first < slots_[a].first);
+    const int order[2] = {b_first ? b : a, b_first ? a : b};
+    auto wake = deadline;
+    bool again = false;
+    for (int k = 0; k < 2; ++k) {
+      const int r = poll_slot_locked(order[k], now, wake);
+      if (r > 0) {
+        *which = order[k];
+        return r;
+      }
+      again = again || r < 0;
+    }
+    if (again) continue;
+    if (now >= deadline) return 0;
+    slots_[a].cv->wait_until(lk, wake);   // shared with b (pair_slots)
   }
   return -1;
 }
