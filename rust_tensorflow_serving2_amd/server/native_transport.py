@@ -91,10 +91,12 @@ class FastEndpoint:
                 # a double-buffered lane drives its twin's slot and graphs too
                 # (registered only here: a slot nobody acquires would strand calls)
                 t = twins.get(lane_idx)
-                spec2 = self.runner.native_lane_spec(t) if t is not None else None
-                if spec2 is not None:
-                    tin, tout = self.runner.lane_host_pointers(t)
-                    srv.set_slot_buffers(self.id, t, tin, tout)
+                spec2 = None
+                if t is not None:
+                    tin, tout = self.runner.lane_host_pointers(t)     # (captures the twin's graphs)
+                    spec2 = self.runner.native_lane_spec(t)
+                    if spec2 is not None:
+                        srv.set_slot_buffers(self.id, t, tin, tout)
                 if srv.start_native_lane(self.id, lane_idx, *spec, slot2=t if spec2 is not None else -1,
                                          buckets2=spec2[2] if spec2 is not None else []):
                     self.native_lanes += 1
