@@ -16,6 +16,8 @@
 // S in {64, 128, 192, 256} (the whole key row in registers; D == 64), and
 // attention_flash_kernel below for any other S up to
 // kMaxAttentionSeq.  The S x S matrix never touches HBM.
+#include <cstdlib>
+
 #include "common.h"
 #include "gemm_common.h"
 #include "launch.h"
@@ -380,10 +382,9 @@ __global__ __launch_bounds__(256) void attention_flash_kernel(const uint16_t* __
   }
 }
 
-template <int S>
+template <int S, int QB = qb_for(S)>
 hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, int H, float scale, long bs, long qs,
                     hipStream_t st) {
-  constexpr int QB = qb_for(S);
   constexpr int lds = (S * D + D * (S + 8) + (QB / 16) * 16 * (S + 8)) * 2;
   static_assert(S % QB == 0 && lds <= 160 * 1024, "attention tile");
   hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&attention_kernel<S, QB>), lds);
@@ -391,6 +392,14 @@ hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, 
   const int grid = B * H * (S / QB);
   hipLaunchKernelGGL((attention_kernel<S, QB>), dim3(grid), dim3(QB * 4), lds, st, qkv, mb, ctx, H, scale, bs, qs);
   return hipGetLastError();
+}
+
+int attn_qb() {
+  static const int v = [] {
+    const char* e = getenv("TFSERVE_ATTN_QB");
+    return e ? atoi(e) : 64;
+  }();
+  return v;
 }
 
 }  // namespace
@@ -401,7 +410,13 @@ hipError_t attention_launch(const uint16_t* qkv, const float* mask_bias, uint16_
   const long bs = mask_bstride, qs = mask_qstride;
   switch (S) {
     case 64: return launch_s<64>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
-    case 128: return launch_s<128>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
+    case 128:
+      // query rows per workgroup (TFSERVE_ATTN_QB: 32 / 64 / 128; experiments)
+      switch (attn_qb()) {
+        case 32: return launch_s<128, 32>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
+        case 128: return launch_s<128, 128>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
+        default: return launch_s<128>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
+      }
     case 192: return launch_s<192>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
     case 256: return launch_s<256>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
     default: {
