@@ -58,6 +58,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from rust_tensorflow_serving2_amd.utils import hip_env  # noqa: E402
+
+hip_env.apply()          # hardware queues for the lanes' streams (before HIP starts)
+
 METRIC = "Predict RPCs/sec + p50 latency, ResNet-50 batch=1/32 at 1/2/4/8 MI355X"
 PREDICT = "/tensorflow.serving.PredictionService/Predict"
 
