@@ -60,7 +60,9 @@ sys.path.insert(0, ROOT)
 
 from rust_tensorflow_serving2_amd.utils import hip_env  # noqa: E402
 
-hip_env.apply()          # hardware queues for the lanes' streams (before HIP starts)
+# hardware queues for the lanes' streams (before HIP starts); 4 for the
+# two-model config 5, whose 8 lanes thrash the caches with more
+hip_env.apply(default="4" if "multi" in sys.argv[1:] else "8")
 
 METRIC = "Predict RPCs/sec + p50 latency, ResNet-50 batch=1/32 at 1/2/4/8 MI355X"
 PREDICT = "/tensorflow.serving.PredictionService/Predict"

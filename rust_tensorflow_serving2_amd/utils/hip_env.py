@@ -9,6 +9,11 @@ the H2D / D2H copies) in ``scripts/probe_concurrency.py``, and the headline
 bench averaged 45.6k vs 40.8k RPC/s over four interleaved pairs on one box
 (``profiles/round3/hw_queues/``).
 
+With two models co-resident (8 lanes) the extra queues let more replays run
+at once than the caches hold: config 5 measured 31.0k vs 35.3k ResNet RPC/s
+and 25.3 vs 10.7 ms p99 during reloads (``profiles/round3/hw_queues/``), so
+callers serving several models pass ``default="4"``.
+
 ``TFSERVE_HW_QUEUES`` overrides the count (0 leaves the environment alone).
 Must run before anything initialises HIP (importing torch does not;
 ``torch.cuda`` calls do).
@@ -16,7 +21,7 @@ Must run before anything initialises HIP (importing torch does not;
 import os
 
 
-def apply() -> None:
-    want = os.environ.get("TFSERVE_HW_QUEUES", "8")
+def apply(default: str = "8") -> None:
+    want = os.environ.get("TFSERVE_HW_QUEUES", default)
     if want and want != "0":
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, int(want))))
