@@ -113,6 +113,13 @@ def parse():
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = CPU servables + gloo (multi-rank launcher tests without a GPU)")
     ap.add_argument("--no-pin", action="store_true", help="do not pin ranks to their GPU's NUMA-node CPUs")
+    ap.add_argument("--pin-threads", action="store_true",
+                    default=os.environ.get("TFSERVE_PIN_THREADS", "0") == "1",
+                    help="after start-up, give each IO / load-generator / lane thread a physical core of "
+                         "its own among the rank's CPUs, least-busy cores first (default off)")
+    ap.add_argument("--llc-groups", type=int, default=int(os.environ.get("TFSERVE_LLC_GROUPS", "0")),
+                    help="narrow the rank's CPUs to its N least-busy last-level-cache groups (CCDs) "
+                         "before pinning (0 = the whole NUMA-node share)")
     return ap.parse_args()
 
 
@@ -177,6 +184,8 @@ def main():
     # this rank (IO, lanes, load generator) inherits the mask
     from rust_tensorflow_serving2_amd.parallel import topology
     placement = topology.plan(local_world)[local]
+    if args.llc_groups > 0 and not args.no_pin:
+        placement.cpus = topology.pick_llcs(placement.cpus, args.llc_groups)
     pinned = False if args.no_pin else topology.pin(placement.cpus)
 
     import torch
@@ -321,9 +330,13 @@ def main():
                                if k in r1 and k in r0}
         return d
 
+    thread_pins = None
+    if args.pin_threads and pinned:
+        thread_pins = topology.pin_hot_threads(("tfs-loadgen", "tfs-h2io", "tfs-nlane"), placement.cpus)
     gpu_info = topology.gpus()
     busy = topology.BusySampler(gpu_info[local].bdf if on_gpu and local < len(gpu_info) else "").start()
     dc0, dio0, dru0, dt0 = topology.thread_cpu(), io_stats(), os.times(), time.perf_counter()
+    pre_contention = topology.HostContention(placement.cpus).start()
     t_pre = time.perf_counter()
     while time.perf_counter() - t_pre < args.prewarm_s:
         check(loadgen.window(64 * per_step, 600.0), "pre-warm")
@@ -331,10 +344,12 @@ def main():
     dsecs = time.perf_counter() - dt0
     diag_window = diag(dc0, topology.thread_cpu(), dio0, io_stats(), dru0, os.times(), dsecs)
     diag_window["window_s"] = round(dsecs, 3)
+    diag_window["host"] = pre_contention.stop()
     if world > 1:
         dist.barrier()
     dev_sync()
     cpu0, io0, ru0, tid0 = topology.thread_cpu(), io_stats(), os.times(), topology.thread_cpu_by_tid()
+    contention = topology.HostContention(placement.cpus).start()
     t0 = time.perf_counter()
     r = loadgen.window(args.steps * per_step, 600.0)
     dev_sync()
@@ -343,6 +358,11 @@ def main():
     elapsed = time.perf_counter() - t0
     cpu_report = diag(cpu0, topology.thread_cpu(), io0, io_stats(), ru0, os.times(), elapsed)
     cpu_report["top_threads"] = topology.top_threads(tid0, topology.thread_cpu_by_tid(), elapsed)
+    # other tenants: busy share of this rank's node / the host, run-queue wait, quota throttling
+    cpu_report["host"] = contention.stop()
+    cpu_report["host"]["threads_on"] = topology.thread_llcs(("tfs-loadgen", "tfs-h2io", "tfs-nlane"))
+    if thread_pins is not None:
+        cpu_report["thread_pins"] = thread_pins
     gpu_busy = busy.stop()
     loadgen.stop(30.0)
     check(r, "timed window")

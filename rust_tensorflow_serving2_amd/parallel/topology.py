@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -307,6 +308,200 @@ def thread_cpu_by_tid(pid: Optional[int] = None) -> Dict[int, Tuple[str, float]]
             with open(f"{base}/{tid}/schedstat") as f:
                 out[int(tid)] = (name, int(f.read().split()[0]) / 1e9)
         except (OSError, ValueError, IndexError):
+            continue
+    return out
+
+
+def runq_wait_by_tid(pid: Optional[int] = None) -> Dict[int, Tuple[str, float]]:
+    """{tid: (thread name, seconds spent runnable but waiting for a CPU)}:
+    schedstat's second field.  Time a busy thread waits on a run queue is CPU
+    contention (other tenants on its CPUs, or the cgroup quota throttling it)."""
+    out: Dict[int, Tuple[str, float]] = {}
+    base = f"/proc/{pid or os.getpid()}/task"
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"{base}/{tid}/comm") as f:
+                name = f.read().strip()
+            with open(f"{base}/{tid}/schedstat") as f:
+                out[int(tid)] = (name, int(f.read().split()[1]) / 1e9)
+        except (OSError, ValueError, IndexError):
+            continue
+    return out
+
+
+def runq_wait_by_group(before: Dict[int, Tuple[str, float]], after: Dict[int, Tuple[str, float]],
+                       elapsed: float) -> Dict[str, float]:
+    """Run-queue wait per thread group over a window, as a fraction of the
+    window summed over the group's threads (1.0 = one thread waited the whole
+    window)."""
+    groups: Dict[str, float] = {}
+    for tid, (name, v) in after.items():
+        g = name.rstrip("0123456789")
+        groups[g] = groups.get(g, 0.0) + v - before.get(tid, (name, 0.0))[1]
+    return {k: round(v / max(elapsed, 1e-9), 3) for k, v in sorted(groups.items(), key=lambda x: -x[1])
+            if v / max(elapsed, 1e-9) >= 0.001}
+
+
+def cpu_times(root: str = "/") -> Dict[int, Tuple[int, int]]:
+    """{cpu: (busy jiffies, total jiffies)} of every CPU of the host, from
+    /proc/stat (it shows the whole machine, other tenants included)."""
+    out: Dict[int, Tuple[int, int]] = {}
+    try:
+        with open(os.path.join(root, "proc/stat")) as f:
+            lines = f.readlines()
+    except OSError:
+        return out
+    for ln in lines:
+        if not ln.startswith("cpu") or ln.startswith("cpu "):
+            continue
+        parts = ln.split()
+        try:
+            cpu = int(parts[0][3:])
+            v = [int(x) for x in parts[1:]]
+        except ValueError:
+            continue
+        idle = v[3] + (v[4] if len(v) > 4 else 0)           # idle + iowait
+        total = sum(v[:8])                                     # guest time is already inside user
+        out[cpu] = (total - idle, total)
+    return out
+
+
+def busy_fraction(before: Dict[int, Tuple[int, int]], after: Dict[int, Tuple[int, int]],
+                  cpus: Optional[Sequence[int]] = None) -> Optional[float]:
+    """Busy share of ``cpus`` (default: all) between two cpu_times() snapshots."""
+    keys = [c for c in (cpus if cpus is not None else after.keys()) if c in before and c in after]
+    busy = sum(after[c][0] - before[c][0] for c in keys)
+    total = sum(after[c][1] - before[c][1] for c in keys)
+    return round(busy / total, 3) if total > 0 else None
+
+
+def cgroup_throttling() -> Dict[str, int]:
+    """cgroup-v2 ``cpu.stat`` counters (nr_periods, nr_throttled, throttled_usec)."""
+    out: Dict[str, int] = {}
+    v = _read("/sys/fs/cgroup/cpu.stat")
+    for ln in (v or "").splitlines():
+        k, _, n = ln.partition(" ")
+        if k in ("nr_periods", "nr_throttled", "throttled_usec") and n.strip().isdigit():
+            out[k] = int(n)
+    return out
+
+
+class HostContention:
+    """What the rest of the machine did to a window: busy share of this
+    process's NUMA-node CPUs and of the whole host (other tenants included),
+    run-queue wait of this process's threads, and cgroup quota throttling."""
+
+    def __init__(self, cpus: Optional[Sequence[int]] = None):
+        self.cpus = list(cpus) if cpus else None
+
+    def start(self) -> "HostContention":
+        self.t0 = time.perf_counter()
+        self.ct0, self.rq0, self.th0 = cpu_times(), runq_wait_by_tid(), cgroup_throttling()
+        return self
+
+    def stop(self) -> dict:
+        secs = time.perf_counter() - self.t0
+        ct1, rq1, th1 = cpu_times(), runq_wait_by_tid(), cgroup_throttling()
+        d = {"host_busy": busy_fraction(self.ct0, ct1),
+             "node_busy": busy_fraction(self.ct0, ct1, self.cpus) if self.cpus else None,
+             "runq_wait": runq_wait_by_group(self.rq0, rq1, secs)}
+        if th1 and self.th0:
+            d["throttled_periods"] = th1.get("nr_throttled", 0) - self.th0.get("nr_throttled", 0)
+            d["throttled_ms"] = round((th1.get("throttled_usec", 0) - self.th0.get("throttled_usec", 0)) / 1e3, 1)
+        return d
+
+
+def llc_groups(cpus: Sequence[int], root: str = "/") -> List[List[int]]:
+    """``cpus`` grouped by last-level cache (``cache/index3/shared_cpu_list``:
+    one group per CCD on EPYC), groups in order of their lowest CPU."""
+    groups: Dict[int, List[int]] = {}
+    for c in cpus:
+        s = _read(os.path.join(root, f"sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list"))
+        key = min(parse_cpulist(s)) if s else -1
+        groups.setdefault(key, []).append(c)
+    return [sorted(v) for _k, v in sorted(groups.items())]
+
+
+def pick_llcs(cpus: Sequence[int], n: int, sample_s: float = 0.2, root: str = "/") -> List[int]:
+    """The CPUs of the ``n`` least-busy last-level-cache groups among ``cpus``
+    (busy share over a ``sample_s`` look at /proc/stat, other tenants included).
+    A loopback benchmark moves every 602 KB request from the load generator's
+    core to an IO thread's core: inside one L3 that copy stays on-die, across
+    CCDs it goes through the fabric."""
+    groups = llc_groups(cpus, root)
+    if n <= 0 or n >= len(groups):
+        return sorted(cpus)
+    a = cpu_times(root)
+    time.sleep(sample_s)
+    b = cpu_times(root)
+    groups.sort(key=lambda g: (busy_fraction(a, b, g) or 0.0, g[0]))
+    return sorted(c for g in groups[:n] for c in g)
+
+
+def thread_llcs(prefixes: Sequence[str], root: str = "/") -> Dict[str, object]:
+    """Where this process's hot threads last ran: {"cpus": {name: cpu},
+    "llcs": distinct last-level caches among them}."""
+    where: Dict[str, int] = {}
+    base = f"/proc/{os.getpid()}/task"
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        tids = []
+    for tid in tids:
+        try:
+            with open(f"{base}/{tid}/comm") as f:
+                name = f.read().strip()
+            if not any(name.startswith(p) for p in prefixes):
+                continue
+            with open(f"{base}/{tid}/stat") as f:
+                fields = f.read().rsplit(")", 1)[1].split()
+            where[f"{name}/{tid}"] = int(fields[36])       # field 39: CPU last run on
+        except (OSError, ValueError, IndexError):
+            continue
+    llcs = set()
+    for c in where.values():
+        s = _read(os.path.join(root, f"sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list"))
+        llcs.add(min(parse_cpulist(s)) if s else c)
+    return {"cpus": dict(sorted(where.items())), "llcs": len(llcs)}
+
+
+def pin_hot_threads(prefixes: Sequence[str], cpus: Sequence[int], sample_s: float = 0.2,
+                    root: str = "/") -> Dict[str, int]:
+    """Give each thread of this process whose name starts with one of
+    ``prefixes`` a physical core of its own, from ``cpus``: cores whose
+    hardware threads were least busy over a ``sample_s`` look at /proc/stat
+    first (other tenants included), one hardware thread per hot thread.
+    Returns {"tid name": cpu}."""
+    a = cpu_times(root)
+    time.sleep(sample_s)
+    b = cpu_times(root)
+    cores: Dict[int, List[int]] = {}
+    for c in cpus:
+        sib = _read(os.path.join(root, f"sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list"))
+        sibs = parse_cpulist(sib) if sib else [c]
+        cores.setdefault(min(sibs), []).append(c)
+
+    def load(core):
+        sib = _read(os.path.join(root, f"sys/devices/system/cpu/cpu{core}/topology/thread_siblings_list"))
+        sibs = parse_cpulist(sib) if sib else [core]
+        return busy_fraction(a, b, sibs) or 0.0
+
+    order = sorted(cores, key=lambda k: (load(k), k))
+    hot = [(tid, name) for tid, (name, _v) in sorted(thread_cpu_by_tid().items())
+           if any(name.startswith(p) for p in prefixes)]
+    out: Dict[str, int] = {}
+    for i, (tid, name) in enumerate(hot):
+        if not order:
+            break
+        cpu = cores[order[i % len(order)]][0]
+        try:
+            os.sched_setaffinity(tid, {cpu})
+            out[f"{tid} {name}"] = cpu
+        except (OSError, ValueError):
             continue
     return out
 

@@ -132,6 +132,35 @@ def test_topology_visible_devices_and_rehearsal(tmp_path, monkeypatch):
     assert r and r["mean"] == 42.0
 
 
+def test_host_contention_probes(tmp_path):
+    """/proc/stat busy shares, run-queue wait and the per-thread core pinning
+    bench.py reports / applies (``--pin-threads``)."""
+    proc = tmp_path / "proc"
+    proc.mkdir()
+    (proc / "stat").write_text("cpu  10 0 10 80 0 0 0 0 0 0\n"
+                               "cpu0 10 0 0 30 0 0 0 0 0 0\n"
+                               "cpu1 0 0 10 50 0 0 0 0 0 0\nintr 1 2\n")
+    a = topology.cpu_times(str(tmp_path))
+    assert a == {0: (10, 40), 1: (10, 60)}
+    b = {0: (30, 60), 1: (10, 80)}                       # cpu0 fully busy since, cpu1 idle
+    assert topology.busy_fraction(a, b) == 0.5
+    assert topology.busy_fraction(a, b, [0]) == 1.0 and topology.busy_fraction(a, b, [1]) == 0.0
+    hc = topology.HostContention(sorted(os.sched_getaffinity(0))).start()
+    sum(i * i for i in range(200000))
+    d = hc.stop()
+    assert d["host_busy"] is None or 0.0 <= d["host_busy"] <= 1.0
+    assert isinstance(d["runq_wait"], dict)
+    before = os.sched_getaffinity(0)
+    try:
+        with open("/proc/self/comm") as f:
+            me = f.read().strip()
+        pins = topology.pin_hot_threads((me,), sorted(before), sample_s=0.02)
+        mine = [cpu for k, cpu in pins.items() if k.startswith(f"{os.getpid()} ")]
+        assert mine and mine[0] in before and os.sched_getaffinity(0) == {mine[0]}
+    finally:
+        os.sched_setaffinity(0, before)
+
+
 def test_cpulist_roundtrip():
     assert topology.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
     assert topology.compress([0, 1, 2, 3, 8, 10, 11]) == "0-3,8,10-11"
