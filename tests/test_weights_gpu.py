@@ -31,7 +31,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, backend, port, path, out_q, regroup=False):
+def _worker(rank, world, backend, port, path, out_q, regroup=False, own_gpu=False):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from rust_tensorflow_serving2_amd import ops
@@ -39,7 +39,7 @@ def _worker(rank, world, backend, port, path, out_q, regroup=False):
     from rust_tensorflow_serving2_amd.parallel.weights import ReplicatedWeightSource
     from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
     try:
-        dev = torch.device("cuda", 0)
+        dev = torch.device("cuda", rank if own_gpu else 0)
         torch.cuda.set_device(dev)
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         kw = {"device_id": dev} if backend == "nccl" else {}
@@ -47,7 +47,7 @@ def _worker(rank, world, backend, port, path, out_q, regroup=False):
         ws = ReplicatedWeightSource(dist.distributed_c10d._get_default_store(), device=dev, load_timeout=300)
         h2d0 = placement.H2D_BYTES
         b = ws.load("resnet", 1, path)
-        s = Servable("resnet", 1, path, ServableOptions(device="cuda:0", max_batch_size=4,
+        s = Servable("resnet", 1, path, ServableOptions(device=str(dev), max_batch_size=4,
                                                          allowed_batch_sizes=(4,)), b, weight_source=ws)
         x = np.random.default_rng(7).random((4, 224, 224, 3), dtype=np.float32)
         out = s.run("serving_default", {"input": x}, ["classes", "probabilities"])
@@ -62,7 +62,7 @@ def _worker(rank, world, backend, port, path, out_q, regroup=False):
             store.add("tfs/gen", 1)
             b0 = res["bcast"]
             b2 = ws.load("resnet", 2, path)
-            s2 = Servable("resnet", 2, path, ServableOptions(device="cuda:0", max_batch_size=4,
+            s2 = Servable("resnet", 2, path, ServableOptions(device=str(dev), max_batch_size=4,
                                                               allowed_batch_sizes=(4,)), b2, weight_source=ws)
             out2 = s2.run("serving_default", {"input": x}, ["classes", "probabilities"])
             res.update(gen=ws.gen, regroups=ws.stats.get("regroups", 0),
@@ -77,11 +77,11 @@ def _worker(rank, world, backend, port, path, out_q, regroup=False):
         out_q.put((rank, {"error": f"{e}\n{traceback.format_exc()}"}))
 
 
-def _run(world, backend, path, regroup=False):
+def _run(world, backend, path, regroup=False, own_gpu=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, backend, port, path, q, regroup)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, backend, port, path, q, regroup, own_gpu)) for r in range(world)]
     for p in ps:
         p.start()
     out = dict(q.get(timeout=300) for _ in ps)
@@ -128,3 +128,16 @@ def test_follower_binds_leader_blob_without_host_copies(r50):
     assert fol["h2d"] == 0                         # the follower: not one weight byte host -> device
     assert fol["bound"] >= 0.9 * lead["bcast"] and fol["bound"] > 20e6
     assert fol["tuned_here"] == 0 and fol["remote"] > 0     # the leader's tile picks, no own autotune
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL refuses two ranks on one GPU)")
+def test_rccl_world2_device_broadcast_two_gpus(r50):
+    """Two replicas on two GPUs over RCCL/xGMI, then a replica restart: the
+    follower binds the leader's blob from a device-to-device broadcast (no
+    host copy), both generations, bit-identical outputs."""
+    out = _run(2, "nccl", r50, regroup=True, own_gpu=True)
+    lead, fol = out[0], out[1]
+    np.testing.assert_array_equal(lead["probs"], fol["probs"])
+    np.testing.assert_array_equal(lead["probs2"], fol["probs2"])
+    assert fol["h2d"] == 0 and fol["bound"] > 20e6
+    assert lead["bcast2"] > 20e6 and fol["regroups"] >= 1 and fol["pg"] == "ProcessGroupNCCL"
