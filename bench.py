@@ -352,11 +352,14 @@ def main():
     diag_window["host"] = pre_contention.stop()
     if world > 1:
         dist.barrier()
+    t_s = time.perf_counter()
     dev_sync()
+    start_sync_ms = (time.perf_counter() - t_s) * 1e3
     cpu0, io0, ru0, tid0 = topology.thread_cpu(), io_stats(), os.times(), topology.thread_cpu_by_tid()
     contention = topology.HostContention(placement.cpus).start()
     t0 = time.perf_counter()
     r = loadgen.window(args.steps * per_step, 600.0)
+    t_last = time.perf_counter()
     dev_sync()
     if world > 1:
         dist.barrier()
@@ -364,6 +367,11 @@ def main():
     cpu_report = diag(cpu0, topology.thread_cpu(), io0, io_stats(), ru0, os.times(), elapsed)
     cpu_report["top_threads"] = topology.top_threads(tid0, topology.thread_cpu_by_tid(), elapsed)
     # other tenants: busy share of this rank's node / the host, run-queue wait, quota throttling
+    # the closing synchronize waits for the batches already in flight behind the
+    # last counted completion (the load generator never drains): its share of
+    # the window, which a short --steps window feels most
+    cpu_report["end_sync_ms"] = round((t0 + elapsed - t_last) * 1e3, 3)
+    cpu_report["start_sync_ms"] = round(start_sync_ms, 3)
     cpu_report["host"] = contention.stop()
     cpu_report["host"]["threads_on"] = topology.thread_llcs(("tfs-loadgen", "tfs-h2io", "tfs-nlane"))
     if thread_pins is not None:
