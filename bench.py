@@ -34,7 +34,9 @@ code.  Under torchrun ``--gpus`` must equal ``WORLD_SIZE``.
 
 Placement.  Every rank pins itself (before any thread exists) to a disjoint set
 of CPUs on its GPU's NUMA node (``parallel/topology.py``): its IO threads,
-lanes, pinned batch slots and load generator stay next to its GPU.
+lanes, pinned batch slots and load generator stay next to its GPU.  Within
+that share it keeps the two least-busy L3 groups (``--llc-groups``, default 2):
+the load generator's request copies then stay on-die.
 
 Diagnostics (always on).  Over a diagnostic window -- the pre-warm + warmup
 traffic, >= 1 s, long enough to be meaningful when the timed window is only a
