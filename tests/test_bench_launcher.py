@@ -161,6 +161,27 @@ def test_host_contention_probes(tmp_path):
         os.sched_setaffinity(0, before)
 
 
+def test_llc_groups_and_pick(tmp_path):
+    """L3 groups from cache/index3/shared_cpu_list; pick_llcs keeps the
+    least-busy groups (per /proc/stat) and returns everything when asked for
+    as many groups as exist."""
+    cpus = list(range(8))
+    for c in cpus:
+        d = tmp_path / f"sys/devices/system/cpu/cpu{c}/cache/index3"
+        d.mkdir(parents=True)
+        lo = (c // 4) * 4
+        (d / "shared_cpu_list").write_text(f"{lo}-{lo + 3}\n")
+    assert topology.llc_groups(cpus, str(tmp_path)) == [[0, 1, 2, 3], [4, 5, 6, 7]]
+    assert topology.pick_llcs(cpus, 2, root=str(tmp_path)) == cpus
+    assert topology.pick_llcs(cpus, 0, root=str(tmp_path)) == cpus
+    (tmp_path / "proc").mkdir()
+    (tmp_path / "proc/stat").write_text("".join(f"cpu{c} 0 0 0 100 0 0 0 0\n" for c in cpus))
+    # a static /proc/stat reads as idle everywhere: ties go to the lowest group
+    assert topology.pick_llcs(cpus, 1, sample_s=0.0, root=str(tmp_path)) == [0, 1, 2, 3]
+    on = topology.thread_llcs(("no-such-thread",), root=str(tmp_path))
+    assert on == {"cpus": {}, "llcs": 0}
+
+
 def test_cpulist_roundtrip():
     assert topology.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
     assert topology.compress([0, 1, 2, 3, 8, 10, 11]) == "0-3,8,10-11"
