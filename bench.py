@@ -62,9 +62,29 @@ sys.path.insert(0, ROOT)
 
 from rust_tensorflow_serving2_amd.utils import hip_env  # noqa: E402
 
-# hardware queues for the lanes' streams (before HIP starts); 4 for the
-# two-model config 5, whose 8 lanes thrash the caches with more
-hip_env.apply(default="4" if "multi" in sys.argv[1:] else "8")
+
+
+def _hw_queues_default() -> str:
+    """Hardware queues for the lanes' streams (set before HIP starts): 8 for
+    one server per GPU; 4 for the two-model config 5, whose 8 lanes thrash the
+    caches with more; and 8 / ranks-per-GPU when ranks share a GPU (the
+    one-GPU rehearsal of --gpus N), so the processes' queues together stay
+    within what the GPU's scheduler runs without time-slicing them (2 ranks at
+    8 queues each measured 15.0k RPC/s in total, GPU 100 % busy, against 41.5k
+    with 4 each earlier in the round: profiles/round3/rehearsal_queues/,
+    profiles/round3/bench2_gloo_rehearsal_final.log)."""
+    if "multi" in sys.argv[1:]:
+        return "4"
+    n = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")) or 1)
+    if n > 1:
+        from rust_tensorflow_serving2_amd.parallel import topology
+        share = -(-n // max(1, len(topology.gpus())))
+        if share > 1:
+            return str(max(2, 8 // share))
+    return "8"
+
+
+hip_env.apply(default=_hw_queues_default())
 
 METRIC = "Predict RPCs/sec + p50 latency, ResNet-50 batch=1/32 at 1/2/4/8 MI355X"
 PREDICT = "/tensorflow.serving.PredictionService/Predict"
