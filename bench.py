@@ -63,7 +63,6 @@ sys.path.insert(0, ROOT)
 from rust_tensorflow_serving2_amd.utils import hip_env  # noqa: E402
 
 
-
 def _hw_queues_default() -> str:
     """Hardware queues for the lanes' streams (set before HIP starts): 8 for
     one server per GPU; 4 for the two-model config 5, whose 8 lanes thrash the
