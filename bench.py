@@ -155,13 +155,32 @@ def launch_ranks(args) -> int:
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
+    def die_with_parent():
+        # the child gets SIGTERM when the launcher dies, however it dies (this
+        # runs in the forked child before exec; the launcher never touches HIP)
+        import ctypes
+        try:
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))   # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
-                                      start_new_session=True))
+                                      start_new_session=True, preexec_fn=die_with_parent))
+
+    class _Stop(Exception):
+        pass
+
+    def on_signal(signum, _frame):
+        raise _Stop(signum)
+    # a driver timeout (SIGTERM) or a lost terminal (SIGHUP) ends the ranks
+    # too: they sit in their own sessions and would otherwise keep the GPUs
+    # at a barrier until the process-group timeout
+    old = {sg: signal.signal(sg, on_signal) for sg in (signal.SIGTERM, signal.SIGHUP)}
     rc = 0
     try:
         live = list(procs)
@@ -176,12 +195,17 @@ def launch_ranks(args) -> int:
                     for q in live:          # one rank failed: the collective cannot finish
                         q.send_signal(signal.SIGTERM)
             time.sleep(0.05)
-    except KeyboardInterrupt:
+    except (KeyboardInterrupt, _Stop) as e:
         for p in procs:
             if p.poll() is None:
-                p.send_signal(signal.SIGTERM)
-        rc = 130
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except OSError:
+                    p.send_signal(signal.SIGTERM)
+        rc = 128 + e.args[0] if isinstance(e, _Stop) else 130
     finally:
+        for sg, h in old.items():
+            signal.signal(sg, h)
         for p in procs:
             try:
                 p.wait(timeout=20)
@@ -193,6 +217,7 @@ def launch_ranks(args) -> int:
 
 def main():
     args = parse()
+    exit_code = 0
     if args.device == "cpu":
         args.c1_requests = min(args.c1_requests, 20)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -276,7 +301,10 @@ def main():
         from rust_tensorflow_serving2_amd.parallel.weights import ReplicatedWeightSource
         # the leader compiles + tunes once; the other ranks bind its packed bf16
         # device weights (RCCL broadcast; the gloo rehearsal stages via the host)
-        weight_source = ReplicatedWeightSource(dist.distributed_c10d._get_default_store(), device=device)
+        # share=True on the CPU too: the gloo test of this launcher rehearses
+        # the same leader-broadcast / follower-bind protocol
+        weight_source = ReplicatedWeightSource(dist.distributed_c10d._get_default_store(), device=device,
+                                               share=True)
     sopts = ServableOptions(device=str(device), max_batch_size=args.batch, lanes=args.lanes,
                             allowed_batch_sizes=tuple(sorted({1, 2, 4, 8, 16, args.batch})))
     port = (args.port + local) if args.port else 0
@@ -464,7 +492,11 @@ def main():
     my_diag = {"placement": dict(placement.as_dict(), pinned=pinned,
                                  bdf=gpu_info[local].bdf if local < len(gpu_info) else None),
                "gpu_busy_pct": gpu_busy, "timed": cpu_report, "prewarm": diag_window,
-               "ref_client": my_ref_diag}
+               "ref_client": my_ref_diag,
+               "rank_timing": {"rank": rank, "ok": int(r["ok"]), "elapsed_s": round(elapsed, 6),
+                               "start_sync_ms": cpu_report["start_sync_ms"],
+                               "end_sync_ms": cpu_report["end_sync_ms"]},
+               "rccl": weight_source.report() if weight_source is not None else None}
     if world > 1:
         allv = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allv, mine)
@@ -512,7 +544,21 @@ def main():
         }
         if ref is not None:
             out.update(ref)
+        rccl_bad = []
+        if world > 1:
+            out["per_rank"] = [d["rank_timing"] for d in all_diag]
+            out["rccl"] = [d["rccl"] for d in all_diag]
+            rccl_bad = rccl_problems(out["rccl"], world)
+            out["rccl_ok"] = not rccl_bad
+            if rccl_bad:
+                out["rccl_problems"] = rccl_bad
         print(json.dumps(out), flush=True)
+        if rccl_bad:
+            # fail loudly: a follower that silently fell back to disk / its own
+            # host copy would otherwise look exactly like a working broadcast
+            print("bench.py: weight replication did not run over the collective on every rank: "
+                  + "; ".join(rccl_bad), file=sys.stderr, flush=True)
+            exit_code = 3
     server.stop()
     if world > 1:
         dist.barrier()
@@ -520,6 +566,32 @@ def main():
             from rust_tensorflow_serving2_amd.parallel.replicas import shm_cleanup
             shm_cleanup(route_group)
         dist.destroy_process_group()
+    if exit_code:
+        sys.exit(exit_code)
+
+
+def rccl_problems(reports, world: int) -> list:
+    """What is wrong with the ranks' weight-replication reports (empty = every
+    follower received the leader's compiled device weights over the group's
+    collective and copied no weight byte host -> device itself)."""
+    bad = []
+    if len(reports) != world or any(r is None for r in reports):
+        return [f"{sum(r is not None for r in reports)} of {world} ranks reported"]
+    for r in reports:
+        who = f"rank {r['rank']}"
+        if r["world"] != world:
+            bad.append(f"{who}: group of {r['world']}")
+        if r["leader"]:
+            if r["broadcast_bytes"] <= 0:
+                bad.append(f"{who} (leader): broadcast nothing")
+            continue
+        if r["disk_loads"] > 0:
+            bad.append(f"{who}: {r['disk_loads']} model load(s) from disk")
+        if r["weight_h2d_bytes"] > 0:
+            bad.append(f"{who}: copied {r['weight_h2d_bytes']} weight bytes host->device")
+        if r["bcast_loads"] < 1 or r["bound_bytes"] <= 0:
+            bad.append(f"{who}: received {r['bcast_loads']} load(s) / {r['bound_bytes']} weight bytes")
+    return bad
 
 
 if __name__ == "__main__":

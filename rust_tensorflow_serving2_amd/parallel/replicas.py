@@ -268,6 +268,14 @@ def launch(argv: Sequence[str], nproc: int, module: str = "rust_tensorflow_servi
                 # the weight-broadcast group lost a member: a new generation, whose
                 # group (live ranks + the replacement) forms at the leader's next event
                 store.add("tfs/gen", 1)
+                # ... and its last heartbeat must not make it look alive for
+                # dead_after_s more (the bump comes first: a rank without a
+                # heartbeat key counts as alive to the weight source, which
+                # gates generation >= 1 on membership instead)
+                try:
+                    store.delete_key(f"tfs/hb/{i}")
+                except Exception:
+                    pass
                 if restarts[i] >= max_restarts:
                     log.error("replica %d (pid %d) exited with %d; restart budget spent", i, p.pid, r)
                     rc = rc or r

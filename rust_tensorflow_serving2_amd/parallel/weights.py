@@ -41,9 +41,18 @@ standalone ``ProcessGroupNCCL`` / ``ProcessGroupGloo``: the dead process is no
 member of it) before it joins that event's collective, so later loads are
 broadcast again on every GPU.  A replacement skips events of older generations
 (their groups ran without it) and reads the models the group loaded before it
-existed from disk.  While a replica is down (its heartbeat stale) the leader
-loads from disk and says so in the model's marker, so no rank waits for a
-collective that could not complete.  The reference has no multi-GPU path at all
+existed from disk.
+
+Membership.  A generation's group is used only once every rank has joined it:
+each rank writes ``tfs/pg/g<gen>/member/<rank>`` -- the replacement when its
+weight source starts (after it has fixed the first event it will consume),
+a survivor when its event thread sees the bump.  Until all ``world`` members
+are present (or while a heartbeat is stale) the leader loads from disk and
+says so in the model's marker, so no rank waits for a collective that could
+not complete; heartbeats alone are not enough, because a dead rank's last
+heartbeat stays fresh for ``dead_after_s`` after the supervisor's bump.  A
+collective that raises drops its group: the leader bumps the generation, so
+the next event forms a fresh one.  The reference has no multi-GPU path at all
 (SURVEY.md §2.4-2.5: one TF Serving container, ``serving/rundocker.sh:15``);
 the supersede-on-reload contract this keeps fast on every GPU is
 ``model_service.proto:19-21``.
@@ -100,13 +109,32 @@ class LoadError(RuntimeError):
     pass
 
 
+class _CommError(RuntimeError):
+    """A follower's collective failed (not the leader's load): fall back to disk."""
+
+
 _META_DT = {T.DT_FLOAT: torch.float32, T.DT_HALF: torch.float16, T.DT_BFLOAT16: torch.bfloat16,
             T.DT_DOUBLE: torch.float64}
 
 
-def _sync(device: torch.device):
-    if device.type == "cuda":
-        torch.cuda.synchronize(device)
+class _StreamMark:
+    """Stream-ordered completion of a collective on ``device``: an event
+    recorded on the current stream (which ``Work.wait()`` has made wait for the
+    process group's stream) that only THIS thread's host side waits for.  A
+    device-wide ``torch.cuda.synchronize()`` here would also wait for every
+    serving lane's in-flight graph replays on the GPU -- a hot reload on a busy
+    replica would stall behind all of them."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.ev = None
+        if device.type == "cuda":
+            self.ev = torch.cuda.Event(enable_timing=False)
+            self.ev.record(torch.cuda.current_stream(device))
+
+    def wait(self) -> None:
+        if self.ev is not None:
+            self.ev.synchronize()
 
 
 def broadcast_meta(path: Optional[str], root: int, comm: "_Comm") -> sm.SavedModelBundle:
@@ -148,7 +176,9 @@ def broadcast_blob(blob: Optional[torch.Tensor], manifest, root: int, comm: "_Co
     device = comm.device
     if comm.rank != root:
         blob = torch.empty(placement.blob_bytes(manifest), dtype=torch.uint8, device=device)
-    _sync(device)
+    # ordering is stream-based: the root's blob was packed by copies on the
+    # current stream, and ProcessGroupNCCL makes its own stream wait for the
+    # current one before the collective; no device-wide synchronize
     t0 = time.perf_counter()
     if device.type == "cuda" and comm.backend == "gloo":
         host = blob.cpu()                      # gloo rehearsal of the device path: staged through the host
@@ -157,7 +187,7 @@ def broadcast_blob(blob: Optional[torch.Tensor], manifest, root: int, comm: "_Co
             blob.copy_(host)
     else:
         comm.bcast_tensor(blob, root)          # RCCL: device to device over xGMI
-    _sync(device)
+    _StreamMark(device).wait()                 # this collective (and the copy) only
     if stats is not None:
         stats["broadcast_s"] = stats.get("broadcast_s", 0.0) + time.perf_counter() - t0
         stats["broadcast_bytes"] = stats.get("broadcast_bytes", 0) + int(blob.numel())
@@ -256,7 +286,8 @@ class ReplicatedWeightSource:
         self.dead_after_s = dead_after_s
         self.announce_wait_s = float(os.environ.get("TFSERVE_SHARE_WAIT_S", "20"))
         self.prefix = prefix
-        self.stats: dict = {"gen": 0, "regroups": 0, "disk_loads": 0}
+        self.stats: dict = {"gen": 0, "regroups": 0, "disk_loads": 0, "bcast_loads": 0, "broadcast_bytes": 0,
+                            "broadcast_s": 0.0, "programs": 0, "comm_failures": 0}
         self._lock = threading.Lock()           # leader: one collective at a time, seq order
         self._pending: Dict[Tuple, Future] = {}
         self._parked: Dict[Tuple, Tuple[float, object]] = {}
@@ -271,8 +302,12 @@ class ReplicatedWeightSource:
         if not restarted and self.min_gen == 0 and dist.is_initialized():
             pg = group if group is not None else dist.distributed_c10d._get_default_group()
             self.comm = _Comm(pg, self.rank, self.world, self.backend, device, 0)
-        # followers consume events from the one after the newest at start-up
+        # followers consume events from the one after the newest at start-up;
+        # fixed BEFORE joining the generation, so every event the leader
+        # publishes once it sees this rank as a member is one it consumes
         self._first_seq = int(self.store.add(f"{prefix}/seq", 0)) + 1 if restarted else 1
+        self._member_gen = -1
+        self._join(self.min_gen)
         if self.rank != leader and self.share:
             self._thread = threading.Thread(target=self._follow, name="tfs-wev", daemon=True)
             self._thread.start()
@@ -305,6 +340,47 @@ class ReplicatedWeightSource:
 
     def _all_alive(self) -> bool:
         return all(self._alive(r) for r in range(self.world) if r != self.rank)
+
+    @staticmethod
+    def _member_key(gen: int, rank: int) -> str:
+        return f"tfs/pg/g{gen}/member/{rank}"
+
+    def _join(self, gen: int) -> None:
+        """Declare this rank a member of generation ``gen``'s group."""
+        if gen < 0 or gen <= self._member_gen:
+            return
+        try:
+            self.store.set(self._member_key(gen, self.rank), "1")
+            self._member_gen = gen
+        except Exception:
+            pass
+
+    def _group_ready(self, gen: int) -> bool:
+        """Every rank joined generation ``gen`` and every heartbeat is fresh.
+        Generation 0 is the group every rank started in (no restart yet)."""
+        if gen < 0 or not self._all_alive():
+            return False
+        if gen == 0:
+            return True
+        self._join(gen)
+        try:
+            return all(self.store.check([self._member_key(gen, r)]) for r in range(self.world))
+        except Exception:
+            return False
+
+    def _comm_failed(self, comm: "_Comm", e: Exception) -> None:
+        """A collective on ``comm`` raised: never reuse its group.  The leader
+        opens a new generation so the next event forms a fresh one."""
+        self.stats["comm_failures"] = self.stats.get("comm_failures", 0) + 1
+        log.warning("rank %d: collective of generation %d failed (%s); dropping the group", self.rank, comm.gen, e)
+        if self.comm is comm:
+            self._old_comms.append(comm)
+            self.comm = None
+        if self.is_leader:
+            try:
+                self.store.add(GEN_KEY, 1)
+            except Exception:
+                pass
 
     def _ensure_comm(self, gen: int) -> _Comm:
         """The process group of generation ``gen`` (formed on first use: every
@@ -347,26 +423,37 @@ class ReplicatedWeightSource:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         seq = self._first_seq
+        idle = 0
         while not self._stop.is_set():
             key = f"{self.prefix}/{seq}"
             if not self.store.check([key]):     # non-blocking poll (lets close() end the thread)
+                idle += 1
+                if idle % 5 == 0:                 # a survivor joins a bumped generation
+                    self._join(self._current_gen())
                 self._stop.wait(0.02)
                 continue
+            idle = 0
             ev = json.loads(self.store.get(key).decode())
             seq += 1
             gen = int(ev[-1])
             if gen < self.min_gen:
                 continue                          # a collective of a group this process never joined
             k = tuple(ev[:4]) if ev[0] == "prog" else tuple(ev[:3])
+            comm = None
             try:
+                self._join(gen)
                 comm = self._ensure_comm(gen)
                 if ev[0] == "load":
                     res = broadcast_meta(None, self.leader, comm)
                 else:
                     res = broadcast_blob(None, None, self.leader, comm, self.stats)
                 err = None
-            except Exception as e:
+            except LoadError as e:                # the leader's own load failed (broadcast as an error)
                 res, err = None, e
+            except Exception as e:                # the collective itself: fall back to disk
+                if comm is not None:
+                    self._comm_failed(comm, e)
+                res, err = None, _CommError(str(e))
             self._deliver(k, res, err)
 
     def _deliver(self, k, res, err):
@@ -396,6 +483,8 @@ class ReplicatedWeightSource:
                 if fut is None:
                     fut = self._pending[k] = Future()
         if parked is not None:
+            if isinstance(parked[1], _CommError):
+                return fallback()
             if isinstance(parked[1], Exception):
                 raise parked[1]
             return parked[1]
@@ -403,6 +492,8 @@ class ReplicatedWeightSource:
         while True:
             try:
                 return fut.result(timeout=0.5)
+            except _CommError:
+                return fallback()
             except FutureTimeout:
                 leader_down = self.group_broken()
                 m = self._marker(*disk_marker) if disk_marker else None
@@ -429,16 +520,26 @@ class ReplicatedWeightSource:
         if self.is_leader:
             with self._lock:
                 gen = self._current_gen()
-                if gen < 0 or not self._all_alive():
-                    # a replica is down (being restarted): no collective can complete
+                if not self._group_ready(gen):
+                    # a replica is down or its replacement has not joined yet:
+                    # no collective could complete
                     self.store.set(self._marker_key(name, version), json.dumps({"gen": gen, "mode": "disk"}))
                     return self._disk_load(key, path)
                 self.store.set(self._marker_key(name, version), json.dumps({"gen": gen, "mode": "bcast"}))
                 # publish first: forming a new generation's group is itself a
                 # rendezvous the followers join when they see this event
                 self._publish(["load", name, int(version), path, gen])
-                comm = self._ensure_comm(gen)
-                return broadcast_meta(path, self.leader, comm)
+                comm = None
+                try:
+                    comm = self._ensure_comm(gen)
+                    return broadcast_meta(path, self.leader, comm)
+                except LoadError:
+                    raise
+                except Exception as e:
+                    if comm is not None:
+                        self._comm_failed(comm, e)
+                    self.store.set(self._marker_key(name, version), json.dumps({"gen": gen, "mode": "disk"}))
+                    return self._disk_load(key, path)
         m = self._marker(name, version)
         if m is not None and (m.get("mode") == "disk" or int(m.get("gen", 0)) < self.min_gen):
             # the leader broadcast it before this process existed, or not at all
@@ -462,13 +563,19 @@ class ReplicatedWeightSource:
         if self.is_leader:
             with self._lock:
                 gen = self._current_gen()
-                if gen < 0 or not self._all_alive():
+                if not self._group_ready(gen):
                     return
                 self.store.set(self._announce_key(name, version, key), "1")
                 self._publish(["prog", name, int(version), key, gen])
-                comm = self._ensure_comm(gen)
-                blob, man = placement.export_weights(program)
-                broadcast_blob(blob, man, self.leader, comm, self.stats)
+                comm = None
+                try:
+                    comm = self._ensure_comm(gen)
+                    blob, man = placement.export_weights(program)
+                    broadcast_blob(blob, man, self.leader, comm, self.stats)
+                except Exception as e:          # followers recompile from disk (they got _CommError)
+                    if comm is None:
+                        raise
+                    self._comm_failed(comm, e)
             return
 
         def rebuild():
@@ -528,6 +635,21 @@ class ReplicatedWeightSource:
                 return None
             time.sleep(0.02)
         return json.loads(self.store.get(sk).decode())
+
+    def report(self) -> dict:
+        """This rank's replication figures (bench.py's ``rccl`` block):
+        backend, group size, generation, bytes / seconds of device-blob
+        broadcast, loads received over the collective vs read from disk, and
+        the weight bytes this process copied host -> device itself (a
+        follower that really bound the leader's blob copies none)."""
+        st = dict(self.stats)
+        return {"backend": self.backend, "world": self.world, "rank": self.rank, "leader": self.is_leader,
+                "gen": self.gen, "broadcast_bytes": int(st.get("broadcast_bytes", 0)),
+                "broadcast_s": round(float(st.get("broadcast_s", 0.0)), 6),
+                "programs": int(st.get("programs", 0)), "bound_bytes": int(st.get("bound_bytes", 0)),
+                "bcast_loads": int(st.get("bcast_loads", 0)), "disk_loads": int(st.get("disk_loads", 0)),
+                "comm_failures": int(st.get("comm_failures", 0)),
+                "weight_h2d_bytes": int(placement.H2D_BYTES)}
 
     def close(self):
         self._stop.set()

@@ -46,6 +46,69 @@ def test_bench_gpus2_self_launch_cpu(tmp_path):
         assert a and b and not (a & b)
         assert all(d["placement"]["pinned"] for d in diags)
     assert out["ref_client_errors"] == 0
+    # the weight replication the driver's scaling run depends on: the follower
+    # received the leader's compiled weights over the collective (gloo here,
+    # RCCL on the GPUs), read nothing from disk, copied no weight to a device
+    assert out["rccl_ok"] is True and "rccl_problems" not in out, out.get("rccl_problems")
+    lead, fol = out["rccl"]
+    assert lead["leader"] and lead["backend"] == "gloo" and lead["world"] == 2
+    assert lead["broadcast_bytes"] > 0 and lead["programs"] >= 1
+    assert not fol["leader"] and fol["disk_loads"] == 0 and fol["weight_h2d_bytes"] == 0
+    assert fol["bcast_loads"] >= 1 and fol["bound_bytes"] > 0
+    assert fol["broadcast_bytes"] == lead["broadcast_bytes"] and fol["broadcast_s"] >= 0
+    pr = out["per_rank"]
+    assert [x["rank"] for x in pr] == [0, 1] and all(x["ok"] > 0 and x["elapsed_s"] > 0 for x in pr)
+    assert all("start_sync_ms" in x and "end_sync_ms" in x for x in pr)
+
+
+def test_rccl_problems_flags_silent_fallbacks():
+    """bench.py exits non-zero (after printing its line) when a follower did
+    not really receive the broadcast."""
+    sys.path.insert(0, ROOT)
+    import bench
+    lead = {"rank": 0, "leader": True, "world": 2, "broadcast_bytes": 10, "disk_loads": 0, "weight_h2d_bytes": 5,
+            "bcast_loads": 0, "bound_bytes": 0}
+    good = {"rank": 1, "leader": False, "world": 2, "broadcast_bytes": 10, "disk_loads": 0, "weight_h2d_bytes": 0,
+            "bcast_loads": 1, "bound_bytes": 10}
+    assert bench.rccl_problems([lead, good], 2) == []
+    assert bench.rccl_problems([lead, dict(good, disk_loads=1)], 2)
+    assert bench.rccl_problems([lead, dict(good, weight_h2d_bytes=8)], 2)
+    assert bench.rccl_problems([lead, dict(good, bound_bytes=0)], 2)
+    assert bench.rccl_problems([dict(lead, broadcast_bytes=0), good], 2)
+    assert bench.rccl_problems([lead, None], 2)
+
+
+@pytest.mark.timeout(200)
+def test_bench_launcher_forwards_sigterm(tmp_path):
+    """A driver timeout (SIGTERM to the launcher) ends the ranks too, although
+    each runs in its own session."""
+    import signal
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["TMPDIR"] = str(tmp_path)
+    cmd = [sys.executable, BENCH, "--gpus", "2", "--device", "cpu", "--model", "tiny", "--image-size", "32",
+           "--steps", "100000000", "--warmup", "1", "--prewarm-s", "0.2", "--io-threads", "1",
+           "--client-threads", "1", "--connections", "1", "--lanes", "1"]
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, cwd=str(tmp_path))
+    ranks = []
+    deadline = time.time() + 120
+    while time.time() < deadline and len(ranks) < 2:
+        out = subprocess.run(["pgrep", "-P", str(p.pid)], capture_output=True, text=True).stdout.split()
+        ranks = [int(x) for x in out]
+        time.sleep(0.2)
+    assert len(ranks) == 2
+    time.sleep(3.0)
+    p.send_signal(signal.SIGTERM)
+    p.wait(timeout=60)
+    assert p.returncode != 0
+    deadline = time.time() + 30
+    while time.time() < deadline and any(os.path.exists(f"/proc/{r}") and
+                                         open(f"/proc/{r}/stat").read().split()[2] != "Z" for r in ranks):
+        time.sleep(0.2)
+    alive = [r for r in ranks if os.path.exists(f"/proc/{r}")]
+    for r in alive:
+        os.kill(r, signal.SIGKILL)
+    assert not alive, alive
 
 
 def test_bench_rejects_gpus_world_mismatch(tmp_path):

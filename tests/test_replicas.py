@@ -327,3 +327,88 @@ def test_restart_reforms_weight_broadcast_group(tiny_resnet_path, tmp_path):
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, 9)
             proc.wait()
+
+
+def test_reload_right_after_replica_kill_does_not_hang(tiny_resnet_path, tmp_path):
+    """A reload issued while a killed follower is still being replaced (its
+    last heartbeat fresh, the generation already bumped) must not block in a
+    broadcast the dead rank -- or its replacement, which starts after the
+    event -- can never join: the leader gates the new generation on
+    membership and loads from disk until every rank has joined.  Once the
+    replacement is up, the next reload is broadcast again."""
+    import json
+    import shutil
+    import signal as sig
+    from rust_tensorflow_serving2_amd.client import ModelDescription, TensorflowServing
+    from rust_tensorflow_serving2_amd.schema import serving
+    base = str(tmp_path / "r")
+    shutil.copytree(os.path.join(tiny_resnet_path, "1"), os.path.join(base, "1"))
+    port = _free_port()
+    logf = str(tmp_path / "replicas.log")
+    stats_dir = str(tmp_path / "stats")
+    env = dict(os.environ, PYTHONPATH=ROOT, TFSERVE_STATS_DIR=stats_dir, TFSERVE_SHARE_WEIGHTS="1",
+               TFSERVE_SHARE_WAIT_S="5")
+    env.pop("WORLD_SIZE", None)
+    proc = subprocess.Popen([sys.executable, "-m", "rust_tensorflow_serving2_amd.server", f"--port={port}",
+                             "--model_name=r", f"--model_base_path={base}", "--num_gpus=3", "--device=cpu",
+                             "--host=127.0.0.1", "--file_system_poll_wait_seconds=0", "--log_level=WARNING",
+                             "--io_threads=1"],
+                            env=env, stdout=open(logf, "w"), stderr=subprocess.STDOUT, text=True,
+                            start_new_session=True)
+
+    def ready_count():
+        return open(logf).read().count("ready:")
+
+    x = np.random.default_rng(0).random((1, 32, 32, 3), dtype=np.float32)
+
+    async def predict(version=None):
+        c = await TensorflowServing.new().hostname("127.0.0.1").port(port).build()
+        return await c.predict_tensors(ModelDescription("r", version) if version else "r", {"input": x})
+
+    async def reload():
+        c = await TensorflowServing.new().hostname("127.0.0.1").port(port).build()
+        return await c.reload([serving.ModelConfig(name="r", base_path=base, model_platform="tensorflow")])
+
+    try:
+        deadline = time.time() + 240
+        while time.time() < deadline and proc.poll() is None and ready_count() < 3:
+            time.sleep(0.2)
+        assert ready_count() == 3, open(logf).read()[-3000:]
+        p1 = asyncio.run(predict())["probabilities"]
+        time.sleep(1.0)
+        st = _stats(stats_dir)
+        victim = 1
+        vpid = next(p for (r, p) in st if r == victim)
+        shutil.copytree(os.path.join(base, "1"), os.path.join(base, "2"))
+        os.kill(vpid, sig.SIGKILL)
+        time.sleep(0.5)                                   # the supervisor has bumped the generation
+        t0 = time.time()
+        resp = asyncio.run(reload())
+        took = time.time() - t0
+        assert resp.status.error_code == 0, resp.status.error_message
+        assert took < 60, took                            # not a collective waiting for the dead rank
+        np.testing.assert_allclose(asyncio.run(predict(2))["probabilities"], p1, rtol=1e-5, atol=1e-6)
+
+        deadline = time.time() + 240
+        while time.time() < deadline and ready_count() < 4:
+            time.sleep(0.2)
+        assert ready_count() == 4, open(logf).read()[-3000:]
+        time.sleep(1.5)
+        shutil.copytree(os.path.join(base, "1"), os.path.join(base, "3"))
+        resp = asyncio.run(reload())
+        assert resp.status.error_code == 0, resp.status.error_message
+        np.testing.assert_allclose(asyncio.run(predict(3))["probabilities"], p1, rtol=1e-5, atol=1e-6)
+        time.sleep(1.0)
+        now = {r: s for (r, p), s in _stats(stats_dir).items() if p != vpid}
+        surv = now[2]["weights"]
+        # version 2 went to disk (the group was not complete); version 3 over the broadcast
+        assert surv["gen"] >= 1 and surv["disk_loads"] >= 1 and surv["bcast_loads"] >= 2, surv
+        assert now[victim]["weights"]["bcast_loads"] >= 1, now[victim]
+        assert proc.poll() is None
+    finally:
+        os.killpg(proc.pid, 15)
+        try:
+            proc.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, 9)
+            proc.wait()
