@@ -1088,9 +1088,7 @@ def fuse_conv_chain(g, order, fed, fetch_refs, device, opts):
 
 
 def default_passes(options=None):
-    from .flow import fuse_flow
     from .patterns import bert_passes, late_passes
     return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_dual_conv, fuse_post_activation,
                                                                  fuse_stem_pool, fuse_matmul, fuse_classifier_head,
-                                                                 fuse_dense_softmax, fuse_conv_chain] + late_passes() + \
-        [fuse_flow]
+                                                                 fuse_dense_softmax, fuse_conv_chain] + late_passes()

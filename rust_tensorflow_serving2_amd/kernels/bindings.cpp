@@ -11,7 +11,6 @@
 
 #include "launch.h"
 #include "cgemm.h"
-#include "flow.h"
 
 namespace {
 
@@ -34,7 +33,7 @@ bool is_cgemm_cfg(int64_t cfg) {
 
 // halo-tiled 3x3 stride-1 conv configs (halo.hip)
 bool is_halo_cfg(int64_t cfg) {
-  return cfg >= tfsk::kHaloCfgBase && cfg < tfsk::kHaloCfgBase + tfsk::kNumHaloConfigs;
+  return cfg >= 0 && cfg < (1 << 20) && tfsk::halo_cfg_id(int(cfg));
 }
 
 hipError_t launch_any(const tfsk::IGemmArgs& a, int a_mode, int64_t cfg, hipStream_t st) {
@@ -726,44 +725,6 @@ Tensor attention(const Tensor& qkv, const c10::optional<Tensor>& mask_bias, int6
 
 }  // namespace
 
-// A chain of conv layers as one persistent launch (flow.hip).  table: int32
-// [kFlowMaxSteps + nsteps * 48] (graph/flow.py builds it); arena / entry / out:
-// the bases of the table's relative pointers; ctrl: int32 control words, zero
-// when first used and owned by this launch site (a graph keeps its own; the
-// row-block counters count across launches) -- by default a permanent slice
-// of the counter pool, which is only allowed inside a HIP-graph capture.
-void flow_run(const Tensor& table, int64_t nsteps, int64_t ntasks, const Tensor& arena, const Tensor& entry,
-              const Tensor& out, int64_t ctrl_ints, int64_t grid, const c10::optional<Tensor>& ctrl) {
-  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kInt && table.is_contiguous(), "flow_run: table int32");
-  TORCH_CHECK(nsteps > 0 && nsteps <= tfsk::kFlowMaxSteps, "flow_run: 1..", tfsk::kFlowMaxSteps, " steps");
-  TORCH_CHECK(table.numel() == tfsk::kFlowMaxSteps + nsteps * int64_t(sizeof(tfsk::FlowStep) / 4),
-              "flow_run: table size");
-  need(entry, at::kBFloat16, "entry");
-  need(out, at::kBFloat16, "out");
-  TORCH_CHECK(arena.is_cuda() && arena.is_contiguous(), "flow_run: arena");
-  TORCH_CHECK(aligned16(entry) && aligned16(out) && aligned16(arena), "flow_run: 16-B aligned bases");
-  TORCH_CHECK(table.device() == entry.device() && arena.device() == entry.device() && out.device() == entry.device(),
-              "flow_run: tensors on different devices");
-  TORCH_CHECK(ntasks > 0 && grid > 0 && ctrl_ints >= tfsk::kFlowCtrlHead, "flow_run: ntasks / grid / ctrl");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(entry.device());
-  hipStream_t st = cur_stream(entry);
-  tfsk::splitk_counters_prepare(st);   // (allocates the pool on the first eager call; no-op while capturing)
-  int* cp = nullptr;
-  if (ctrl.has_value()) {
-    TORCH_CHECK(ctrl->is_cuda() && ctrl->scalar_type() == at::kInt && ctrl->numel() >= ctrl_ints &&
-                    ctrl->device() == entry.device(), "flow_run: ctrl int32 [>= ctrl_ints]");
-    cp = ctrl->data_ptr<int>();
-  } else {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    TORCH_CHECK(hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone,
-                "flow_run: pass ctrl (zeros) outside a HIP-graph capture");
-    cp = tfsk::splitk_counters(int(ctrl_ints), st);
-    TORCH_CHECK(cp != nullptr, "flow_run: no control words left in the counter pool");
-  }
-  check(tfsk::flow_launch(table.data_ptr(), int(nsteps), int(ntasks), arena.data_ptr(), entry.data_ptr(),
-                          out.data_ptr(), cp, int(grid), st), "flow_run");
-}
-
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels (MFMA implicit-GEMM conv/GEMM, attention, norms, pooling)";
   m.def("conv2d", &conv2d, "NHWC implicit-GEMM conv (+bias +residual +act)", py::arg("x"), py::arg("w"),
@@ -778,10 +739,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_chain_supported", [](int64_t k1, int64_t n1, int64_t n2) {
     return tfsk::conv_chain_supported(int(k1), int(n1), int(n2));
   });
-  m.def("flow_run", &flow_run, "a chain of conv layers as one persistent dataflow launch", py::arg("table"),
-        py::arg("nsteps"), py::arg("ntasks"), py::arg("arena"), py::arg("entry"), py::arg("out"),
-        py::arg("ctrl_ints"), py::arg("grid"), py::arg("ctrl") = py::none());
-  m.def("flow_step_ints", []() { return int64_t(sizeof(tfsk::FlowStep) / 4); });
   m.def("conv2d_dual", &conv2d_dual, "act(conv1x1(h) + conv1x1_stride(x) + bias) as one K-concatenated GEMM",
         py::arg("h"), py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"), py::arg("sw"), py::arg("act") = 0,
         py::arg("cfg") = 36, py::arg("out") = py::none(), py::arg("splits") = 1,
@@ -827,6 +784,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("seq"));
   m.def("attention", &attention, py::arg("qkv"), py::arg("mask_bias"), py::arg("heads"), py::arg("scale"),
         py::arg("out") = py::none(), py::arg("mask_bstride") = 0, py::arg("mask_qstride") = 0);
+  m.def("splitk_counters_set_owner", [](int64_t owner) { tfsk::splitk_counters_set_owner(owner); },
+        "tag the split-K counter slices this thread's captures take (0 = none)");
+  m.def("splitk_counters_release", [](int64_t owner) { return tfsk::splitk_counters_release(owner); },
+        "return an owner's captured split-K counter slices to the pool");
+  m.def("splitk_counters_captured_in_use", []() { return tfsk::splitk_counters_captured_in_use(); });
   m.def("num_configs", []() { return tfsk::kNumIGemmConfigs; });
   m.def("cgemm_configs", []() {
     std::vector<int> v;
@@ -837,6 +799,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("halo_configs", []() {
     std::vector<int> v;
     for (int c = 0; c < tfsk::kNumHaloConfigs; ++c) v.push_back(tfsk::kHaloCfgBase + c);
+    for (int c = 0; c < tfsk::kNumHaloRbConfigs; ++c) v.push_back(tfsk::kHaloRbCfgBase + c);
     return v;
   });
   m.def("config_tile", [](int cfg) {

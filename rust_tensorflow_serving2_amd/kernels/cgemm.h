@@ -40,6 +40,13 @@ long halo_tiles(const IGemmArgs& a, int cfg);
 // chunks (kt_per_split counts 64-channel chunks).
 constexpr int kHaloCfgBase = 48;
 constexpr int kNumHaloConfigs = 9;
+// register-B halo kernel (weights straight into MFMA registers, one barrier per chunk)
+constexpr int kHaloRbCfgBase = 80;
+constexpr int kNumHaloRbConfigs = 9;
+inline bool halo_cfg_id(int cfg) {
+  return (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) ||
+         (cfg >= kHaloRbCfgBase && cfg < kHaloRbCfgBase + kNumHaloRbConfigs);
+}
 bool halo_supported(const IGemmArgs& a);
 int halo_config_bm(int cfg);
 int halo_config_bn(int cfg);

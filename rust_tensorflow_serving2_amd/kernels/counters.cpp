@@ -1,9 +1,11 @@
 // Split-K arrival counter pool (see launch.h splitk_counters).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "launch.h"
 
@@ -11,25 +13,47 @@ namespace tfsk {
 
 namespace {
 constexpr int kPoolInts = 1 << 22;   // 16 MB per device
-// Used by the split-K fixup (TFSERVE_SPLITK_FIXUP=1, opt-in) and by the
-// control words of captured flow launches (flow.hip, kernels/flow.h).
-// [0, kCapInts): permanent slices for launches captured into HIP graphs (a
-// graph node keeps its counters for the graph's lifetime; slices are never
-// returned, so repeated captures -- tuning candidates, reloads, more buckets
-// or lanes -- use the 3.75M ints up, after which launches fall back to the
-// reduce launch, logged once); [kCapInts, kPoolInts): a ring for eager
-// launches (autotuning, warm-up), reused cyclically.  A maximal take (32K
-// ints) wraps the 256K-int ring after 8 launches; reuse is still safe because
-// eager launches are stream-ordered and counters return to zero when a
-// tile's last slice arrives, before the next launch on the stream starts.
+// Used by the split-K fixup (TFSERVE_SPLITK_FIXUP=1, opt-in).
+// [0, kCapInts): slices for launches captured into HIP graphs (a graph node
+// keeps its counters for the graph's lifetime).  A capture made under an
+// owner token (splitk_counters_set_owner, set by the Python runtime around
+// each graph capture) returns its slices to a free list when the runtime
+// releases the token as the graph is destroyed -- tuning candidates and
+// reload cycles no longer use the range up; slices taken without an owner
+// stay taken.  [kCapInts, kPoolInts): a ring for eager launches (autotuning,
+// warm-up), reused cyclically.  A maximal take (32K ints) wraps the 256K-int
+// ring after 8 launches; reuse is still safe because eager launches are
+// stream-ordered and counters return to zero when a tile's last slice
+// arrives, before the next launch on the stream starts (which is also why a
+// released slice is zero again: every replay of its graph completed).
 constexpr int kCapInts = 15 << 18;
+struct Range {
+  int off, len;
+};
 struct Pool {
   int* base = nullptr;
   int used = 0;
   int ring = kCapInts;
+  std::vector<Range> free_list;                     // released captured slices
+  std::map<int64_t, std::vector<Range>> owned;      // owner token -> its captured slices
 };
 std::mutex g_mu;
 std::map<int, Pool> g_pools;
+thread_local int64_t g_owner = 0;
+
+// first fit from the free list (splitting the range), else -1
+int take_free(Pool& p, int take) {
+  for (size_t i = 0; i < p.free_list.size(); ++i) {
+    Range& r = p.free_list[i];
+    if (r.len < take) continue;
+    const int off = r.off;
+    r.off += take;
+    r.len -= take;
+    if (r.len == 0) p.free_list.erase(p.free_list.begin() + long(i));
+    return off;
+  }
+  return -1;
+}
 
 bool capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -70,18 +94,63 @@ int* splitk_counters(int n, hipStream_t s) {
     p.ring += take;
     return r;
   }
-  if (p.used + take > kCapInts) {
-    static bool warned = false;
-    if (!warned) {
-      warned = true;
-      fprintf(stderr, "[tfserve] split-K counter pool for captured graphs is used up; "
-                      "further captures reduce split-K in a separate launch\n");
+  int off = take_free(p, take);
+  if (off < 0) {
+    if (p.used + take > kCapInts) {
+      static bool warned = false;
+      if (!warned) {
+        warned = true;
+        fprintf(stderr, "[tfserve] split-K counter pool for captured graphs is used up; "
+                        "further captures reduce split-K in a separate launch\n");
+      }
+      return nullptr;
     }
-    return nullptr;
+    off = p.used;
+    p.used += take;
   }
-  int* r = p.base + p.used;
-  p.used += take;
-  return r;
+  if (g_owner != 0) p.owned[g_owner].push_back(Range{off, take});
+  return p.base + off;
+}
+
+void splitk_counters_set_owner(int64_t owner) { g_owner = owner; }
+
+int64_t splitk_counters_release(int64_t owner) {
+  std::lock_guard<std::mutex> g(g_mu);
+  int64_t n = 0;
+  for (auto& kv : g_pools) {
+    Pool& p = kv.second;
+    auto it = p.owned.find(owner);
+    if (it == p.owned.end()) continue;
+    for (const Range& r : it->second) {
+      p.free_list.push_back(r);
+      n += r.len;
+    }
+    p.owned.erase(it);
+    // coalesce adjacent ranges (keeps first-fit effective over many cycles)
+    std::sort(p.free_list.begin(), p.free_list.end(), [](const Range& a, const Range& b) { return a.off < b.off; });
+    std::vector<Range> merged;
+    for (const Range& r : p.free_list) {
+      if (!merged.empty() && merged.back().off + merged.back().len == r.off) merged.back().len += r.len;
+      else merged.push_back(r);
+    }
+    // a free range that ends at the bump pointer gives the space back to it
+    if (!merged.empty() && merged.back().off + merged.back().len == p.used) {
+      p.used = merged.back().off;
+      merged.pop_back();
+    }
+    p.free_list.swap(merged);
+  }
+  return n;
+}
+
+int64_t splitk_counters_captured_in_use() {
+  std::lock_guard<std::mutex> g(g_mu);
+  int64_t n = 0;
+  for (auto& kv : g_pools) {
+    n += kv.second.used;
+    for (const Range& r : kv.second.free_list) n -= r.len;
+  }
+  return n;
 }
 
 }  // namespace tfsk

@@ -88,6 +88,12 @@ struct IGemmArgs {
 int* splitk_counters(int n, hipStream_t s);
 // Allocates and zeroes this device's pool (no-op while `s` is capturing).
 void splitk_counters_prepare(hipStream_t s);
+// Captured slices taken on this thread while `owner` != 0 belong to that
+// owner; splitk_counters_release(owner) returns them to the pool (call it when
+// the graph captured under the token is destroyed).  Returns the ints freed.
+void splitk_counters_set_owner(int64_t owner);
+int64_t splitk_counters_release(int64_t owner);
+int64_t splitk_counters_captured_in_use();
 
 // kAStem7x7x3: fp32 NHWC input with C == 3 and a 7-wide filter (the ResNet
 // stem) — compile-time geometry for the operand gather.

@@ -8,8 +8,10 @@ back to PyTorch, so a GPU test that passes has run the native kernels.
 from __future__ import annotations
 
 import contextlib
+import itertools
 import os
 import threading
+import weakref
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
@@ -152,7 +154,10 @@ CGEMM = {32: (128, 128), 33: (128, 128), 34: (64, 128), 35: (128, 64), 36: (64, 
 TILES.update(CGEMM)
 # halo-tiled 3x3 stride-1 conv (kernels/halo.hip): config id -> (output pixels per tile, BN)
 HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 128), 53: (64, 128), 54: (64, 64),
-        55: (128, 64), 56: (256, 64)}
+        55: (128, 64), 56: (256, 64),
+        # register-B variant (weights straight into the MFMA registers, one barrier per 64-channel chunk)
+        80: (128, 64), 81: (64, 64), 82: (128, 128), 83: (64, 128), 84: (256, 64), 85: (128, 128), 86: (64, 64),
+        87: (128, 64), 88: (256, 64)}
 TILES.update(HALO)
 
 
@@ -362,6 +367,29 @@ def graph_tune(keys: Dict[Tuple, int], time_fn: Callable[[], float], top: int = 
             base = best_t
     _GRAPH_TUNED.update(keys)
     return changed
+
+
+_OWNER_SEQ = itertools.count(1)
+
+
+@contextlib.contextmanager
+def capture_owner(graph):
+    """Around a HIP-graph capture: the split-K arrival counters its launches
+    take (TFSERVE_SPLITK_FIXUP=1) belong to ``graph`` and go back to the pool
+    when the graph object is collected, so tuning candidates and reload
+    cycles do not use the counter pool up (kernels/counters.cpp)."""
+    try:
+        h = hip()
+    except KernelsUnavailable:
+        yield None
+        return
+    tok = next(_OWNER_SEQ)
+    h.splitk_counters_set_owner(tok)
+    try:
+        yield tok
+    finally:
+        h.splitk_counters_set_owner(0)
+        weakref.finalize(graph, h.splitk_counters_release, tok)
 
 
 _FLUSH: Dict[int, torch.Tensor] = {}

@@ -264,7 +264,8 @@ class GpuRunner:
                 lane.pool = src.pool
             else:
                 lane.pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(graph, pool=lane.pool, stream=lane.stream, capture_error_mode="thread_local"):
+        with ops.capture_owner(graph), \
+                torch.cuda.graph(graph, pool=lane.pool, stream=lane.stream, capture_error_mode="thread_local"):
             outs = self._finish(self.program.run(ins))
         # replay once now: a graph's first launch uploads it to the device
         # (milliseconds), which must not land on the first live batch of a
@@ -280,8 +281,9 @@ class GpuRunner:
     def _replay_ms(self, lane: _Lane, ins: List[torch.Tensor], reps: int = 3, iters: int = 6) -> float:
         """Capture the program with the current tile picks and time its replay
         (best of ``reps`` averages over ``iters`` replays; the graph is dropped)."""
+        from .. import ops
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=lane.stream, capture_error_mode="thread_local"):
+        with ops.capture_owner(graph), torch.cuda.graph(graph, stream=lane.stream, capture_error_mode="thread_local"):
             self._finish(self.program.run(ins))
         best = float("inf")
         with torch.cuda.stream(lane.stream):
@@ -314,11 +316,12 @@ class GpuRunner:
         replayed at once on ``k`` lanes' streams: the throughput regime of a
         loaded server (best of ``reps`` rounds of ``iters`` replays per stream;
         the graphs are dropped)."""
+        from .. import ops
         streams = [l.stream for l in self.lanes[:k]]
         graphs = []
         for st in streams:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=st, capture_error_mode="thread_local"):
+            with ops.capture_owner(g), torch.cuda.graph(g, stream=st, capture_error_mode="thread_local"):
                 self._finish(self.program.run(ins))
             graphs.append(g)
         for g, st in zip(graphs, streams):

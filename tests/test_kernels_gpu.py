@@ -104,7 +104,7 @@ def test_cgemm_conv_matches_fp32(shape, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
 
 
-HALO_CFGS = list(range(48, 57))
+HALO_CFGS = list(range(48, 57)) + list(range(80, 89))
 HALO_SHAPES = [
     # N, H, W, Cin, Cout, pads            (3x3 stride 1; ResNet-50 stages + edge cases)
     (2, 56, 56, 64, 64, (1, 1, 1, 1)),
@@ -603,6 +603,32 @@ def test_splitk_in_kernel_fixup_inside_graph(cfg, splits, shape, post, monkeypat
         assert torch.equal(out, eager), (out.float() - eager.float()).abs().max()
         if post:
             assert torch.equal(out2, eager2)
+
+
+def test_splitk_counter_slices_return_with_their_graph(monkeypatch):
+    """Counter slices a captured split-K launch takes go back to the pool when
+    the graph captured under ops.capture_owner is collected: repeated
+    capture / destroy cycles (graph tuning, reloads) do not use the pool up."""
+    import gc
+    from rust_tensorflow_serving2_amd import ops
+    monkeypatch.setenv("TFSERVE_SPLITK_FIXUP", "1")
+    x = rnd(2, 14, 14, 256, seed=71).to(BF).to(DEV)
+    wt = pack_w(rnd(3, 3, 256, 256, scale=1 / 48, seed=72).to(BF).float())
+    out = torch.empty(2, 14, 14, 256, device=DEV, dtype=BF)
+    hip().conv2d(x, wt, None, None, 3, 3, 1, 1, 1, 1, 1, 1, act=0, cfg=51, out=out, splits=4)   # pool allocated
+    torch.cuda.synchronize()
+    base = hip().splitk_counters_captured_in_use()
+    stream = torch.cuda.Stream()
+    for cycle in range(3):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(stream), ops.capture_owner(g), torch.cuda.graph(g, stream=stream):
+            hip().conv2d(x, wt, None, None, 3, 3, 1, 1, 1, 1, 1, 1, act=0, cfg=51, out=out, splits=4)
+        assert hip().splitk_counters_captured_in_use() > base
+        g.replay()
+        torch.cuda.synchronize()
+        del g
+        gc.collect()
+        assert hip().splitk_counters_captured_in_use() == base, cycle
 
 
 # ResNet stem fused with its max pool (stem.hip): fp32 RGB in, pooled bf16 out.
