@@ -83,7 +83,7 @@ def _hw_queues_default() -> str:
     return "8"
 
 
-hip_env.apply(default=_hw_queues_default())
+hip_env.apply(default=_hw_queues_default(), force=True)
 
 METRIC = "Predict RPCs/sec + p50 latency, ResNet-50 batch=1/32 at 1/2/4/8 MI355X"
 PREDICT = "/tensorflow.serving.PredictionService/Predict"

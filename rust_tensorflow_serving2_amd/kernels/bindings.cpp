@@ -448,6 +448,13 @@ Tensor stem_pool(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t P
   TORCH_CHECK(PT >= 0 && PB >= 0 && PL >= 0 && PR >= 0 && PPT >= 0 && PPT <= 2 && PPL >= 0 && PPL <= 2 &&
               PPB >= 0 && PPR >= 0, "stem_pool: bad padding");
   TORCH_CHECK(w.device() == x.device() && bias.device() == x.device(), "stem_pool: tensors on different devices");
+  if (xb16 && x.numel() % 2) {
+    // the bf16 path reads whole aligned dwords: an odd element count's last
+    // pixel reads 2 B past the tensor, which must still lie in its storage
+    const int64_t avail = int64_t(x.storage().nbytes()) - int64_t(x.storage_offset()) * 2;
+    TORCH_CHECK(avail >= x.numel() * 2 + 2, "stem_pool: a bf16 input with an odd element count needs 2 B of "
+                "storage past its end (pad the allocation)");
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), cout = w.size(0);
   const int Hc = (H + PT + PB - 7) / 2 + 1, Wc = (W + PL + PR - 7) / 2 + 1;

@@ -139,8 +139,9 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
   // as the two aligned dwords covering the pixel's channels -- 2 loads per
   // pixel instead of one per channel -- and its bf16 halves are staged as
   // they are: the same patch bits as the fp32 path.  (The record count is
-  // rounded up to whole dwords: the last pixel's second dword may run 2 B past
-  // the tensor, inside its 512-B allocation granule.)
+  // rounded up to whole dwords: with an odd element count the last pixel's
+  // second dword runs 2 B past the tensor; the binding requires the storage to
+  // extend that far -- bindings.cpp stem_pool.)
   constexpr uint32_t kEsz = XB16 ? 2u : 4u;
   const long xbytes = long(p.N) * p.H * p.W * p.C * kEsz;
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(

@@ -2,7 +2,7 @@ import sys
 
 from ..utils import hip_env
 
-hip_env.apply()          # before the runtime starts (the lanes' streams need their own queues)
+hip_env.apply(hip_env.server_default(sys.argv[1:]))   # before the runtime starts (lanes need their own queues)
 
 from .cli import main  # noqa: E402
 
