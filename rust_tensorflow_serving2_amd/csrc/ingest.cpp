@@ -1,8 +1,10 @@
 // fp32 -> bf16 ingest conversion (see ingest.h).  AVX-512 BF16 when the CPU
 // has it (one vcvtne2ps2bf16 per 32 values), scalar round-to-nearest-even
-// otherwise.  Both give the same bits for every input: NaNs stay NaN and
-// fp32 denormals (|x| < 1.2e-38, which vcvtne2ps2bf16 reads as zero) become
-// signed zeros in the scalar path too.
+// otherwise.  Both give the same bits for every input, and the same bits as
+// the device's v_cvt_pk_bf16_f32 under HIP's default fp32 mode (denormals
+// kept): NaNs stay NaN and fp32 denormals round to bf16 denormals.
+// vcvtne2ps2bf16 reads denormal inputs as zero, so a 32-value block holding
+// one goes through the scalar path (one mask test per block otherwise).
 #include "ingest.h"
 
 #include <cstring>
@@ -14,7 +16,6 @@ namespace {
 
 inline uint16_t bf16_rne(uint32_t u) {
   if ((u & 0x7fffffffu) > 0x7f800000u) return uint16_t((u >> 16) | 0x40u);   // quiet NaN
-  if ((u & 0x7f800000u) == 0) return uint16_t((u >> 16) & 0x8000u);         // denormal -> signed zero
   return uint16_t((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
 
@@ -32,6 +33,15 @@ void convert_avx512(uint16_t* dst, const uint8_t* src, size_t n) {
   for (; i + 32 <= n; i += 32) {
     const __m512 a = _mm512_loadu_ps(reinterpret_cast<const float*>(src + 4 * i));
     const __m512 b = _mm512_loadu_ps(reinterpret_cast<const float*>(src + 4 * i + 64));
+    // denormal lanes: exponent 0, mantissa != 0
+    const __m512i ex = _mm512_set1_epi32(0x7f800000), mt = _mm512_set1_epi32(0x007fffff);
+    const __m512i ia = _mm512_castps_si512(a), ib = _mm512_castps_si512(b);
+    const __mmask16 da = _mm512_mask_test_epi32_mask(_mm512_testn_epi32_mask(ia, ex), ia, mt);
+    const __mmask16 db = _mm512_mask_test_epi32_mask(_mm512_testn_epi32_mask(ib, ex), ib, mt);
+    if (__builtin_expect((da | db) != 0, 0)) {
+      convert_scalar(dst + i, src + 4 * i, 32);
+      continue;
+    }
     // (b, a): the low 16 lanes of the result come from the second operand
     const __m512bh r = _mm512_cvtne2ps_pbh(b, a);
     _mm512_storeu_si512(reinterpret_cast<void*>(dst + i), reinterpret_cast<__m512i>(r));

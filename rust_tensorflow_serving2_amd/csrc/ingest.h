@@ -5,9 +5,10 @@
 // as bf16 rows: the IO threads convert while they copy a request into its
 // pinned batch row, so the row, the host->device copy and the kernel's read
 // are half the bytes of the fp32 wire tensor.  Rounding is round-to-nearest-
-// even, the same as the device conversion (v_cvt_pk_bf16_f32), so the
-// results are bit-identical to feeding fp32 (fp32 denormals, |x| < 1.2e-38,
-// become signed zeros).
+// even, the same as the device conversion (v_cvt_pk_bf16_f32, fp32
+// denormals kept as bf16 denormals), so the results are bit-identical to
+// feeding fp32 (tests/test_ingest.py pins the host bits, including
+// denormals; tests/test_resnet_gpu.py the device parity).
 #pragma once
 #include <cstddef>
 #include <cstdint>

@@ -20,13 +20,13 @@ PREDICT = "/tensorflow.serving.PredictionService/Predict"
 
 
 def bf16_ref(x: np.ndarray) -> np.ndarray:
-    """Round-to-nearest-even fp32 -> bf16 bits; NaN stays NaN, denormals -> signed 0."""
+    """Round-to-nearest-even fp32 -> bf16 bits; NaN stays NaN, fp32 denormals
+    round to bf16 denormals (the device's v_cvt_pk_bf16_f32 under HIP's default
+    fp32 mode, which keeps denormals)."""
     u = x.astype(np.float32).view(np.uint32).astype(np.uint64)
     r = ((u + 0x7fff + ((u >> 16) & 1)) >> 16).astype(np.uint16)
     nan = (u & 0x7fffffff) > 0x7f800000
     r[nan] = ((u[nan] >> 16) | 0x40).astype(np.uint16)
-    den = (u & 0x7f800000) == 0
-    r[den] = ((u[den] >> 16) & 0x8000).astype(np.uint16)
     return r
 
 
@@ -48,6 +48,18 @@ def test_conversion_matches_rne_reference(n):
     assert np.all(np.isnan(bf16_to_f32(got[nan])))
     if n >= 10:   # ties go to even: 1 + 2^-8 -> 1.0, 1 + 3 * 2^-8 -> 1 + 2^-6
         assert bf16_to_f32(got[8:10]).tolist() == [1.0, 1.0 + 2 ** -6]
+
+
+@pytest.mark.parametrize("where", [0, 5, 31, 32, 63, 64])
+def test_denormals_keep_their_bits_in_every_block(where):
+    """A denormal anywhere in a 32-value block (the AVX-512 path's unit, whose
+    instruction reads denormals as zero) rounds exactly like the scalar path."""
+    x = np.full(96, 1.5, np.float32)
+    x[where] = np.float32(3e-39)
+    x[(where + 7) % 96] = np.float32(-1.17e-38)
+    got = np.frombuffer(_C.ingest_f32_to_bf16(x.tobytes()), np.uint16)
+    np.testing.assert_array_equal(got, bf16_ref(x))
+    assert got[where] != 0 and bf16_to_f32(got[where:where + 1])[0] > 0
 
 
 def test_torch_agrees_on_normal_values():

@@ -153,6 +153,10 @@ def test_bf16_ingest_is_bit_identical_to_fp32_feed(resnet50, monkeypatch):
     from rust_tensorflow_serving2_amd.utils import tensors as T
     monkeypatch.setattr(ops, "AUTOTUNE", False)
     x = np.random.default_rng(9).random((4, 224, 224, 3), dtype=np.float32) * 255.0
+    # denormal pixels too: the host rounds them to bf16 denormals, as the
+    # stem's device conversion does (csrc/ingest.h)
+    x[0, :8, :8, :] = np.float32(3e-39)
+    x[1, 100:104, 50:60, 1] = np.float32(-1.1e-38)
     outs = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("TFSERVE_BF16_INGEST", mode)
