@@ -288,7 +288,6 @@ class FusedMatMul:
         b = bias if bias is not None else zeros(self.n, w_kn)
         self.np = -(-self.n // 8) * 8 if (pad_n and self.n % 8 and self.k % 64 == 0) else self.n
         self.device = device
-        self.emit_stats = False       # graph pass fold_layernorm: also emit per-row statistics
         if self.use_hip:
             w_nk = w_kn.t().contiguous()
             if self.np != self.n:
@@ -300,47 +299,7 @@ class FusedMatMul:
             self.w_ref = to_device(w_kn.float(), device)
             self.b_ref = to_device(b.float(), device)
 
-    def fold_ln(self, gamma: torch.Tensor, beta: torch.Tensor) -> None:
-        """This GEMM's A operand is LayerNorm(x) with (gamma, beta): keep
-        W' = W * gamma (bf16), colsum[n] = sum_k W'[n][k] and b' = b + W beta,
-        so y = rstd * (x W'^T - mu * colsum) + b' runs on the raw x
-        (kernels: ln_a).  On a follower replica these are shape-only and get
-        bound to the leader's values like every other weight."""
-        w = self.w.float()                    # [N][K] (K unpadded: fold_layernorm needs K % 64 == 0)
-        g = gamma.float().reshape(1, -1).to(w.device)
-        wf = (w * g).to(BF16)
-        self.w_ln = to_device(wf.contiguous(), self.device)
-        self.colsum_ln = to_device(wf.float().sum(1).contiguous(), self.device)
-        self.b_ln = to_device((self.b.float() + w @ beta.float().reshape(-1).to(w.device)).contiguous(), self.device)
-
-    def _call_ln(self, ins):
-        """The LayerNorm-folding GEMM (kernels: IGemmArgs ln_*)."""
-        from ..ops import ACT, hip, tuned_config
-        from .patterns import LazyLN, RawWithStats
-        H = hip()
-        xa, ra = ins[0], (ins[1] if len(ins) > 1 else None)
-        lazy_a = xa if isinstance(xa, LazyLN) and hasattr(self, "w_ln") else None
-        lazy_r = ra if isinstance(ra, LazyLN) else None
-        x = lazy_a.raw if lazy_a is not None else _to_bf16(O.to_torch(xa)).contiguous()
-        r = lazy_r.raw if lazy_r is not None else (None if ra is None else _to_bf16(O.to_torch(ra)).contiguous())
-        w, b = (self.w_ln, self.b_ln) if lazy_a is not None else (self.w, self.b)
-        M = x.numel() // self.k
-        modes = (int(self.emit_stats), lazy_a is not None, lazy_r is not None)
-        kw = dict(want_stats=self.emit_stats)
-        if lazy_a is not None:
-            kw.update(a_stats=lazy_a.stats, a_n=float(self.k), a_eps=lazy_a.eps, colsum=self.colsum_ln)
-        if lazy_r is not None:
-            kw.update(r_stats=lazy_r.stats, r_n=float(self.n), r_eps=lazy_r.eps, r_gamma=lazy_r.g, r_beta=lazy_r.b)
-        key = ("mmln", M, self.n, self.k, r is not None, self.act) + modes
-        run = lambda c, s: H.linear_ln(x, w, b, r, ACT[self.act], c, False, **kw)  # noqa: E731
-        cfg, _s = tuned_config(key, M, self.n, run, self.k, True, True, cgemm_only=True, no_split=True,
-                               n_multiple=self.emit_stats)
-        y, stats = run(cfg, 1)
-        return [RawWithStats(y, stats)] if self.emit_stats else [y]
-
     def __call__(self, ctx, node, ins):
-        if self.use_hip and (self.emit_stats or any(hasattr(v, "stats") for v in ins)):
-            return self._call_ln(ins)
         x = O.to_torch(ins[0])
         res = O.to_torch(ins[1]) if len(ins) > 1 else None
         if not self.use_hip:
@@ -452,7 +411,7 @@ def _impl_op(ctx, node, ins):
 
 
 for _op in ("_FusedConv2D", "_FusedDualConv", "_FusedMatMul", "_GlobalAvgPool", "_MaxPool", "_SoftmaxArgMax", "_LayerNorm",
-            "_FusedQKV", "_Attention", "_EmbeddingLN", "_KeyMaskAdder", "_DenseSoftmax", "_LazyLayerNorm"):
+            "_FusedQKV", "_Attention", "_EmbeddingLN", "_KeyMaskAdder", "_DenseSoftmax"):
     O.OPS[_op] = _impl_op
 
 

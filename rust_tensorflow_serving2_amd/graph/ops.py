@@ -68,8 +68,6 @@ class Ctx:
 def to_torch(v, device=None) -> torch.Tensor:
     if isinstance(v, torch.Tensor):
         return v if device is None or v.device == device else v.to(device)
-    if hasattr(v, "materialize"):          # a deferred value (patterns.LazyLN): computed on demand
-        return to_torch(v.materialize(), device)
     a = np.asarray(v)
     if a.dtype == np.uint16:
         t = torch.from_numpy(a.astype(np.int32)).to(torch.int32)

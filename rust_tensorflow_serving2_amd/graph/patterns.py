@@ -112,95 +112,6 @@ class LayerNormOp:
         return [y if not x.is_cuda else y.to(x.dtype)]
 
 
-# ------------------------------------------------------------------ LayerNorm folding
-# BERT's post-LN blocks without LayerNorm kernels.  The GEMM that produces a
-# LayerNorm's input (O-projection / FFN2, with the residual fused) also emits
-# per-row partial statistics of its output (kernels: IGemmArgs ln_out); the
-# LayerNorm node then only pairs that raw tensor with the statistics and its
-# gamma / beta (LazyLN, no launch).  Its consumers apply it inside their own
-# GEMM: as the A operand through weights pre-scaled by gamma, a column-sum
-# correction and a bias that absorbed beta (ln_a), or as the residual,
-# normalised per element in the epilogue (ln_r).  Any other consumer
-# materialises the LayerNorm with the standalone kernel.
-class RawWithStats:
-    """A GEMM output plus its per-row [M][parts][2] sum / sum-of-squares."""
-
-    def __init__(self, raw: torch.Tensor, stats: torch.Tensor):
-        self.raw, self.stats = raw, stats
-
-    def materialize(self) -> torch.Tensor:
-        return self.raw
-
-
-class LazyLN:
-    """LayerNorm(raw) with gamma / beta / eps, not yet computed."""
-
-    def __init__(self, raw: torch.Tensor, stats: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float):
-        self.raw, self.stats, self.g, self.b, self.eps = raw, stats, g, b, eps
-        self._value = None
-
-    def materialize(self) -> torch.Tensor:
-        if self._value is None:
-            from ..ops import hip
-            self._value = hip().layernorm(self.raw.contiguous(), None, self.g, self.b, self.eps)
-        return self._value
-
-
-class LazyLayerNormOp:
-    """A folded LayerNorm: no kernel when its input carries statistics."""
-    children = ("ln",)
-
-    def __init__(self, ln: "LayerNormOp"):
-        self.ln = ln
-
-    def __call__(self, ctx, node, ins):
-        x = ins[0]
-        if isinstance(x, RawWithStats):
-            return [LazyLN(x.raw, x.stats, self.ln.g, self.ln.b, self.ln.eps)]
-        return self.ln(ctx, node, ins)
-
-
-def fold_layernorm(g, order, fed, fetch_refs, device, opts):
-    """_LayerNorm(_FusedMatMul(...)) whose consumers are all GEMMs (A operand or
-    residual) -> the producer emits row statistics, the LayerNorm becomes
-    _LazyLayerNorm, A-consumers get gamma / beta folded into their weights."""
-    from .fused import FusedMatMul, _Ctx
-    c = _Ctx(g, order, fed, fetch_refs, device, opts)
-    if not c.use_hip:
-        return
-    for name in order:
-        ln = g.nodes.get(name)
-        if ln is None or ln.op != "_LayerNorm" or name in c.fetch_nodes or len(ln.inputs) != 1:
-            continue
-        impl = ln.attrs.get("_impl")
-        if type(impl) is not LayerNormOp or not impl.use_hip:
-            continue
-        src = g.nodes.get(ln.inputs[0][0])
-        if src is None or src.op != "_FusedMatMul" or ln.inputs[0][1] != 0 or c.only_consumer(src.name) is not ln:
-            continue
-        pimpl = src.attrs.get("_impl")
-        H = impl.g.numel()
-        if not isinstance(pimpl, FusedMatMul) or not pimpl.use_hip or pimpl.out_f32 or pimpl.np != pimpl.n or \
-                pimpl.n != H or H % 64 or pimpl.k % 64:
-            continue
-        cons = c.cons.get(name, [])
-        ok = bool(cons)
-        for cn, pos, oi in cons:
-            cimpl = g.nodes[cn].attrs.get("_impl")
-            if g.nodes[cn].op not in ("_FusedMatMul", "_FusedQKV") or oi != 0 or not isinstance(cimpl, FusedMatMul) \
-                    or not cimpl.use_hip or pos not in (0, 1) or (pos == 0 and (cimpl.k != H or cimpl.k % 64)):
-                ok = False
-        if not ok:
-            continue
-        pimpl.emit_stats = True
-        for cn, pos, _oi in cons:
-            if pos == 0:
-                g.nodes[cn].attrs["_impl"].fold_ln(impl.g, impl.b)
-        ln.op = "_LazyLayerNorm"
-        ln.attrs = {"_impl": LazyLayerNormOp(impl)}
-        c.refresh()
-
-
 MAX_ATTENTION_SEQ = 4096      # kernels/launch.h kMaxAttentionSeq
 
 
@@ -718,11 +629,10 @@ def bert_passes():
 
 
 def late_passes():
-    """Passes over the fused graph (after every GEMM is a _FusedMatMul).
-    LayerNorm folding is opt-in (TFSERVE_LN_FOLD=1): it saves the 24 LayerNorm
-    launches of BERT-base but confines the QKV / FFN1 GEMMs to the 4-wave tiles
-    whose registers fit the fold epilogue, and on MI355X that costs more than
-    it saves (b32 engine 2.17 ms folded vs 1.58 ms unfolded, profiles/round3/
-    ln_fold.md)."""
-    import os
-    return [fold_layernorm] if os.environ.get("TFSERVE_LN_FOLD", "0") == "1" else []
+    """Passes over the fused graph (after every GEMM is a _FusedMatMul).  None
+    today: the LayerNorm-folding pass of round 3 (row statistics from the
+    producing GEMM, normalisation inside the consuming GEMMs) measured slower
+    than the standalone LayerNorm kernel -- b32 engine 2.17 vs 1.58 ms, the
+    fold epilogue confined QKV / FFN1 to tiles whose registers fit it
+    (profiles/round3/ln_fold.md) -- and was removed in round 4."""
+    return []

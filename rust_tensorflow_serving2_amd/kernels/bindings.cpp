@@ -287,91 +287,6 @@ Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   return y;
 }
 
-// x @ w^T with the LayerNorm-fold modes (launch.h IGemmArgs ln_*); cgemm
-// configs only, no split-K.  Returns (y, stats) where stats is the
-// [M][N / BN][2] per-part sum / sum-of-squares of y when want_stats.
-std::tuple<Tensor, c10::optional<Tensor>> linear_ln(
-    const Tensor& x, const Tensor& w, const Tensor& bias, const c10::optional<Tensor>& residual, int64_t act,
-    int64_t cfg, bool out_f32, bool want_stats, const c10::optional<Tensor>& a_stats, int64_t a_rowmul,
-    double a_n, double a_eps, const c10::optional<Tensor>& colsum, const c10::optional<Tensor>& r_stats,
-    double r_n, double r_eps, const c10::optional<Tensor>& r_gamma, const c10::optional<Tensor>& r_beta) {
-  TORCH_CHECK(is_cgemm_cfg(cfg) && tfsk::cgemm_ln_ok(int(cfg)),
-              "linear_ln needs a cgemm tile config with the LayerNorm-fold epilogue (cgemm_ln_ok)");
-  const bool strided = !x.is_contiguous();
-  if (strided) {
-    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 &&
-                    x.stride(0) >= x.size(1) && x.stride(0) % 8 == 0,
-                "x must be contiguous or a row-strided 2-D bf16 view");
-  } else {
-    need(x, at::kBFloat16, "x");
-  }
-  need(w, at::kBFloat16, "w");
-  need(bias, at::kFloat, "bias");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  const int K = x.size(-1);
-  const int M = x.numel() / K;
-  const int lda = strided ? int(x.stride(0)) : K;
-  const int N = w.size(0), ldb = w.size(1);
-  TORCH_CHECK(ldb >= K && K % 8 == 0 && ldb % 8 == 0 && bias.numel() == N, "linear_ln: shapes");
-  auto sizes = x.sizes().vec();
-  sizes.back() = N;
-  Tensor y = torch::empty(sizes, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
-  tfsk::IGemmArgs a{};
-  a.a = x.data_ptr(); a.b = bf16p(w);
-  a.a_bytes = M > 0 ? (int64_t(M - 1) * lda + K) * 2 : 0;
-  a.b_bytes = w.numel() * 2;
-  TORCH_CHECK(a.a_bytes < 0x7ffffff0LL && a.b_bytes < 0x7ffffff0LL, "linear_ln operands must be < 2 GiB");
-  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb;
-  a.bias = bias.data_ptr<float>();
-  if (residual.has_value()) {
-    need(*residual, at::kBFloat16, "residual");
-    TORCH_CHECK(residual->numel() == y.numel(), "residual shape must match the output");
-    a.residual = bf16p(*residual);
-    a.ldr = N;
-  }
-  a.act = act; a.out = y.data_ptr(); a.ldc = N; a.out_f32 = out_f32; a.alpha = 1.f;
-  a.splits = 1;
-  c10::optional<Tensor> stats;
-  if (want_stats) {
-    const int bn = tfsk::cgemm_config_bn(int(cfg));
-    TORCH_CHECK(N % bn == 0, "linear_ln: the stats need N % BN == 0 (N ", N, ", BN ", bn, ")");
-    stats = torch::empty({M, N / bn, 2}, x.options().dtype(at::kFloat));
-    a.ln_mode |= 1;
-    a.ln_out = stats->data_ptr<float>();
-    a.ln_out_parts = N / bn;
-  }
-  if (a_stats.has_value()) {
-    need(*a_stats, at::kFloat, "a_stats");
-    TORCH_CHECK(colsum.has_value() && colsum->numel() == N, "ln_a needs colsum [N]");
-    need(*colsum, at::kFloat, "colsum");
-    TORCH_CHECK(a_stats->dim() == 3 && a_stats->size(2) == 2 && a_stats->size(0) >= int64_t(M - 1) * a_rowmul + 1,
-                "a_stats must be [rows, parts, 2] covering every A row");
-    a.ln_mode |= 2;
-    a.ln_a = a_stats->data_ptr<float>();
-    a.ln_a_parts = int(a_stats->size(1));
-    a.ln_a_rowmul = int(a_rowmul);
-    a.ln_a_n = float(a_n);
-    a.ln_a_eps = float(a_eps);
-    a.ln_colsum = colsum->data_ptr<float>();
-  }
-  if (r_stats.has_value()) {
-    TORCH_CHECK(residual.has_value() && r_gamma.has_value() && r_beta.has_value(), "ln_r needs the residual");
-    need(*r_stats, at::kFloat, "r_stats");
-    need(*r_gamma, at::kFloat, "r_gamma");
-    need(*r_beta, at::kFloat, "r_beta");
-    TORCH_CHECK(r_stats->dim() == 3 && r_stats->size(0) == M && r_stats->size(2) == 2 && r_gamma->numel() == N &&
-                    r_beta->numel() == N, "r_stats [M, parts, 2], gamma / beta [N]");
-    a.ln_mode |= 4;
-    a.ln_r = r_stats->data_ptr<float>();
-    a.ln_r_parts = int(r_stats->size(1));
-    a.ln_r_n = float(r_n);
-    a.ln_r_eps = float(r_eps);
-    a.ln_r_gamma = r_gamma->data_ptr<float>();
-    a.ln_r_beta = r_beta->data_ptr<float>();
-  }
-  TORCH_CHECK(tfsk::cgemm_launch(a, tfsk::kADense, int(cfg), cur_stream(x)) == hipSuccess, "linear_ln launch failed");
-  return {y, stats};
-}
 
 Tensor dense_softmax(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, int64_t n) {
   need(x, at::kFloat, "x");
@@ -765,14 +680,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w"), py::arg("bias"), py::arg("n"));
   m.def("softmax_argmax", &softmax_argmax, py::arg("logits"), py::arg("want_probs") = true,
         py::arg("want_classes") = true, py::arg("probs_out") = py::none(), py::arg("classes_out") = py::none());
-  m.def("cgemm_ln_ok", [](int64_t cfg) { return is_cgemm_cfg(cfg) && tfsk::cgemm_ln_ok(int(cfg)); },
-        "tile config supports linear_ln", py::arg("cfg"));
-  m.def("linear_ln", &linear_ln, "x @ w^T + bias (+residual) with LayerNorm folding (cgemm, no split-K)",
-        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("residual") = py::none(), py::arg("act") = 0,
-        py::arg("cfg") = 0, py::arg("out_f32") = false, py::arg("want_stats") = false,
-        py::arg("a_stats") = py::none(), py::arg("a_rowmul") = 1, py::arg("a_n") = 1.0, py::arg("a_eps") = 1e-12,
-        py::arg("colsum") = py::none(), py::arg("r_stats") = py::none(), py::arg("r_n") = 1.0,
-        py::arg("r_eps") = 1e-12, py::arg("r_gamma") = py::none(), py::arg("r_beta") = py::none());
   m.def("dense_softmax", &dense_softmax, "softmax(x @ w[:n]^T + bias[:n]) for n <= 16 labels (x f32)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("n"));
   m.def("key_mask_adder", &key_mask_adder, "(one - m) * scale as f32", py::arg("m"), py::arg("one"),

@@ -25,8 +25,6 @@ inline bool cgemm_cfg_id(int cfg) {
 bool cgemm_supported(const IGemmArgs& a, int a_mode);
 int cgemm_config_bm(int cfg);
 int cgemm_config_bn(int cfg);
-// the tile config has the LayerNorm-fold epilogue (IGemmArgs ln_*) compiled in
-bool cgemm_ln_ok(int cfg);
 hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t stream);
 // the config can finish split-K in-kernel (IGemmArgs::counters)
 bool cgemm_fixup_ok(int cfg);

@@ -57,10 +57,7 @@ struct CG {
   static constexpr int PASSES = LDS_EPI_FULL > 160 * 1024 ? 2 : 1;
   static constexpr int RPP = BM / PASSES;
   static constexpr int LDS_EPI = RPP * CS_LD * 4;
-  // LayerNorm-fold row statistics (6 floats per tile row) live past the fp32 tile
-  static constexpr int LN_OFF = LDS_EPI;
-  static constexpr int LDS_EPI_LN = LDS_EPI + 24 * BM;
-  static constexpr int LDS = LDS_MAIN > LDS_EPI_LN ? LDS_MAIN : LDS_EPI_LN;
+  static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
   static_assert(RPP % WM == 0, "epilogue passes split the tile at wave-row boundaries");
   static_assert(APW >= 1 && BPW >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "DMA piece split");
   static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
@@ -72,7 +69,7 @@ template <int BM, int BN, int NT>
 __device__ __forceinline__ void prefetch_residual(const IGemmArgs& p, int m0, int n0, int tid,
                                                   uint4 (&rpre)[Epi<BM, BN, NT>::PRE > 0 ? Epi<BM, BN, NT>::PRE : 1]) {
   using E = Epi<BM, BN, NT>;
-  if (E::PRE == 0 || !p.residual || p.splits > 1 || p.ln_mode || (p.N % 8) || (p.ldr % 8)) return;
+  if (E::PRE == 0 || !p.residual || p.splits > 1 || (p.N % 8) || (p.ldr % 8)) return;
 #pragma unroll
   for (int it = 0; it < E::PRE; ++it) {
     int row, col;
@@ -122,61 +119,12 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
   }
 }
 
-// The LayerNorm-fold epilogue (IGemmArgs ln_*): per chunk, un-normalised A
-// rows and / or residual rows are normalised with the tile's row statistics,
-// and the stored values' per-row sum / sum of squares accumulate in LDS; after
-// the pass, one thread per row writes this tile's part of the statistics.
-template <int RPP, int BN, int NT, int CS_LD, int ACT>
-__device__ __forceinline__ void epilogue_rows_ln(const IGemmArgs& p, const float* Cs, int mp, int n0, int tid,
-                                                 const float4 b0, const float4 b1, const LnRows& L,
-                                                 const LnCols& C, int r0) {
-  using E = Epi<RPP, BN, NT>;
-  const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-  // every residual chunk of the pass in flight at once (the accumulators are
-  // dead by now: registers are free), then the arithmetic
-  uint4 rr[E::ITERS];
-#pragma unroll
-  for (int it = 0; it < E::ITERS; ++it) {
-    int row, col;
-    const bool in = epi_rowcol<RPP, BN, NT>(tid, it, row, col);
-    const int m = mp + row, n = n0 + col;
-    rr[it] = (p.residual && in && m < p.M && n < p.N)
-                 ? *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n)
-                 : make_uint4(0, 0, 0, 0);
-  }
-#pragma unroll
-  for (int it = 0; it < E::ITERS; ++it) {
-    int row, col;
-    if (!epi_rowcol<RPP, BN, NT>(tid, it, row, col)) continue;
-    const int m = mp + row, n = n0 + col;
-    if (m >= p.M || n >= p.N) continue;
-    epi_chunk_ln<ACT>(p, Cs + row * CS_LD + col, m, n, r0 + row, bv, L, C, rr[it]);
-  }
-  if (p.ln_mode & 1) {
-    __syncthreads();
-    if (tid < RPP && mp + tid < p.M) {
-      float* o = p.ln_out + (size_t(mp + tid) * p.ln_out_parts + n0 / BN) * 2;
-      o[0] = L.sum[r0 + tid];
-      o[1] = L.sq[r0 + tid];
-    }
-  }
-}
-
 // Waves per SIMD the register allocation must leave room for: the 4-wave
 // 32-KB tiles (64x64, 2 slots) fit 5 workgroups per CU by LDS, i.e. 5 waves
 // per SIMD, which needs <= 102 VGPRs (unconstrained they took 128: 4 per CU)
 template <int BM, int BN, int WGM, int WGN, int S>
 constexpr int cg_waves_per_eu() {
   return (WGM * WGN == 4 && CG<BM, BN, WGM, WGN, S>::LDS <= 32 * 1024) ? 5 : 1;
-}
-
-// LayerNorm-fold epilogue compiled in: 4-wave one-pass tiles with the full
-// register file (not the 5-waves-per-SIMD 32-KB tiles, nor the 8-wave tiles,
-// whose register budgets the extra epilogue state would spill: measured with
-// -Rpass-analysis=kernel-resource-usage)
-template <int BM, int BN, int WGM, int WGN, int S>
-constexpr bool cg_ln_ok() {
-  return CG<BM, BN, WGM, WGN, S>::PASSES == 1 && cg_waves_per_eu<BM, BN, WGM, WGN, S>() == 1 && WGM * WGN == 4;
 }
 
 template <int BM, int BN, int WGM, int WGN, int S, int AM>
@@ -416,21 +364,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
   wait_vmcnt<0>();
   __syncthreads();
   if (dbg & 8) return;
-  // LayerNorm-fold row statistics (ordered before their use by the pass barrier below)
-  const LnRows L{reinterpret_cast<float*>(smem + G::LN_OFF), reinterpret_cast<float*>(smem + G::LN_OFF) + BM,
-                 reinterpret_cast<float*>(smem + G::LN_OFF) + 2 * BM, reinterpret_cast<float*>(smem + G::LN_OFF) + 3 * BM,
-                 reinterpret_cast<float*>(smem + G::LN_OFF) + 4 * BM, reinterpret_cast<float*>(smem + G::LN_OFF) + 5 * BM};
-  // this thread's epilogue column vectors (loaded once; the thread's column is fixed)
-  LnCols C;
-  if constexpr (cg_ln_ok<BM, BN, WGM, WGN, S>()) {
-    if (p.ln_mode && p.splits <= 1) {
-      ln_prepare<BM>(p, m0, tid, L);
-      int row0, col0;
-      epi_rowcol<G::RPP, BN, G::NT>(tid, 0, row0, col0);
-      ln_cols(p, n0 + col0, C);
-    }
-  }
-
   // ---- epilogue: stage the fp32 tile in LDS, then coalesced row chunks
   // (G::PASSES row passes of G::RPP rows when the whole fp32 tile does not fit)
   float* Cs = reinterpret_cast<float*>(smem);
@@ -507,16 +440,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
           }
           return;
         }
-      }
-      continue;
-    }
-    if constexpr (cg_ln_ok<BM, BN, WGM, WGN, S>()) if (p.ln_mode) {
-      switch (p.act) {
-        case kActRelu: epilogue_rows_ln<RPP, BN, G::NT, G::CS_LD, kActRelu>(p, Cs, mp, n0, tid, bias0, bias1, L, C, ps * RPP); break;
-        case kActGeluTanh: epilogue_rows_ln<RPP, BN, G::NT, G::CS_LD, kActGeluTanh>(p, Cs, mp, n0, tid, bias0, bias1, L, C, ps * RPP); break;
-        case kActGeluErf: epilogue_rows_ln<RPP, BN, G::NT, G::CS_LD, kActGeluErf>(p, Cs, mp, n0, tid, bias0, bias1, L, C, ps * RPP); break;
-        case kActTanh: epilogue_rows_ln<RPP, BN, G::NT, G::CS_LD, kActTanh>(p, Cs, mp, n0, tid, bias0, bias1, L, C, ps * RPP); break;
-        default: epilogue_rows_ln<RPP, BN, G::NT, G::CS_LD, 0>(p, Cs, mp, n0, tid, bias0, bias1, L, C, ps * RPP); break;
       }
       continue;
     }
@@ -604,24 +527,6 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
 }
 
 }  // namespace
-
-bool cgemm_ln_ok(int cfg) {
-  switch (cfg_index(cfg)) {
-#define TFSK_LN(i, BM_, BN_, WGM_, WGN_, S_) \
-  case i: return cg_ln_ok<BM_, BN_, WGM_, WGN_, S_>();
-    TFSK_LN(0, 128, 128, 2, 2, 3) TFSK_LN(1, 128, 128, 2, 2, 2) TFSK_LN(2, 64, 128, 2, 2, 4)
-    TFSK_LN(3, 128, 64, 2, 2, 4) TFSK_LN(4, 64, 64, 2, 2, 4) TFSK_LN(5, 256, 128, 4, 2, 3)
-    TFSK_LN(6, 128, 256, 2, 4, 3) TFSK_LN(7, 128, 128, 2, 4, 4) TFSK_LN(8, 64, 256, 1, 4, 3)
-    TFSK_LN(9, 256, 64, 4, 1, 3) TFSK_LN(10, 64, 64, 2, 2, 2) TFSK_LN(11, 64, 128, 2, 2, 2)
-    TFSK_LN(12, 128, 64, 2, 2, 2) TFSK_LN(13, 128, 96, 2, 2, 3) TFSK_LN(14, 128, 96, 2, 2, 4)
-    TFSK_LN(15, 64, 96, 2, 2, 3) TFSK_LN(16, 64, 64, 1, 2, 2) TFSK_LN(17, 64, 64, 1, 2, 3)
-    TFSK_LN(18, 64, 64, 2, 1, 3) TFSK_LN(19, 128, 64, 2, 1, 2) TFSK_LN(20, 64, 128, 1, 2, 2)
-    TFSK_LN(21, 128, 64, 2, 1, 3) TFSK_LN(22, 64, 128, 1, 2, 3) TFSK_LN(23, 64, 64, 2, 2, 3)
-    TFSK_LN(24, 256, 192, 4, 2, 2)
-#undef TFSK_LN
-    default: return false;
-  }
-}
 
 bool cgemm_fixup_ok(int cfg) {
   // the in-kernel split-K fixup needs the whole fp32 tile in LDS at once (one pass)

@@ -205,127 +205,5 @@ __device__ __forceinline__ void epi_chunk(const IGemmArgs& p, const float* src, 
   if (p.out2) post_chunk(p, m, n, v);
 }
 
-// ---- LayerNorm folding (IGemmArgs ln_*): per-row statistics in LDS.
-// Row r of the tile: mean / rstd of A's rows (ln_a) and of the residual's rows
-// (ln_r), and the running sum / sum of squares of the stored output (ln_out).
-struct LnRows {
-  float* mu_a;
-  float* rs_a;
-  float* mu_r;
-  float* rs_r;
-  float* sum;
-  float* sq;
-};
-
-__device__ __forceinline__ void ln_row_stats(const float* st, int parts, float n, float eps, float& mu,
-                                             float& rstd) {
-  float s1 = 0.f, s2 = 0.f;
-  for (int q = 0; q < parts; ++q) {
-    s1 += st[2 * q];
-    s2 += st[2 * q + 1];
-  }
-  mu = s1 / n;
-  const float var = fmaxf(s2 / n - mu * mu, 0.f);
-  rstd = rsqrtf(var + eps);
-}
-
-// threads tid < BM fill the tile's row statistics (rows past M get zeros)
-template <int BM>
-__device__ __forceinline__ void ln_prepare(const IGemmArgs& p, int m0, int tid, const LnRows& L) {
-  if (tid < BM) {
-    const int m = m0 + tid;
-    float mu = 0.f, rs = 0.f;
-    if ((p.ln_mode & 2) && m < p.M)
-      ln_row_stats(p.ln_a + size_t(m) * p.ln_a_rowmul * p.ln_a_parts * 2, p.ln_a_parts, p.ln_a_n, p.ln_a_eps, mu, rs);
-    L.mu_a[tid] = mu;
-    L.rs_a[tid] = rs;
-    mu = rs = 0.f;
-    if ((p.ln_mode & 4) && m < p.M)
-      ln_row_stats(p.ln_r + size_t(m) * p.ln_r_parts * 2, p.ln_r_parts, p.ln_r_n, p.ln_r_eps, mu, rs);
-    L.mu_r[tid] = mu;
-    L.rs_r[tid] = rs;
-    L.sum[tid] = 0.f;
-    L.sq[tid] = 0.f;
-  }
-}
-
-__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
-  const float4 a = *reinterpret_cast<const float4*>(p);
-  const float4 b = *reinterpret_cast<const float4*>(p + 4);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-
-// The per-column vectors of the LayerNorm modes for this thread's (fixed)
-// epilogue column, loaded once per tile (colsum for ln_a, gamma / beta for ln_r).
-struct LnCols {
-  float cs[8], g[8], b[8];
-};
-
-__device__ __forceinline__ void ln_cols(const IGemmArgs& p, int n, LnCols& c) {
-  const bool in = n + 8 <= p.N;
-  if ((p.ln_mode & 2) && in) load8(p.ln_colsum + n, c.cs);
-  else
-#pragma unroll
-    for (int e = 0; e < 8; ++e) c.cs[e] = 0.f;
-  if ((p.ln_mode & 4) && in) {
-    load8(p.ln_r_gamma + n, c.g);
-    load8(p.ln_r_beta + n, c.b);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) c.g[e] = c.b[e] = 0.f;
-  }
-}
-
-// One 8-column chunk with the LayerNorm modes (row r of the tile = row m;
-// rr = the raw residual chunk, already loaded)
-template <int ACT>
-__device__ __forceinline__ void epi_chunk_ln(const IGemmArgs& p, const float* src, int m, int n, int r,
-                                             const float (&bv)[8], const LnRows& L, const LnCols& C,
-                                             const uint4 rr) {
-  float v[8];
-  load8(src, v);
-  const float alpha = p.alpha;
-  if (p.ln_mode & 2) {
-    const float mu = L.mu_a[r], rs = L.rs_a[r];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = rs * (v[e] * alpha - mu * C.cs[e]) + bv[e];
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = v[e] * alpha + bv[e];
-  }
-  if (p.residual) {
-    const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-    float rv[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      rv[2 * e] = __uint_as_float(w[e] << 16);
-      rv[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
-    }
-    if (p.ln_mode & 4) {
-      const float mu = L.mu_r[r], rs = L.rs_r[r];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) rv[e] = (rv[e] - mu) * rs * C.g[e] + C.b[e];
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += rv[e];
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = act_fn<ACT>(v[e]);
-  if (p.ln_mode & 1) {
-    // statistics of the values as stored (bf16-rounded) -- what the consumer reads
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float q = p.out_f32 ? v[e] : static_cast<float>(static_cast<__bf16>(v[e]));
-      s1 += q;
-      s2 += q * q;
-    }
-    atomicAdd(L.sum + r, s1);
-    atomicAdd(L.sq + r, s2);
-  }
-  store_chunk(p, p.out, m, n, v);
-  if (p.out2) post_chunk(p, m, n, v);
-}
-
 }  // namespace gemm
 }  // namespace tfsk

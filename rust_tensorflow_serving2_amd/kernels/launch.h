@@ -56,28 +56,6 @@ struct IGemmArgs {
   // arrival counter per tile (zero between launches); the last slice to arrive
   // sums the slabs and runs the epilogue, then re-zeroes its counter
   int* counters;
-  // LayerNorm folding (cgemm, splits == 1; BERT's post-LN blocks without LN
-  // kernels).  ln_mode bits: 1 = ln_out, 2 = ln_a, 4 = ln_r.
-  //  ln_out [M][ln_out_parts][2]: per row of the stored (bf16-rounded) output,
-  //    the sum and sum of squares over this tile's BN columns (part n0 / BN);
-  //  ln_a: A holds un-normalised rows whose per-part stats are ln_a
-  //    [.][ln_a_parts][2] (A row m -> stats row m * ln_a_rowmul); the weights
-  //    were pre-scaled by gamma, ln_colsum[n] = sum_k W'[n][k], and the bias
-  //    absorbed beta: v = rstd_m * (acc - mu_m * ln_colsum[n]) + bias[n];
-  //  ln_r: the residual holds un-normalised rows (stats ln_r, same layout):
-  //    r' = (r - mu_m) * rstd_m * ln_r_gamma[n] + ln_r_beta[n].
-  int ln_mode;
-  float* ln_out;
-  int ln_out_parts;
-  const float* ln_a;
-  int ln_a_parts, ln_a_rowmul;
-  float ln_a_n, ln_a_eps;
-  const float* ln_colsum;
-  const float* ln_r;
-  int ln_r_parts;
-  float ln_r_n, ln_r_eps;
-  const float* ln_r_gamma;
-  const float* ln_r_beta;
 };
 
 // Per-device pool of zeroed split-K arrival counters: a launch captured into a

@@ -171,18 +171,6 @@ def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
     return s
 
 
-_LN_OK: Dict[int, bool] = {}
-
-
-def _ln_ok(cfg: int) -> bool:
-    if cfg not in _LN_OK:
-        try:
-            _LN_OK[cfg] = bool(hip().cgemm_ln_ok(cfg))
-        except (KernelsUnavailable, AttributeError):
-            _LN_OK[cfg] = False
-    return _LN_OK[cfg]
-
-
 def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
                halo: bool = False, no_split: bool = False, n_multiple: bool = False):
     """(tile config, split-K) pairs worth timing for an M x N x K problem
@@ -220,8 +208,6 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
             continue   # 96-wide tiles: only where they divide N (BERT's 768 / 2304 / 3072)
         if n_multiple and N % bn:
             continue   # per-tile row statistics need whole tiles along N (LayerNorm folding)
-        if no_split and cgemm_only and not _ln_ok(cfg):
-            continue   # (the LayerNorm-fold GEMMs: only configs with that epilogue compiled in)
         tiles = -(-M // bm) * -(-N // bn)
         for s in (1, 2, 4, 8, 16):
             if s > 1 and (no_split or nk // s < 2 or tiles >= 1024 or tiles * s > 4096):

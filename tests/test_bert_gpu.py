@@ -20,9 +20,7 @@ def bert_base(tmp_path_factory):
     return path
 
 
-@pytest.mark.parametrize("fold", ["0", "1"])
-def test_bert_base_gpu_matches_cpu(bert_base, fold, monkeypatch):
-    monkeypatch.setenv("TFSERVE_LN_FOLD", fold)
+def test_bert_base_gpu_matches_cpu(bert_base):
     from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
     gpu = Servable("bert", 1, bert_base, ServableOptions(device="cuda:0", max_batch_size=8))
     cpu = Servable("bert", 1, bert_base, ServableOptions(device="cpu"))
@@ -42,12 +40,7 @@ def test_bert_base_gpu_matches_cpu(bert_base, fold, monkeypatch):
     runner = next(iter(gpu._runners.values()))
     hist = runner.program.op_histogram()
     assert hist["_Attention"] == 12 and hist["_FusedQKV"] == 12
-    if fold == "1":
-        # LayerNorm folding: 23 of the 24 encoder LayerNorms run inside the GEMMs
-        # around them (the last one feeds the pooler's strided slice: one kernel)
-        assert hist["_LazyLayerNorm"] == 23 and hist["_LayerNorm"] == 1
-    else:
-        assert "_LazyLayerNorm" not in hist and hist["_LayerNorm"] == 24
+    assert hist["_LayerNorm"] == 24
     assert hist["_EmbeddingLN"] == 1 and hist["_KeyMaskAdder"] == 1 and "GatherV2" not in hist
 
 

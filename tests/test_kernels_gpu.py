@@ -711,61 +711,6 @@ def test_key_mask_adder_matches_fp32():
     torch.testing.assert_close(hip().key_mask_adder(mf.to(DEV), 1.0, 2.5).cpu(), (1.0 - mf) * 2.5)
 
 
-def _ln_ref(x, g, b, eps):
-    return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), g, b, eps)
-
-
-def _part_stats(y, bn):
-    """[M][N / bn][2] per-part sum / sum of squares of the bf16 values."""
-    yf = y.float().reshape(y.shape[0], -1, bn)
-    return torch.stack([yf.sum(-1), (yf * yf).sum(-1)], -1)
-
-
-@pytest.mark.parametrize("cfg,bn", [(36, 64), (45, 96), (43, 128), (40, 256)])
-def test_linear_ln_fold_modes_match_fp32(cfg, bn):
-    """LayerNorm folding (BERT post-LN): the producer GEMM emits per-row part
-    statistics, a consumer GEMM applies LN to its A operand through gamma-scaled
-    weights + column sums + a beta-folded bias, and to its residual per element."""
-    M, H, F = 256, 768, 3072
-    eps = 1e-12
-    H_ = hip()
-    x = rnd(M, H, seed=41).to(BF)
-    w = rnd(H, H, scale=1 / math.sqrt(H), seed=42).to(BF)
-    b = rnd(H, scale=0.1, seed=43)
-    res = rnd(M, H, seed=44).to(BF)
-    # (1) producer: y = x W^T + b + res, with statistics
-    y, st = H_.linear_ln(x.to(DEV), w.to(DEV), b.to(DEV), res.to(DEV), 0, cfg, False, want_stats=True)
-    ref = x.float() @ w.float().t() + b + res.float()
-    assert (y.float().cpu() - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
-    assert st.shape == (M, H // bn, 2)
-    torch.testing.assert_close(st.cpu(), _part_stats(y.cpu(), bn), rtol=1e-4, atol=1e-2)
-    # (2) consumer of LN(y) as A: FFN1 with GELU, gamma / beta folded
-    g = 1.0 + rnd(H, scale=0.1, seed=45)
-    be = rnd(H, scale=0.1, seed=46)
-    w1 = rnd(F, H, scale=1 / math.sqrt(H), seed=47).to(BF)
-    b1 = rnd(F, scale=0.1, seed=48)
-    wf = (w1.float() * g[None, :]).to(BF)
-    colsum = wf.float().sum(1)
-    bf = b1 + w1.float() @ be
-    z, _ = H_.linear_ln(y, wf.to(DEV), bf.to(DEV), None, ACT["gelu_tanh"], cfg, False, a_stats=st, a_n=float(H),
-                        a_eps=eps, colsum=colsum.to(DEV))
-    zref = F_gelu(_ln_ref(y.cpu(), g, be, eps).to(BF).float() @ w1.float().t() + b1)
-    assert (z.float().cpu() - zref).abs().max().item() < 4e-2 * max(1.0, zref.abs().max().item())
-    # (3) residual LN(y) (+ statistics of the new output): FFN2-like
-    i = rnd(M, F, seed=49).to(BF)
-    w2 = rnd(H, F, scale=1 / math.sqrt(F), seed=50).to(BF)
-    b2 = rnd(H, scale=0.1, seed=51)
-    o, st2 = H_.linear_ln(i.to(DEV), w2.to(DEV), b2.to(DEV), y, 0, cfg, False, want_stats=True, r_stats=st,
-                          r_n=float(H), r_eps=eps, r_gamma=g.to(DEV), r_beta=be.to(DEV))
-    oref = i.float() @ w2.float().t() + b2 + _ln_ref(y.cpu(), g, be, eps)
-    assert (o.float().cpu() - oref).abs().max().item() < 3e-2 * oref.abs().max().item()
-    torch.testing.assert_close(st2.cpu(), _part_stats(o.cpu(), bn), rtol=1e-4, atol=1e-2)
-
-
-def F_gelu(x):
-    return F.gelu(x, approximate="tanh")
-
-
 @pytest.mark.parametrize("k1,n1,n2", [(64, 256, 64), (64, 256, 128), (128, 512, 128), (128, 512, 256)])
 @pytest.mark.parametrize("m,with_res,act1,act2", [(4 * 56 * 56, True, "relu", "relu"), (77, False, "none", "relu"),
                                                    (130, True, "relu", "none")])
