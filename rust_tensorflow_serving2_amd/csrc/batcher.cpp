@@ -335,41 +335,6 @@ int Endpoint::acquire(int slot, int timeout_ms, std::vector<std::pair<int, int>>
   return -1;
 }
 
-void Endpoint::pair_slots(int a, int b) {
-  std::lock_guard<std::mutex> g(mu_);
-  const int N = int(slots_.size());
-  if (a < 0 || b < 0 || a >= N || b >= N || a == b) return;
-  slots_[b].cv = slots_[a].cv;
-}
-
-int Endpoint::acquire_any(int a, int b, int timeout_ms, int* which) {
-  std::unique_lock<std::mutex> lk(mu_);
-  const int N = int(slots_.size());
-  if (a < 0 || b < 0 || a >= N || b >= N) return -1;
-  const auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
-  while (!closed_) {
-    const auto now = Clock::now();
-    // the batch that opened first goes first (FIFO across the two slots)
-    const bool b_first = slots_[b].state != kFree && slots_[b].reserved > 0 &&
-                         (slots_[a].state == kFree || slots_[a].reserved == 0 || slots_[b].first < slots_[a].first);
-    const int order[2] = {b_first ? b : a, b_first ? a : b};
-    auto wake = deadline;
-    bool again = false;
-    for (int k = 0; k < 2; ++k) {
-      const int r = poll_slot_locked(order[k], now, wake);
-      if (r > 0) {
-        *which = order[k];
-        return r;
-      }
-      again = again || r < 0;
-    }
-    if (again) continue;
-    if (now >= deadline) return 0;
-    slots_[a].cv->wait_until(lk, wake);   // shared with b (pair_slots)
-  }
-  return -1;
-}
-
 void Endpoint::complete(int slot, Server& srv) {
   Slot& s = slots_[slot];
   ModelSpecView spec;

@@ -124,12 +124,6 @@ class Endpoint {
   // are appended to it (the worker copies them to the device right away) and
   // the call also returns 0 early whenever new rows are available.
   int acquire(int slot, int timeout_ms, std::vector<std::pair<int, int>>* ranges = nullptr);
-  // A lane driving two slots (double-buffered: the next batch's H2D and launch
-  // are issued while the previous one runs): the batch of whichever of slot
-  // a / b is ready first (the older one when both are); *which = its slot.
-  // pair_slots() makes the two slots share one condition variable first.
-  void pair_slots(int a, int b);
-  int acquire_any(int a, int b, int timeout_ms, int* which);
   // when the slot's current batch opened (first row reserved); for tracing
   Clock::time_point slot_opened(int slot) {
     std::lock_guard<std::mutex> g(mu_);
@@ -170,7 +164,7 @@ class Endpoint {
 
  private:
   int open_slot_locked(int n);
-  // one look at a slot for acquire / acquire_any (caller holds mu_): > 0 the
+  // one look at a slot for acquire (caller holds mu_): > 0 the
   // slot's batch was taken (rows), 0 not ready (wake <- when to look again),
   // -1 its state just changed (look again now)
   int poll_slot_locked(int slot, Clock::time_point now, Clock::time_point& wake);

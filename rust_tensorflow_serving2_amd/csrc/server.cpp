@@ -166,15 +166,8 @@ struct LaneBucket {
 class NativeLane {
  public:
   NativeLane(Server* srv, std::shared_ptr<Endpoint> ep, int slot, int device, void* stream,
-             std::vector<LaneBucket> buckets, int slot2 = -1, std::vector<LaneBucket> buckets2 = {})
-      : srv_(srv), ep_(std::move(ep)), slot_(slot), device_(device), stream_(stream), buckets_(std::move(buckets)),
-        slot2_(slot2), buckets2_(std::move(buckets2)) {
-    std::sort(buckets2_.begin(), buckets2_.end(), [](auto& a, auto& b) { return a.rows < b.rows; });
-    if (slot2_ >= 0 && buckets2_.size() == buckets_.size()) {
-      ep_->pair_slots(slot_, slot2_);
-    } else {
-      slot2_ = -1;
-    }
+             std::vector<LaneBucket> buckets)
+      : srv_(srv), ep_(std::move(ep)), slot_(slot), device_(device), stream_(stream), buckets_(std::move(buckets)) {
     // fault injection for tests (same spec as utils/faults.py):
     // TFSERVE_FAULT=lane_every=N fails every Nth batch, lane_after=N every
     // batch after the first N of this lane (a device that went bad)
@@ -202,7 +195,7 @@ class NativeLane {
     }
     if (const char* t = getenv("TFSERVE_LANE_TIMEOUT_MS")) timeout_floor_ms_ = std::max(1, std::atoi(t));
     const char* eager_env = getenv("TFSERVE_EAGER_H2D");
-    eager_ = eager_ && eager_env && std::atoi(eager_env) != 0 && slot2_ < 0;
+    eager_ = eager_ && eager_env && std::atoi(eager_env) != 0;
     th_ = std::thread([this] { run(); });
   }
   ~NativeLane() { join(); }
@@ -305,142 +298,12 @@ class NativeLane {
                                     c.row_bytes * size_t(r.second), kHipMemcpyHostToDevice, copy_stream_);
     return e;
   }
-  // ---- double-buffered mode (two slots, two graph sets reading two device
-  // input buffers, one stream): the next batch's H2D runs on a copy stream
-  // while the previous batch computes, and its graph is queued right behind
-  // it, so the lane's stream never idles for the host round trip (wake,
-  // respond, acquire, H2D) between its batches.
-  struct Side {
-    void* done = nullptr;
-    void* copied = nullptr;
-    int n = 0;
-    int bucket = -1;
-    Clock::time_point t_acq, t_issue;
-  };
-  // H2D (copy stream) -> graph + D2H (lane stream, after the copy) -> done event
-  int issue_side(HipRt& rt, Side& sd, const std::vector<LaneBucket>& bs, int n) {
-    const LaneBucket* b = nullptr;
-    for (auto& x : bs)
-      if (x.rows >= n) {
-        b = &x;
-        break;
-      }
-    if (!b) return -1;
-    sd.bucket = int(b - bs.data());
-    int e = 0;
-    for (auto& c : b->in)
-      if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
-                                  c.row_bytes * size_t(n), kHipMemcpyHostToDevice, copy_stream_);
-    if (!e) e = rt.event_record(sd.copied, copy_stream_);
-    if (!e) e = rt.stream_wait_event(stream_, sd.copied, 0);
-    if (!e) e = rt.launch(b->exec, stream_);
-    for (auto& c : b->out)
-      if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
-                                  c.row_bytes * size_t(n), kHipMemcpyDeviceToHost, stream_);
-    if (!e) e = rt.event_record(sd.done, stream_);
-    return e;
-  }
-  // wait for a side's batch and answer it; false when the device hung
-  bool finish_side(HipRt& rt, Side& sd, int slot, int issue_err) {
-    int e = issue_err;
-    if (!e) e = wait(rt, sd.done, sd.t_issue, deadline_from(Clock::now()), ema_us_[sd.bucket]);
-    if (e == kLaneHung) {
-      errors++;
-      ep_->fail_dead(slot, *srv_, 14 /*UNAVAILABLE*/, "GPU batch timed out (device not responding)");
-      return false;
-    }
-    if (e != 0) {
-      errors++;
-      std::string why = e > 0 && rt.err ? std::string(rt.err(e)) : std::string("no graph for this batch");
-      ep_->fail(slot, *srv_, 13 /*INTERNAL*/, "GPU batch failed: " + why);
-      return true;
-    }
-    const auto t_done = Clock::now();
-    const double us = std::chrono::duration<double, std::micro>(t_done - sd.t_issue).count();
-    double& ema = ema_us_[sd.bucket];
-    ema = ema <= 0 ? us : 0.8 * ema + 0.2 * us;
-    batches++;
-    const double ms = std::chrono::duration<double, std::milli>(t_done - sd.t_acq).count();
-    mean_ms_ = batches == 1 ? ms : 0.9 * mean_ms_ + 0.1 * ms;
-    const bool tracing = trace_buf().on.load(std::memory_order_relaxed);
-    const auto t_open = tracing ? ep_->slot_opened(slot) : t_done;
-    ep_->complete(slot, *srv_);
-    if (tracing)
-      trace_buf().add({ep_->id, slot, sd.n, us_of(t_open), us_of(sd.t_acq), us_of(sd.t_issue), us_of(t_done),
-                       us_of(Clock::now())});
-    return true;
-  }
-  void run_paired(HipRt& rt) {
-    Side sides[2];
-    bool ok = rt.stream_create && rt.stream_wait_event &&
-              rt.stream_create(&copy_stream_, kHipStreamNonBlocking) == 0;
-    for (auto& sd : sides)
-      ok = ok && rt.event_create(&sd.done, kHipEventDisableTiming) == 0 &&
-           rt.event_create(&sd.copied, kHipEventDisableTiming) == 0;
-    const int slots[2] = {slot_, slot2_};
-    const std::vector<LaneBucket>* bsets[2] = {&buckets_, &buckets2_};
-    int pending = -1, pending_err = 0;
-    bool hung = false;
-    while (ok) {
-      int which = -1;
-      // with a batch in flight only look (a partly filled batch waits for its
-      // deadline or for the device to go idle); else wait for one
-      const int n = ep_->acquire_any(slot_, slot2_, pending >= 0 ? 0 : 100, &which);
-      if (n < 0) break;   // endpoint closed
-      if (n == 0) {
-        if (pending >= 0) {
-          hung = !finish_side(rt, sides[pending], slots[pending], pending_err);
-          pending = -1;
-          if (hung) break;
-        }
-        continue;
-      }
-      const int side = which == slot_ ? 0 : 1;
-      Side& sd = sides[side];
-      sd.n = n;
-      sd.t_acq = Clock::now();
-      ++seen_;
-      int e = 0;
-      bool issued = false;
-      if ((fault_every_ > 0 && seen_ % uint64_t(fault_every_) == 0) ||
-          (fault_after_ >= 0 && seen_ > uint64_t(fault_after_))) {
-        errors++;
-        ep_->fail(slots[side], *srv_, 13 /*INTERNAL*/, "injected fault (TFSERVE_FAULT)");
-      } else {
-        sd.t_issue = Clock::now();
-        e = issue_side(rt, sd, *bsets[side], n);
-        issued = true;
-      }
-      if (pending >= 0) {
-        hung = !finish_side(rt, sides[pending], slots[pending], pending_err);
-        pending = -1;
-        if (hung) break;
-      }
-      if (issued) {
-        pending = side;
-        pending_err = e;
-      }
-    }
-    if (pending >= 0 && !hung) hung = !finish_side(rt, sides[pending], slots[pending], pending_err);
-    dead = hung;
-    if (hung) return;   // the wedged stream still references these: leak them rather than block
-    for (auto& sd : sides) {
-      if (sd.done) rt.event_destroy(sd.done);
-      if (sd.copied) rt.event_destroy(sd.copied);
-    }
-    if (copy_stream_ && rt.stream_destroy) rt.stream_destroy(copy_stream_);
-  }
-
   void run() {
     pthread_setname_np(pthread_self(), "tfs-nlane");
     prctl(PR_SET_TIMERSLACK, 1000UL);     // 1-us timer slack for the completion naps (wait())
     ema_us_.assign(buckets_.size(), 0.0);
     HipRt& rt = hip_rt();
     rt.set_device(device_);
-    if (slot2_ >= 0) {
-      run_paired(rt);
-      return;
-    }
     void* done = nullptr;
     if (rt.event_create(&done, kHipEventDisableTiming) != 0) done = nullptr;
     if (eager_ && (!rt.stream_create || !rt.stream_wait_event ||
@@ -516,8 +379,6 @@ class NativeLane {
   int slot_, device_;
   void* stream_;
   std::vector<LaneBucket> buckets_;
-  int slot2_ = -1;                       // double-buffered mode: the second slot and its graphs
-  std::vector<LaneBucket> buckets2_;
   bool eager_ = false;
   void* copy_stream_ = nullptr;
   void* copied_ = nullptr;
@@ -732,7 +593,7 @@ void register_server(py::module_& m) {
         s.join_lanes(id);
       })
       .def("start_native_lane", [](PyServer& s, int id, int slot, int device, uintptr_t stream,
-                                   const py::list& buckets, int slot2, const py::list& buckets2) {
+                                   const py::list& buckets) {
         auto ep = s.fast->endpoint(id);
         if (!ep || buckets.empty() || !hip_rt().load()) return false;
         auto parse = [](const py::list& l) {
@@ -756,10 +617,9 @@ void register_server(py::module_& m) {
         };
         std::lock_guard<std::mutex> g(s.lmu);
         s.lanes.push_back(std::make_unique<NativeLane>(s.srv.get(), ep, slot, device, reinterpret_cast<void*>(stream),
-                                                       parse(buckets), slot2, parse(buckets2)));
+                                                       parse(buckets)));
         return true;
-      }, py::arg("endpoint"), py::arg("slot"), py::arg("device"), py::arg("stream"), py::arg("buckets"),
-         py::arg("slot2") = -1, py::arg("buckets2") = py::list())
+      }, py::arg("endpoint"), py::arg("slot"), py::arg("device"), py::arg("stream"), py::arg("buckets"))
       .def("enable_router", [](PyServer& s, const std::string& group, int rank, int world, int ncells,
                                size_t req_cap, size_t resp_cap, int margin) {
         if (s.router) throw std::runtime_error("router already enabled");
@@ -811,20 +671,6 @@ void register_server(py::module_& m) {
         if (!ep) return -1;
         py::gil_scoped_release nogil;
         return ep->acquire(slot, timeout_ms);
-      })
-      .def("pair_slots", [](PyServer& s, int id, int a, int b) {
-        auto ep = s.fast->endpoint(id, true);
-        if (ep) ep->pair_slots(a, b);
-      })
-      .def("acquire_any", [](PyServer& s, int id, int a, int b, int timeout_ms) -> py::tuple {
-        auto ep = s.fast->endpoint(id, true);
-        if (!ep) return py::make_tuple(-1, -1);
-        int which = -1, n = 0;
-        {
-          py::gil_scoped_release nogil;
-          n = ep->acquire_any(a, b, timeout_ms, &which);
-        }
-        return py::make_tuple(n, which);
       })
       .def("complete", [](PyServer& s, int id, int slot) {
         auto ep = s.fast->endpoint(id, true);

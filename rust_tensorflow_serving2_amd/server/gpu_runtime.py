@@ -64,11 +64,8 @@ def _torch_dtype(dt: int) -> torch.dtype:
 
 
 class _Lane:
-    def __init__(self, device, stream=None, pool_src: "Optional[_Lane]" = None):
-        # a twin lane (double-buffered native lanes) shares its primary's stream
-        # and graph pool: the two replay strictly one after the other
-        self.stream = stream if stream is not None else torch.cuda.Stream(device=device)
-        self.pool_src = pool_src
+    def __init__(self, device):
+        self.stream = torch.cuda.Stream(device=device)
         self.lock = threading.Lock()
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.static_in: Dict[int, List[torch.Tensor]] = {}
@@ -117,19 +114,10 @@ class GpuRunner:
         # staged as bf16: converted on ingest (csrc/ingest.h) or by the H2D
         # staging copy, half the pinned / PCIe / device bytes
         self.slot_dtypes = [T.DT_BFLOAT16 if self._bf16_feed(i, s) else s.dtype for i, s in enumerate(in_specs)]
-        # TFSERVE_LANE_SIDES=2: every fast lane gets a twin (second pinned slot,
-        # device input buffer and graph set on the same stream), so its C++
-        # worker keeps the next batch's H2D and graph queued behind the running
-        # one (csrc/server.cpp NativeLane::run_paired)
-        self.twins: Dict[int, int] = {}
         self.n_primary = max(1, lanes) + 1
         if self.batched:
             with torch.cuda.device(self.device):
                 self.lanes = [_Lane(self.device) for _ in range(self.n_primary)]
-                if int(os.environ.get("TFSERVE_LANE_SIDES", "1")) == 2:
-                    for i in range(max(1, self.n_primary - 1)):
-                        self.twins[i] = len(self.lanes)
-                        self.lanes.append(_Lane(self.device, stream=self.lanes[i].stream, pool_src=self.lanes[i]))
                 for lane in self.lanes:
                     self._alloc_host(lane)
 
@@ -257,13 +245,7 @@ class GpuRunner:
         # the n live rows of a batch, not the whole bucket
         graph = torch.cuda.CUDAGraph()
         if lane.pool is None and lane.share_pool:
-            src = lane.pool_src
-            if src is not None:
-                if src.pool is None:
-                    src.pool = torch.cuda.graph_pool_handle()
-                lane.pool = src.pool
-            else:
-                lane.pool = torch.cuda.graph_pool_handle()
+            lane.pool = torch.cuda.graph_pool_handle()
         with ops.capture_owner(graph), \
                 torch.cuda.graph(graph, pool=lane.pool, stream=lane.stream, capture_error_mode="thread_local"):
             outs = self._finish(self.program.run(ins))

@@ -80,30 +80,16 @@ class FastEndpoint:
             in_ptrs, out_ptrs = self.runner.lane_host_pointers(lane_idx)
             srv.set_slot_buffers(self.id, lane_idx, in_ptrs, out_ptrs)
         self.native_lanes = 0
-        twins = getattr(self.runner, "twins", {})
         slots = 0
         for lane_idx in lanes:
             self.runner.claim(lane_idx)
             # C++ lane worker (graph launch without Python) when every bucket graph
             # carries its own host copies; the Python worker otherwise
             spec = self.runner.native_lane_spec(lane_idx) if NATIVE_LANES else None
-            if spec is not None:
-                # a double-buffered lane drives its twin's slot and graphs too
-                # (registered only here: a slot nobody acquires would strand calls)
-                t = twins.get(lane_idx)
-                spec2 = None
-                if t is not None:
-                    tin, tout = self.runner.lane_host_pointers(t)     # (captures the twin's graphs)
-                    spec2 = self.runner.native_lane_spec(t)
-                    if spec2 is not None:
-                        srv.set_slot_buffers(self.id, t, tin, tout)
-                if srv.start_native_lane(self.id, lane_idx, *spec, slot2=t if spec2 is not None else -1,
-                                         buckets2=spec2[2] if spec2 is not None else []):
-                    self.native_lanes += 1
-                    slots += 2 if spec2 is not None else 1
-                    continue
-                if spec2 is not None:
-                    srv.set_slot_buffers(self.id, t, [], [])     # (a slot without buffers is never opened)
+            if spec is not None and srv.start_native_lane(self.id, lane_idx, *spec):
+                self.native_lanes += 1
+                slots += 1
+                continue
             slots += 1
             th = threading.Thread(target=self._work, args=(lane_idx,), daemon=True,
                                   name=f"tfs-gpu-{servable.name}-{lane_idx}")

@@ -236,59 +236,3 @@ def test_close_answers_every_unstarted_request():
     assert 1 <= codes.count("OK") <= 4 and codes.count("UNAVAILABLE") >= 10, codes
 
 
-def test_paired_slots_one_lane_drives_two():
-    """A double-buffered lane (csrc/server.cpp NativeLane::run_paired) takes
-    the batches of two paired slots with acquire_any: while one batch is "in
-    flight" it only polls (timeout 0) the other slot, completes the older
-    batch first, and every request is answered exactly once with its rows."""
-    srv = _C.Http2Server("127.0.0.1", 0, 2)
-    ep = srv.add_endpoint("m", 1, "serving_default", [("x", T.DT_FLOAT, [ROW])], [("y", T.DT_FLOAT, [ROW])], 4, 2000)
-    bufs = {}
-    for k in (0, 1):
-        bufs[k] = (np.zeros((4, ROW), np.float32), np.zeros((4, ROW), np.float32))
-        srv.set_slot_buffers(ep, k, [bufs[k][0].ctypes.data], [bufs[k][1].ctypes.data])
-    srv.pair_slots(ep, 0, 1)
-    srv.set_route("m", "serving_default", -1, ep)
-    srv.set_route("m", "serving_default", 1, ep)
-    stop = threading.Event()
-    seen = []
-
-    def lane():
-        pending = None
-        while not stop.is_set():
-            n, which = srv.acquire_any(ep, 0, 1, 0 if pending is not None else 50)
-            if n < 0:
-                break
-            if n == 0:
-                if pending is not None:           # nothing new: finish the batch in flight
-                    srv.complete(ep, pending)
-                    pending = None
-                continue
-            assert which in (0, 1) and which != pending
-            xin, yout = bufs[which]
-            yout[:n] = xin[:n] * 2 + 1
-            seen.append((which, n))
-            if pending is not None:
-                srv.complete(ep, pending)
-            pending = which
-        if pending is not None:
-            srv.complete(ep, pending)
-
-    th = threading.Thread(target=lane, daemon=True)
-    srv.start()
-    th.start()
-    try:
-        rng = np.random.default_rng(5)
-        xs = [rng.standard_normal((1, ROW)).astype(np.float32) for _ in range(40)]
-        bodies = [native.encode_predict_request(native.spec_tuple("m", 1, None, ""), {"x": x}) for x in xs]
-        with cf.ThreadPoolExecutor(10) as ex:
-            outs = list(ex.map(lambda b: _call(srv.port, b), bodies))
-        for x, raw in zip(xs, outs):
-            np.testing.assert_allclose(_y(raw), x * 2 + 1, rtol=1e-6)
-        assert sum(n for _w, n in seen) == 40
-        assert {w for w, _n in seen} == {0, 1}            # both slots carried batches
-    finally:
-        stop.set()
-        srv.remove_endpoint(ep)
-        th.join(timeout=5)
-        srv.stop()

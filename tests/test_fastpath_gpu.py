@@ -257,47 +257,3 @@ def test_request_logging_on_the_gpu_fast_path(tmp_path, monkeypatch, ingest):
         srv.stop()
 
 
-def test_double_buffered_native_lanes(tmp_path, monkeypatch):
-    """TFSERVE_LANE_SIDES=2: each C++ lane drives two slots / device input
-    buffers / graph sets on one stream (NativeLane::run_paired).  Many
-    concurrent rows come back to their own callers, batches alternate between
-    the two slots, injected faults fail only their batch, and the loadgen sees
-    no errors."""
-    from rust_tensorflow_serving2_amd.models import resnet
-    import time
-    monkeypatch.setenv("TFSERVE_LANE_SIDES", "2")
-    base = str(tmp_path / "resnet")
-    resnet.export(os.path.join(base, "1"), blocks=(1, 1, 1, 1), width=16, num_classes=10, image_size=32, seed=8)
-    so = ServableOptions(device="cuda:0", max_batch_size=4, allowed_batch_sizes=(1, 2, 4), lanes=2)
-    srv = ModelServer(ServerOptions(port=0, host="127.0.0.1", model_name="resnet", model_base_path=base,
-                                    device="cuda:0", transport="native", servable=so,
-                                    file_system_poll_wait_seconds=0, batch_timeout_us=300)).start()
-    try:
-        tr = srv.transports[0]
-        for _ in range(300):
-            if tr.stats().get("endpoints"):
-                break
-            time.sleep(0.05)
-        eps = list(tr._eps.values())
-        assert eps and eps[0].native_lanes == 2
-        assert len(eps[0].runner.twins) == 2
-        spec = native.spec_tuple("resnet", None, None, "")
-        rng = np.random.default_rng(3)
-        xs = [rng.random((1 + (i % 2), 32, 32, 3), dtype=np.float32) for i in range(40)]
-        bodies = [native.encode_predict_request(spec, {"input": x}) for x in xs]
-
-        async def go():
-            async with grpc.aio.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
-                stub = ch.unary_unary(PREDICT)
-                return await asyncio.gather(*[stub(b) for b in bodies])
-        outs = asyncio.run(go())
-        for x, raw in zip(xs, outs):
-            ref = serving.PredictResponse.FromString(srv.core.predict(native.encode_predict_request(spec, {"input": x})))
-            got = np.array(serving.PredictResponse.FromString(raw).outputs["probabilities"].float_val)
-            np.testing.assert_allclose(got, np.array(ref.outputs["probabilities"].float_val), atol=2e-4)
-        r = _C.run_loadgen("127.0.0.1", srv.port, PREDICT, bodies[:8], 600, 32, 4, 2, 120.0)
-        assert r["ok"] == 600 and r["errors"] == 0, r["first_error"]
-        stats = srv.transports[0].srv.native_lane_stats()
-        assert stats and sum(s[1] for s in stats) > 0 and sum(s[2] for s in stats) == 0
-    finally:
-        srv.stop()
