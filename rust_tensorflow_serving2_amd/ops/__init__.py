@@ -52,7 +52,7 @@ ACT = {"none": 0, "relu": 1, "gelu_tanh": 2, "gelu_erf": 3, "tanh": 4}
 
 # ------------------------------------------------------------------ autotune
 _TUNED: Dict[Tuple, int] = {}
-_TUNE_LOCK = threading.Lock()
+_TUNE_LOCK = threading.RLock()   # re-entrant: an op choosing between implementations tunes its parts inside
 AUTOTUNE = os.environ.get("TFSERVE_AUTOTUNE", "1") != "0"
 # per key: [(median cold launch ms, (config, splits))] ascending, from tuned_config
 _TUNE_TIMES: Dict[Tuple, List[Tuple[float, Tuple[int, int]]]] = {}
@@ -231,10 +231,14 @@ def _ensure_cache() -> None:
 
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
                  dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-                 halo: bool = False, no_split: bool = False, n_multiple: bool = False) -> Tuple[int, int]:
+                 halo: bool = False, no_split: bool = False, n_multiple: bool = False,
+                 explicit: Optional[List[Tuple[int, int]]] = None,
+                 default: Optional[Tuple[int, int]] = None) -> Tuple[int, int]:
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
-    heuristic is used)."""
+    heuristic is used).  ``explicit``: time exactly these candidates (an op
+    choosing between whole implementations, e.g. graph/fused.py TailConv);
+    ``default``: the pick without autotuning."""
     rec = getattr(_REC, "keys", None)
     if rec is not None:
         rec[key] = rec.get(key, 0) + 1
@@ -249,6 +253,8 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
             _GRAPH_TUNED.add(key)          # the leader already graph-tuned it
         return remote
     if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
+        if default is not None:
+            return default
         c = (36 if no_split else 42) if cgemm_only else heuristic_config(M, N)
         return c, 1 if no_split else heuristic_splits(M, N, K, c)
     with _TUNE_LOCK:
@@ -258,7 +264,9 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
         best, best_t = None, float("inf")
         times = []
         flush = _flush_buffer()
-        for c, s in candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, n_multiple):
+        cands = explicit if explicit is not None else \
+            candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, n_multiple)
+        for c, s in cands:
             launch(c, s)   # warm (also sets the kernel's LDS attribute)
             samples = []
             for _rep in range(5):

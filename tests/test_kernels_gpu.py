@@ -139,6 +139,64 @@ def test_halo_conv_matches_fp32(shape, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
 
 
+TAIL_SHAPES = [
+    # N, H, W, C, N3          (3x3 SAME -> expand 1x1 + shortcut; ResNet-50 stages + an odd image)
+    (2, 56, 56, 64, 256),
+    (2, 28, 28, 128, 512),
+    (3, 14, 14, 256, 1024),
+    (1, 13, 17, 128, 256),
+    (2, 7, 9, 256, 384),
+]
+
+
+@pytest.mark.parametrize("shape", TAIL_SHAPES)
+@pytest.mark.parametrize("cfg", [0, 1])
+def test_bottleneck_tail_matches_fp32(shape, cfg):
+    """The fused bottleneck tail (kernels/tail.hip) vs fp32 torch: 3x3 SAME +
+    bias + ReLU, rounded to bf16 (the tile the kernel keeps in LDS), expand
+    1x1 + bias + shortcut + ReLU; with and without the shortcut / activations."""
+    n, h, w, c, n3 = shape
+    x = rnd(n, h, w, c, seed=21).to(BF)
+    w2 = rnd(3, 3, c, c, scale=1 / math.sqrt(9 * c), seed=22).to(BF).float()
+    b2 = rnd(c, scale=0.1, seed=23)
+    w3 = rnd(n3, c, scale=1 / math.sqrt(c), seed=24).to(BF)
+    b3 = rnd(n3, scale=0.1, seed=25)
+    res = rnd(n, h, w, n3, seed=26).to(BF)
+    for with_res, act in ((True, "relu"), (False, "none")):
+        y2 = ref_conv(x, w2, b2, 1, (1, 1, 1, 1), None, act).to(BF).float()
+        ref = y2.reshape(-1, c) @ w3.float().t() + b3
+        if with_res:
+            ref = ref + res.float().reshape(-1, n3)
+        if act == "relu":
+            ref = torch.relu(ref)
+        ref = ref.reshape(n, h, w, n3)
+        y = hip().bottleneck_tail(x.to(DEV), pack_w(w2), b2.to(DEV), w3.to(DEV), b3.to(DEV),
+                                  res.to(DEV) if with_res else None, ACT[act], ACT[act], cfg)
+        torch.cuda.synchronize()
+        assert y.shape == (n, h, w, n3)
+        err = (y.float().cpu() - ref).abs().max().item()
+        assert err < 3e-2 * max(1.0, ref.abs().max().item()), (with_res, act, err)
+
+
+def test_bottleneck_tail_exact_integers():
+    """Small integer operands (every intermediate and output exact in bf16 and
+    fp32): every pixel of every block position and every expand column must
+    match bit for bit -- catches a mis-shifted halo row, a wrong channel
+    permutation between the two GEMMs or a swizzle slip that tolerances hide."""
+    n, h, w, c, n3 = 2, 14, 14, 256, 512
+    g = torch.Generator().manual_seed(9)
+    x = torch.randint(-1, 2, (n, h, w, c), generator=g).float()
+    w2 = torch.randint(-1, 2, (3, 3, c, c), generator=g).float() * (torch.rand(3, 3, c, c, generator=g) < 0.01)
+    w3 = torch.randint(-1, 2, (n3, c), generator=g).float() * (torch.rand(n3, c, generator=g) < 0.05)
+    y2 = ref_conv(x, w2, torch.zeros(c), 1, (1, 1, 1, 1))
+    ref = (y2.reshape(-1, c) @ w3.t()).reshape(n, h, w, n3)
+    assert y2.abs().max() <= 256 and ref.abs().max() <= 256       # exact in bf16
+    for cfg in (0, 1):
+        y = hip().bottleneck_tail(x.to(BF).to(DEV), pack_w(w2), torch.zeros(c, device=DEV), w3.to(BF).to(DEV),
+                                  torch.zeros(n3, device=DEV), None, 0, 0, cfg)
+        assert torch.equal(y.float().cpu(), ref), cfg
+
+
 def test_halo_exact_identity_taps():
     """Integer-valued operands (exact in bf16 and fp32): every output pixel of
     every tile position, tap and channel chunk must match bit for bit — catches
