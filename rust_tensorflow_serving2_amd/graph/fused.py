@@ -214,8 +214,10 @@ class FusedConv:
         halo = aligned and not self.c4 and kh == 3 and kw == 3 and self.sh == 1 and self.sw == 1
         kw_post, outs = _post_kwargs(self, out)
         run = lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s, **kw_post)  # noqa
+        dense = (not self.c4 and kh == 1 and kw == 1 and self.sh == 1 and self.sw == 1 and
+                 not any((pt, pb, pl, pr)) and self.post is None)
         cfg, splits = tuned_config(key, M, self.cout, run, K, dma, aligned, halo=halo,
-                                   cgemm_only=self.post is not None)
+                                   cgemm_only=self.post is not None, dense=dense)
         run(cfg, splits)
         return outs
 
@@ -326,7 +328,8 @@ class FusedMatMul:
         key = ("mm", M, n, self.k, res is not None, self.out_f32, self.act) + \
             ((x.stride(0),) if not x.is_contiguous() else ())
         run = lambda c, s: H.linear(x, w, b, res, ACT[self.act], c, self.out_f32, 1.0, out, s)  # noqa
-        cfg, splits = tuned_config(key, M, n, run, self.k, True, self.k % 64 == 0)
+        cfg, splits = tuned_config(key, M, n, run, self.k, True, self.k % 64 == 0,
+                                   dense=True)
         y = run(cfg, splits)
         return [y[:, :self.n] if padded else y]
 

@@ -36,8 +36,13 @@ bool is_halo_cfg(int64_t cfg) {
   return cfg >= 0 && cfg < (1 << 20) && tfsk::halo_cfg_id(int(cfg));
 }
 
+bool is_ws_cfg(int64_t cfg) {
+  return cfg >= 0 && cfg < (1 << 20) && tfsk::ws_cfg_id(int(cfg));
+}
+
 hipError_t launch_any(const tfsk::IGemmArgs& a, int a_mode, int64_t cfg, hipStream_t st) {
   if (is_halo_cfg(cfg)) return tfsk::halo_launch(a, int(cfg), st);
+  if (is_ws_cfg(cfg)) return tfsk::ws_launch(a, int(cfg), st);
   return is_cgemm_cfg(cfg) ? tfsk::cgemm_launch(a, a_mode, int(cfg), st) : tfsk::igemm_launch(a, a_mode, int(cfg), st);
 }
 
@@ -51,8 +56,17 @@ bool split_fixup_enabled() {
 }
 
 void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, const Tensor& like, hipStream_t st) {
-  TORCH_CHECK((cfg >= 0 && cfg < tfsk::kNumIGemmConfigs) || is_cgemm_cfg(cfg) || is_halo_cfg(cfg),
-              "bad tile config ", cfg);
+  TORCH_CHECK((cfg >= 0 && cfg < tfsk::kNumIGemmConfigs) || is_cgemm_cfg(cfg) || is_halo_cfg(cfg) ||
+              is_ws_cfg(cfg), "bad tile config ", cfg);
+  if (is_ws_cfg(cfg)) {
+    a.splits = 1;
+    a.kt_per_split = (a.K + 63) / 64;
+    a.ws = nullptr;
+    TORCH_CHECK(a_mode == tfsk::kADense && tfsk::ws_supported(a, int(cfg)),
+                "weight-stationary config ", cfg, " needs a dense GEMM whose weight slice fits in LDS");
+    TORCH_CHECK(launch_any(a, a_mode, cfg, st) == hipSuccess, "conv/GEMM launch failed");
+    return;
+  }
   TORCH_CHECK(!is_cgemm_cfg(cfg) || tfsk::cgemm_supported(a, a_mode),
               "tile config ", cfg, " needs 64-aligned operands (K % 64, C % 64)");
   TORCH_CHECK(!is_halo_cfg(cfg) || (a_mode == tfsk::kAIm2col && tfsk::halo_supported(a)),
@@ -768,6 +782,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("config_tile", [](int cfg) {
     if (is_halo_cfg(cfg)) return std::make_pair(tfsk::halo_config_bm(cfg), tfsk::halo_config_bn(cfg));
     if (is_cgemm_cfg(cfg)) return std::make_pair(tfsk::cgemm_config_bm(cfg), tfsk::cgemm_config_bn(cfg));
+    if (is_ws_cfg(cfg)) return std::make_pair(tfsk::ws_config_bm(cfg), tfsk::ws_config_bn(cfg));
     return std::make_pair(tfsk::igemm_config_bm(cfg), tfsk::igemm_config_bn(cfg));
   });
 }

@@ -421,11 +421,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_rb_kernel(IGemmArgs p) {
   auto issue_halo = [&](int c) {
     char* dst = smem + ((c - c0) & 1) * G::HALO_B;
     const uint32_t soff = uint32_t(c) * (KT * 2);
+    dma_fence();                        // the weight loads keep their place around the DMAs (gemm_common.h)
 #pragma unroll
     for (int j = 0; j < G::HPW; ++j) {
       const uint32_t v = h_off[j];
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(dst + (wid * G::HPW + j) * 1024), 16, v, soff, 0, 0);
     }
+    dma_fence();
   };
   typedef bf16x8 BFrag[G::TN][2];
   auto load_b = [&](int c, int u, BFrag& dst) {
@@ -435,7 +437,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_rb_kernel(IGemmArgs p) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const uint32_t v = b_off[j] + uint32_t(kk * 16);
-        dst[j][kk] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, v, soff, 0));
+        dst[j][kk] = __builtin_bit_cast(bf16x8, ordered_load16(rsB, v, soff));
       }
   };
 
@@ -492,6 +494,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_rb_kernel(IGemmArgs p) {
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
       if (u == 0) {
+        dma_fence();
         wait_vmcnt<WAIT_HALO>();
         lds_barrier();
         if (!LAST) issue_halo(c + 1);

@@ -105,11 +105,13 @@ __global__ __launch_bounds__(kTailNT) void tail_kernel(TailArgs p) {
   auto issue_halo = [&](int c) {
     char* dst = smem + (c & 1) * G::HALO_B;
     const uint32_t soff = uint32_t(c) * (KT * 2);
+    dma_fence();                        // the weight loads keep their place around the DMAs (gemm_common.h)
 #pragma unroll
     for (int j = 0; j < G::HPW; ++j) {
       const uint32_t v = h_off[j];
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsX, (lds_ptr_t)(dst + (wn * G::HPW + j) * 1024), 16, v, soff, 0, 0);
     }
+    dma_fence();
   };
 
   // ---- 3x3 weights: this lane's columns wn * WN1 + j * 16 + fr, channels fq * 16 .. +15 of a chunk
@@ -124,8 +126,7 @@ __global__ __launch_bounds__(kTailNT) void tail_kernel(TailArgs p) {
     for (int j = 0; j < G::TN1; ++j)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
-        dst[j][kk] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsW2, b2_off[j] + kk * 16u,
-                                                                                      soff, 0));
+        dst[j][kk] = __builtin_bit_cast(bf16x8, ordered_load16(rsW2, b2_off[j] + kk * 16u, soff));
   };
 
   // A rows: output pixel i * 16 + fr of the block -> halo row of tap (0, 0)
@@ -174,6 +175,7 @@ __global__ __launch_bounds__(kTailNT) void tail_kernel(TailArgs p) {
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
       if (u == 0) {
+        dma_fence();
         wait_vmcnt<WAIT_HALO>();
         lds_barrier();
         if (!LAST) issue_halo(c + 1);
@@ -243,8 +245,7 @@ __global__ __launch_bounds__(kTailNT) void tail_kernel(TailArgs p) {
 #pragma unroll
       for (int kk = 0; kk < KK2; ++kk)   // kk = 2 * k-tile + half: channels 64 * (kk / 2) + fq * 16 + 8 * (kk % 2)
         dst[j][kk] = __builtin_bit_cast(
-            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsW3, b3_off[j] + uint32_t((kk >> 1) * 128 + (kk & 1) * 16),
-                                                          soff, 0));
+            bf16x8, ordered_load16(rsW3, b3_off[j] + uint32_t((kk >> 1) * 128 + (kk & 1) * 16), soff));
   };
   // this lane's epilogue item: slab row rl2, 8-column chunk cc2 of the wave's 32
   const int rl2 = lane >> 2, cc2 = lane & 3;

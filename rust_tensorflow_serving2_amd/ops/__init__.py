@@ -159,6 +159,9 @@ HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 12
         80: (128, 64), 81: (64, 64), 82: (128, 128), 83: (64, 128), 84: (256, 64), 85: (128, 128), 86: (64, 64),
         87: (128, 64), 88: (256, 64)}
 TILES.update(HALO)
+# weight-stationary GEMM (kernels/wsgemm.hip; dense A only): config id -> (rows per wave round, BN)
+WS = {96: (128, 64), 97: (128, 128), 98: (256, 64), 99: (64, 128), 100: (64, 256), 101: (256, 32), 102: (128, 96)}
+TILES.update(WS)
 
 
 def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
@@ -172,7 +175,7 @@ def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
 
 
 def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-               halo: bool = False, no_split: bool = False, n_multiple: bool = False):
+               halo: bool = False, no_split: bool = False, n_multiple: bool = False, dense: bool = False):
     """(tile config, split-K) pairs worth timing for an M x N x K problem
     (``dma``: the operand mode uses the direct-to-LDS path, so the deeper
     DMA-ring configs apply; ``aligned64``: K and the conv channels are
@@ -191,8 +194,13 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
                 if s > 1 and (nch // s < 1 or tiles >= 512 or tiles * s > 2048):
                     continue
                 out.append((cfg, s))
+    if dense and aligned64 and K % 64 == 0 and N % 8 == 0:
+        # weight-stationary: the BN x K weight slice + 4 epilogue slabs fit in LDS
+        for cfg, (_bm, bn) in WS.items():
+            if bn * K * 2 + 4 * 16 * (bn + 4) * 4 <= 160 * 1024 and not (bn > 64 and N <= bn // 2):
+                out.append((cfg, 1))
     for cfg, (bm, bn) in TILES.items():
-        if cfg in HALO:
+        if cfg in HALO or cfg in WS:
             continue
         if cfg in DMA_ONLY and (not dma or (cfg in (4, 5, 6, 7) and nk < 3)):
             continue
@@ -232,7 +240,7 @@ def _ensure_cache() -> None:
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
                  dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
                  halo: bool = False, no_split: bool = False, n_multiple: bool = False,
-                 explicit: Optional[List[Tuple[int, int]]] = None,
+                 explicit: Optional[List[Tuple[int, int]]] = None, dense: bool = False,
                  default: Optional[Tuple[int, int]] = None) -> Tuple[int, int]:
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
@@ -265,7 +273,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
         times = []
         flush = _flush_buffer()
         cands = explicit if explicit is not None else \
-            candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, n_multiple)
+            candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, n_multiple, dense)
         for c, s in cands:
             launch(c, s)   # warm (also sets the kernel's LDS attribute)
             samples = []

@@ -21,6 +21,7 @@ LAYERS = {
     "s1_3x3": (56, 64, 64, 3, 1, False), "s2_3x3s2": (56, 128, 128, 3, 2, False), "s2_3x3": (28, 128, 128, 3, 1, False),
     "s3_3x3s2": (28, 256, 256, 3, 2, False), "s3_3x3": (14, 256, 256, 3, 1, False),
     "s4_3x3s2": (14, 512, 512, 3, 2, False), "s4_3x3": (7, 512, 512, 3, 1, False),
+    "s1_1x1_in": (56, 256, 64, 1, 1, False), "s1_1x1_out": (56, 64, 256, 1, 1, True),
     "s2_1x1_in": (28, 512, 128, 1, 1, False), "s2_1x1_out": (28, 128, 512, 1, 1, True),
     "s3_1x1_in": (14, 1024, 256, 1, 1, False), "s3_1x1_out": (14, 256, 1024, 1, 1, True),
     "s4_1x1_in": (7, 2048, 512, 1, 1, False), "s4_1x1_out": (7, 512, 2048, 1, 1, True),
@@ -71,7 +72,7 @@ def main():
         b = torch.zeros(cout, device="cuda")
         halo = k == 3 and s == 1 and cin % 64 == 0
         res = []
-        for cfg, sp in candidates(M, N, K, True, cin % 64 == 0, halo=halo):
+        for cfg, sp in candidates(M, N, K, True, cin % 64 == 0, halo=halo, dense=(k == 1 and s == 1)):
             def fn(i, cfg=cfg, sp=sp):
                 j = i % 8
                 hip().conv2d(xs[j], ws[j], b, rs[j], k, k, s, s, pad, pad, pad, pad, ACT["relu"], cfg, outs[j],

@@ -235,6 +235,45 @@ def test_cgemm_linear_matches_fp32(m, n, k, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (act, err)
 
 
+WS_CFGS = list(range(96, 103))
+WS_SHAPES = [
+    # M, N, K       (ResNet-50 1x1 convs at small batch, BERT-base projections, tails)
+    (2 * 56 * 56, 64, 256), (2 * 28 * 28, 512, 128), (3 * 14 * 14, 256, 1024), (2 * 7 * 7, 2048, 512),
+    (256, 768, 768), (77, 136, 64), (1000, 96, 2048),
+]
+
+
+@pytest.mark.parametrize("shape", WS_SHAPES)
+@pytest.mark.parametrize("cfg", WS_CFGS)
+def test_weight_stationary_gemm_matches_fp32(shape, cfg):
+    """Weight-stationary GEMM (kernels/wsgemm.hip: the weight slice resident in
+    LDS, A rows straight into registers, persistent over M) vs fp32, with bias
+    + residual + each activation; configs whose slice does not fit refuse."""
+    m, n, k = shape
+    x = rnd(m, k, seed=17).to(BF)
+    w = rnd(n, k, scale=1 / math.sqrt(k), seed=18).to(BF)
+    b = rnd(n, scale=0.1, seed=19)
+    res = rnd(m, n, seed=20).to(BF)
+    ref = x.float() @ w.float().t() + b + res.float()
+    bn = hip().config_tile(cfg)[1]
+    if bn * k * 2 + 4 * 16 * (bn + 4) * 4 > 160 * 1024:
+        with pytest.raises(RuntimeError, match="weight-stationary"):
+            hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), res.to(DEV), 0, cfg, False)
+        return
+    for act, fn, out_f32 in (("none", lambda t: t, False), ("relu", torch.relu, True),
+                             ("gelu_tanh", lambda t: F.gelu(t, approximate="tanh"), False)):
+        y = hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), res.to(DEV), ACT[act], cfg, out_f32)
+        err = (y.float().cpu() - fn(ref)).abs().max().item()
+        assert err < 3e-2 * max(1.0, ref.abs().max().item()), (act, err)
+    # the 1x1 conv path (NHWC rows, no residual)
+    if m % 4 == 0:
+        xx = x.reshape(1, 4, m // 4, k)
+        wt = w.float().t().reshape(1, 1, k, n)
+        y = hip().conv2d(xx.to(DEV), pack_w(wt), b.to(DEV), None, 1, 1, 1, 1, 0, 0, 0, 0, act=ACT["relu"], cfg=cfg)
+        refc = torch.relu(x.float() @ w.float().t() + b).reshape(1, 4, m // 4, n)
+        assert (y.float().cpu() - refc).abs().max().item() < 3e-2 * max(1.0, refc.abs().max().item())
+
+
 @pytest.mark.parametrize("cfg", CGEMM_CFGS)
 def test_cgemm_asymmetric_identity(cfg):
     """A = I, asymmetric B (exact in bf16 / fp32): catches a transposed or
