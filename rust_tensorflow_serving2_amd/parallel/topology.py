@@ -515,7 +515,52 @@ def top_threads(before: Dict[int, Tuple[str, float]], after: Dict[int, Tuple[str
         if d > 0:
             rows.append([name, tid, round(d / max(elapsed, 1e-9), 2), tid == os.getpid()])
     rows.sort(key=lambda r: -r[2])
-    return rows[:n]
+    rows = rows[:n]
+    who = python_thread_sites()
+    for r in rows:
+        # a busy thread the kernel only knows by the process name: say which
+        # Python thread (and where it is) or which kernel wait it sits in
+        if r[1] in who:
+            r.append(who[r[1]])
+        else:
+            r.append(_kernel_state(r[1]))
+    return rows
+
+
+def python_thread_sites() -> Dict[int, str]:
+    """{native thread id: "name @ file:line in function"} of this process's
+    Python threads (innermost frame)."""
+    import sys
+    import threading
+    frames = sys._current_frames()
+    out: Dict[int, str] = {}
+    for t in threading.enumerate():
+        nid = getattr(t, "native_id", None)
+        f = frames.get(t.ident)
+        if nid is None:
+            continue
+        where = ""
+        if f is not None:
+            where = f" @ {os.path.basename(f.f_code.co_filename)}:{f.f_lineno} in {f.f_code.co_name}"
+        out[nid] = f"py:{t.name}{where}"
+    return out
+
+
+def _kernel_state(tid: int) -> str:
+    """A native (non-Python) thread's scheduler state and wait channel."""
+    base = f"/proc/{os.getpid()}/task/{tid}"
+    state = wchan = ""
+    try:
+        with open(f"{base}/stat") as f:
+            state = f.read().rsplit(")", 1)[1].split()[0]
+    except (OSError, IndexError):
+        pass
+    try:
+        with open(f"{base}/wchan") as f:
+            wchan = f.read().strip()
+    except OSError:
+        pass
+    return f"native:{state}:{wchan or '-'}"
 
 
 def thread_cpu(pid: Optional[int] = None) -> Dict[str, float]:
