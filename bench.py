@@ -589,6 +589,9 @@ def rccl_problems(reports, world: int) -> list:
             bad.append(f"{who}: {r['disk_loads']} model load(s) from disk")
         if r["weight_h2d_bytes"] > 0:
             bad.append(f"{who}: copied {r['weight_h2d_bytes']} weight bytes host->device")
+        if r.get("recompiles", 0) > 0:
+            bad.append(f"{who}: compiled {r['recompiles']} program(s) from disk "
+                       f"({'; '.join(r.get('recompile_reasons', []))})")
         if r["bcast_loads"] < 1 or r["bound_bytes"] <= 0:
             bad.append(f"{who}: received {r['bcast_loads']} load(s) / {r['bound_bytes']} weight bytes")
     return bad

@@ -77,7 +77,7 @@ def weight_refs(program) -> List[Tuple[Ref, torch.Tensor]]:
             return
         seen.add(id(impl))
         for k, i, t in _tensor_attrs(impl):
-            if t.device.type == dev.type and t.numel() > 0:
+            if (t.device.type == dev.type or t.is_meta) and t.numel() > 0:
                 out.append(((impl, k, i), t))
         for child in getattr(impl, "children", ()):   # fused ops built from other fused ops
             visit(getattr(impl, child))
@@ -85,7 +85,8 @@ def weight_refs(program) -> List[Tuple[Ref, torch.Tensor]]:
     for fn, node, _ins, _outs in program.steps:
         visit(node.attrs.get("_impl"))
     for pos, (slot, v) in enumerate(program.const_slots):
-        if isinstance(v, torch.Tensor) and v.device.type == dev.type and v.numel() > 0 and \
+        # a follower's host program keeps shape-only (meta) weights until bound
+        if isinstance(v, torch.Tensor) and (v.device.type == dev.type or v.is_meta) and v.numel() > 0 and \
                 (v.is_floating_point() or v.is_meta or dev.type != "cpu"):
             out.append(((program, "const_slots", pos), v))
     return out

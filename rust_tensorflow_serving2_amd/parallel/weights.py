@@ -484,16 +484,17 @@ class ReplicatedWeightSource:
                     fut = self._pending[k] = Future()
         if parked is not None:
             if isinstance(parked[1], _CommError):
-                return fallback()
+                return fallback(f"the collective failed: {parked[1]}")
             if isinstance(parked[1], Exception):
                 raise parked[1]
             return parked[1]
-        deadline = time.time() + (self.load_timeout if timeout is None else timeout)
+        start = time.time()
+        deadline = start + (self.load_timeout if timeout is None else timeout)
         while True:
             try:
                 return fut.result(timeout=0.5)
-            except _CommError:
-                return fallback()
+            except _CommError as e:
+                return fallback(f"the collective failed: {e}")
             except FutureTimeout:
                 leader_down = self.group_broken()
                 m = self._marker(*disk_marker) if disk_marker else None
@@ -502,7 +503,8 @@ class ReplicatedWeightSource:
                     with self._lock:
                         self._pending.pop(k, None)
                     if leader_down or skipped or fallback_on_timeout:
-                        return fallback()
+                        return fallback("leader down" if leader_down else "leader loaded from disk" if skipped
+                                        else f"no broadcast within {deadline - start:.0f} s")
                     raise LoadError(f"timed out waiting for the leader rank to broadcast {what}")
 
     def _disk_load(self, key, path):
@@ -545,7 +547,7 @@ class ReplicatedWeightSource:
             # the leader broadcast it before this process existed, or not at all
             return self._disk_load(key, path)
         b = self._await(("load", name, int(version)), f"{name} version {version}",
-                        lambda: self._disk_load(key, path), disk_marker=(name, int(version)))
+                        lambda why="": self._disk_load(key, path), disk_marker=(name, int(version)))
         if key not in self._disk:
             self.stats["bcast_loads"] = self.stats.get("bcast_loads", 0) + 1
         return b
@@ -578,9 +580,10 @@ class ReplicatedWeightSource:
                     self._comm_failed(comm, e)
             return
 
-        def rebuild():
+        def rebuild(why="the collective failed"):
             if recompile is None:
                 raise LoadError("the leader did not broadcast this program's weights")
+            self._note_recompile(key, why)
             return ("recompiled", recompile())
         # a runner the leader does not build (one only this replica's traffic
         # asked for) is compiled from disk: wait for the leader to announce it
@@ -591,7 +594,8 @@ class ReplicatedWeightSource:
             if time.time() > deadline or self.group_broken():
                 with self._lock:
                     self._pending.pop(k, None)
-                res = rebuild()
+                res = rebuild("leader down" if self.group_broken() else
+                              f"not announced within {self.announce_wait_s:g} s")
                 program.__dict__.update(res[1].__dict__)
                 return
             time.sleep(0.02)
@@ -608,9 +612,18 @@ class ReplicatedWeightSource:
                         key, e)
             if recompile is None:
                 raise
+            self._note_recompile(key, f"manifest mismatch: {e}")
             program.__dict__.update(recompile().__dict__)
             return
         self.stats["bound_bytes"] = self.stats.get("bound_bytes", 0) + n
+
+    def _note_recompile(self, key: str, why: str) -> None:
+        """A follower compiled a program from disk instead of binding the
+        leader's broadcast (its weights then went host -> device)."""
+        log.warning("follower compiles runner %s from disk: %s", key, why)
+        with self._lock:
+            self.stats["recompiles"] = self.stats.get("recompiles", 0) + 1
+            self.stats.setdefault("recompile_reasons", []).append(f"{key}: {why}")
 
     def _announce_key(self, name: str, version: int, key: str) -> str:
         return f"{self.prefix}/progs/{name}/{int(version)}/{key}"
@@ -649,6 +662,8 @@ class ReplicatedWeightSource:
                 "programs": int(st.get("programs", 0)), "bound_bytes": int(st.get("bound_bytes", 0)),
                 "bcast_loads": int(st.get("bcast_loads", 0)), "disk_loads": int(st.get("disk_loads", 0)),
                 "comm_failures": int(st.get("comm_failures", 0)),
+                "recompiles": int(st.get("recompiles", 0)),
+                "recompile_reasons": list(st.get("recompile_reasons", []))[:4],
                 "weight_h2d_bytes": int(placement.H2D_BYTES)}
 
     def close(self):

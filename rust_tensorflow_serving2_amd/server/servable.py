@@ -154,6 +154,7 @@ class Servable:
         self.bundle = bundle or sm.load(path, verify=options.verify_checksums)
         self.signatures = self.bundle.signatures
         self._runners: Dict[tuple, Runner] = {}
+        self._by_tensors: Dict[str, Runner] = {}
         self._lock = threading.Lock()
         self.in_flight = 0
         self._cv = threading.Condition()
@@ -195,11 +196,19 @@ class Servable:
             if r is None:
                 _k, sig = self.signature(sig_name)
                 ins, outs = _specs(sig.inputs), _specs(sig.outputs)
-                try:
-                    r = self._make_runner([ins[a] for a in in_aliases], [outs[a] for a in out_aliases])
-                except CompileError as e:
-                    raise E.ServingError(E.INVALID_ARGUMENT if "not found" in str(e) else E.UNIMPLEMENTED,
-                                         str(e)) from None
+                in_specs, out_specs = [ins[a] for a in in_aliases], [outs[a] for a in out_aliases]
+                # alias sets that name the same tensors (warm-up's sorted outputs,
+                # a request's filter) share ONE runner: one compile, one set of
+                # captured graphs, one weight broadcast between replicas
+                tkey = runner_key(in_specs, out_specs)
+                r = self._by_tensors.get(tkey)
+                if r is None:
+                    try:
+                        r = self._make_runner(in_specs, out_specs)
+                    except CompileError as e:
+                        raise E.ServingError(E.INVALID_ARGUMENT if "not found" in str(e) else E.UNIMPLEMENTED,
+                                             str(e)) from None
+                    self._by_tensors[tkey] = r
                 self._runners[key] = r
         return r
 
@@ -281,6 +290,7 @@ class Servable:
 
     def unload(self):
         self._runners.clear()
+        self._by_tensors.clear()
         self.bundle = None
         if self.options.is_gpu:
             from .gpu_runtime import CAPTURE_LOCK

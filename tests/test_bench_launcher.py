@@ -55,6 +55,9 @@ def test_bench_gpus2_self_launch_cpu(tmp_path):
     assert lead["broadcast_bytes"] > 0 and lead["programs"] >= 1
     assert not fol["leader"] and fol["disk_loads"] == 0 and fol["weight_h2d_bytes"] == 0
     assert fol["bcast_loads"] >= 1 and fol["bound_bytes"] > 0
+    assert fol["recompiles"] == 0, fol["recompile_reasons"]
+    # every runner the follower built was bound to a broadcast blob
+    assert fol["bound_bytes"] * lead["programs"] >= lead["broadcast_bytes"] * fol["programs"] * 0.9
     assert fol["broadcast_bytes"] == lead["broadcast_bytes"] and fol["broadcast_s"] >= 0
     pr = out["per_rank"]
     assert [x["rank"] for x in pr] == [0, 1] and all(x["ok"] > 0 and x["elapsed_s"] > 0 for x in pr)
