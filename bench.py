@@ -129,6 +129,12 @@ def parse():
                          "(the reference client's channel pattern, src/lib.rs:132-138) with min(concurrency, 128) "
                          "x N calls in flight while every rank serves; reported as ref_client_rps + the share each "
                          "GPU served (per-stream routing; 0 = skip)")
+    ap.add_argument("--ref-client-bodies", type=int, default=2,
+                    help="distinct request bodies the reference-client phase replays.  The reference encodes "
+                         "every request right before writing it (src/lib.rs:229-257: pixels -> float_val -> "
+                         "prost -> tonic), so the bytes it sends are cache-hot; 2 bodies (1.2 MB) stay in the "
+                         "LLC like that, 64 cold 602-KB bodies (38.5 MB) would add a DRAM read per call that the "
+                         "reference's client does not make")
     ap.add_argument("--cpu-report", action="store_true",
                     help="(always on now; kept for old command lines) per-thread-group CPU of the windows")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -449,7 +455,8 @@ def main():
             # connection task runs on one runtime thread at a time)
             # enough calls in flight to feed every GPU's batch pipeline (the
             # router keeps them on rank 0 until its own pipeline is full)
-            lg2 = _C.LoadGen("127.0.0.1", server.port, PREDICT, bodies, min(conc, 128) * world, 2, 2)
+            ref_bodies = bodies[:max(1, args.ref_client_bodies)]
+            lg2 = _C.LoadGen("127.0.0.1", server.port, PREDICT, ref_bodies, min(conc, 128) * world, 2, 2)
             lg2.run(max(64, args.ref_client_requests // 10), 120.0)
             s0 = served()
             rc0, rio0, rru0, rt0 = topology.thread_cpu(), io_stats(), os.times(), time.perf_counter()
@@ -460,6 +467,11 @@ def main():
             dist.barrier()
         my_ref_diag = diag(rc0, topology.thread_cpu(), rio0, io_stats(), rru0, os.times(),
                            time.perf_counter() - rt0)
+        if ref is not None:
+            # the two client threads live only inside lg2.run (not in the
+            # per-thread snapshots): the process total minus the named groups
+            named = sum(v for k, v in my_ref_diag.items() if k.startswith(("tfs-", "python")))
+            my_ref_diag["client_threads_cores"] = round(my_ref_diag["process_total"] - named, 2)
         share = torch.tensor([float(served() - s0)], dtype=torch.float64, device=coll_dev)
         if world > 1:
             parts = [torch.zeros_like(share) for _ in range(world)]
@@ -471,6 +483,7 @@ def main():
             tot = max(1.0, sum(share_v))
             ref = {"ref_client_rps": round(ref["ok"] / max(ref["elapsed_s"], 1e-9), 1),
                    "ref_client_errors": ref["errors"], "ref_client_in_flight": min(conc, 128) * world,
+                   "ref_client_bodies": max(1, args.ref_client_bodies),
                    "ref_client_gpu_share": [round(v / tot, 3) for v in share_v]}
 
     # latency mode: one client, one connection, one call in flight (the

@@ -57,35 +57,37 @@ def main():
         raise SystemExit(f"need two dispatches of {a.replay!r}, found {len(idx)}")
     rep = rows[idx[-2]:idx[-1]]
     sq = {"GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"}
-    extra = sorted({n for _k, d in rep for n in d} - sq)
-    if extra:
-        # memory counters: per dispatch, MB (FETCH_SIZE / WRITE_SIZE are KB in rocprofv3) and totals
-        print(f"{'#':>3} {'kernel':60s} {'kcycles':>9} " + " ".join(f"{n:>14}" for n in extra))
-        tot = defaultdict(float)
-        cyc_t = 0.0
-        for i, (k, d) in enumerate(rep):
-            cyc = d.get("GRBM_GUI_ACTIVE", 0.0) / 8
-            cyc_t += cyc
-            for n in extra:
-                tot[n] += d.get(n, 0.0)
-            print(f"{i:3d} {_short(k):60s} {cyc / 1e3:9.1f} " + " ".join(f"{d.get(n, 0.0):14.1f}" for n in extra))
-        print(f"replay: {len(rep)} dispatches, {cyc_t / 1e3:.1f} kcycles; totals: " +
-              ", ".join(f"{n}={tot[n]:.1f}" for n in extra))
-        return
+    have = {n for _k, d in rep for n in d}
+    # memory / instruction counters: per dispatch (FETCH_SIZE / WRITE_SIZE are KB in rocprofv3) and totals
+    extra = sorted(have - sq)
+    util_cols = "SQ_VALU_MFMA_BUSY_CYCLES" in have
+    head = f"{'#':>3} {'kernel':60s} {'kcycles':>9}"
+    if util_cols:
+        head += f" {'mfma%':>6} {'wait%':>6} {'active%':>7}"
+    print(head + "".join(f" {n:>14}" for n in extra))
+    tot = defaultdict(float)
     tot_busy = tot_cyc = 0.0
-    print(f"{'#':>3} {'kernel':60s} {'kcycles':>9} {'mfma%':>6} {'wait%':>6} {'active%':>7}")
     for i, (k, d) in enumerate(rep):
         cyc = d.get("GRBM_GUI_ACTIVE", 0.0) / 8
-        busy = d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
-        util = busy / (1024 * cyc) if cyc else 0.0
-        wc = d.get("SQ_WAVE_CYCLES", 0.0)
-        wait = d.get("SQ_WAIT_ANY", 0.0) / wc if wc else 0.0
-        act = d.get("SQ_ACTIVE_INST_ANY", 0.0) / wc if wc else 0.0
-        tot_busy += busy
         tot_cyc += cyc
-        print(f"{i:3d} {_short(k):60s} {cyc / 1e3:9.1f} {100 * util:6.1f} {100 * wait:6.1f} {100 * act:7.1f}")
-    print(f"replay: {len(rep)} dispatches, {tot_cyc / 1e3:.1f} kcycles, "
-          f"MFMA busy {100 * tot_busy / (1024 * tot_cyc) if tot_cyc else 0:.1f}% of SIMD-cycles")
+        line = f"{i:3d} {_short(k):60s} {cyc / 1e3:9.1f}"
+        if util_cols:
+            busy = d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+            tot_busy += busy
+            wc = d.get("SQ_WAVE_CYCLES", 0.0)
+            util = busy / (1024 * cyc) if cyc else 0.0
+            wait = d.get("SQ_WAIT_ANY", 0.0) / wc if wc else 0.0
+            act = d.get("SQ_ACTIVE_INST_ANY", 0.0) / wc if wc else 0.0
+            line += f" {100 * util:6.1f} {100 * wait:6.1f} {100 * act:7.1f}"
+        for n in extra:
+            tot[n] += d.get(n, 0.0)
+        print(line + "".join(f" {d.get(n, 0.0):14.1f}" for n in extra))
+    summary = f"replay: {len(rep)} dispatches, {tot_cyc / 1e3:.1f} kcycles"
+    if util_cols:
+        summary += f", MFMA busy {100 * tot_busy / (1024 * tot_cyc) if tot_cyc else 0:.1f}% of SIMD-cycles"
+    if extra:
+        summary += "; totals: " + ", ".join(f"{n}={tot[n]:.1f}" for n in extra)
+    print(summary)
 
 
 if __name__ == "__main__":
