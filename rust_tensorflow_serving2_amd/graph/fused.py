@@ -214,10 +214,8 @@ class FusedConv:
         halo = aligned and not self.c4 and kh == 3 and kw == 3 and self.sh == 1 and self.sw == 1
         kw_post, outs = _post_kwargs(self, out)
         run = lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s, **kw_post)  # noqa
-        dense = (not self.c4 and kh == 1 and kw == 1 and self.sh == 1 and self.sw == 1 and
-                 not any((pt, pb, pl, pr)) and self.post is None)
         cfg, splits = tuned_config(key, M, self.cout, run, K, dma, aligned, halo=halo,
-                                   cgemm_only=self.post is not None, dense=dense)
+                                   cgemm_only=self.post is not None)
         run(cfg, splits)
         return outs
 
@@ -328,8 +326,7 @@ class FusedMatMul:
         key = ("mm", M, n, self.k, res is not None, self.out_f32, self.act) + \
             ((x.stride(0),) if not x.is_contiguous() else ())
         run = lambda c, s: H.linear(x, w, b, res, ACT[self.act], c, self.out_f32, 1.0, out, s)  # noqa
-        cfg, splits = tuned_config(key, M, n, run, self.k, True, self.k % 64 == 0,
-                                   dense=True)
+        cfg, splits = tuned_config(key, M, n, run, self.k, True, self.k % 64 == 0)
         y = run(cfg, splits)
         return [y[:, :self.n] if padded else y]
 
@@ -604,51 +601,6 @@ class ChainConv:
 
 
 O.OPS["_ChainConv"] = _impl_op
-
-
-class TailConv:
-    """A bottleneck's 3x3 conv (SAME, stride 1, + bias, act) and the expand
-    1x1 conv that reads exactly its output (+ bias, + shortcut, act) as one
-    kernel (``hip().bottleneck_tail``, kernels/tail.hip): the 3x3's output
-    tile stays in LDS and is never written.  Per batch size the tuner times
-    the fused kernel (two pixel-block sizes) against the two separate convs
-    (config -1) and keeps the faster; the pick replicates like every tile
-    pick.  Inputs ``[x (3x3 input), shortcut]``; SURVEY.md S8 fused epilogues,
-    for the reference client's ResNet (/root/reference/src/lib.rs:229-257)."""
-
-    children = ("a", "b")
-
-    def __init__(self, a: FusedConv, b: FusedConv):
-        self.a, self.b = a, b
-        self.use_hip = a.use_hip and b.use_hip
-        self.name = b.name
-
-    def __call__(self, ctx, node, ins):
-        x = O.to_torch(ins[0])
-        res = O.to_torch(ins[1]) if len(ins) > 1 else None
-        a, b = self.a, self.b
-        if not (self.use_hip and x.is_cuda and x.dim() == 4 and x.shape[-1] == a.cin):
-            y2 = a(ctx, node, [x])[0]
-            return b(ctx, node, [y2] + ([res] if res is not None else []))
-        from ..ops import ACT, hip, tuned_config
-        H = hip()
-        xb = _to_bf16(x).contiguous()
-        rb = None if res is None else _to_bf16(res).contiguous()
-        n, h, w, _ = xb.shape
-        out = torch.empty((n, h, w, b.cout), device=xb.device, dtype=BF16)
-
-        def run(c, s):
-            if c < 0:
-                y2 = a(ctx, node, [xb])[0]
-                return b(ctx, node, [y2] + ([rb] if rb is not None else []))[0]
-            return H.bottleneck_tail(xb, a.w, a.b, b.w, b.b, rb, ACT[a.act], ACT[b.act], c, out)
-        cands = [(c, 1) for c in (0, 1) if H.tail_supported(a.cin, b.cout, c)] + [(-1, 1)]
-        key = ("tail", tuple(xb.shape), b.cout, rb is not None, a.act, b.act)
-        cfg, _s = tuned_config(key, n * h * w, b.cout, run, 9 * a.cin, explicit=cands, default=(-1, 1))
-        return [run(cfg, 1)]
-
-
-O.OPS["_TailConv"] = _impl_op
 
 _PASSTHROUGH = ("Identity", "Squeeze", "Reshape")
 
@@ -1094,55 +1046,8 @@ def fuse_conv_chain(g, order, fed, fetch_refs, device, opts):
         c.refresh()
 
 
-def _tail_3x3(impl) -> bool:
-    return (isinstance(impl, FusedConv) and impl.kh == 3 and impl.kw == 3 and impl.sh == 1 and impl.sw == 1 and
-            not impl.c4 and impl.post is None and impl.act in ("relu", "none") and impl.cin == impl.cout and
-            (impl.padding == "SAME" or (impl.padding == "EXPLICIT" and tuple(impl.pads) == (1, 1, 1, 1))))
-
-
-TAIL_CHANNELS_DEFAULT = (128, 256)           # stages 3-4; stage 2 keeps its expand -> reduce chain
-
-
-def fuse_bottleneck_tail(g, order, fed, fetch_refs, device, opts):
-    """``_FusedConv2D`` A (3x3 SAME stride 1, C -> C, act, single input) whose
-    only consumer is ``_FusedConv2D`` B (1x1 C -> N3, shortcut input, act)
-    -> ``_TailConv(A's input, B's shortcut)``.  GPU programs only; stages
-    with C in TAIL_CHANNELS_DEFAULT (``TFSERVE_TAIL=0`` disables it, ``all``
-    adds C = 64, ``force`` applies it on the CPU too: the op then runs both
-    reference convs).  Runs before fuse_conv_chain, which keeps stage 2."""
-    import os
-    mode = os.environ.get("TFSERVE_TAIL", "0")      # (off until measured on the GPU)
-    chans = (64, 128, 256) if mode == "all" else TAIL_CHANNELS_DEFAULT
-    c = _Ctx(g, order, fed, fetch_refs, device, opts)
-    if mode == "0" or (not c.use_hip and mode != "force"):
-        return
-    for name in order:
-        an = g.nodes.get(name)
-        if an is None or an.op != "_FusedConv2D" or name in c.fetch_nodes or len(an.inputs) != 1:
-            continue
-        a = an.attrs["_impl"]
-        if not _tail_3x3(a) or a.cin not in chans:
-            continue
-        cons = c.cons.get(name, [])
-        if len(cons) != 1 or cons[0][1] != 0 or cons[0][2] != 0:
-            continue
-        bnode = g.nodes[cons[0][0]]
-        if bnode.op != "_FusedConv2D" or len(bnode.inputs) != 2:
-            continue
-        b = bnode.attrs["_impl"]
-        if not _chainable_1x1(b) or b.cin != a.cout or b.cout % 128:
-            continue
-        bnode.op = "_TailConv"
-        bnode.inputs = [an.inputs[0], bnode.inputs[1]]
-        bnode.attrs = {"_impl": TailConv(a, b)}
-        bnode.ctrl = _merge_ctrl([an, bnode])
-        del g.nodes[name]
-        c.refresh()
-
-
 def default_passes(options=None):
     from .patterns import bert_passes, late_passes
     return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_dual_conv, fuse_post_activation,
                                                                  fuse_stem_pool, fuse_matmul, fuse_classifier_head,
-                                                                 fuse_dense_softmax, fuse_bottleneck_tail,
-                                                                 fuse_conv_chain] + late_passes()
+                                                                 fuse_dense_softmax, fuse_conv_chain] + late_passes()

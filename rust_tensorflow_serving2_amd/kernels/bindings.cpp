@@ -36,13 +36,8 @@ bool is_halo_cfg(int64_t cfg) {
   return cfg >= 0 && cfg < (1 << 20) && tfsk::halo_cfg_id(int(cfg));
 }
 
-bool is_ws_cfg(int64_t cfg) {
-  return cfg >= 0 && cfg < (1 << 20) && tfsk::ws_cfg_id(int(cfg));
-}
-
 hipError_t launch_any(const tfsk::IGemmArgs& a, int a_mode, int64_t cfg, hipStream_t st) {
   if (is_halo_cfg(cfg)) return tfsk::halo_launch(a, int(cfg), st);
-  if (is_ws_cfg(cfg)) return tfsk::ws_launch(a, int(cfg), st);
   return is_cgemm_cfg(cfg) ? tfsk::cgemm_launch(a, a_mode, int(cfg), st) : tfsk::igemm_launch(a, a_mode, int(cfg), st);
 }
 
@@ -56,17 +51,8 @@ bool split_fixup_enabled() {
 }
 
 void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, const Tensor& like, hipStream_t st) {
-  TORCH_CHECK((cfg >= 0 && cfg < tfsk::kNumIGemmConfigs) || is_cgemm_cfg(cfg) || is_halo_cfg(cfg) ||
-              is_ws_cfg(cfg), "bad tile config ", cfg);
-  if (is_ws_cfg(cfg)) {
-    a.splits = 1;
-    a.kt_per_split = (a.K + 63) / 64;
-    a.ws = nullptr;
-    TORCH_CHECK(a_mode == tfsk::kADense && tfsk::ws_supported(a, int(cfg)),
-                "weight-stationary config ", cfg, " needs a dense GEMM whose weight slice fits in LDS");
-    TORCH_CHECK(launch_any(a, a_mode, cfg, st) == hipSuccess, "conv/GEMM launch failed");
-    return;
-  }
+  TORCH_CHECK((cfg >= 0 && cfg < tfsk::kNumIGemmConfigs) || is_cgemm_cfg(cfg) || is_halo_cfg(cfg),
+              "bad tile config ", cfg);
   TORCH_CHECK(!is_cgemm_cfg(cfg) || tfsk::cgemm_supported(a, a_mode),
               "tile config ", cfg, " needs 64-aligned operands (K % 64, C % 64)");
   TORCH_CHECK(!is_halo_cfg(cfg) || (a_mode == tfsk::kAIm2col && tfsk::halo_supported(a)),
@@ -443,51 +429,6 @@ std::vector<Tensor> conv_chain(const Tensor& x, const Tensor& w1, const Tensor& 
   return {y1, y2};
 }
 
-// A bottleneck's 3x3 (SAME, stride 1) + expand 1x1 + shortcut as one kernel
-// (tail.hip): y = act3(act2(conv3x3(x) + b2) w3^T + b3 + residual), NHWC bf16.
-Tensor bottleneck_tail(const Tensor& x, const Tensor& w2, const Tensor& b2, const Tensor& w3, const Tensor& b3,
-                       const c10::optional<Tensor>& residual, int64_t act2, int64_t act3, int64_t cfg,
-                       const c10::optional<Tensor>& out) {
-  need(x, at::kBFloat16, "x");
-  need(w2, at::kBFloat16, "w2");
-  need(w3, at::kBFloat16, "w3");
-  need(b2, at::kFloat, "b2");
-  need(b3, at::kFloat, "b3");
-  TORCH_CHECK(x.dim() == 4, "bottleneck_tail: x must be NHWC");
-  const int C = x.size(3), N3 = w3.size(0);
-  TORCH_CHECK(w2.dim() == 2 && w2.size(0) == C && w2.size(1) >= 9 * C && w2.size(1) % 8 == 0,
-              "bottleneck_tail: w2 must be [C][>= 9 C]");
-  TORCH_CHECK(w3.dim() == 2 && w3.size(1) >= C && w3.size(1) % 8 == 0, "bottleneck_tail: w3 must be [N3][>= C]");
-  TORCH_CHECK(tfsk::tail_supported(C, N3, int(cfg)), "bottleneck_tail: unsupported C=", C, " N3=", N3, " cfg=", cfg);
-  TORCH_CHECK(b2.numel() == C && b3.numel() == N3, "bottleneck_tail: bias sizes");
-  TORCH_CHECK(w2.device() == x.device() && w3.device() == x.device() && b2.device() == x.device() &&
-                  b3.device() == x.device(), "bottleneck_tail: tensors on different devices");
-  TORCH_CHECK(aligned16(x) && aligned16(w2) && aligned16(w3) && aligned16(b2) && aligned16(b3),
-              "bottleneck_tail: 16-B aligned operands");
-  const uint16_t* rp = nullptr;
-  if (residual.has_value()) {
-    need(*residual, at::kBFloat16, "residual");
-    TORCH_CHECK(residual->numel() == x.size(0) * x.size(1) * x.size(2) * int64_t(N3) && aligned16(*residual),
-                "bottleneck_tail: residual must be [n][h][w][N3]");
-    rp = bf16p(*residual);
-  }
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  Tensor y;
-  if (out.has_value()) {
-    need(*out, at::kBFloat16, "out");
-    TORCH_CHECK(out->numel() == x.size(0) * x.size(1) * x.size(2) * int64_t(N3) && aligned16(*out),
-                "bottleneck_tail: out must be [n][h][w][N3]");
-    y = *out;
-  } else {
-    y = torch::empty({x.size(0), x.size(1), x.size(2), N3}, x.options());
-  }
-  check(tfsk::tail_launch(bf16p(x), bf16p(w2), int(w2.size(1)), b2.data_ptr<float>(), bf16p(w3), int(w3.size(1)),
-                          b3.data_ptr<float>(), rp, bf16p_mut(y), int(x.size(0)), int(x.size(1)), int(x.size(2)), C,
-                          N3, int(act2), int(act3), int(cfg), cur_stream(x)),
-        "bottleneck_tail");
-  return y;
-}
-
 Tensor global_avgpool(const Tensor& x, const c10::optional<Tensor>& out) {
   need(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "global_avgpool: NHWC with C % 8 == 0");
@@ -720,10 +661,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_chain_supported", [](int64_t k1, int64_t n1, int64_t n2) {
     return tfsk::conv_chain_supported(int(k1), int(n1), int(n2));
   });
-  m.def("bottleneck_tail", &bottleneck_tail, "3x3 conv -> expand 1x1 + shortcut in one kernel", py::arg("x"),
-        py::arg("w2"), py::arg("b2"), py::arg("w3"), py::arg("b3"), py::arg("residual"), py::arg("act2") = 1,
-        py::arg("act3") = 1, py::arg("cfg") = 0, py::arg("out") = py::none());
-  m.def("tail_supported", [](int64_t c, int64_t n3, int64_t cfg) { return tfsk::tail_supported(int(c), int(n3), int(cfg)); });
   m.def("conv2d_dual", &conv2d_dual, "act(conv1x1(h) + conv1x1_stride(x) + bias) as one K-concatenated GEMM",
         py::arg("h"), py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"), py::arg("sw"), py::arg("act") = 0,
         py::arg("cfg") = 36, py::arg("out") = py::none(), py::arg("splits") = 1,
@@ -776,13 +713,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("halo_configs", []() {
     std::vector<int> v;
     for (int c = 0; c < tfsk::kNumHaloConfigs; ++c) v.push_back(tfsk::kHaloCfgBase + c);
-    for (int c = 0; c < tfsk::kNumHaloRbConfigs; ++c) v.push_back(tfsk::kHaloRbCfgBase + c);
     return v;
   });
   m.def("config_tile", [](int cfg) {
     if (is_halo_cfg(cfg)) return std::make_pair(tfsk::halo_config_bm(cfg), tfsk::halo_config_bn(cfg));
     if (is_cgemm_cfg(cfg)) return std::make_pair(tfsk::cgemm_config_bm(cfg), tfsk::cgemm_config_bn(cfg));
-    if (is_ws_cfg(cfg)) return std::make_pair(tfsk::ws_config_bm(cfg), tfsk::ws_config_bn(cfg));
     return std::make_pair(tfsk::igemm_config_bm(cfg), tfsk::igemm_config_bn(cfg));
   });
 }

@@ -38,23 +38,8 @@ long halo_tiles(const IGemmArgs& a, int cfg);
 // chunks (kt_per_split counts 64-channel chunks).
 constexpr int kHaloCfgBase = 48;
 constexpr int kNumHaloConfigs = 9;
-// register-B halo kernel (weights straight into MFMA registers, one barrier per chunk)
-constexpr int kHaloRbCfgBase = 80;
-constexpr int kNumHaloRbConfigs = 9;
-inline bool halo_cfg_id(int cfg) {
-  return (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) ||
-         (cfg >= kHaloRbCfgBase && cfg < kHaloRbCfgBase + kNumHaloRbConfigs);
-}
+inline bool halo_cfg_id(int cfg) { return cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs; }
 bool halo_supported(const IGemmArgs& a);
-// Weight-stationary GEMM (wsgemm.hip): dense A (kADense) only, no split-K, no
-// post output; the BN x K weight slice must fit in LDS next to the epilogue slabs.
-constexpr int kWsCfgBase = 96;
-constexpr int kNumWsConfigs = 7;
-inline bool ws_cfg_id(int cfg) { return cfg >= kWsCfgBase && cfg < kWsCfgBase + kNumWsConfigs; }
-bool ws_supported(const IGemmArgs& a, int cfg);
-int ws_config_bm(int cfg);
-int ws_config_bn(int cfg);
-hipError_t ws_launch(const IGemmArgs& a, int cfg, hipStream_t stream);
 int halo_config_bm(int cfg);
 int halo_config_bn(int cfg);
 hipError_t halo_launch(const IGemmArgs& a, int cfg, hipStream_t stream);

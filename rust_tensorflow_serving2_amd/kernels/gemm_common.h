@@ -86,24 +86,6 @@ __device__ __forceinline__ float4 buffer_f4(__amdgpu_buffer_rsrc_t rs, uint32_t 
   return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
 
-// A 16-B buffer load into registers.  The kernels that count their own
-// vmcnt waits over a mix of register loads and LDS DMAs (halo_rb, tail,
-// wsgemm) rely on the issue order they wrote, and hipcc moves plain loads
-// across the LDS-DMA builtins freely: in the first bottleneck-tail build it
-// hoisted weight loads above and between the halo DMAs, and a vmcnt(4) meant
-// for "only the four weight loads are younger" left four halo pieces in
-// flight (garbage).  So every such kernel fences its DMA issue with
-// dma_fence() (a scheduling + compiler memory barrier).  (Volatile loads --
-// aux bit 31 -- would also keep the order, but gfx950 lowers them to sc0 sc1:
-// they skip the L1 the waves sharing a weight slice hit.)
-__device__ __forceinline__ u32x4 ordered_load16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
-  return __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
-}
-__device__ __forceinline__ void dma_fence() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 // This thread's 8 bias values (its epilogue column is fixed), loaded before the
 // K loop so the latency of the load hides under it.  Branch-free buffer loads:
 // a guarded `if (ok) b = *p` became a conditional block whose register moves

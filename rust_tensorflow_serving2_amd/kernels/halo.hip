@@ -330,189 +330,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
                                                               bias1);
 }
 
-// ---- register-B variant (halo_rb_kernel) -----------------------------------
-// The weights go straight from L2 into the MFMA B registers: no B ring in LDS
-// and no barrier per tap -- one barrier per 64-channel chunk (the halo double
-// buffer) instead of nine.  The LDS-ring kernel above waits at every tap for
-// its 8-16 KB weight slice to land by LDS-DMA with 2 slices in flight, which
-// caps a CU's intake near the ~25 GB/s of the ldsdma-fill row of
-// MI355X_MICROARCH.md; here each wave keeps two taps of B fragments in flight
-// in registers (3 register slots) and the compiler's own vmcnt waits order
-// them.  B is read from the im2col weight layout [Cout][9 * C] as it is: the
-// 64 channels of a chunk are split over the four lane groups (fq) as 16
-// channels each, kk picks the 8-channel half, so one lane's two 16-B loads
-// are adjacent and a row's 128 B are covered by the wave; the A fragment
-// reads apply the same channel permutation (an exact reordering of the k sum).
-template <int BM, int BN, int WGM, int WGN, int HR>
-struct HRB {
-  static constexpr int NW = WGM * WGN, NT = 64 * NW;
-  static constexpr int WM = BM / WGM, WN = BN / WGN;
-  static constexpr int TM = WM / 16, TN = WN / 16;
-  static constexpr int HPW = HR / (8 * NW);        // halo 1-KB DMA pieces per wave per chunk
-  static constexpr int LPT = 2 * TN;               // B register loads per wave per tap
-  static constexpr int HALO_B = HR * 128;
-  static constexpr int CS_LD = BN + 4;
-  static constexpr int LDS_EPI = BM * CS_LD * 4;
-  static constexpr int lds(int nbuf) { return nbuf * HALO_B > LDS_EPI ? nbuf * HALO_B : LDS_EPI; }
-  static_assert(HPW >= 1 && HR % (8 * NW) == 0, "halo DMA split");
-  static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
-  static_assert(lds(2) <= 160 * 1024, "LDS budget");
-};
-
-template <int BM, int BN, int WGM, int WGN, int HR>
-__global__ __launch_bounds__(64 * WGM * WGN) void halo_rb_kernel(IGemmArgs p) {
-  using G = HRB<BM, BN, WGM, WGN, HR>;
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  char* const smem = reinterpret_cast<char*>(smem_raw);
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-  const int TH = p.TH, TW = p.TW, HW2 = TW + 2;
-  const int Ho = p.Ho, Wo = p.Wo, H = p.H, W = p.W, C = p.C;
-  const int tph = (Ho + TH - 1) / TH, tpw = (Wo + TW - 1) / TW;
-  const int nbn = (p.N + BN - 1) / BN;
-
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int bn = wg % nbn;
-  int r_ = wg / nbn;
-  const int tw = r_ % tpw;
-  r_ /= tpw;
-  const int th = r_ % tph;
-  const int img = r_ / tph;
-  const int h0 = th * TH, w0 = tw * TW, n0 = bn * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WGN, wn = wid % WGN;
-  const int prow = lane >> 3;
-  const uint32_t kc = uint32_t(((lane & 7) ^ prow) * 8);
-  const int fr = lane & 15, fq = lane >> 4;
-
-  const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.a), 0, int(p.a_bytes), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.b), 0, int(p.b_bytes), 0x00020000);
-
-  const int hrows = (TH + 2) * HW2;
-  const float inv_hw2 = 1.f / float(HW2);
-  uint32_t h_off[G::HPW];
-#pragma unroll
-  for (int j = 0; j < G::HPW; ++j) {
-    const int r = (wid * G::HPW + j) * 8 + prow;
-    const int rr = fdiv(r, HW2, inv_hw2);
-    const int hh = h0 - p.PT + rr, ww = w0 - p.PL + (r - rr * HW2);
-    const bool ok = r < hrows && unsigned(hh) < unsigned(H) && unsigned(ww) < unsigned(W);
-    h_off[j] = ok ? (uint32_t((img * H + hh) * W + ww) * uint32_t(C) + kc) * 2u : kOOB;
-  }
-  // B fragment j of this lane: column n, channels fq*16 .. +15 of each chunk
-  uint32_t b_off[G::TN];
-#pragma unroll
-  for (int j = 0; j < G::TN; ++j) {
-    const int n = n0 + wn * G::WN + j * 16 + fr;
-    b_off[j] = n < p.N ? (uint32_t(n) * uint32_t(p.ldb) + uint32_t(fq * 16)) * 2u : kOOB;
-  }
-
-  const int nch = C / KT;
-  int c0 = 0, c1 = nch;
-  if (p.splits > 1) {
-    c0 = blockIdx.y * p.kt_per_split;
-    c1 = min(nch, c0 + p.kt_per_split);
-  }
-
-  auto issue_halo = [&](int c) {
-    char* dst = smem + ((c - c0) & 1) * G::HALO_B;
-    const uint32_t soff = uint32_t(c) * (KT * 2);
-    dma_fence();                        // the weight loads keep their place around the DMAs (gemm_common.h)
-#pragma unroll
-    for (int j = 0; j < G::HPW; ++j) {
-      const uint32_t v = h_off[j];
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(dst + (wid * G::HPW + j) * 1024), 16, v, soff, 0, 0);
-    }
-    dma_fence();
-  };
-  typedef bf16x8 BFrag[G::TN][2];
-  auto load_b = [&](int c, int u, BFrag& dst) {
-    const uint32_t soff = uint32_t(u * C + c * KT) * 2u;
-#pragma unroll
-    for (int j = 0; j < G::TN; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const uint32_t v = b_off[j] + uint32_t(kk * 16);
-        dst[j][kk] = __builtin_bit_cast(bf16x8, ordered_load16(rsB, v, soff));
-      }
-  };
-
-  int hrow0[G::TM];
-#pragma unroll
-  for (int i = 0; i < G::TM; ++i) {
-    const int px = wm * G::WM + i * 16 + fr;
-    const int ph = px / TW;
-    hrow0[i] = px < TH * TW ? ph * HW2 + (px - ph * TW) : 0;
-  }
-
-  f32x4 acc[G::TM][G::TN];
-#pragma unroll
-  for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](const char* hb, const BFrag& bq, int tap_off) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[G::TM];
-#pragma unroll
-      for (int i = 0; i < G::TM; ++i) {
-        const int hr = hrow0[i] + tap_off;
-        const uint32_t addr = uint32_t(hr) * 128u + ((uint32_t((fq * 2 + kk) ^ (hr & 7))) << 4);
-        af[i] = *reinterpret_cast<const bf16x8*>(hb + addr);
-      }
-#pragma unroll
-      for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-        for (int j = 0; j < G::TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bq[j][kk], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  float4 bias0, bias1;
-  prefetch_bias<BM, BN, G::NT>(p, n0, tid, bias0, bias1);
-
-  // steps (chunk c, tap u): B(c, u) sits in register slot u % 3, loaded two
-  // taps ahead.  The halo of chunk c went out at tap 0 of chunk c - 1 (the
-  // prologue for c0); at tap 0 of chunk c at most B(c, 0) and B(c, 1) are
-  // younger vector-memory operations of this wave that may still be in
-  // flight, so vmcnt(2 * LPT) + a barrier = every wave's halo landed and no
-  // wave still reads the other buffer, which the next halo DMA then fills.
-  BFrag bq[3];
-  issue_halo(c0);
-  load_b(c0, 0, bq[0]);
-  load_b(c0, 1, bq[1]);
-  constexpr int WAIT_HALO = 2 * G::LPT < 63 ? 2 * G::LPT : 63;
-
-  auto chunk = [&](auto last_tag, int c) {
-    constexpr bool LAST = decltype(last_tag)::value;
-    const char* hb = smem + ((c - c0) & 1) * G::HALO_B;
-#pragma unroll
-    for (int u = 0; u < 9; ++u) {
-      if (u == 0) {
-        dma_fence();
-        wait_vmcnt<WAIT_HALO>();
-        lds_barrier();
-        if (!LAST) issue_halo(c + 1);
-      }
-      if (u + 2 < 9) load_b(c, u + 2, bq[(u + 2) % 3]);
-      else if (!LAST) load_b(c + 1, u + 2 - 9, bq[(u + 2) % 3]);
-      compute(hb, bq[u % 3], (u / 3) * HW2 + (u % 3));
-    }
-  };
-  for (int c = c0; c < c1 - 1; ++c) chunk(std::false_type{}, c);
-  chunk(std::true_type{}, c1 - 1);
-  wait_vmcnt<0>();
-  __syncthreads();
-
-  halo_epilogue<BM, BN, G::NT, G::TM, G::TN, G::WM, G::WN>(p, acc, smem, h0, w0, img, n0, wm, wn, tid, bias0,
-                                                              bias1);
-}
-
 // Output block (TH, TW) for a BM-pixel tile whose halo fits HR rows: fewest
 // tiles first, then the smallest halo (least re-read input).
 bool pick_block(int Ho, int Wo, int BM, int HR, int& TH, int& TW) {
@@ -558,38 +375,13 @@ hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int BM, int BN, int WGM, int WGN, int HR>
-hipError_t launch_halo_rb_cfg(const IGemmArgs& a0, hipStream_t s) {
-  using G = HRB<BM, BN, WGM, WGN, HR>;
-  IGemmArgs a = a0;
-  if (!pick_block(a.Ho, a.Wo, BM, HR, a.TH, a.TW)) return hipErrorInvalidValue;
-  const int nch = a.C / KT;
-  const int splits = a.splits > 1 ? a.splits : 1;
-  if (splits > 1 && a.kt_per_split <= 0) return hipErrorInvalidValue;
-  const int per = splits > 1 ? a.kt_per_split : nch;
-  const int nimg = a.M / (a.Ho * a.Wo);
-  const long tiles = long(nimg) * ((a.Ho + a.TH - 1) / a.TH) * ((a.Wo + a.TW - 1) / a.TW) * ((a.N + BN - 1) / BN);
-  if (tiles == 0) return hipSuccess;
-  if (tiles >= (1L << 31)) return hipErrorInvalidValue;
-  const int lds = G::lds(per > 1 ? 2 : 1);
-  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&halo_rb_kernel<BM, BN, WGM, WGN, HR>), G::lds(2));
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((halo_rb_kernel<BM, BN, WGM, WGN, HR>), dim3(unsigned(tiles), splits), dim3(G::NT), lds, s, a);
-  return hipGetLastError();
-}
-
-// per config index (halo_cfg_index): LDS-ring configs, then register-B configs
-constexpr int kHAll = kNumHaloConfigs + kNumHaloRbConfigs;
-constexpr int kHBM[kHAll] = {256, 128, 128, 64, 256, 64, 64, 128, 256,
-                             128, 64, 128, 64, 256, 128, 64, 128, 256};
-constexpr int kHBN[kHAll] = {64, 128, 64, 64, 128, 128, 64, 64, 64,
-                             64, 64, 128, 128, 64, 128, 64, 64, 64};
-constexpr int kHHR[kHAll] = {320, 192, 192, 128, 320, 128, 128, 192, 320,     // halo rows (HR)
-                             192, 128, 192, 128, 320, 192, 128, 192, 320};
+// per config index (halo_cfg_index)
+constexpr int kHBM[kNumHaloConfigs] = {256, 128, 128, 64, 256, 64, 64, 128, 256};
+constexpr int kHBN[kNumHaloConfigs] = {64, 128, 64, 64, 128, 128, 64, 64, 64};
+constexpr int kHHR[kNumHaloConfigs] = {320, 192, 192, 128, 320, 128, 128, 192, 320};     // halo rows (HR)
 
 int halo_cfg_index(int cfg) {
   if (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) return cfg - kHaloCfgBase;
-  if (cfg >= kHaloRbCfgBase && cfg < kHaloRbCfgBase + kNumHaloRbConfigs) return kNumHaloConfigs + cfg - kHaloRbCfgBase;
   return -1;
 }
 
@@ -628,16 +420,6 @@ hipError_t halo_launch(const IGemmArgs& a, int cfg, hipStream_t s) {
     case 6: return launch_halo_cfg<64, 64, 2, 2, 128, 9>(a, s);     // 104 KB, waves 32x32
     case 7: return launch_halo_cfg<128, 64, 2, 2, 192, 9>(a, s);    // 120 KB, waves 64x32
     case 8: return launch_halo_cfg<256, 64, 4, 1, 320, 9>(a, s);    // 152 KB, waves 64x64
-    // register-B kernel: LDS = 2 halo buffers (or the fp32 epilogue tile)
-    case 9: return launch_halo_rb_cfg<128, 64, 2, 2, 192>(a, s);    // 48 KB, waves 64x32
-    case 10: return launch_halo_rb_cfg<64, 64, 2, 2, 128>(a, s);    // 32 KB, waves 32x32
-    case 11: return launch_halo_rb_cfg<128, 128, 2, 2, 192>(a, s);  // 66 KB, waves 64x64
-    case 12: return launch_halo_rb_cfg<64, 128, 1, 4, 128>(a, s);   // 33 KB, waves 64x32 (B private per wave)
-    case 13: return launch_halo_rb_cfg<256, 64, 4, 1, 320>(a, s);   // 80 KB, waves 64x64
-    case 14: return launch_halo_rb_cfg<128, 128, 1, 4, 192>(a, s);  // 66 KB, waves 128x32 (B private)
-    case 15: return launch_halo_rb_cfg<64, 64, 1, 2, 128>(a, s);    // 32 KB, 2 waves of 64x32 (B private)
-    case 16: return launch_halo_rb_cfg<128, 64, 1, 2, 192>(a, s);   // 48 KB, 2 waves of 128x32 (B private)
-    case 17: return launch_halo_rb_cfg<256, 64, 2, 2, 320>(a, s);   // 80 KB, waves 128x32
     default: return hipErrorInvalidValue;
   }
 }

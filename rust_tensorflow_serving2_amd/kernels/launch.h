@@ -115,14 +115,6 @@ bool conv_chain_supported(int K1, int N1, int N2);
 hipError_t conv_chain_launch(const uint16_t* x, const uint16_t* w1, int ldw1, const float* b1, const uint16_t* res,
                              uint16_t* y1, const uint16_t* w2, int ldw2, const float* b2, uint16_t* y2, int M, int K1,
                              int N1, int N2, int act1, int act2, hipStream_t s);
-// A bottleneck's tail in one launch (tail.hip): y = act3(act2(conv3x3_same(x)
-// + b2) w3^T + b3 + res); x NHWC [nimg][H][W][C], w2 [C][ldw2] (k = tap * C +
-// c), w3 [N3][ldw3], res / y [nimg*H*W][N3].  cfg 0 / 1: larger / smaller
-// pixel block per workgroup.
-bool tail_supported(int C, int N3, int cfg);
-hipError_t tail_launch(const uint16_t* x, const uint16_t* w2, int ldw2, const float* b2, const uint16_t* w3,
-                       int ldw3, const float* b3, const uint16_t* res, uint16_t* y, int nimg, int H, int W, int C,
-                       int N3, int act2, int act3, int cfg, hipStream_t s);
 // NHWC bf16 max-pool (TF SAME/VALID padding given explicitly).  With `scale`
 // (and `shift`): y = act(max * scale[c] + shift[c]) — a folded inference
 // BatchNorm (+ ReLU when act == 1) applied after the pooling.

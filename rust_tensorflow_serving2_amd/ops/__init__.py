@@ -52,7 +52,7 @@ ACT = {"none": 0, "relu": 1, "gelu_tanh": 2, "gelu_erf": 3, "tanh": 4}
 
 # ------------------------------------------------------------------ autotune
 _TUNED: Dict[Tuple, int] = {}
-_TUNE_LOCK = threading.RLock()   # re-entrant: an op choosing between implementations tunes its parts inside
+_TUNE_LOCK = threading.Lock()
 AUTOTUNE = os.environ.get("TFSERVE_AUTOTUNE", "1") != "0"
 # per key: [(median cold launch ms, (config, splits))] ascending, from tuned_config
 _TUNE_TIMES: Dict[Tuple, List[Tuple[float, Tuple[int, int]]]] = {}
@@ -154,14 +154,8 @@ CGEMM = {32: (128, 128), 33: (128, 128), 34: (64, 128), 35: (128, 64), 36: (64, 
 TILES.update(CGEMM)
 # halo-tiled 3x3 stride-1 conv (kernels/halo.hip): config id -> (output pixels per tile, BN)
 HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 128), 53: (64, 128), 54: (64, 64),
-        55: (128, 64), 56: (256, 64),
-        # register-B variant (weights straight into the MFMA registers, one barrier per 64-channel chunk)
-        80: (128, 64), 81: (64, 64), 82: (128, 128), 83: (64, 128), 84: (256, 64), 85: (128, 128), 86: (64, 64),
-        87: (128, 64), 88: (256, 64)}
+        55: (128, 64), 56: (256, 64)}
 TILES.update(HALO)
-# weight-stationary GEMM (kernels/wsgemm.hip; dense A only): config id -> (rows per wave round, BN)
-WS = {96: (128, 64), 97: (128, 128), 98: (256, 64), 99: (64, 128), 100: (64, 256), 101: (256, 32), 102: (128, 96)}
-TILES.update(WS)
 
 
 def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
@@ -175,7 +169,7 @@ def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
 
 
 def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-               halo: bool = False, no_split: bool = False, n_multiple: bool = False, dense: bool = False):
+               halo: bool = False, no_split: bool = False, n_multiple: bool = False):
     """(tile config, split-K) pairs worth timing for an M x N x K problem
     (``dma``: the operand mode uses the direct-to-LDS path, so the deeper
     DMA-ring configs apply; ``aligned64``: K and the conv channels are
@@ -194,13 +188,8 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
                 if s > 1 and (nch // s < 1 or tiles >= 512 or tiles * s > 2048):
                     continue
                 out.append((cfg, s))
-    if dense and aligned64 and K % 64 == 0 and N % 8 == 0:
-        # weight-stationary: the BN x K weight slice + 4 epilogue slabs fit in LDS
-        for cfg, (_bm, bn) in WS.items():
-            if bn * K * 2 + 4 * 16 * (bn + 4) * 4 <= 160 * 1024 and not (bn > 64 and N <= bn // 2):
-                out.append((cfg, 1))
     for cfg, (bm, bn) in TILES.items():
-        if cfg in HALO or cfg in WS:
+        if cfg in HALO:
             continue
         if cfg in DMA_ONLY and (not dma or (cfg in (4, 5, 6, 7) and nk < 3)):
             continue
@@ -239,14 +228,10 @@ def _ensure_cache() -> None:
 
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
                  dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-                 halo: bool = False, no_split: bool = False, n_multiple: bool = False,
-                 explicit: Optional[List[Tuple[int, int]]] = None, dense: bool = False,
-                 default: Optional[Tuple[int, int]] = None) -> Tuple[int, int]:
+                 halo: bool = False, no_split: bool = False, n_multiple: bool = False) -> Tuple[int, int]:
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
-    heuristic is used).  ``explicit``: time exactly these candidates (an op
-    choosing between whole implementations, e.g. graph/fused.py TailConv);
-    ``default``: the pick without autotuning."""
+    heuristic is used)."""
     rec = getattr(_REC, "keys", None)
     if rec is not None:
         rec[key] = rec.get(key, 0) + 1
@@ -261,8 +246,6 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
             _GRAPH_TUNED.add(key)          # the leader already graph-tuned it
         return remote
     if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
-        if default is not None:
-            return default
         c = (36 if no_split else 42) if cgemm_only else heuristic_config(M, N)
         return c, 1 if no_split else heuristic_splits(M, N, K, c)
     with _TUNE_LOCK:
@@ -272,8 +255,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
         best, best_t = None, float("inf")
         times = []
         flush = _flush_buffer()
-        cands = explicit if explicit is not None else \
-            candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, n_multiple, dense)
+        cands = candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, n_multiple)
         for c, s in cands:
             launch(c, s)   # warm (also sets the kernel's LDS attribute)
             samples = []

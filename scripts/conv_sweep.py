@@ -72,7 +72,7 @@ def main():
         b = torch.zeros(cout, device="cuda")
         halo = k == 3 and s == 1 and cin % 64 == 0
         res = []
-        for cfg, sp in candidates(M, N, K, True, cin % 64 == 0, halo=halo, dense=(k == 1 and s == 1)):
+        for cfg, sp in candidates(M, N, K, True, cin % 64 == 0, halo=halo):
             def fn(i, cfg=cfg, sp=sp):
                 j = i % 8
                 hip().conv2d(xs[j], ws[j], b, rs[j], k, k, s, s, pad, pad, pad, pad, ACT["relu"], cfg, outs[j],

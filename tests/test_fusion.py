@@ -188,29 +188,6 @@ def test_conv_chain_pass_pairs_expand_with_next_reduce(models_dir, monkeypatch):
     assert hist["_FusedConv2D"] + 2 * hist["_ChainConv"] + 2 * hist.get("_FusedDualConv", 0) == convs, hist
 
 
-def test_bottleneck_tail_pass_fuses_3x3_with_expand(models_dir, monkeypatch):
-    """Stages with 128 / 256 bottleneck channels: every stride-1 3x3 whose only
-    consumer is its block's expand 1x1 (with the shortcut) becomes one
-    _TailConv(3x3 input, shortcut); the first block of a stage (stride-2 3x3)
-    stays unfused; the fused program still equals the unfused interpreter."""
-    from rust_tensorflow_serving2_amd.models import resnet
-    monkeypatch.setenv("TFSERVE_TAIL", "force")           # the pass is GPU-only by default
-    path = os.path.join(str(models_dir), "tail_resnet", "1")
-    resnet.export(path, blocks=(1, 2, 3, 1), width=64, num_classes=10, image_size=32, seed=6)
-    ref, fused = _pair(path)
-    x = np.random.default_rng(4).random((2, 32, 32, 3), dtype=np.float32)
-    a = ref.run("serving_default", {"input": x}, ["classes", "probabilities"])
-    b = fused.run("serving_default", {"input": x}, ["classes", "probabilities"])
-    np.testing.assert_allclose(a["probabilities"], b["probabilities"], atol=1e-5)
-    np.testing.assert_array_equal(a["classes"], b["classes"])
-    hist = fused.runner("serving_default", ["input"], ["classes", "probabilities"]).program.op_histogram()
-    assert hist["_TailConv"] == 1 + 2, hist               # stage 3: 1 of 2 blocks, stage 4: 2 of 3
-    monkeypatch.setenv("TFSERVE_TAIL", "0")
-    _r, off = _pair(path)
-    hist0 = off.runner("serving_default", ["input"], ["classes", "probabilities"]).program.op_histogram()
-    assert "_TailConv" not in hist0
-
-
 def test_activation_release_plan(tiny_resnet_path):
     """The program drops each value after its last reader (compile-time
     liveness): results are unchanged and far fewer values are alive at once."""

@@ -104,7 +104,7 @@ def test_cgemm_conv_matches_fp32(shape, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
 
 
-HALO_CFGS = list(range(48, 57)) + list(range(80, 89))
+HALO_CFGS = list(range(48, 57))
 HALO_SHAPES = [
     # N, H, W, Cin, Cout, pads            (3x3 stride 1; ResNet-50 stages + edge cases)
     (2, 56, 56, 64, 64, (1, 1, 1, 1)),
@@ -137,64 +137,6 @@ def test_halo_conv_matches_fp32(shape, cfg):
         err = (y.float().cpu() - ref).abs().max().item()
         assert y.shape == (n, ho, wo, cout)
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
-
-
-TAIL_SHAPES = [
-    # N, H, W, C, N3          (3x3 SAME -> expand 1x1 + shortcut; ResNet-50 stages + an odd image)
-    (2, 56, 56, 64, 256),
-    (2, 28, 28, 128, 512),
-    (3, 14, 14, 256, 1024),
-    (1, 13, 17, 128, 256),
-    (2, 7, 9, 256, 384),
-]
-
-
-@pytest.mark.parametrize("shape", TAIL_SHAPES)
-@pytest.mark.parametrize("cfg", [0, 1])
-def test_bottleneck_tail_matches_fp32(shape, cfg):
-    """The fused bottleneck tail (kernels/tail.hip) vs fp32 torch: 3x3 SAME +
-    bias + ReLU, rounded to bf16 (the tile the kernel keeps in LDS), expand
-    1x1 + bias + shortcut + ReLU; with and without the shortcut / activations."""
-    n, h, w, c, n3 = shape
-    x = rnd(n, h, w, c, seed=21).to(BF)
-    w2 = rnd(3, 3, c, c, scale=1 / math.sqrt(9 * c), seed=22).to(BF).float()
-    b2 = rnd(c, scale=0.1, seed=23)
-    w3 = rnd(n3, c, scale=1 / math.sqrt(c), seed=24).to(BF)
-    b3 = rnd(n3, scale=0.1, seed=25)
-    res = rnd(n, h, w, n3, seed=26).to(BF)
-    for with_res, act in ((True, "relu"), (False, "none")):
-        y2 = ref_conv(x, w2, b2, 1, (1, 1, 1, 1), None, act).to(BF).float()
-        ref = y2.reshape(-1, c) @ w3.float().t() + b3
-        if with_res:
-            ref = ref + res.float().reshape(-1, n3)
-        if act == "relu":
-            ref = torch.relu(ref)
-        ref = ref.reshape(n, h, w, n3)
-        y = hip().bottleneck_tail(x.to(DEV), pack_w(w2), b2.to(DEV), w3.to(DEV), b3.to(DEV),
-                                  res.to(DEV) if with_res else None, ACT[act], ACT[act], cfg)
-        torch.cuda.synchronize()
-        assert y.shape == (n, h, w, n3)
-        err = (y.float().cpu() - ref).abs().max().item()
-        assert err < 3e-2 * max(1.0, ref.abs().max().item()), (with_res, act, err)
-
-
-def test_bottleneck_tail_exact_integers():
-    """Small integer operands (every intermediate and output exact in bf16 and
-    fp32): every pixel of every block position and every expand column must
-    match bit for bit -- catches a mis-shifted halo row, a wrong channel
-    permutation between the two GEMMs or a swizzle slip that tolerances hide."""
-    n, h, w, c, n3 = 2, 14, 14, 256, 512
-    g = torch.Generator().manual_seed(9)
-    x = torch.randint(-1, 2, (n, h, w, c), generator=g).float()
-    w2 = torch.randint(-1, 2, (3, 3, c, c), generator=g).float() * (torch.rand(3, 3, c, c, generator=g) < 0.01)
-    w3 = torch.randint(-1, 2, (n3, c), generator=g).float() * (torch.rand(n3, c, generator=g) < 0.05)
-    y2 = ref_conv(x, w2, torch.zeros(c), 1, (1, 1, 1, 1))
-    ref = (y2.reshape(-1, c) @ w3.t()).reshape(n, h, w, n3)
-    assert y2.abs().max() <= 256 and ref.abs().max() <= 256       # exact in bf16
-    for cfg in (0, 1):
-        y = hip().bottleneck_tail(x.to(BF).to(DEV), pack_w(w2), torch.zeros(c, device=DEV), w3.to(BF).to(DEV),
-                                  torch.zeros(n3, device=DEV), None, 0, 0, cfg)
-        assert torch.equal(y.float().cpu(), ref), cfg
 
 
 def test_halo_exact_identity_taps():
@@ -233,45 +175,6 @@ def test_cgemm_linear_matches_fp32(m, n, k, cfg):
         y = hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), res.to(DEV), ACT[act], cfg, out_f32)
         err = (y.float().cpu() - fn(ref)).abs().max().item()
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (act, err)
-
-
-WS_CFGS = list(range(96, 103))
-WS_SHAPES = [
-    # M, N, K       (ResNet-50 1x1 convs at small batch, BERT-base projections, tails)
-    (2 * 56 * 56, 64, 256), (2 * 28 * 28, 512, 128), (3 * 14 * 14, 256, 1024), (2 * 7 * 7, 2048, 512),
-    (256, 768, 768), (77, 136, 64), (1000, 96, 2048),
-]
-
-
-@pytest.mark.parametrize("shape", WS_SHAPES)
-@pytest.mark.parametrize("cfg", WS_CFGS)
-def test_weight_stationary_gemm_matches_fp32(shape, cfg):
-    """Weight-stationary GEMM (kernels/wsgemm.hip: the weight slice resident in
-    LDS, A rows straight into registers, persistent over M) vs fp32, with bias
-    + residual + each activation; configs whose slice does not fit refuse."""
-    m, n, k = shape
-    x = rnd(m, k, seed=17).to(BF)
-    w = rnd(n, k, scale=1 / math.sqrt(k), seed=18).to(BF)
-    b = rnd(n, scale=0.1, seed=19)
-    res = rnd(m, n, seed=20).to(BF)
-    ref = x.float() @ w.float().t() + b + res.float()
-    bn = hip().config_tile(cfg)[1]
-    if bn * k * 2 + 4 * 16 * (bn + 4) * 4 > 160 * 1024:
-        with pytest.raises(RuntimeError, match="weight-stationary"):
-            hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), res.to(DEV), 0, cfg, False)
-        return
-    for act, fn, out_f32 in (("none", lambda t: t, False), ("relu", torch.relu, True),
-                             ("gelu_tanh", lambda t: F.gelu(t, approximate="tanh"), False)):
-        y = hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), res.to(DEV), ACT[act], cfg, out_f32)
-        err = (y.float().cpu() - fn(ref)).abs().max().item()
-        assert err < 3e-2 * max(1.0, ref.abs().max().item()), (act, err)
-    # the 1x1 conv path (NHWC rows, no residual)
-    if m % 4 == 0:
-        xx = x.reshape(1, 4, m // 4, k)
-        wt = w.float().t().reshape(1, 1, k, n)
-        y = hip().conv2d(xx.to(DEV), pack_w(wt), b.to(DEV), None, 1, 1, 1, 1, 0, 0, 0, 0, act=ACT["relu"], cfg=cfg)
-        refc = torch.relu(x.float() @ w.float().t() + b).reshape(1, 4, m // 4, n)
-        assert (y.float().cpu() - refc).abs().max().item() < 3e-2 * max(1.0, refc.abs().max().item())
 
 
 @pytest.mark.parametrize("cfg", CGEMM_CFGS)
