@@ -50,7 +50,14 @@ bool split_fixup_enabled() {
   return v && v[0] == '1';
 }
 
+// scripts/wg_trace.py: per-workgroup phase stamps of the next GEMM / conv
+// launches (a device int64 buffer of 8 per workgroup; None turns it off)
+long long* g_trace = nullptr;
+int g_trace_cap = 0;
+
 void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, const Tensor& like, hipStream_t st) {
+  a.trace = g_trace;
+  a.trace_cap = g_trace_cap;
   TORCH_CHECK((cfg >= 0 && cfg < tfsk::kNumIGemmConfigs) || is_cgemm_cfg(cfg) || is_halo_cfg(cfg),
               "bad tile config ", cfg);
   TORCH_CHECK(!is_cgemm_cfg(cfg) || tfsk::cgemm_supported(a, a_mode),
@@ -703,16 +710,28 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_counters_release", [](int64_t owner) { return tfsk::splitk_counters_release(owner); },
         "return an owner's captured split-K counter slices to the pool");
   m.def("splitk_counters_captured_in_use", []() { return tfsk::splitk_counters_captured_in_use(); });
+  m.def("set_wg_trace", [](const c10::optional<Tensor>& t) {
+    if (!t.has_value()) {
+      g_trace = nullptr;
+      g_trace_cap = 0;
+      return;
+    }
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous(), "trace: int64 device tensor");
+    g_trace = reinterpret_cast<long long*>(t->data_ptr<int64_t>());
+    g_trace_cap = int(std::min<int64_t>(t->numel() / 8, 1 << 30));
+  }, "per-workgroup wall-clock stamps of the following GEMM / conv launches (None: off)");
   m.def("num_configs", []() { return tfsk::kNumIGemmConfigs; });
   m.def("cgemm_configs", []() {
     std::vector<int> v;
     for (int c = 0; c < tfsk::kNumCGemmConfigs; ++c) v.push_back(tfsk::kCGemmCfgBase + c);
     for (int c = 0; c < tfsk::kNumCGemmConfigs2; ++c) v.push_back(tfsk::kCGemmCfgBase2 + c);
+    for (int c = 0; c < tfsk::kNumCGemmPfConfigs; ++c) v.push_back(tfsk::kCGemmPfCfgBase + c);
     return v;
   });
   m.def("halo_configs", []() {
     std::vector<int> v;
     for (int c = 0; c < tfsk::kNumHaloConfigs; ++c) v.push_back(tfsk::kHaloCfgBase + c);
+    for (int c = 0; c < tfsk::kNumHaloConfigs; ++c) v.push_back(tfsk::kHaloPfCfgBase + c);
     return v;
   });
   m.def("config_tile", [](int cfg) {

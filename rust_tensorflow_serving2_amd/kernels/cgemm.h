@@ -11,9 +11,13 @@ constexpr int kNumCGemmConfigs = 16;
 // a second id range (after the halo ids): 2-wave and 3-deep variants
 constexpr int kCGemmCfgBase2 = 64;
 constexpr int kNumCGemmConfigs2 = 9;
+// a third range: fragment-prefetch (PF) builds of 11 of the tiles above
+constexpr int kCGemmPfCfgBase = 96;
+constexpr int kNumCGemmPfConfigs = 11;
 inline bool cgemm_cfg_id(int cfg) {
   return (cfg >= kCGemmCfgBase && cfg < kCGemmCfgBase + kNumCGemmConfigs) ||
-         (cfg >= kCGemmCfgBase2 && cfg < kCGemmCfgBase2 + kNumCGemmConfigs2);
+         (cfg >= kCGemmCfgBase2 && cfg < kCGemmCfgBase2 + kNumCGemmConfigs2) ||
+         (cfg >= kCGemmPfCfgBase && cfg < kCGemmPfCfgBase + kNumCGemmPfConfigs);
 }
 
 // Operand requirements (else cgemm_launch returns hipErrorInvalidValue):
@@ -38,7 +42,12 @@ long halo_tiles(const IGemmArgs& a, int cfg);
 // chunks (kt_per_split counts 64-channel chunks).
 constexpr int kHaloCfgBase = 48;
 constexpr int kNumHaloConfigs = 9;
-inline bool halo_cfg_id(int cfg) { return cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs; }
+// the same halo tiles with the fragment-prefetch step pipeline (PF)
+constexpr int kHaloPfCfgBase = 80;
+inline bool halo_cfg_id(int cfg) {
+  return (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) ||
+         (cfg >= kHaloPfCfgBase && cfg < kHaloPfCfgBase + kNumHaloConfigs);
+}
 bool halo_supported(const IGemmArgs& a);
 int halo_config_bm(int cfg);
 int halo_config_bn(int cfg);

@@ -122,13 +122,17 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
 // Waves per SIMD the register allocation must leave room for: the 4-wave
 // 32-KB tiles (64x64, 2 slots) fit 5 workgroups per CU by LDS, i.e. 5 waves
 // per SIMD, which needs <= 102 VGPRs (unconstrained they took 128: 4 per CU)
-template <int BM, int BN, int WGM, int WGN, int S>
+template <int BM, int BN, int WGM, int WGN, int S, bool PF>
 constexpr int cg_waves_per_eu() {
-  return (WGM * WGN == 4 && CG<BM, BN, WGM, WGN, S>::LDS <= 32 * 1024) ? 5 : 1;
+  return (!PF && WGM * WGN == 4 && CG<BM, BN, WGM, WGN, S>::LDS <= 32 * 1024) ? 5 : 1;
 }
 
-template <int BM, int BN, int WGM, int WGN, int S, int AM>
-__global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, S>())) void cgemm_kernel(IGemmArgs p) {
+// PF: fragment-prefetch step pipeline -- step t's fragments are read from LDS
+// right after its barrier while the MFMAs of step t - 1 (fragments already in
+// registers) issue, so neither the LDS read latency nor the barrier sits
+// between a k-tile landing and its MFMAs (halo.hip uses the same scheme).
+template <int BM, int BN, int WGM, int WGN, int S, int AM, bool PF>
+__global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, S, PF>())) void cgemm_kernel(IGemmArgs p) {
   using G = CG<BM, BN, WGM, WGN, S>;
   constexpr bool IM2COL = (AM == 1), DUAL = (AM == 2), STEM = (AM == 3);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -152,6 +156,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
   // (timing only; results are garbage)
   const int dbg = p.act >= 100 ? p.act - 100 : 0;
   if (dbg & 4) return;
+  trace_stamp(p, 0);
   const bool do_dma = !(dbg & 1), do_mma = !(dbg & 2);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -324,6 +329,32 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
+  struct Frags {
+    bf16x8 a[2][G::TM], b[2][G::TN];
+  };
+  auto load_frags = [&](Frags& f, int slot) {
+    const char* sa = smem + slot * G::A_ST * 2;
+    const char* sb = smem + (S * G::A_ST + slot * G::B_ST) * 2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+        f.a[kk][i] = *reinterpret_cast<const bf16x8*>(sa + (kk ? ra1 : ra0) + i * 16 * KT * 2);
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j)
+        f.b[kk][j] = *reinterpret_cast<const bf16x8*>(sb + (kk ? rb1 : rb0) + j * 16 * KT * 2);
+    }
+  };
+  auto mma = [&](const Frags& f) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[kk][i], f.b[kk][j], acc[i][j], 0, 0, 0);
+  };
+  Frags prev;
 
   uint4 rpre[Epi<BM, BN, G::NT>::PRE > 0 ? Epi<BM, BN, G::NT>::PRE : 1];
   if constexpr (G::PASSES == 1) prefetch_residual<BM, BN, G::NT>(p, m0, n0, tid, rpre);
@@ -356,13 +387,30 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
         else wait_vmcnt<0>();
         // ... and every wave's (and every wave is done reading slot (t-1) % S)
         lds_barrier();
+        if (t == 0) trace_stamp(p, 1);
         if (t + S - 1 < nk && do_dma) issue((u + S - 1) % S);
-        if (do_mma) compute(u);
+        if constexpr (PF) {
+          // pinned: the scheduler would hoist the register-only MFMAs above
+          // the barrier and sink the reads to their uses
+          __builtin_amdgcn_sched_barrier(0);
+          Frags cur;
+          load_frags(cur, u);
+          __builtin_amdgcn_sched_barrier(0);
+          if (t > 0 && do_mma) mma(prev);
+          __builtin_amdgcn_sched_barrier(0);
+          prev = cur;
+        } else {
+          if (do_mma) compute(u);
+        }
       }
     }
   }
+  if constexpr (PF) {
+    if (nk > 0 && do_mma) mma(prev);
+  }
   wait_vmcnt<0>();
   __syncthreads();
+  trace_stamp(p, 2);
   if (dbg & 8) return;
   // ---- epilogue: stage the fp32 tile in LDS, then coalesced row chunks
   // (G::PASSES row passes of G::RPP rows when the whole fp32 tile does not fit)
@@ -454,9 +502,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
       default: epilogue_rows<RPP, BN, G::NT, G::CS_LD, 0, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1); break;
     }
   }
+  trace_stamp(p, 3);
 }
 
-template <int BM, int BN, int WGM, int WGN, int S, int AM>
+template <int BM, int BN, int WGM, int WGN, int S, int AM, bool PF = false>
 hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
   using G = CG<BM, BN, WGM, WGN, S>;
   IGemmArgs a = a0;
@@ -465,9 +514,9 @@ hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
   if (splits > 1) a.kt_per_split = (nk + splits - 1) / splits;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
-  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, AM>), G::LDS);
+  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF>), G::LDS);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((cgemm_kernel<BM, BN, WGM, WGN, S, AM>), dim3(tiles, splits), dim3(G::NT), G::LDS, s, a);
+  hipLaunchKernelGGL((cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF>), dim3(tiles, splits), dim3(G::NT), G::LDS, s, a);
   return hipGetLastError();
 }
 
@@ -479,9 +528,32 @@ constexpr int kBM[kAll] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256, 64, 64
 constexpr int kBN[kAll] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64, 64, 128, 64, 96, 96, 96,
                            64, 64, 64, 64, 128, 64, 128, 64, 192};
 
-// config id -> index into the tables (both id ranges)
+// PF config ids kCGemmPfCfgBase + i: the fragment-prefetch build of table index kPfOf[i]
+// (the 8-wave 256 x 128 / 128 x 256 / 256 x 192 tiles spill with two fragment sets: not built)
+constexpr int kPfOf[kNumCGemmPfConfigs] = {0, 2, 3, 4, 7, 9, 10, 11, 12, 13, 23};
+
+// config id -> index into the tables (all id ranges)
 int cfg_index(int cfg) {
+  if (cfg >= kCGemmPfCfgBase) return kPfOf[cfg - kCGemmPfCfgBase];
   return cfg < kCGemmCfgBase2 ? cfg - kCGemmCfgBase : kNumCGemmConfigs + (cfg - kCGemmCfgBase2);
+}
+
+template <int AM>
+hipError_t launch_mode_pf(const IGemmArgs& a, int idx, hipStream_t s) {
+  switch (idx) {
+    case 0: return launch_cfg<128, 128, 2, 2, 3, AM, true>(a, s);
+    case 2: return launch_cfg<64, 128, 2, 2, 4, AM, true>(a, s);
+    case 3: return launch_cfg<128, 64, 2, 2, 4, AM, true>(a, s);
+    case 4: return launch_cfg<64, 64, 2, 2, 4, AM, true>(a, s);
+    case 7: return launch_cfg<128, 128, 2, 4, 4, AM, true>(a, s);
+    case 9: return launch_cfg<256, 64, 4, 1, 3, AM, true>(a, s);
+    case 10: return launch_cfg<64, 64, 2, 2, 2, AM, true>(a, s);
+    case 11: return launch_cfg<64, 128, 2, 2, 2, AM, true>(a, s);
+    case 12: return launch_cfg<128, 64, 2, 2, 2, AM, true>(a, s);
+    case 13: return launch_cfg<128, 96, 2, 2, 3, AM, true>(a, s);
+    case 23: return launch_cfg<64, 64, 2, 2, 3, AM, true>(a, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <int AM>
@@ -556,6 +628,15 @@ int cgemm_config_bn(int cfg) { return kBN[cfg_index(cfg)]; }
 
 hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) {
   if (!cgemm_cfg_id(cfg) || !cgemm_supported(a, a_mode)) return hipErrorInvalidValue;
+  if (cfg >= kCGemmPfCfgBase) {
+    const int idx = cfg_index(cfg);
+    switch (a_mode) {
+      case kAIm2col: return launch_mode_pf<1>(a, idx, s);
+      case kADual: return launch_mode_pf<2>(a, idx, s);
+      case kAC4: return launch_mode_pf<3>(a, idx, s);
+      default: return launch_mode_pf<0>(a, idx, s);
+    }
+  }
   cfg = cfg_index(cfg);
   switch (a_mode) {
     case kAIm2col: return launch_mode<1>(a, cfg, s);

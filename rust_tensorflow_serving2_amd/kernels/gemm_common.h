@@ -86,6 +86,20 @@ __device__ __forceinline__ float4 buffer_f4(__amdgpu_buffer_rsrc_t rs, uint32_t 
   return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
 
+// Workgroup phase trace (profiling only, p.trace == nullptr in production):
+// stamp k of this workgroup = the steady wall clock (100 MHz), written by
+// thread 0 with a vector store; stamp 0 also records the XCC / SE / CU id.
+__device__ __forceinline__ void trace_stamp(const IGemmArgs& p, int k) {
+  if (p.trace != nullptr && threadIdx.x == 0) {
+    const long wgi = long(blockIdx.y) * gridDim.x + blockIdx.x;
+    if (wgi < p.trace_cap) {
+      long long* d = p.trace + wgi * 8;
+      d[k] = wall_clock64();
+      if (k == 0) d[7] = __smid();
+    }
+  }
+}
+
 // This thread's 8 bias values (its epilogue column is fixed), loaded before the
 // K loop so the latency of the load hides under it.  Branch-free buffer loads:
 // a guarded `if (ok) b = *p` became a conditional block whose register moves

@@ -161,7 +161,7 @@ __device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, const f32x4 (&
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int HR, int S>
+template <int BM, int BN, int WGM, int WGN, int HR, int S, bool PF>
 __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) {
   using G = HG<BM, BN, WGM, WGN, HR, S>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -183,6 +183,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
   const int img = r_ / tph;
   const int h0 = th * TH, w0 = tw * TW, n0 = bn * BN;
 
+  trace_stamp(p, 0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WGN, wn = wid % WGN;
@@ -261,26 +262,43 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
 #pragma unroll
     for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](const char* hb, const char* sb, int tap_off) {
+  // one tap's operand fragments (both 32-deep k halves of the 64-channel chunk)
+  struct Frags {
+    bf16x8 a[2][G::TM], b[2][G::TN];
+  };
+  auto load_frags = [&](Frags& f, const char* hb, const char* sb, int tap_off) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[G::TM], bfr[G::TN];
 #pragma unroll
       for (int i = 0; i < G::TM; ++i) {
         const int hr = hrow0[i] + tap_off;
         const uint32_t addr = uint32_t(hr) * 128u + ((uint32_t((kk * 4 + fq) ^ (hr & 7))) << 4);
-        af[i] = *reinterpret_cast<const bf16x8*>(hb + addr);
+        f.a[kk][i] = *reinterpret_cast<const bf16x8*>(hb + addr);
       }
 #pragma unroll
       for (int j = 0; j < G::TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(sb + (kk ? rb1 : rb0) + j * 16 * KT * 2);
+        f.b[kk][j] = *reinterpret_cast<const bf16x8*>(sb + (kk ? rb1 : rb0) + j * 16 * KT * 2);
+    }
+  };
+  auto mma = [&](const Frags& f) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < G::TM; ++i)
 #pragma unroll
         for (int j = 0; j < G::TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[kk][i], f.b[kk][j], acc[i][j], 0, 0, 0);
   };
+  auto compute = [&](const char* hb, const char* sb, int tap_off) {
+    Frags f;
+    load_frags(f, hb, sb, tap_off);
+    mma(f);
+  };
+  // PF: the fragments of step t are read from LDS right after step t's
+  // barrier, and the MFMAs of step t - 1 (fragments already in registers) run
+  // while those reads are in flight -- the LDS latency and the barrier no
+  // longer sit between a step's data landing and its MFMAs
+  Frags prev;
 
   float4 bias0, bias1;
   prefetch_bias<BM, BN, G::NT>(p, n0, tid, bias0, bias1);
@@ -316,18 +334,34 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
         default: wait_vmcnt<40>(); break;
       }
       lds_barrier();   // every wave's DMAs landed; the slot / buffer about to be refilled is read-free
+      if (u == 0 && c == c0) trace_stamp(p, 1);
       if (!LAST && u == 0) issue_halo(c + 1);
       if (!LAST || u + D < 9) issue_b(c + (u + D) / 9, (u + D) % 9, (u + D) % G::S);
-      compute(hb, ring + (u % G::S) * G::B_B, (u / 3) * HW2 + (u % 3));
+      if constexpr (PF) {
+        // the scheduler would hoist the (register-only) MFMAs of the previous
+        // step above the barrier and sink these reads to their uses: pin both
+        __builtin_amdgcn_sched_barrier(0);
+        Frags cur;
+        load_frags(cur, hb, ring + (u % G::S) * G::B_B, (u / 3) * HW2 + (u % 3));
+        __builtin_amdgcn_sched_barrier(0);
+        if (u > 0 || c > c0) mma(prev);
+        __builtin_amdgcn_sched_barrier(0);   // (and keep them above the next step's barrier)
+        prev = cur;
+      } else {
+        compute(hb, ring + (u % G::S) * G::B_B, (u / 3) * HW2 + (u % 3));
+      }
     }
   };
   for (int c = c0; c < c1 - 1; ++c) chunk(std::false_type{}, c);
   chunk(std::true_type{}, c1 - 1);
+  if constexpr (PF) mma(prev);
   wait_vmcnt<0>();
   __syncthreads();
+  trace_stamp(p, 2);
 
   halo_epilogue<BM, BN, G::NT, G::TM, G::TN, G::WM, G::WN>(p, acc, smem, h0, w0, img, n0, wm, wn, tid, bias0,
                                                               bias1);
+  trace_stamp(p, 3);
 }
 
 // Output block (TH, TW) for a BM-pixel tile whose halo fits HR rows: fewest
@@ -354,7 +388,7 @@ bool pick_block(int Ho, int Wo, int BM, int HR, int& TH, int& TW) {
   return best_tiles > 0;
 }
 
-template <int BM, int BN, int WGM, int WGN, int HR, int S>
+template <int BM, int BN, int WGM, int WGN, int HR, int S, bool PF = false>
 hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
   using G = HG<BM, BN, WGM, WGN, HR, S>;
   IGemmArgs a = a0;
@@ -368,9 +402,9 @@ hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
   if (tiles == 0) return hipSuccess;
   if (tiles >= (1L << 31)) return hipErrorInvalidValue;
   const int lds = G::lds(per > 1 ? 2 : 1);
-  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&halo_conv_kernel<BM, BN, WGM, WGN, HR, S>), G::lds(2));
+  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&halo_conv_kernel<BM, BN, WGM, WGN, HR, S, PF>), G::lds(2));
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((halo_conv_kernel<BM, BN, WGM, WGN, HR, S>), dim3(unsigned(tiles), splits), dim3(G::NT), lds, s,
+  hipLaunchKernelGGL((halo_conv_kernel<BM, BN, WGM, WGN, HR, S, PF>), dim3(unsigned(tiles), splits), dim3(G::NT), lds, s,
                      a);
   return hipGetLastError();
 }
@@ -382,6 +416,7 @@ constexpr int kHHR[kNumHaloConfigs] = {320, 192, 192, 128, 320, 128, 128, 192, 3
 
 int halo_cfg_index(int cfg) {
   if (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) return cfg - kHaloCfgBase;
+  if (cfg >= kHaloPfCfgBase && cfg < kHaloPfCfgBase + kNumHaloConfigs) return cfg - kHaloPfCfgBase;
   return -1;
 }
 
@@ -408,6 +443,20 @@ int halo_config_bn(int cfg) { return kHBN[halo_cfg_index(cfg)]; }
 
 hipError_t halo_launch(const IGemmArgs& a, int cfg, hipStream_t s) {
   if (!halo_cfg_id(cfg) || !halo_supported(a)) return hipErrorInvalidValue;
+  if (cfg >= kHaloPfCfgBase) {
+    switch (halo_cfg_index(cfg)) {   // the same tiles with the fragment-prefetch step pipeline
+      case 0: return launch_halo_cfg<256, 64, 4, 1, 320, 3, true>(a, s);
+      case 1: return launch_halo_cfg<128, 128, 2, 2, 192, 3, true>(a, s);
+      case 2: return launch_halo_cfg<128, 64, 2, 2, 192, 3, true>(a, s);
+      case 3: return launch_halo_cfg<64, 64, 2, 2, 128, 3, true>(a, s);
+      // (4: the 8-wave 256 x 128 tile spills with two fragment sets; not built)
+      case 5: return launch_halo_cfg<64, 128, 2, 2, 128, 3, true>(a, s);
+      case 6: return launch_halo_cfg<64, 64, 2, 2, 128, 9, true>(a, s);
+      case 7: return launch_halo_cfg<128, 64, 2, 2, 192, 9, true>(a, s);
+      case 8: return launch_halo_cfg<256, 64, 4, 1, 320, 9, true>(a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (halo_cfg_index(cfg)) {
     // LDS = 2 halo buffers (HR x 128 B; one when C == 64) + S B slots (BN x 128 B)
     case 0: return launch_halo_cfg<256, 64, 4, 1, 320, 3>(a, s);    // 104 KB (64 KB for C == 64), waves 64x64

@@ -56,6 +56,10 @@ struct IGemmArgs {
   // arrival counter per tile (zero between launches); the last slice to arrive
   // sums the slabs and runs the epilogue, then re-zeroes its counter
   int* counters;
+  // profiling (scripts/wg_trace.py): per-workgroup wall-clock stamps, 8 int64
+  // per workgroup (blockIdx.y * gridDim.x + blockIdx.x), nullptr in production
+  long long* trace;
+  int trace_cap;        // workgroups the trace buffer holds
 };
 
 // Per-device pool of zeroed split-K arrival counters: a launch captured into a

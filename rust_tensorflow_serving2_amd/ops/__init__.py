@@ -151,10 +151,15 @@ CGEMM = {32: (128, 128), 33: (128, 128), 34: (64, 128), 35: (128, 64), 36: (64, 
          42: (64, 64), 43: (64, 128), 44: (128, 64), 45: (128, 96), 46: (128, 96), 47: (64, 96),
          64: (64, 64), 65: (64, 64), 66: (64, 64), 67: (128, 64), 68: (64, 128), 69: (128, 64), 70: (64, 128),
          71: (64, 64), 72: (256, 192)}
+# fragment-prefetch (PF) builds of 11 of those tiles (kernels/cgemm.hip kPfOf)
+CGEMM_PF_OF = [32, 34, 35, 36, 39, 41, 42, 43, 44, 45, 71]
+CGEMM.update({96 + k: CGEMM[base] for k, base in enumerate(CGEMM_PF_OF)})
 TILES.update(CGEMM)
 # halo-tiled 3x3 stride-1 conv (kernels/halo.hip): config id -> (output pixels per tile, BN)
 HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 128), 53: (64, 128), 54: (64, 64),
         55: (128, 64), 56: (256, 64)}
+# the same tiles with the fragment-prefetch step pipeline (halo.hip PF)
+HALO.update({cfg + 32: tile for cfg, tile in list(HALO.items()) if cfg != 52})
 TILES.update(HALO)
 
 

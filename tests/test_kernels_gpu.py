@@ -76,7 +76,7 @@ def test_conv_matches_fp32(shape, cfg, splits):
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
 
 
-CGEMM_CFGS = list(range(32, 48)) + list(range(64, 73))
+CGEMM_CFGS = list(range(32, 48)) + list(range(64, 73)) + list(range(96, 107))
 CGEMM_CONV_SHAPES = [s for s in CONV_SHAPES if s[3] % 64 == 0] + [
     (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)),   # tiny image: most taps hit padding at the border rows
     (1, 15, 13, 64, 192, 3, 2, (0, 1, 1, 1)),  # odd sizes, asymmetric pads, N tail
@@ -104,7 +104,7 @@ def test_cgemm_conv_matches_fp32(shape, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
 
 
-HALO_CFGS = list(range(48, 57))
+HALO_CFGS = list(range(48, 57)) + [80, 81, 82, 83, 85, 86, 87, 88]
 HALO_SHAPES = [
     # N, H, W, Cin, Cout, pads            (3x3 stride 1; ResNet-50 stages + edge cases)
     (2, 56, 56, 64, 64, (1, 1, 1, 1)),
