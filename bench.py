@@ -109,7 +109,12 @@ def parse():
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--transport", default="native", choices=["native", "grpc"])
     ap.add_argument("--batch-timeout-us", type=int, default=2000)
-    ap.add_argument("--distinct-requests", type=int, default=64, help="distinct pre-encoded request bodies")
+    ap.add_argument("--distinct-requests", type=int, default=4,
+                    help="distinct pre-encoded request bodies per rank.  The reference client encodes every "
+                         "request right before writing it (src/lib.rs:229-257), so the bytes it sends are "
+                         "cache-hot; 4 bodies (2.4 MB) stay in the LLC like that, where 64 (38.5 MB) added a "
+                         "DRAM read per call to the co-located load generator (53.1k / 53.7k vs 49.0k / "
+                         "51.3k RPC/s, profiles/round4/s7)")
     ap.add_argument("--lanes", type=int, default=4, help="GPU lanes (batch slots in flight) per rank")
     ap.add_argument("--model", default="resnet50",
                     choices=["resnet50", "resnet50-v2", "tiny", "bert-base", "multi"],
@@ -528,7 +533,8 @@ def main():
             f"Predict RPCs/sec + p50 latency, BERT-base seq={args.seq_len} dynamic batching on MI355X"
         model_label = {"resnet50": "ResNet-50 v1.5", "resnet50-v2": "ResNet-50 v2", "tiny": "tiny-transport-probe",
                        "bert-base": f"BERT-base seq {args.seq_len}"}[args.model]
-        data = ("synthetic 224x224x3 f32 images (float_val, batch-1 PredictRequests as the Rust client sends), "
+        data = ("synthetic 224x224x3 f32 images (float_val, batch-1 PredictRequests as the Rust client sends; "
+                f"{args.distinct_requests} distinct pre-encoded bodies per rank), "
                 f"random-init {'ResNet-50 v2' if args.model == 'resnet50-v2' else 'ResNet-50 v1.5'} weights") \
             if args.model != "bert-base" else \
             "synthetic int32 token ids / masks, random-init BERT-base weights"

@@ -38,10 +38,21 @@ def main():
     ap.add_argument("--layers", nargs="*", default=["s1_3x3", "s3_3x3", "s3_1x1_in"])
     ap.add_argument("--cfgs", nargs="*", default=["48:1", "51:1", "50:1", "42:1"],
                     help="tile config:split-K pairs (each is tried on every layer it supports)")
+    ap.add_argument("--gemm", nargs="*", default=[], help="dense GEMMs MxNxK (hip().linear) instead of conv layers")
     a = ap.parse_args()
     n = a.batch
     H = hip()
-    for name in a.layers:
+    for shape in a.gemm:
+        M, N, K = (int(v) for v in shape.split("x"))
+        xs = [torch.randn(M, K, device="cuda").to(BF) for _ in range(8)]
+        ws = [(torch.randn(N, K, device="cuda") * 0.05).to(BF) for _ in range(8)]
+        outs = [torch.empty(M, N, device="cuda", dtype=BF) for _ in range(8)]
+        b = torch.zeros(N, device="cuda")
+        for cs in a.cfgs:
+            cfg, sp = (int(x) for x in cs.split(":"))
+            report(f"gemm{shape}", cfg, sp,
+                   lambda j, cfg=cfg, sp=sp: H.linear(xs[j], ws[j], b, None, ACT["none"], cfg, False, 1.0, outs[j], sp))
+    for name in a.layers if not a.gemm else []:
         h, cin, cout, k, s, resid = LAYERS[name]
         pad = k // 2
         ho = (h + 2 * pad - k) // s + 1
@@ -53,56 +64,57 @@ def main():
         b = torch.zeros(cout, device="cuda")
         for cs in a.cfgs:
             cfg, sp = (int(x) for x in cs.split(":"))
+            report(name, cfg, sp, lambda j, cfg=cfg, sp=sp: H.conv2d(
+                xs[j], ws[j], b, rs[j], k, k, s, s, pad, pad, pad, pad, ACT["relu"], cfg, outs[j], False, sp))
 
-            def run(j):
-                H.conv2d(xs[j], ws[j], b, rs[j], k, k, s, s, pad, pad, pad, pad, ACT["relu"], cfg, outs[j], False, sp)
-            try:
-                for j in range(8):
-                    run(j)
-                torch.cuda.synchronize()
-            except RuntimeError as e:
-                print(json.dumps({"layer": name, "cfg": cfg, "splits": sp, "error": str(e)[:100]}), flush=True)
-                continue
-            # untraced event time of the same launch (copy 7 after 0..6)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            for j in range(7):
-                run(j)
-            e0.record()
-            run(7)
-            e1.record()
-            e1.synchronize()
-            ev_us = e0.elapsed_time(e1) * 1e3
-            tr = torch.zeros(1 << 20, 8, dtype=torch.int64, device="cuda")
-            for j in range(7):
-                run(j)
-            H.set_wg_trace(tr)
-            run(7)
-            H.set_wg_trace(None)
-            torch.cuda.synchronize()
-            t = tr.cpu()
-            used = t[:, 0] > 0
-            t = t[used]
-            nwg = int(t.shape[0])
-            t0 = int(t[:, 0].min())
-            st = ((t[:, 0] - t0).double() * TICK_US).tolist()
-            first = ((t[:, 1] - t[:, 0]).double() * TICK_US).tolist()
-            loop = ((t[:, 2] - t[:, 1]).double() * TICK_US).tolist()
-            epi = ((t[:, 3] - t[:, 2]).double() * TICK_US).tolist()
-            life = ((t[:, 3] - t[:, 0]).double() * TICK_US).tolist()
-            span = float((t[:, 3].max() - t0) * TICK_US)
-            cus = t[:, 7].tolist()
-            per_cu = {}
-            for c in cus:
-                per_cu[c] = per_cu.get(c, 0) + 1
-            print(json.dumps({
-                "layer": name, "cfg": cfg, "splits": sp, "workgroups": nwg, "event_us": round(ev_us, 2),
-                "span_us": round(span, 2), "cus": len(per_cu), "max_wg_per_cu": max(per_cu.values()),
-                "start_us": {"p50": round(q(st, .5), 2), "p90": round(q(st, .9), 2), "max": round(max(st), 2)},
-                "first_data_us": {"p50": round(q(first, .5), 2), "p90": round(q(first, .9), 2)},
-                "kloop_us": {"p50": round(q(loop, .5), 2), "p90": round(q(loop, .9), 2)},
-                "epilogue_us": {"p50": round(q(epi, .5), 2), "p90": round(q(epi, .9), 2)},
-                "wg_life_us": {"p50": round(q(life, .5), 2), "p90": round(q(life, .9), 2)},
-            }), flush=True)
+
+def report(name, cfg, sp, run):
+    H = hip()
+    try:
+        for j in range(8):
+            run(j)
+        torch.cuda.synchronize()
+    except RuntimeError as e:
+        print(json.dumps({"layer": name, "cfg": cfg, "splits": sp, "error": str(e)[:100]}), flush=True)
+        return
+    # untraced event time of the same launch (copy 7 after 0..6)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for j in range(7):
+        run(j)
+    e0.record()
+    run(7)
+    e1.record()
+    e1.synchronize()
+    ev_us = e0.elapsed_time(e1) * 1e3
+    tr = torch.zeros(1 << 20, 8, dtype=torch.int64, device="cuda")
+    for j in range(7):
+        run(j)
+    H.set_wg_trace(tr)
+    run(7)
+    H.set_wg_trace(None)
+    torch.cuda.synchronize()
+    t = tr.cpu()
+    t = t[t[:, 0] > 0]
+    nwg = int(t.shape[0])
+    t0 = int(t[:, 0].min())
+    st = ((t[:, 0] - t0).double() * TICK_US).tolist()
+    first = ((t[:, 1] - t[:, 0]).double() * TICK_US).tolist()
+    loop = ((t[:, 2] - t[:, 1]).double() * TICK_US).tolist()
+    epi = ((t[:, 3] - t[:, 2]).double() * TICK_US).tolist()
+    life = ((t[:, 3] - t[:, 0]).double() * TICK_US).tolist()
+    span = float((t[:, 3].max() - t0) * TICK_US)
+    per_cu = {}
+    for c in t[:, 7].tolist():
+        per_cu[c] = per_cu.get(c, 0) + 1
+    print(json.dumps({
+        "layer": name, "cfg": cfg, "splits": sp, "workgroups": nwg, "event_us": round(ev_us, 2),
+        "span_us": round(span, 2), "cus": len(per_cu), "max_wg_per_cu": max(per_cu.values()),
+        "start_us": {"p50": round(q(st, .5), 2), "p90": round(q(st, .9), 2), "max": round(max(st), 2)},
+        "first_data_us": {"p50": round(q(first, .5), 2), "p90": round(q(first, .9), 2)},
+        "kloop_us": {"p50": round(q(loop, .5), 2), "p90": round(q(loop, .9), 2)},
+        "epilogue_us": {"p50": round(q(epi, .5), 2), "p90": round(q(epi, .9), 2)},
+        "wg_life_us": {"p50": round(q(life, .5), 2), "p90": round(q(life, .9), 2)},
+    }), flush=True)
 
 
 if __name__ == "__main__":
