@@ -370,12 +370,18 @@ Tensor stem_pool(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t P
   TORCH_CHECK(PT >= 0 && PB >= 0 && PL >= 0 && PR >= 0 && PPT >= 0 && PPT <= 2 && PPL >= 0 && PPL <= 2 &&
               PPB >= 0 && PPR >= 0, "stem_pool: bad padding");
   TORCH_CHECK(w.device() == x.device() && bias.device() == x.device(), "stem_pool: tensors on different devices");
+  Tensor xin = x;
   if (xb16 && x.numel() % 2) {
     // the bf16 path reads whole aligned dwords: an odd element count's last
-    // pixel reads 2 B past the tensor, which must still lie in its storage
+    // pixel reads 2 B past the tensor, which must still lie in its storage;
+    // otherwise the kernel reads a copy with one element of padding (the
+    // serving path's ingest buffers are padded, so it never copies)
     const int64_t avail = int64_t(x.storage().nbytes()) - int64_t(x.storage_offset()) * 2;
-    TORCH_CHECK(avail >= x.numel() * 2 + 2, "stem_pool: a bf16 input with an odd element count needs 2 B of "
-                "storage past its end (pad the allocation)");
+    if (avail < x.numel() * 2 + 2 || !x.is_contiguous()) {
+      Tensor padded = torch::zeros({x.numel() + 1}, x.options());
+      padded.narrow(0, 0, x.numel()).copy_(x.reshape({-1}));
+      xin = padded.narrow(0, 0, x.numel()).view(x.sizes());
+    }
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), cout = w.size(0);
@@ -394,7 +400,7 @@ Tensor stem_pool(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t P
     sc = post_scale->data_ptr<float>();
     sh = post_shift->data_ptr<float>();
   }
-  check(tfsk::stem_pool_launch(x.data_ptr(), xb16, bf16p(w), int(w.size(1)), bias.data_ptr<float>(), bf16p_mut(y), N,
+  check(tfsk::stem_pool_launch(xin.data_ptr(), xb16, bf16p(w), int(w.size(1)), bias.data_ptr<float>(), bf16p_mut(y), N,
                                H, W, C, cout, int(PT), int(PL), Hc, Wc, int(PPT), int(PPL), Hp, Wp, int(act), sc, sh,
                                int(post_act), cur_stream(x)), "stem_pool");
   return y;
