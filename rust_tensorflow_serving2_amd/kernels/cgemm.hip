@@ -435,6 +435,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
       // raw (alpha-scaled) partial slab of this K slice; splitk_reduce applies the epilogue
       const float alpha = p.alpha;
       float* ws = p.ws + size_t(blockIdx.y) * M * N;
+      const __amdgpu_buffer_rsrc_t wsr = splitk_rsrc(p);
       constexpr int CPR = BN / 8;
       const bool v4 = (N % 4 == 0);
       for (int c = tid; c < RPP * CPR; c += G::NT) {
@@ -449,7 +450,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
           a.x *= alpha; a.y *= alpha; a.z *= alpha; a.w *= alpha;
           b.x *= alpha; b.y *= alpha; b.z *= alpha; b.w *= alpha;
           if (p.counters != nullptr) {
-            splitk_store8(dst, a, b);
+            splitk_store8(p, wsr, m, n, a, b);
           } else {
             *reinterpret_cast<float4*>(dst) = a;
             *reinterpret_cast<float4*>(dst + 4) = b;
@@ -460,14 +461,17 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
       }
       if constexpr (G::PASSES == 1) {
         if (p.counters != nullptr) {
-          if (!splitk_arrive(p, blockIdx.x)) return;
+          if (!splitk_arrive(p, blockIdx.x)) {
+            trace_stamp(p, 3);
+            return;
+          }
           // the last slice: every slab of the tile summed into Cs, then the epilogue
           for (int c = tid; c < RPP * CPR; c += G::NT) {
             const int row = c / CPR, col = (c - row * CPR) * 8;
             const int m = mp + row, n = n0 + col;
             if (m >= M || n >= N) continue;
             float4 lo, hi;
-            splitk_sum8(p, m, n, lo, hi);
+            splitk_sum8(p, wsr, m, n, lo, hi);
             *reinterpret_cast<float4*>(Cs + row * G::CS_LD + col) = lo;
             *reinterpret_cast<float4*>(Cs + row * G::CS_LD + col + 4) = hi;
           }
@@ -486,6 +490,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
             case kActTanh: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActTanh, false>(q, Cs, mp, n0, tid, r1, qb0, qb1); break;
             default: epilogue_rows<RPP, BN, G::NT, G::CS_LD, 0, false>(q, Cs, mp, n0, tid, r1, qb0, qb1); break;
           }
+          trace_stamp(p, 3);
           return;
         }
       }

@@ -127,10 +127,26 @@ __device__ __forceinline__ void prefetch_bias(const IGemmArgs& p, int n0, int ti
 // the whole L2 and its acquire invalidates it, which made the fixed-up layers
 // slower than a separate reduce launch (MI355X_MICROARCH.md 'handoff-flag':
 // write-through payload + drained vmcnt + flag).
-__device__ __forceinline__ void splitk_store8(float* dst, const float4 a, const float4 b) {
-  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-  for (int e = 0; e < 8; ++e) __hip_atomic_store(dst + e, v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// The split-K workspace (splits slabs of M x N fp32) as a buffer resource.
+// Slab stores and the last slice's slab loads are 16-B buffer accesses with
+// the sc1 cache policy (aux 16): agent-coherent, i.e. written through / read
+// past the XCD's own L2, which other XCDs' workgroups do not see -- the same
+// encoding `__hip_atomic_store/load(..., __HIP_MEMORY_SCOPE_AGENT)` gets, but
+// 16 B per lane instead of one dword (8x fewer instructions; the per-dword
+// form made a split tile's fixup epilogue 3-7 us, profiles/round4/s9).
+constexpr int kCpolAgent = 16;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t splitk_rsrc(const IGemmArgs& p) {
+  const long bytes = long(p.splits) * p.M * p.N * 4;
+  return __builtin_amdgcn_make_buffer_rsrc(p.ws, 0, int(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000);
+}
+
+// 8 fp32 partials of this slice (blockIdx.y) at (m, n), agent-coherent.
+__device__ __forceinline__ void splitk_store8(const IGemmArgs& p, __amdgpu_buffer_rsrc_t rs, int m, int n,
+                                              const float4 a, const float4 b) {
+  const uint32_t voff = (uint32_t(m) * uint32_t(p.N) + uint32_t(n)) * 4u;
+  const uint32_t soff = uint32_t(blockIdx.y) * uint32_t(p.M) * uint32_t(p.N) * 4u;
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), rs, voff, soff, kCpolAgent);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), rs, voff + 16u, soff, kCpolAgent);
 }
 
 __device__ __forceinline__ bool splitk_arrive(const IGemmArgs& p, int t) {
@@ -146,14 +162,20 @@ __device__ __forceinline__ bool splitk_arrive(const IGemmArgs& p, int t) {
   return s_last;
 }
 
-// Sum of the `splits` slabs for 8 columns at (m, n) (agent-scope loads).
-__device__ __forceinline__ void splitk_sum8(const IGemmArgs& p, int m, int n, float4& lo, float4& hi) {
+// Sum of the `splits` slabs for 8 columns at (m, n) (agent-coherent loads, all
+// slices issued before the first add).
+__device__ __forceinline__ void splitk_sum8(const IGemmArgs& p, __amdgpu_buffer_rsrc_t rs, int m, int n,
+                                            float4& lo, float4& hi) {
+  const uint32_t voff = (uint32_t(m) * uint32_t(p.N) + uint32_t(n)) * 4u;
+  const uint32_t slab = uint32_t(p.M) * uint32_t(p.N) * 4u;
   float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const size_t slab = size_t(p.M) * p.N;
-  float* src = p.ws + size_t(m) * p.N + n;
-  for (int s = 0; s < p.splits; ++s)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += __hip_atomic_load(src + s * slab + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int s = 0; s < p.splits; ++s) {
+    const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, s * slab, kCpolAgent));
+    const float4 b =
+        __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16u, s * slab, kCpolAgent));
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+    v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  }
   lo = make_float4(v[0], v[1], v[2], v[3]);
   hi = make_float4(v[4], v[5], v[6], v[7]);
 }

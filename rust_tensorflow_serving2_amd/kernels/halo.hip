@@ -100,6 +100,7 @@ __device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, const f32x4 (&
   if (p.splits > 1) {
     const float alpha = p.alpha;
     float* ws = p.ws + size_t(blockIdx.y) * p.M * p.N;
+    const __amdgpu_buffer_rsrc_t wsr = splitk_rsrc(p);
 #pragma unroll 1
     for (int it = 0; it < E::ITERS; ++it) {
       int row, col;
@@ -113,13 +114,16 @@ __device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, const f32x4 (&
       b.x *= alpha; b.y *= alpha; b.z *= alpha; b.w *= alpha;
       float* dst = ws + size_t(m) * p.N + n;
       if (p.counters != nullptr) {
-        splitk_store8(dst, a, b);
+        splitk_store8(p, wsr, m, n, a, b);
       } else {
         *reinterpret_cast<float4*>(dst) = a;
         *reinterpret_cast<float4*>(dst + 4) = b;
       }
     }
-    if (p.counters == nullptr || !splitk_arrive(p, blockIdx.x)) return;
+    if (p.counters == nullptr || !splitk_arrive(p, blockIdx.x)) {
+      trace_stamp(p, 3);
+      return;
+    }
     // the last slice of this tile: every slab summed back into Cs, then the
     // epilogue below with the bias the split path did not prefetch
 #pragma unroll 1
@@ -129,7 +133,7 @@ __device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, const f32x4 (&
       const int m = out_row(row), n = n0 + col;
       if (m < 0 || n >= p.N) continue;
       float4 lo, hi;
-      splitk_sum8(p, m, n, lo, hi);
+      splitk_sum8(p, wsr, m, n, lo, hi);
       *reinterpret_cast<float4*>(Cs + row * CS_LD + col) = lo;
       *reinterpret_cast<float4*>(Cs + row * CS_LD + col + 4) = hi;
     }

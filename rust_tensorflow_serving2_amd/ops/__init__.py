@@ -271,6 +271,11 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
                 # (Timing warm back-to-back bursts instead picked configs that
                 # lost in the graph, e.g. BERT FFN1 on 64x64 tiles.)
                 flush.zero_()
+                # keep the GPU busy while the host records the start event and
+                # issues the launch, so the sample is the kernel's own time, as
+                # in a graph replay, not the host's per-launch work (which is
+                # larger for split-K candidates: workspace, counter slice)
+                torch.cuda._sleep(_HOST_SHADOW_CYCLES)
                 start = torch.cuda.Event(enable_timing=True)
                 end = torch.cuda.Event(enable_timing=True)
                 start.record()
@@ -382,6 +387,9 @@ def capture_owner(graph):
 
 
 _FLUSH: Dict[int, torch.Tensor] = {}
+
+
+_HOST_SHADOW_CYCLES = 150_000      # ~60 us of GPU spin: longer than the host's launch path
 
 
 def _flush_buffer() -> torch.Tensor:

@@ -10,4 +10,5 @@ scripts/gpu_session.sh \
  "b_def1:200:python bench.py --steps 2000 --warmup 100 --ref-client-requests 0" \
  "b_wide1:300:TFSERVE_GRAPH_TUNE_TOP=12 TFSERVE_GRAPH_TUNE_RATIO=2.5 python bench.py --steps 2000 --warmup 100 --ref-client-requests 0" \
  "b_def2:200:python bench.py --steps 2000 --warmup 100 --ref-client-requests 0" \
- "b_wide2:300:TFSERVE_GRAPH_TUNE_TOP=12 TFSERVE_GRAPH_TUNE_RATIO=2.5 python bench.py --steps 2000 --warmup 100 --ref-client-requests 0"
+ "b_wide2:300:TFSERVE_GRAPH_TUNE_TOP=12 TFSERVE_GRAPH_TUNE_RATIO=2.5 python bench.py --steps 2000 --warmup 100 --ref-client-requests 0" \
+ "b1split:300:TFSERVE_SPLITK_FIXUP=1 python scripts/wg_trace.py --batch 1 --layers s2_3x3 s3_3x3 s3_1x1_in s4_3x3 s4_1x1_in --cfgs 51:1 51:2 51:4 36:1 36:2 36:4 54:1 54:4"

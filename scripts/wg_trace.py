@@ -95,6 +95,9 @@ def report(name, cfg, sp, run):
     torch.cuda.synchronize()
     t = tr.cpu()
     t = t[t[:, 0] > 0]
+    # split-K slices that are not their tile's last arriver leave after the
+    # slab store without the exit stamp: their exit = the end of their K loop
+    t[:, 3] = torch.where(t[:, 3] > 0, t[:, 3], t[:, 2])
     nwg = int(t.shape[0])
     t0 = int(t[:, 0].min())
     st = ((t[:, 0] - t0).double() * TICK_US).tolist()
