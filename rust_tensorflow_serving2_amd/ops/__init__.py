@@ -174,7 +174,7 @@ def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
 
 
 def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-               halo: bool = False, no_split: bool = False, n_multiple: bool = False):
+               halo: bool = False, no_split: bool = False):
     """(tile config, split-K) pairs worth timing for an M x N x K problem
     (``dma``: the operand mode uses the direct-to-LDS path, so the deeper
     DMA-ring configs apply; ``aligned64``: K and the conv channels are
@@ -208,8 +208,6 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
             continue   # mostly-empty tiles
         if bn % 64 and N % bn:
             continue   # 96-wide tiles: only where they divide N (BERT's 768 / 2304 / 3072)
-        if n_multiple and N % bn:
-            continue   # per-tile row statistics need whole tiles along N (LayerNorm folding)
         tiles = -(-M // bm) * -(-N // bn)
         for s in (1, 2, 4, 8, 16):
             if s > 1 and (no_split or nk // s < 2 or tiles >= 1024 or tiles * s > 4096):
@@ -233,7 +231,7 @@ def _ensure_cache() -> None:
 
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
                  dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-                 halo: bool = False, no_split: bool = False, n_multiple: bool = False) -> Tuple[int, int]:
+                 halo: bool = False, no_split: bool = False) -> Tuple[int, int]:
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
     heuristic is used)."""
@@ -260,7 +258,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
         best, best_t = None, float("inf")
         times = []
         flush = _flush_buffer()
-        cands = candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, n_multiple)
+        cands = candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split)
         for c, s in cands:
             launch(c, s)   # warm (also sets the kernel's LDS attribute)
             samples = []
