@@ -563,9 +563,10 @@ def test_maxpool_post_affine():
 ])
 def test_splitk_in_kernel_fixup_inside_graph(cfg, splits, shape, post, monkeypatch):
     """Captured in a HIP graph, split-K finishes in-kernel (the last slice of a
-    tile sums the slabs and runs the epilogue; no reduce launch).  Every replay
-    (the tile counters re-zero themselves) equals the eager result, which uses
-    the separate reduce kernel, and the fp32 reference."""
+    tile sums the slabs -- 16-B agent-coherent stores / loads -- and runs the
+    epilogue; no reduce launch).  Every replay (the tile counters re-zero
+    themselves) equals the eager result (the same fixup on a ring slice of
+    counters) and the fp32 reference."""
     monkeypatch.setenv("TFSERVE_SPLITK_FIXUP", "1")
     n, h, w, cin, cout, k, s, pads = shape
     x = rnd(n, h, w, cin, seed=61).to(BF)
