@@ -465,7 +465,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
             trace_stamp(p, 3);
             return;
           }
-          // the last slice: every slab of the tile summed into Cs, then the epilogue
+          // the last slice: every slab of the tile summed into Cs, then the
+          // epilogue (unrolled: every chunk's slab loads in flight together)
+#pragma unroll
           for (int c = tid; c < RPP * CPR; c += G::NT) {
             const int row = c / CPR, col = (c - row * CPR) * 8;
             const int m = mp + row, n = n0 + col;

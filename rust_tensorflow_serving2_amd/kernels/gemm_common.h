@@ -162,19 +162,31 @@ __device__ __forceinline__ bool splitk_arrive(const IGemmArgs& p, int t) {
   return s_last;
 }
 
-// Sum of the `splits` slabs for 8 columns at (m, n) (agent-coherent loads, all
-// slices issued before the first add).
+// Sum of the `splits` slabs for 8 columns at (m, n): agent-coherent loads,
+// four slices per round all in flight at once (slices past `splits` read
+// past the descriptor's records: zeros).  A rolled one-slice-per-trip loop
+// paid a full memory-side round trip per slice: the last arriver's epilogue
+// took ~5 us at 4 slices (profiles/round4/s10).
 __device__ __forceinline__ void splitk_sum8(const IGemmArgs& p, __amdgpu_buffer_rsrc_t rs, int m, int n,
                                             float4& lo, float4& hi) {
+  constexpr int NS = 4;
   const uint32_t voff = (uint32_t(m) * uint32_t(p.N) + uint32_t(n)) * 4u;
   const uint32_t slab = uint32_t(p.M) * uint32_t(p.N) * 4u;
   float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < p.splits; ++s) {
-    const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, s * slab, kCpolAgent));
-    const float4 b =
-        __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16u, s * slab, kCpolAgent));
-    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
-    v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  for (int s0 = 0; s0 < p.splits; s0 += NS) {
+    u32x4 a[NS], b[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const uint32_t soff = uint32_t(min(s0 + j, p.splits)) * slab;
+      a[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, kCpolAgent);
+      b[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16u, soff, kCpolAgent);
+    }
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const float4 x = __builtin_bit_cast(float4, a[j]), y = __builtin_bit_cast(float4, b[j]);
+      v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
+      v[4] += y.x; v[5] += y.y; v[6] += y.z; v[7] += y.w;
+    }
   }
   lo = make_float4(v[0], v[1], v[2], v[3]);
   hi = make_float4(v[4], v[5], v[6], v[7]);

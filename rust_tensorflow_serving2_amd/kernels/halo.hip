@@ -31,6 +31,7 @@
 //     the workgroups sharing one halo run on one XCD (shared L2);
 //   * split-K over channel chunks (gridDim.y), partial slabs indexed by the
 //     output pixel row, reduced by splitk_reduce like every other GEMM.
+#include <algorithm>
 #include <type_traits>
 
 #include "gemm_common.h"
@@ -75,6 +76,7 @@ __device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, const f32x4 (&
                                               float4 bias1) {
   constexpr int CS_LD = BN + 4;
   const int TH = p.TH, TW = p.TW, Ho = p.Ho, Wo = p.Wo;
+  const int TI = p.TI > 1 ? p.TI : 1, nimg = p.M / (Ho * Wo);
   const int lane = tid & 63, fr = lane & 15, fq = lane >> 4;
   // ---- epilogue: fp32 tile staged in LDS; row = output pixel of the block
   float* Cs = reinterpret_cast<float*>(smem);
@@ -88,11 +90,12 @@ __device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, const f32x4 (&
   __syncthreads();
 
   auto out_row = [&](int row) -> int {   // global GEMM row of tile row `row`, or -1
-    if (row >= TH * TW) return -1;
-    const int ph = row / TW, pw = row - ph * TW;
+    if (row >= TI * TH * TW) return -1;
+    const int ii = row / (TH * TW), r2 = row - ii * (TH * TW);
+    const int ph = r2 / TW, pw = r2 - ph * TW;
     const int h = h0 + ph, w = w0 + pw;
-    if (h >= Ho || w >= Wo) return -1;
-    return (img * Ho + h) * Wo + w;
+    if (h >= Ho || w >= Wo || img + ii >= nimg) return -1;
+    return ((img + ii) * Ho + h) * Wo + w;
   };
 
   using E = Epi<BM, BN, NT>;
@@ -126,7 +129,8 @@ __device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, const f32x4 (&
     }
     // the last slice of this tile: every slab summed back into Cs, then the
     // epilogue below with the bias the split path did not prefetch
-#pragma unroll 1
+    // (unrolled: every chunk's slab loads in flight together)
+#pragma unroll
     for (int it = 0; it < E::ITERS; ++it) {
       int row, col;
       if (!epi_rowcol<BM, BN, NT>(tid, it, row, col)) continue;
@@ -176,6 +180,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
   const int Ho = p.Ho, Wo = p.Wo, H = p.H, W = p.W, C = p.C;
   const int tph = (Ho + TH - 1) / TH, tpw = (Wo + TW - 1) / TW;
   const int nbn = (p.N + BN - 1) / BN;
+  const int TI = p.TI > 1 ? p.TI : 1, nimg = p.M / (Ho * Wo);
+  const int HB = (TH + 2) * HW2;                  // halo rows of one image's block
 
   // ---- tile of this workgroup: (image, tile row, tile col, channel slice)
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -184,7 +190,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
   const int tw = r_ % tpw;
   r_ /= tpw;
   const int th = r_ % tph;
-  const int img = r_ / tph;
+  const int img = (r_ / tph) * TI;                // first image of the tile
   const int h0 = th * TH, w0 = tw * TW, n0 = bn * BN;
 
   trace_stamp(p, 0);
@@ -199,17 +205,20 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.b), 0, int(p.b_bytes), 0x00020000);
 
-  // ---- per-lane halo DMA offsets: halo row r = pixel (h0 - PT + r / HW2, w0 - PL + r % HW2)
-  const int hrows = (TH + 2) * HW2;
-  const float inv_hw2 = 1.f / float(HW2);
+  // ---- per-lane halo DMA offsets: halo row r = image ii = r / HB of the tile,
+  // pixel (h0 - PT + q / HW2, w0 - PL + q % HW2) with q = r % HB
+  const int hrows = TI * HB;
+  const float inv_hw2 = 1.f / float(HW2), inv_hb = 1.f / float(HB);
   uint32_t h_off[G::HPW];
 #pragma unroll
   for (int j = 0; j < G::HPW; ++j) {
     const int r = (wid * G::HPW + j) * 8 + prow;
-    const int rr = fdiv(r, HW2, inv_hw2);
-    const int hh = h0 - p.PT + rr, ww = w0 - p.PL + (r - rr * HW2);
-    const bool ok = r < hrows && unsigned(hh) < unsigned(H) && unsigned(ww) < unsigned(W);
-    h_off[j] = ok ? (uint32_t((img * H + hh) * W + ww) * uint32_t(C) + kc) * 2u : kOOB;
+    const int ii = TI > 1 ? fdiv(r, HB, inv_hb) : 0;
+    const int q = r - ii * HB;
+    const int rr = fdiv(q, HW2, inv_hw2);
+    const int hh = h0 - p.PT + rr, ww = w0 - p.PL + (q - rr * HW2);
+    const bool ok = r < hrows && img + ii < nimg && unsigned(hh) < unsigned(H) && unsigned(ww) < unsigned(W);
+    h_off[j] = ok ? (uint32_t(((img + ii) * H + hh) * W + ww) * uint32_t(C) + kc) * 2u : kOOB;
   }
   uint32_t b_off[G::BPW];
 #pragma unroll
@@ -254,8 +263,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
 #pragma unroll
   for (int i = 0; i < G::TM; ++i) {
     const int px = wm * G::WM + i * 16 + fr;
-    const int ph = px / TW;
-    hrow0[i] = px < TH * TW ? ph * HW2 + (px - ph * TW) : 0;
+    const int ii = px / (TH * TW), p2 = px - ii * (TH * TW);
+    const int ph = p2 / TW;
+    hrow0[i] = px < TI * TH * TW ? ii * HB + ph * HW2 + (p2 - ph * TW) : 0;
   }
   const uint32_t rb0 = uint32_t(((wn * G::WN + fr) * KT + ((fq ^ (fr & 7)) * 8)) * 2);
   const uint32_t rb1 = uint32_t(((wn * G::WN + fr) * KT + (((4 + fq) ^ (fr & 7)) * 8)) * 2);
@@ -392,17 +402,31 @@ bool pick_block(int Ho, int Wo, int BM, int HR, int& TH, int& TW) {
   return best_tiles > 0;
 }
 
+// Whole images per tile when one image's output block and halo fit BM / HR
+// several times (7x7 and 14x14 maps): the tile's weight stream then serves TI
+// images, cutting the layer's weight traffic (= M-tiles x weights) by TI; the
+// launcher's split-K restores the workgroup count.  1 otherwise.
+int pick_images(const IGemmArgs& a, int BM, int HR) {
+  if (a.TH != a.Ho || a.TW != a.Wo) return 1;
+  const int nimg = a.M / (a.Ho * a.Wo);
+  int ti = std::min(BM / (a.Ho * a.Wo), HR / ((a.Ho + 2) * (a.Wo + 2)));
+  ti = std::min(ti, nimg);
+  return ti > 1 ? ti : 1;
+}
+
 template <int BM, int BN, int WGM, int WGN, int HR, int S, bool PF = false>
 hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
   using G = HG<BM, BN, WGM, WGN, HR, S>;
   IGemmArgs a = a0;
   if (!pick_block(a.Ho, a.Wo, BM, HR, a.TH, a.TW)) return hipErrorInvalidValue;
+  a.TI = pick_images(a, BM, HR);
   const int nch = a.C / KT;
   const int splits = a.splits > 1 ? a.splits : 1;
   if (splits > 1 && a.kt_per_split <= 0) return hipErrorInvalidValue;
   const int per = splits > 1 ? a.kt_per_split : nch;
   const int nimg = a.M / (a.Ho * a.Wo);
-  const long tiles = long(nimg) * ((a.Ho + a.TH - 1) / a.TH) * ((a.Wo + a.TW - 1) / a.TW) * ((a.N + BN - 1) / BN);
+  const long tiles = long((nimg + a.TI - 1) / a.TI) * ((a.Ho + a.TH - 1) / a.TH) * ((a.Wo + a.TW - 1) / a.TW) *
+                     ((a.N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
   if (tiles >= (1L << 31)) return hipErrorInvalidValue;
   const int lds = G::lds(per > 1 ? 2 : 1);
@@ -432,7 +456,9 @@ long halo_tiles(const IGemmArgs& a0, int cfg) {
   if (c < 0) return 0;
   if (!pick_block(a.Ho, a.Wo, kHBM[c], kHHR[c], a.TH, a.TW)) return 0;
   const int nimg = a.M / (a.Ho * a.Wo);
-  return long(nimg) * ((a.Ho + a.TH - 1) / a.TH) * ((a.Wo + a.TW - 1) / a.TW) * ((a.N + kHBN[c] - 1) / kHBN[c]);
+  const int ti = pick_images(a, kHBM[c], kHHR[c]);
+  return long((nimg + ti - 1) / ti) * ((a.Ho + a.TH - 1) / a.TH) * ((a.Wo + a.TW - 1) / a.TW) *
+         ((a.N + kHBN[c] - 1) / kHBN[c]);
 }
 
 bool halo_supported(const IGemmArgs& a) {

@@ -42,8 +42,10 @@ struct IGemmArgs {
   const void* a2;
   int64_t a2_bytes;
   int K1;
-  // halo conv (halo.hip): output pixel block per workgroup (set by the launcher)
-  int TH, TW;
+  // halo conv (halo.hip): output pixel block per workgroup (set by the launcher);
+  // TI > 1: the block is TI whole images (small feature maps: fewer M-tiles,
+  // so each weight byte a workgroup streams serves TI images)
+  int TH, TW, TI;
   // post-activation output (cgemm / halo / split-K reduce): out2 = act2(v *
   // scale2 + shift2) per output channel, v = the epilogue value stored to
   // `out` — a ResNet v2 block's sum and the next block's pre-activation

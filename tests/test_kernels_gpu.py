@@ -114,6 +114,8 @@ HALO_SHAPES = [
     (1, 13, 17, 192, 72, (1, 1, 1, 1)),    # odd image, 3 chunks, N tail (72 % BN != 0)
     (2, 9, 11, 64, 136, (0, 0, 0, 0)),     # VALID (no padding)
     (1, 5, 6, 128, 64, (2, 0, 1, 1)),      # asymmetric top pad
+    (5, 7, 7, 128, 64, (1, 1, 1, 1)),      # whole-image tiles: up to 3 images per tile, last tile partial
+    (4, 6, 5, 64, 72, (0, 2, 1, 1)),       # whole-image tiles with asymmetric pads
 ]
 
 
