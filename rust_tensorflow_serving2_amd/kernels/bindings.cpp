@@ -41,13 +41,20 @@ hipError_t launch_any(const tfsk::IGemmArgs& a, int a_mode, int64_t cfg, hipStre
   return is_cgemm_cfg(cfg) ? tfsk::cgemm_launch(a, a_mode, int(cfg), st) : tfsk::igemm_launch(a, a_mode, int(cfg), st);
 }
 
-// TFSERVE_SPLITK_FIXUP=1: inside HIP-graph captures, finish split-K in-kernel
-// (no reduce launch).  Off by default: on ResNet-50 it measured neutral (b1
-// 0.391 vs 0.385 ms, b32 0.865 vs 0.873 ms on one box) -- the last slice's
-// slab reads cost about what the reduce launch did.
-bool split_fixup_enabled() {
+// Split-K finishing in-kernel (the last slice of a tile sums the slabs and
+// runs the epilogue; no reduce launch).  TFSERVE_SPLITK_FIXUP: "1" always,
+// "0" never, unset / "auto": launches of fewer than kFixupAutoTiles tiles,
+// i.e. the small-batch layers whose few workgroups each run a long K loop
+// (b1: 0.377-0.380 vs 0.394-0.395 ms per replay with it on, b32: 0.792-0.799
+// vs 0.770-0.786 ms when every layer may use it: there the write-through slab
+// traffic of large tiles costs more than the reduce launch,
+// profiles/round4/s11).
+constexpr long kFixupAutoTiles = 128;
+int split_fixup_mode() {
   const char* v = std::getenv("TFSERVE_SPLITK_FIXUP");
-  return v && v[0] == '1';
+  if (v && v[0] == '1') return 1;
+  if (v && v[0] == '0') return 0;
+  return 2;
 }
 
 // scripts/wg_trace.py: per-workgroup phase stamps of the next GEMM / conv
@@ -80,14 +87,14 @@ void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, cons
   a.splits = int(splits);
   a.kt_per_split = per;
   a.ws = ws.data_ptr<float>();
-  // With TFSERVE_SPLITK_FIXUP=1 (opt-in, see split_fixup_enabled) cgemm /
+  // With the fixup on (split_fixup_mode: launches under kFixupAutoTiles tiles by default) cgemm /
   // halo finish split-K in-kernel (the last slice of each tile reduces): one
   // launch instead of two; eager launches (autotuning) then use the fixup too,
   // so the tuner times the split-K candidates as the graph runs them.
   // Otherwise, or when no counters are left, a separate reduce launch.
   a.counters = nullptr;
-  if (split_fixup_enabled() && a.N % 8 == 0 && ((is_cgemm_cfg(cfg) && tfsk::cgemm_fixup_ok(int(cfg))) || is_halo_cfg(cfg))) {
-    tfsk::splitk_counters_prepare(st);
+  const int fixup = split_fixup_mode();
+  if (fixup != 0 && a.N % 8 == 0 && ((is_cgemm_cfg(cfg) && tfsk::cgemm_fixup_ok(int(cfg))) || is_halo_cfg(cfg))) {
     long tiles = 0;
     if (is_halo_cfg(cfg)) {
       tiles = tfsk::halo_tiles(a, int(cfg));
@@ -95,7 +102,10 @@ void run_igemm(tfsk::IGemmArgs& a, int a_mode, int64_t cfg, int64_t splits, cons
       const int bm = tfsk::cgemm_config_bm(int(cfg)), bn = tfsk::cgemm_config_bn(int(cfg));
       tiles = long((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
     }
-    if (tiles > 0 && tiles < (1L << 24)) a.counters = tfsk::splitk_counters(int(tiles), st);
+    if (tiles > 0 && tiles < (1L << 24) && (fixup == 1 || tiles < kFixupAutoTiles)) {
+      tfsk::splitk_counters_prepare(st);
+      a.counters = tfsk::splitk_counters(int(tiles), st);
+    }
   }
   TORCH_CHECK(launch_any(a, a_mode, cfg, st) == hipSuccess, "conv/GEMM (split-K) launch failed");
   if (a.counters == nullptr)

@@ -13,7 +13,7 @@ namespace tfsk {
 
 namespace {
 constexpr int kPoolInts = 1 << 22;   // 16 MB per device
-// Used by the split-K fixup (TFSERVE_SPLITK_FIXUP=1, opt-in).
+// Used by the split-K fixup (bindings.cpp split_fixup_mode: small launches by default).
 // [0, kCapInts): slices for launches captured into HIP graphs (a graph node
 // keeps its counters for the graph's lifetime).  A capture made under an
 // owner token (splitk_counters_set_owner, set by the Python runtime around

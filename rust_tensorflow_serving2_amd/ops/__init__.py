@@ -367,7 +367,7 @@ _OWNER_SEQ = itertools.count(1)
 @contextlib.contextmanager
 def capture_owner(graph):
     """Around a HIP-graph capture: the split-K arrival counters its launches
-    take (TFSERVE_SPLITK_FIXUP=1) belong to ``graph`` and go back to the pool
+    take (the split-K fixup) belong to ``graph`` and go back to the pool
     when the graph object is collected, so tuning candidates and reload
     cycles do not use the counter pool up (kernels/counters.cpp)."""
     try:
