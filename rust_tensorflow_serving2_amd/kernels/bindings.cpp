@@ -43,17 +43,20 @@ hipError_t launch_any(const tfsk::IGemmArgs& a, int a_mode, int64_t cfg, hipStre
 
 // Split-K finishing in-kernel (the last slice of a tile sums the slabs and
 // runs the epilogue; no reduce launch).  TFSERVE_SPLITK_FIXUP: "1" always,
-// "0" never, unset / "auto": launches of fewer than kFixupAutoTiles tiles,
-// i.e. the small-batch layers whose few workgroups each run a long K loop
-// (b1: 0.377-0.380 vs 0.394-0.395 ms per replay with it on, b32: 0.792-0.799
-// vs 0.770-0.786 ms when every layer may use it: there the write-through slab
-// traffic of large tiles costs more than the reduce launch,
-// profiles/round4/s11).
+// "0" never.  Otherwise the serving runtime decides per batch bucket while it
+// tunes and captures (set_splitk_fixup: on for the small buckets, whose few
+// workgroups each run a long K loop -- b1 0.371-0.374 vs 0.391-0.394 ms per
+// replay -- off for the large ones, where the write-through slab traffic cost
+// more than the reduce launch when every small launch used it: b32 0.816-0.824 vs 0.780-0.786 ms; per bucket: 0.771-0.773 vs 0.781-0.794,
+// profiles/round4/s13), and outside that launches of fewer than
+// kFixupAutoTiles tiles use it.
 constexpr long kFixupAutoTiles = 128;
+int g_fixup_override = -1;
 int split_fixup_mode() {
   const char* v = std::getenv("TFSERVE_SPLITK_FIXUP");
   if (v && v[0] == '1') return 1;
   if (v && v[0] == '0') return 0;
+  if (g_fixup_override >= 0) return g_fixup_override;
   return 2;
 }
 
@@ -736,6 +739,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     g_trace = reinterpret_cast<long long*>(t->data_ptr<int64_t>());
     g_trace_cap = int(std::min<int64_t>(t->numel() / 8, 1 << 30));
   }, "per-workgroup wall-clock stamps of the following GEMM / conv launches (None: off)");
+  m.def("set_splitk_fixup", [](int64_t mode) { g_fixup_override = mode < 0 ? -1 : (mode ? 1 : 0); },
+        "in-kernel split-K for the following launches: 1 on, 0 off, -1 default (env, else small launches)");
   m.def("num_configs", []() { return tfsk::kNumIGemmConfigs; });
   m.def("cgemm_configs", []() {
     std::vector<int> v;

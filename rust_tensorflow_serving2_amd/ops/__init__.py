@@ -361,6 +361,26 @@ def graph_tune(keys: Dict[Tuple, int], time_fn: Callable[[], float], top: int = 
     return changed
 
 
+FIXUP_MAX_BUCKET = 8     # batch buckets up to this finish split-K in-kernel
+
+
+@contextlib.contextmanager
+def splitk_fixup_for_bucket(bucket: int):
+    """Around a bucket's tuning + capture: in-kernel split-K (no reduce launch)
+    for the small buckets, the separate reduce for the large ones (see
+    kernels/bindings.cpp split_fixup_mode for the measurements)."""
+    try:
+        h = hip()
+    except KernelsUnavailable:
+        yield
+        return
+    h.set_splitk_fixup(1 if bucket <= FIXUP_MAX_BUCKET else 0)
+    try:
+        yield
+    finally:
+        h.set_splitk_fixup(-1)
+
+
 _OWNER_SEQ = itertools.count(1)
 
 

@@ -199,7 +199,8 @@ class GpuRunner:
         return lane
 
     def _capture(self, lane: _Lane, b: int) -> None:
-        with CAPTURE_LOCK:
+        from .. import ops
+        with CAPTURE_LOCK, ops.splitk_fixup_for_bucket(b):
             self._capture_locked(lane, b)
 
     def _capture_locked(self, lane: _Lane, b: int) -> None:
