@@ -4,10 +4,11 @@
 # via the headline bench.
 set -o pipefail
 export TMPDIR=/tmp
-D=gpurun_out/r4l
+D=gpurun_out/${CHECK_DIR:-r4l}
 mkdir -p $D
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/gpu_suite.log 2>&1 &&
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $D/driver20.log 2>&1 &&
 timeout -k 10 300 python -u scripts/bench_engine.py --model resnet50 --batch 1 32 > $D/engine.log 2>&1 &&
 timeout -k 10 300 python -u scripts/bench_engine.py --model resnet50 --batch 1 32 > $D/engine2.log 2>&1 &&
 timeout -k 10 300 python -u bench.py --steps 2000 --warmup 100 > $D/bench2000.log 2>&1 &&
@@ -16,5 +17,5 @@ python scripts/replay_kernels.py $(find /tmp/prof_kt1 -name '*.db' | head -1) --
 rc=$?
 rm -rf /tmp/prof_kt1
 tail -3 $D/gpu_suite.log
-grep -h '^{' $D/engine.log $D/engine2.log $D/bench2000.log | cut -c1-220
+grep -h '^{' $D/driver20.log $D/engine.log $D/engine2.log $D/bench2000.log | cut -c1-220
 exit $rc
