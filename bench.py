@@ -129,7 +129,7 @@ def parse():
     ap.add_argument("--c1-requests", type=int, default=200,
                     help="after the timed window: batch-1 round trips at concurrency 1 over one connection "
                          "(reported as p50_c1_ms; 0 = skip)")
-    ap.add_argument("--ref-client-requests", type=int, default=6000,
+    ap.add_argument("--ref-client-requests", type=int, default=20000,
                     help="after the timed window: rank 0 drives this many Predicts over 2 HTTP/2 connections "
                          "(the reference client's channel pattern, src/lib.rs:132-138) with min(concurrency, 128) "
                          "x N calls in flight while every rank serves; reported as ref_client_rps + the share each "
