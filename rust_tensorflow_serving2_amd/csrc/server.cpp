@@ -247,7 +247,7 @@ class NativeLane {
       rx.push("tfs.gpu_wait");
     }
     const size_t bi = size_t(b - buckets_.data());
-    if (!e) e = wait(rt, done, t_issue, deadline_from(Clock::now()), ema_us_[bi]);
+    if (!e) e = wait(rt, done, t_issue, deadline_from(Clock::now()), ema_us_[bi], b->rows <= kSpinTailRows);
     if (!e) {
       const double us = std::chrono::duration<double, std::micro>(Clock::now() - t_issue).count();
       ema_us_[bi] = ema_us_[bi] <= 0 ? us : 0.8 * ema_us_[bi] + 0.2 * us;
@@ -263,9 +263,15 @@ class NativeLane {
   // ONE nap for most of this bucket's expected issue->done time (a running
   // average), then polls every ~8 us.  The lane thread runs with 1-us timer
   // slack, so a nap ends when asked (the default 50-us slack made each 40-us
-  // nap ~90 us, which a batch-1 request paid in full).  Gives up after
+  // nap ~90 us, which a batch-1 request paid in full).  Small buckets
+  // (`spin_tail`: the latency-bound, low-load regime -- a batch-1 request
+  // waits on nothing else) poll the last quarter with yields only, so the
+  // completion is seen within ~1 us instead of up to one 8-us nap; the large
+  // buckets of the throughput regime keep napping.  Gives up after
   // `deadline` (a hung kernel or wedged stream): returns kLaneHung.
-  static int wait(HipRt& rt, void* ev, Clock::time_point t_issue, Clock::time_point deadline, double expect_us) {
+  static constexpr int kSpinTailRows = 4;
+  static int wait(HipRt& rt, void* ev, Clock::time_point t_issue, Clock::time_point deadline, double expect_us,
+                  bool spin_tail) {
     if (expect_us > 60.0) {
       const auto wake = t_issue + std::chrono::microseconds(int64_t(0.75 * expect_us));
       if (Clock::now() < wake && rt.event_query(ev) == kHipErrorNotReady) std::this_thread::sleep_until(wake);
@@ -273,7 +279,8 @@ class NativeLane {
     for (int i = 0;; ++i) {
       const int e = rt.event_query(ev);
       if (e != kHipErrorNotReady) return e;
-      if (i < 8) {
+      if (i < 8 || (spin_tail && i < (1 << 20))) {
+        if (spin_tail && (i & 1023) == 1023 && Clock::now() > deadline) return kLaneHung;
         std::this_thread::yield();
       } else {
         if ((i & 63) == 0 && Clock::now() > deadline) return kLaneHung;
