@@ -5,6 +5,7 @@
 // pre-allocated outputs via the `out=` forms), and validates shapes on the host
 // before anything touches the GPU.
 #include <cstdlib>
+#include <algorithm>
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -512,9 +513,19 @@ std::vector<Tensor> classifier_head(const Tensor& x, const Tensor& w, const Tens
   Tensor part = torch::empty({int64_t(tfsk::classifier_head_ws_floats(M, K, Np))}, x.options().dtype(at::kFloat));
   Tensor probs = torch::empty({M, n}, x.options().dtype(at::kFloat));
   Tensor classes = torch::empty({M}, x.options().dtype(at::kLong));
+  // small batches: one launch that hands off through an arrival counter (its
+  // last workgroup runs the softmax rows serially, so only up to
+  // TFSERVE_HEAD_FUSED rows, default 4, at most 16; 0 keeps three launches)
+  int* counter = nullptr;
+  const char* hf = std::getenv("TFSERVE_HEAD_FUSED");
+  const int fused_max = hf && hf[0] ? std::min(16, std::atoi(hf)) : 4;
+  if (M <= fused_max) {
+    tfsk::splitk_counters_prepare(cur_stream(x));
+    counter = tfsk::splitk_counters(1, cur_stream(x));
+  }
   check(tfsk::classifier_head_launch(bf16p(x), bf16p(w), bias.data_ptr<float>(), part.data_ptr<float>(),
                                      probs.data_ptr<float>(), classes.data_ptr<int64_t>(), M, HW, K, Np, int(n),
-                                     cur_stream(x)),
+                                     cur_stream(x), counter),
         "classifier_head");
   return {probs, classes};
 }

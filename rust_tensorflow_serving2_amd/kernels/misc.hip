@@ -786,13 +786,209 @@ hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, 
   return hipGetLastError();
 }
 
+// Small-batch head (M <= 16 rows, HW <= 64 positions) in ONE launch instead
+// of gap_rows + fc_partial + softmax_argmax (three ~5-us launches at b1):
+//   * each fc workgroup (K slice, 32 columns) pools its own K slice first:
+//     (row, 8-channel chunk, position quarter) per thread, every position's
+//     load in flight, the quarters met in LDS -> bf16 pooled slice in LDS
+//     (the same bf16 rounding as gap_rows);
+//   * the fc partial as fc_partial_kernel, A fragments from that LDS slice;
+//   * partials stored agent-coherent (sc1: visible to the other XCDs), then
+//     one arrival count per workgroup; the LAST workgroup to arrive sums the
+//     KS partials + bias per logit and runs softmax / argmax for the M rows
+//     (the split-K fixup's hand-off, kernels/gemm_common.h), and re-zeroes
+//     the counter for the next launch.
+constexpr int kHeadSmallM = 16, kHeadSmallHW = 64;
+template <int KSTEPS>
+__global__ __launch_bounds__(256) void head_small_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                         const float* __restrict__ bias, float* __restrict__ part,
+                                                         float* __restrict__ probs, int64_t* __restrict__ classes,
+                                                         int* __restrict__ counter, int M, int HW, int K, int Np,
+                                                         int N, float inv_hw) {
+  constexpr int KSLICE = KSTEPS * 32 * 4;            // channels per workgroup (4 waves)
+  __shared__ __attribute__((aligned(16))) uint16_t pooled[kHeadSmallM][KSLICE];
+  __shared__ float quarter[4][64][9];
+  __shared__ float red[3][16][33];
+  __shared__ int s_last;
+  __shared__ float smx[4], ssum[4];
+  __shared__ int sarg[4];
+  const int ks = blockIdx.x, ns = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int kbase = ks * KSLICE;
+  // weights (B fragments of this wave's K range) and the bias (used by
+  // whichever workgroup arrives last) are issued first: their round trips
+  // overlap the pooling's instead of following it
+  const int kw = KSLICE / 4, kl = wid * kw;       // this wave's offset in the slice
+  const int n0 = ns * kHeadCols;
+  bf16x8 bfr[KSTEPS][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + j * 16 + fr;
+#pragma unroll
+    for (int t = 0; t < KSTEPS; ++t)
+      bfr[t][j] = n < Np ? *reinterpret_cast<const bf16x8*>(w + long(n) * K + kbase + kl + t * 32 + fq * 8)
+                         : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  float bv[kSmPer];
+#pragma unroll
+  for (int k = 0; k < kSmPer; ++k) {
+    const int c = k * 256 + tid;
+    bv[k] = bias[c < N ? c : N - 1];
+  }
+  // ---- pool this K slice: thread = (chunk of 8 channels, position quarter)
+  constexpr int CHUNKS = KSLICE / 8;                // <= 64 at K = 2048
+  static_assert(CHUNKS <= 64, "one chunk per lane of a quarter");
+  const int ch = tid & 63, qtr = tid >> 6;
+  for (int m = 0; m < M; ++m) {
+    float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ch < CHUNKS) {
+      const uint16_t* px = x + (long(m) * HW) * K + kbase + ch * 8;
+      uint4 v[kHeadSmallHW / 4];
+#pragma unroll
+      for (int j = 0; j < kHeadSmallHW / 4; ++j) {   // positions qtr, qtr + 4, ...: clamped, masked below
+        const int hw = qtr + 4 * j;
+        v[j] = *reinterpret_cast<const uint4*>(px + long(hw < HW ? hw : HW - 1) * K);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < kHeadSmallHW / 4; ++j) {
+        if (qtr + 4 * j >= HW) continue;
+        float f[8];
+        unpack8(v[j], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s8[e] += f[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) quarter[qtr][ch][e] = s8[e];
+    __syncthreads();
+    if (tid < CHUNKS * 8 / 8) {
+      // thread tid: chunk tid, its 8 channels -> bf16 pooled row m
+      uint32_t o[4];
+#pragma unroll
+      for (int e2 = 0; e2 < 4; ++e2) {
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a0 += quarter[q][tid][2 * e2];
+          a1 += quarter[q][tid][2 * e2 + 1];
+        }
+        o[e2] = uint32_t(f32_to_bf16(a0 * inv_hw)) | (uint32_t(f32_to_bf16(a1 * inv_hw)) << 16);
+      }
+      *reinterpret_cast<uint4*>(&pooled[m][tid * 8]) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();
+  }
+  // ---- fc partial of this slice (B fragments and bias already in registers)
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int t = 0; t < KSTEPS; ++t) {
+    const bf16x8 a = fr < M ? *reinterpret_cast<const bf16x8*>(&pooled[fr][kl + t * 32 + fq * 8])
+                            : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[t][j], acc[j], 0, 0, 0);
+  }
+  if (wid > 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wid - 1][fq * 4 + r][j * 16 + fr] = acc[j][r];
+  }
+  __syncthreads();
+  if (wid == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = fq * 4 + r, cc = j * 16 + fr, n = n0 + cc;
+        if (rr < M && n < Np)
+          __hip_atomic_store(part + (long(ks) * M + rr) * Np + n,
+                             acc[j][r] + red[0][rr][cc] + red[1][rr][cc] + red[2][rr][cc], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+  }
+  // ---- arrival; the last workgroup finishes the head
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0) {
+    const int total = gridDim.x * gridDim.y;
+    const int old = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == total - 1;
+    if (s_last) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  for (int m = 0; m < M; ++m) {
+    float v[kSmPer];
+    float mx = -INFINITY;
+    int arg = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+      const int c = k * 256 + tid, cc = c < N ? c : N - 1;
+      float a = bv[k];
+#pragma unroll
+      for (int q = 0; q < kHeadKS; ++q)
+        a += __hip_atomic_load(part + (long(q) * M + m) * Np + cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v[k] = c < N ? a : -INFINITY;
+      if (c < N && (a > mx || (a == mx && c < arg))) { mx = a; arg = c; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(mx, o, 64);
+      const int oa = __shfl_xor(arg, o, 64);
+      if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+    }
+    if (lane == 0) { smx[wid] = mx; sarg[wid] = arg; }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float om = smx[k];
+      const int oa = sarg[k];
+      if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+      v[k] = (k * 256 + tid < N) ? __expf(v[k] - mx) : 0.f;
+      sum += v[k];
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) ssum[wid] = sum;
+    __syncthreads();
+    const float inv = 1.f / (ssum[0] + ssum[1] + ssum[2] + ssum[3]);
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+      const int c = k * 256 + tid;
+      if (c < N) probs[long(m) * N + c] = v[k] * inv;
+    }
+    if (tid == 0) classes[m] = arg;
+    __syncthreads();   // smx / ssum reused by the next row
+  }
+}
+
 hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const float* bias, float* ws, float* probs,
-                                  int64_t* classes, int M, int HW, int K, int Np, int N, hipStream_t s) {
+                                  int64_t* classes, int M, int HW, int K, int Np, int N, hipStream_t s,
+                                  int* counter) {
   if (M <= 0) return hipSuccess;
   if (K % (kHeadKS * 4 * 32) || N > Np || N <= 0 || HW <= 0) return hipErrorInvalidValue;
   const int ksteps = K / kHeadKS / 4 / 32;        // 32-deep MFMA steps per wave
   uint16_t* pooled = reinterpret_cast<uint16_t*>(ws);
   float* part = ws + (size_t(M) * K + 1) / 2;
+  if (counter != nullptr && M <= kHeadSmallM && HW <= kHeadSmallHW && N <= kSmPer * 256 && ksteps <= 4) {
+    const dim3 grid(kHeadKS, (Np + kHeadCols - 1) / kHeadCols);
+    const float inv_hw = 1.f / float(HW);
+    switch (ksteps) {
+      case 1: hipLaunchKernelGGL(head_small_kernel<1>, grid, dim3(256), 0, s, x, w, bias, part, probs, classes,
+                                 counter, M, HW, K, Np, N, inv_hw); break;
+      case 2: hipLaunchKernelGGL(head_small_kernel<2>, grid, dim3(256), 0, s, x, w, bias, part, probs, classes,
+                                 counter, M, HW, K, Np, N, inv_hw); break;
+      case 4: hipLaunchKernelGGL(head_small_kernel<4>, grid, dim3(256), 0, s, x, w, bias, part, probs, classes,
+                                 counter, M, HW, K, Np, N, inv_hw); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(gap_rows_kernel, dim3(M, K / 64), dim3(256), 0, s, x, pooled, HW, K, 1.f / float(HW));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

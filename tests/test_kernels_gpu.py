@@ -463,6 +463,42 @@ def test_classifier_head_matches_fp32(m, hw, k, np_, n):
     assert torch.equal(cls.cpu()[clear], logits.argmax(-1)[clear])
 
 
+@pytest.mark.parametrize("m,hw,k,np_,n", [(1, 49, 2048, 1001, 1001), (2, 49, 2048, 1008, 1001), (4, 64, 1024, 300, 257),
+                                         (7, 3, 512, 10, 10), (16, 49, 2048, 1001, 1001)])
+def test_classifier_head_one_launch_matches_three(monkeypatch, m, hw, k, np_, n):
+    """The small-batch head (pool + dense + arrival-counter hand-off + softmax
+    in ONE launch, misc.hip head_small_kernel) vs the three-launch head and
+    fp32: eager calls back to back (the kernel re-zeroes its counter) and
+    replays of a captured graph."""
+    x = rnd(m, hw, 1, k, seed=44).to(BF).to(DEV)
+    w = rnd(np_, k, scale=0.05, seed=45).to(BF).to(DEV)
+    b = rnd(np_, scale=0.1, seed=46).to(DEV)
+    monkeypatch.setenv("TFSERVE_HEAD_FUSED", "0")
+    p3, c3 = hip().classifier_head(x, w, b, n)
+    monkeypatch.setenv("TFSERVE_HEAD_FUSED", "16")
+    for _ in range(3):
+        p1, c1 = hip().classifier_head(x, w, b, n)
+        assert (p1 - p3).abs().max().item() < 1e-6
+        assert torch.equal(c1, c3)
+    pooled = x.float().cpu().mean(dim=(1, 2)).to(BF).float()
+    ref = torch.softmax((pooled @ w.float().cpu().t() + b.cpu())[:, :n], -1)
+    assert (p1.cpu() - ref).abs().max() < 1e-4
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        hip().classifier_head(x, w, b, n)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        pg, cg = hip().classifier_head(x, w, b, n)
+    for _ in range(3):
+        pg.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert (pg - p3).abs().max().item() < 1e-6
+        assert torch.equal(cg, c3)
+
+
 @pytest.mark.parametrize("s", [64, 128, 256,
                                32, 100, 320, 384, 512])     # KV-block (online softmax) kernel, partial blocks
 def test_attention_matches_fp32(s):
