@@ -8,6 +8,7 @@ back to PyTorch, so a GPU test that passes has run the native kernels.
 from __future__ import annotations
 
 import contextlib
+import gc
 import itertools
 import os
 import threading
@@ -382,6 +383,31 @@ def splitk_fixup_for_bucket(bucket: int):
 
 
 _OWNER_SEQ = itertools.count(1)
+_GC_HOLD = [0]
+_GC_LOCK = threading.Lock()
+
+
+@contextlib.contextmanager
+def _no_gc():
+    """Python's cyclic GC off while a capture runs on this thread: a
+    collection there can finalize an unreachable server's CUDAGraph, whose
+    destructor frees its private pool (hipFree) on the capturing thread --
+    illegal mid-capture, and the C++ error inside a destructor aborts the
+    process (seen once in the GPU suite: abort under "Garbage-collecting" in a
+    fast-path test's capture).  Counted, since captures on several threads
+    overlap; torch.cuda.graph's own gc.collect() still runs before capture."""
+    with _GC_LOCK:
+        _GC_HOLD[0] += 1
+        if _GC_HOLD[0] == 1:
+            _GC_HOLD.append(gc.isenabled())
+            gc.disable()
+    try:
+        yield
+    finally:
+        with _GC_LOCK:
+            _GC_HOLD[0] -= 1
+            if _GC_HOLD[0] == 0 and _GC_HOLD.pop():
+                gc.enable()
 
 
 @contextlib.contextmanager
@@ -389,19 +415,21 @@ def capture_owner(graph):
     """Around a HIP-graph capture: the split-K arrival counters its launches
     take (the split-K fixup) belong to ``graph`` and go back to the pool
     when the graph object is collected, so tuning candidates and reload
-    cycles do not use the counter pool up (kernels/counters.cpp)."""
-    try:
-        h = hip()
-    except KernelsUnavailable:
-        yield None
-        return
-    tok = next(_OWNER_SEQ)
-    h.splitk_counters_set_owner(tok)
-    try:
-        yield tok
-    finally:
-        h.splitk_counters_set_owner(0)
-        weakref.finalize(graph, h.splitk_counters_release, tok)
+    cycles do not use the counter pool up (kernels/counters.cpp).  Python's
+    GC is held off for the capture (``_no_gc``)."""
+    with _no_gc():
+        try:
+            h = hip()
+        except KernelsUnavailable:
+            yield None
+            return
+        tok = next(_OWNER_SEQ)
+        h.splitk_counters_set_owner(tok)
+        try:
+            yield tok
+        finally:
+            h.splitk_counters_set_owner(0)
+            weakref.finalize(graph, h.splitk_counters_release, tok)
 
 
 _FLUSH: Dict[int, torch.Tensor] = {}

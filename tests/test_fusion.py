@@ -207,3 +207,37 @@ def test_activation_release_plan(tiny_resnet_path):
     for u, v in zip(a, b):
         np.testing.assert_array_equal(np.asarray(u), np.asarray(v))
     assert plan_release([], 0, [], [], []) == []
+
+
+def test_capture_holds_off_gc_across_nested_and_threaded_captures():
+    """Graph captures run with Python's GC off (ops._no_gc: a collection there
+    can run a dead server's CUDAGraph destructor on the capturing thread);
+    counted, so overlapping captures on two threads re-enable it only when
+    the last one ends, and a GC the caller had disabled stays disabled."""
+    import gc
+    import threading
+    from rust_tensorflow_serving2_amd import ops
+    assert gc.isenabled()
+    inside, release = threading.Event(), threading.Event()
+
+    def other():
+        with ops._no_gc():
+            inside.set()
+            release.wait(10)
+
+    t = threading.Thread(target=other)
+    t.start()
+    assert inside.wait(10)
+    with ops._no_gc():
+        assert not gc.isenabled()
+    assert not gc.isenabled()           # the other thread's capture still runs
+    release.set()
+    t.join()
+    assert gc.isenabled()
+    gc.disable()
+    try:
+        with ops._no_gc():
+            pass
+        assert not gc.isenabled()
+    finally:
+        gc.enable()
