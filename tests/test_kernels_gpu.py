@@ -656,6 +656,7 @@ def test_splitk_counter_slices_return_with_their_graph(monkeypatch):
     out = torch.empty(2, 14, 14, 256, device=DEV, dtype=BF)
     hip().conv2d(x, wt, None, None, 3, 3, 1, 1, 1, 1, 1, 1, act=0, cfg=51, out=out, splits=4)   # pool allocated
     torch.cuda.synchronize()
+    gc.collect()          # earlier tests' dead graphs return their slices first
     base = hip().splitk_counters_captured_in_use()
     stream = torch.cuda.Stream()
     for cycle in range(3):
