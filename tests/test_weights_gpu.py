@@ -31,7 +31,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, backend, port, path, out_q, regroup=False, own_gpu=False):
+def _worker(rank, world, backend, port, path, out_q, regroup=False, own_gpu=False, concurrent=False):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from rust_tensorflow_serving2_amd import ops
@@ -68,6 +68,31 @@ def _worker(rank, world, backend, port, path, out_q, regroup=False, own_gpu=Fals
             res.update(gen=ws.gen, regroups=ws.stats.get("regroups", 0),
                        bcast2=ws.stats.get("broadcast_bytes", 0) - b0, probs2=out2["probabilities"],
                        pg=type(ws.comm.pg).__name__)
+        if concurrent:
+            # a hot reload broadcast while version 1's lanes keep replaying:
+            # the broadcast is ordered on its own stream (weights.py
+            # _StreamMark), not behind a device-wide synchronize, and the live
+            # replays stay bit-exact while it runs
+            import threading
+            stop, seen = threading.Event(), {"runs": 0, "bad": 0}
+
+            def serve():
+                while not stop.is_set():
+                    o = s.run("serving_default", {"input": x}, ["classes", "probabilities"])
+                    seen["runs"] += 1
+                    seen["bad"] += int(not np.array_equal(o["probabilities"], res["probs"]))
+            t = threading.Thread(target=serve)
+            t.start()
+            b0 = ws.stats.get("broadcast_bytes", 0)
+            b3 = ws.load("resnet", 3, path)
+            s3 = Servable("resnet", 3, path, ServableOptions(device=str(dev), max_batch_size=4,
+                                                              allowed_batch_sizes=(4,)), b3, weight_source=ws)
+            out3 = s3.run("serving_default", {"input": x}, ["classes", "probabilities"])
+            runs_at_v3 = seen["runs"]
+            stop.set()
+            t.join(60)
+            res.update(bcast3=ws.stats.get("broadcast_bytes", 0) - b0, probs3=out3["probabilities"],
+                       runs_during=runs_at_v3, bad_during=seen["bad"], runs_total=seen["runs"])
         ws.close()
         dist.barrier()
         dist.destroy_process_group()
@@ -77,11 +102,11 @@ def _worker(rank, world, backend, port, path, out_q, regroup=False, own_gpu=Fals
         out_q.put((rank, {"error": f"{e}\n{traceback.format_exc()}"}))
 
 
-def _run(world, backend, path, regroup=False, own_gpu=False):
+def _run(world, backend, path, regroup=False, own_gpu=False, concurrent=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, backend, port, path, q, regroup, own_gpu)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, backend, port, path, q, regroup, own_gpu, concurrent)) for r in range(world)]
     for p in ps:
         p.start()
     out = dict(q.get(timeout=300) for _ in ps)
@@ -117,6 +142,20 @@ def test_rccl_regroup_after_restart_world1(r50):
     assert r["gen"] == 1 and r["regroups"] >= 1 and r["pg"] == "ProcessGroupNCCL"
     assert r["bcast2"] > 20e6                     # version 2's weights went through the generation-1 group
     np.testing.assert_array_equal(r["probs"], r["probs2"])
+
+
+def test_rccl_reload_broadcast_while_lanes_replay_world1(r50):
+    """Collective ordering against live lanes on the device: version 1 keeps
+    serving (graph replays on its lanes' streams, in a thread) while version
+    3 loads through RCCL -- its weights broadcast, compile and capture.  The
+    replays during the reload stay bit-identical to before it, and version
+    3's outputs match version 1's (same weights)."""
+    out = _run(1, "nccl", r50, concurrent=True)
+    r = out[0]
+    assert r["bcast3"] > 20e6                     # version 3 went through RCCL
+    assert r["runs_during"] >= 1                   # version 1 was replaying while it loaded
+    assert r["bad_during"] == 0, r
+    np.testing.assert_allclose(r["probs3"], r["probs"], atol=2e-4, rtol=0)   # tile picks may differ
 
 
 def test_follower_binds_leader_blob_without_host_copies(r50):
