@@ -975,7 +975,8 @@ hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const fl
   const int ksteps = K / kHeadKS / 4 / 32;        // 32-deep MFMA steps per wave
   uint16_t* pooled = reinterpret_cast<uint16_t*>(ws);
   float* part = ws + (size_t(M) * K + 1) / 2;
-  if (counter != nullptr && M <= kHeadSmallM && HW <= kHeadSmallHW && N <= kSmPer * 256 && ksteps <= 4) {
+  if (counter != nullptr && M <= kHeadSmallM && HW <= kHeadSmallHW && N <= kSmPer * 256 &&
+      (ksteps == 1 || ksteps == 2 || ksteps == 4)) {
     const dim3 grid(kHeadKS, (Np + kHeadCols - 1) / kHeadCols);
     const float inv_hw = 1.f / float(HW);
     switch (ksteps) {
