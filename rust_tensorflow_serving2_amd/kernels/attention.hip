@@ -33,11 +33,24 @@ constexpr int D = 64;
 // per 12 layers): twice the workgroups outweigh staging K/V twice.
 constexpr int qb_for(int) { return 64; }
 
+// per-workgroup phase stamps (scripts/wg_trace.py --attention; null: off)
+long long* g_attn_trace = nullptr;
+int g_attn_trace_cap = 0;
+__device__ __forceinline__ void attn_stamp(long long* trace, int cap, int k) {
+  if (trace != nullptr && threadIdx.x == 0 && int(blockIdx.x) < cap) {
+    long long* d = trace + long(blockIdx.x) * 8;
+    d[k] = wall_clock64();
+    if (k == 0) d[7] = __smid();
+  }
+}
+
 template <int S, int QB>
 __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __restrict__ qkv,
                                                            const float* __restrict__ mask_bias,
                                                            uint16_t* __restrict__ ctx, int H, float scale,
-                                                           long mask_bstride, long mask_qstride) {
+                                                           long mask_bstride, long mask_qstride,
+                                                           long long* __restrict__ trace, int trace_cap) {
+  attn_stamp(trace, trace_cap, 0);
   constexpr int NTH = QB * 4;            // QB / 16 waves
   constexpr int VT_LD = S + 8;           // Vt row stride (elements): +16 B pad
   constexpr int P_LD = S + 8;
@@ -123,6 +136,7 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
 #pragma unroll
   for (int d = 0; d < 8; ++d) *reinterpret_cast<uint4*>(Vt + (vch * 8 + d) * VT_LD + vcol) = vt8[d];
   __syncthreads();
+  attn_stamp(trace, trace_cap, 1);          // operands staged
 
   // ---- scores
   f32x4 s[NT];
@@ -184,6 +198,7 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
   __syncthreads();   // P strip (wave-private) + nothing else pending; cheap at this size
+  attn_stamp(trace, trace_cap, 2);          // scores + softmax done
 
   // ---- ctx = P V
   f32x4 o[4];
@@ -209,11 +224,16 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): this wave's LDS writes landed
   __builtin_amdgcn_wave_barrier();
+  attn_stamp(trace, trace_cap, 3);          // P V done (wave 0)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int c = j * 64 + lane, row = c >> 3, ch = c & 7;
     *reinterpret_cast<uint4*>(ctx + (long(b) * S + q0 + row) * (long(H) * D) + h * D + ch * 8) =
         *reinterpret_cast<const uint4*>(pw + row * P_LD + ch * 8);
+  }
+  if (trace != nullptr) {
+    __builtin_amdgcn_s_waitcnt(0);          // this wave's stores acknowledged
+    attn_stamp(trace, trace_cap, 4);
   }
 }
 
@@ -390,7 +410,8 @@ hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, 
   hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&attention_kernel<S, QB>), lds);
   if (e != hipSuccess) return e;
   const int grid = B * H * (S / QB);
-  hipLaunchKernelGGL((attention_kernel<S, QB>), dim3(grid), dim3(QB * 4), lds, st, qkv, mb, ctx, H, scale, bs, qs);
+  hipLaunchKernelGGL((attention_kernel<S, QB>), dim3(grid), dim3(QB * 4), lds, st, qkv, mb, ctx, H, scale, bs, qs,
+                     g_attn_trace, g_attn_trace_cap);
   return hipGetLastError();
 }
 
@@ -403,6 +424,11 @@ int attn_qb() {
 }
 
 }  // namespace
+
+void attention_set_trace(long long* trace, int cap) {
+  g_attn_trace = trace;
+  g_attn_trace_cap = trace ? cap : 0;
+}
 
 hipError_t attention_launch(const uint16_t* qkv, const float* mask_bias, uint16_t* ctx, int B, int S, int H,
                             int Dh, float scale, long mask_bstride, long mask_qstride, hipStream_t st) {

@@ -744,11 +744,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (!t.has_value()) {
       g_trace = nullptr;
       g_trace_cap = 0;
+      tfsk::attention_set_trace(nullptr, 0);
       return;
     }
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous(), "trace: int64 device tensor");
     g_trace = reinterpret_cast<long long*>(t->data_ptr<int64_t>());
     g_trace_cap = int(std::min<int64_t>(t->numel() / 8, 1 << 30));
+    tfsk::attention_set_trace(g_trace, g_trace_cap);
   }, "per-workgroup wall-clock stamps of the following GEMM / conv launches (None: off)");
   m.def("set_splitk_fixup", [](int64_t mode) { g_fixup_override = mode < 0 ? -1 : (mode ? 1 : 0); },
         "in-kernel split-K for the following launches: 1 on, 0 off, -1 default (env, else small launches)");

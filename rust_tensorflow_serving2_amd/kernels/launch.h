@@ -171,5 +171,8 @@ constexpr int kMaxAttentionSeq = 4096;
 hipError_t attention_launch(const uint16_t* qkv, const float* mask_bias, uint16_t* ctx, int B, int S,
                             int H, int D, float scale, long mask_bstride, long mask_qstride,
                             hipStream_t stream);
+// per-workgroup phase stamps of the following fixed-S attention launches
+// (entry, staged, softmax, P V, stored; [7] = CU id); nullptr: off
+void attention_set_trace(long long* trace, int cap);
 
 }  // namespace tfsk

@@ -39,9 +39,18 @@ def main():
     ap.add_argument("--cfgs", nargs="*", default=["48:1", "51:1", "50:1", "42:1"],
                     help="tile config:split-K pairs (each is tried on every layer it supports)")
     ap.add_argument("--gemm", nargs="*", default=[], help="dense GEMMs MxNxK (hip().linear) instead of conv layers")
+    ap.add_argument("--attention", nargs="*", default=[],
+                    help="fixed-S attention BxSxH (D = 64, key mask): stamps entry / staged / softmax / PV / stored")
     a = ap.parse_args()
     n = a.batch
     H = hip()
+    for shape in a.attention:
+        B, S, NH = (int(v) for v in shape.split("x"))
+        qkvs = [torch.randn(B, S, 3 * NH * 64, device="cuda").to(BF) for _ in range(8)]
+        mask = torch.zeros(B, S, device="cuda")
+        attention_report(f"attn{shape}", lambda j: H.attention(qkvs[j], mask, NH, 0.125, None, S, 0))
+    if a.attention:
+        return
     for shape in a.gemm:
         M, N, K = (int(v) for v in shape.split("x"))
         xs = [torch.randn(M, K, device="cuda").to(BF) for _ in range(8)]
@@ -66,6 +75,44 @@ def main():
             cfg, sp = (int(x) for x in cs.split(":"))
             report(name, cfg, sp, lambda j, cfg=cfg, sp=sp: H.conv2d(
                 xs[j], ws[j], b, rs[j], k, k, s, s, pad, pad, pad, pad, ACT["relu"], cfg, outs[j], False, sp))
+
+
+def attention_report(name, run):
+    """Phases of the fixed-S attention kernel (kernels/attention.hip stamps)."""
+    H = hip()
+    for j in range(8):
+        run(j)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for j in range(7):
+        run(j)
+    e0.record()
+    run(7)
+    e1.record()
+    e1.synchronize()
+    ev_us = e0.elapsed_time(e1) * 1e3
+    tr = torch.zeros(1 << 20, 8, dtype=torch.int64, device="cuda")
+    for j in range(7):
+        run(j)
+    H.set_wg_trace(tr)
+    run(7)
+    H.set_wg_trace(None)
+    torch.cuda.synchronize()
+    t = tr.cpu()
+    t = t[t[:, 0] > 0]
+    t0 = int(t[:, 0].min())
+    ph = {"start": ((t[:, 0] - t0).double() * TICK_US).tolist()}
+    for k, nm in ((1, "staged"), (2, "softmax"), (3, "pv"), (4, "stored")):
+        ph[nm] = ((t[:, k] - t[:, k - 1]).double() * TICK_US).tolist()
+    ph["life"] = ((t[:, 4] - t[:, 0]).double() * TICK_US).tolist()
+    per_cu = {}
+    for c in t[:, 7].tolist():
+        per_cu[c] = per_cu.get(c, 0) + 1
+    print(json.dumps({"layer": name, "workgroups": int(t.shape[0]), "event_us": round(ev_us, 2),
+                      "span_us": round(float((t[:, 4].max() - t0) * TICK_US), 2), "cus": len(per_cu),
+                      "max_wg_per_cu": max(per_cu.values()),
+                      **{k: {"p50": round(q(v, .5), 2), "p90": round(q(v, .9), 2), "max": round(max(v), 2)}
+                         for k, v in ph.items()}}), flush=True)
 
 
 def report(name, cfg, sp, run):
