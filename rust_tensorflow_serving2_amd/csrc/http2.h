@@ -3,9 +3,12 @@
 // Replaces the transport layer the reference leaves to tonic/hyper/h2 on the
 // client side (src/lib.rs:132-138; Cargo.lock tonic 0.1 / h2 0.2) and to the
 // external TF-Serving container on the server side (serving/rundocker.sh:15).
-// Design: N epoll IO threads, each with its own SO_REUSEPORT listening socket
-// (kernel load-balances connections across threads *and* across server
-// processes, one per GPU); libnghttp2 for framing/HPACK/flow control; request
+// Design: N epoll IO threads; IO thread 0 owns the one SO_REUSEPORT listening
+// socket of this process (the kernel spreads connections across server
+// processes, one per GPU) and hands each accepted connection to the IO thread
+// with the fewest live connections (the kernel's per-thread reuseport hash put
+// the reference client's two connections on ONE thread in about one run in
+// six, halving that run); libnghttp2 for framing/HPACK/flow control; request
 // bodies assembled per stream and dispatched either to the C++ Predict fast
 // path (batcher.h) or to a queue drained by Python control-plane threads.
 // Responses from any thread are posted to the owning IO thread (eventfd).
@@ -193,6 +196,11 @@ class Server {
 
   // Called by IO threads when a request is complete.
   void dispatch(std::unique_ptr<Call> c);
+  // IO thread with the fewest live connections (ties: round-robin), the
+  // acceptor's target for a new connection.
+  IoThread* pick_io();
+  // live connections per IO thread (diagnostics / tests)
+  std::vector<int> io_connections() const;
   size_t max_message() const { return max_message_; }
   ServerStats stats;
 
@@ -210,6 +218,7 @@ class Server {
   std::condition_variable qcv_;
   std::deque<std::unique_ptr<Call>> queue_;
   std::atomic<bool> running_{false};
+  std::atomic<unsigned> next_io_{0};
 };
 
 // ---------------------------------------------------------------- load generator

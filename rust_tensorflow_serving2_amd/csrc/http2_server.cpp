@@ -166,8 +166,27 @@ struct Conn {
 
 class IoThread {
  public:
-  IoThread(Server* srv, int index, const std::string& host, int port)
-      : srv_(srv), index_(index) {
+  IoThread(Server* srv, int index, const std::string& host, int port, bool listener)
+      : srv_(srv), index_(index), port_(port) {
+    if (listener) open_listener(host, port);   // may throw: nothing else is allocated yet
+    ep_ = epoll_create1(0);
+    wake_ = eventfd(0, EFD_NONBLOCK);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = kWakeTag;
+    epoll_ctl(ep_, EPOLL_CTL_ADD, wake_, &ev);
+    if (lfd_ >= 0) {
+      ev.data.u64 = kListenTag;
+      epoll_ctl(ep_, EPOLL_CTL_ADD, lfd_, &ev);
+    }
+    rbuf_.resize(kReadBuf);
+    init_callbacks();
+  }
+
+  // The process's one listening socket (IO thread 0): SO_REUSEPORT so GPU
+  // replicas (processes) share the port; other IO threads get connections
+  // from it through adopt().
+  void open_listener(const std::string& host, int port) {
     lfd_ = socket(AF_INET, SOCK_STREAM, 0);
     if (lfd_ < 0) throw std::runtime_error("socket() failed");
     int one = 1;
@@ -189,21 +208,17 @@ class IoThread {
       ::close(lfd_);
       throw std::runtime_error(std::string("bind failed: ") + strerror(e));
     }
-    if (listen(lfd_, 1024) != 0) throw std::runtime_error("listen failed");
+    if (listen(lfd_, 1024) != 0) {
+      ::close(lfd_);
+      throw std::runtime_error("listen failed");
+    }
     socklen_t len = sizeof(addr);
     getsockname(lfd_, (sockaddr*)&addr, &len);
     port_ = ntohs(addr.sin_port);
     set_nonblock(lfd_);
-    ep_ = epoll_create1(0);
-    wake_ = eventfd(0, EFD_NONBLOCK);
-    epoll_event ev{};
-    ev.events = EPOLLIN;
-    ev.data.u64 = kListenTag;
-    epoll_ctl(ep_, EPOLL_CTL_ADD, lfd_, &ev);
-    ev.data.u64 = kWakeTag;
-    epoll_ctl(ep_, EPOLL_CTL_ADD, wake_, &ev);
-    rbuf_.resize(kReadBuf);
+  }
 
+  void init_callbacks() {
     nghttp2_session_callbacks_new(&cbs_);
     nghttp2_session_callbacks_set_on_begin_headers_callback(cbs_, &IoThread::on_begin_headers);
     nghttp2_session_callbacks_set_on_header_callback(cbs_, &IoThread::on_header);
@@ -217,6 +232,7 @@ class IoThread {
     stop();
     for (auto& kv : conns_) close_conn(kv.second.get(), false);
     conns_.clear();
+    for (int fd : adopt_) ::close(fd);
     if (cbs_) nghttp2_session_callbacks_del(cbs_);
     if (lfd_ >= 0) ::close(lfd_);
     if (ep_ >= 0) ::close(ep_);
@@ -224,6 +240,19 @@ class IoThread {
   }
 
   int port() const { return port_; }
+  int live_connections() const { return nconns_.load(std::memory_order_relaxed); }
+
+  // A connection accepted by the acceptor thread, registered on this thread's
+  // epoll set by this thread (its loop's wake-up adopts it).
+  void adopt(int fd) {
+    nconns_.fetch_add(1, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> g(amu_);
+      adopt_.push_back(fd);
+    }
+    uint64_t one = 1;
+    (void)!write(wake_, &one, sizeof(one));
+  }
 
   void start() {
     running_ = true;
@@ -488,6 +517,27 @@ class IoThread {
     for (;;) {
       int fd = accept4(lfd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
       if (fd < 0) return;
+      IoThread* t = srv_->pick_io();
+      if (t != this) {
+        t->adopt(fd);
+        continue;
+      }
+      nconns_.fetch_add(1, std::memory_order_relaxed);
+      add_conn(fd);
+    }
+  }
+
+  void adopt_pending() {
+    std::vector<int> fds;
+    {
+      std::lock_guard<std::mutex> g(amu_);
+      fds.swap(adopt_);
+    }
+    for (int fd : fds) add_conn(fd);
+  }
+
+  void add_conn(int fd) {
+    {
       int one = 1;
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
       int sz = 4 << 20;
@@ -520,6 +570,7 @@ class IoThread {
       epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
       ::close(c->fd);
       c->fd = -1;
+      nconns_.fetch_sub(1, std::memory_order_relaxed);
     }
     if (c->sess) {
       nghttp2_session_del(c->sess);
@@ -666,6 +717,7 @@ class IoThread {
         if (tag == kWakeTag) {
           uint64_t v;
           while (read(wake_, &v, sizeof(v)) > 0) {}
+          adopt_pending();
           continue;
         }
         auto it = conns_.find(tag);
@@ -703,6 +755,9 @@ class IoThread {
   std::vector<uint8_t> rbuf_;
   std::mutex omu_;
   std::vector<Outgoing> outbox_;
+  std::atomic<int> nconns_{0};       // live + handed-over connections
+  std::mutex amu_;
+  std::vector<int> adopt_;           // accepted by the acceptor, not yet registered
   static thread_local IoThread* tls_self_;
 };
 
@@ -712,9 +767,26 @@ thread_local IoThread* IoThread::tls_self_ = nullptr;
 Server::Server(const std::string& host, int port, int io_threads, size_t max_message)
     : host_(host), port_(port), max_message_(max_message) {
   if (io_threads < 1) io_threads = 1;
-  io_.emplace_back(std::make_unique<IoThread>(this, 0, host, port));
+  io_.emplace_back(std::make_unique<IoThread>(this, 0, host, port, true));
   port_ = io_[0]->port();
-  for (int i = 1; i < io_threads; ++i) io_.emplace_back(std::make_unique<IoThread>(this, i, host, port_));
+  for (int i = 1; i < io_threads; ++i) io_.emplace_back(std::make_unique<IoThread>(this, i, host, port_, false));
+}
+
+std::vector<int> Server::io_connections() const {
+  std::vector<int> v;
+  for (const auto& t : io_) v.push_back(t->live_connections());
+  return v;
+}
+
+IoThread* Server::pick_io() {
+  const unsigned n = unsigned(io_.size());
+  const unsigned start = next_io_.fetch_add(1, std::memory_order_relaxed) % n;
+  IoThread* best = io_[start].get();
+  for (unsigned k = 1; k < n; ++k) {
+    IoThread* t = io_[(start + k) % n].get();
+    if (t->live_connections() < best->live_connections()) best = t;
+  }
+  return best;
 }
 
 Server::~Server() { stop(); }

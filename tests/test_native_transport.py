@@ -82,6 +82,40 @@ def test_persistent_loadgen_reuses_connections(nserver):
     del lg
 
 
+def test_connections_spread_evenly_over_io_threads(nserver):
+    """One acceptor hands each connection to the IO thread with the fewest
+    live connections: the reference client's two connections always land on
+    two threads (the per-thread SO_REUSEPORT hash put both on one thread in
+    about one run in six), and eight connections fill four threads evenly."""
+    import time
+    srv = nserver.transports[0].srv
+
+    def settled():
+        prev = None
+        for _ in range(40):
+            cur = srv.stats()["io_connections"]
+            if cur == prev:
+                return cur
+            prev = cur
+            time.sleep(0.05)
+        return prev
+    body = native.encode_predict_request(native.spec_tuple("hpt", None, None, ""), {"x": np.ones((1, 1), np.float32)})
+    base = settled()
+    assert len(base) >= 2
+    lg2 = _C.LoadGen("127.0.0.1", nserver.port, "/tensorflow.serving.PredictionService/Predict", [body], 4, 2, 2)
+    assert lg2.run(4, 60.0)["ok"] == 4
+    two = settled()
+    grew = [b - a for a, b in zip(base, two)]
+    if max(base) == min(base):
+        assert sorted(grew)[-2:] == [1, 1], (base, two)     # two threads, one connection each
+    lg8 = _C.LoadGen("127.0.0.1", nserver.port, "/tensorflow.serving.PredictionService/Predict", [body], 16, 8, 2)
+    assert lg8.run(16, 60.0)["ok"] == 16
+    eight = settled()
+    assert sum(eight) == sum(two) + 8
+    assert max(eight) - min(eight) <= max(1, max(two) - min(two)), (two, eight)
+    del lg2, lg8
+
+
 def test_continuous_loadgen_windows(nserver):
     """bench.py's steady-state mode: the load generator keeps `concurrency`
     calls in flight from start() to stop(); each window counts exactly its own
