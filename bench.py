@@ -438,6 +438,10 @@ def main():
         cpu_report["thread_pins"] = thread_pins
     gpu_busy = busy.stop()
     loadgen.stop(30.0)
+    # close the window's 16 connections (their socket buffers, up to 4 MB per
+    # direction on each side) before the reference-client phase: after a long
+    # window the phase's recv cost per request rose 15 -> 25-42 us
+    del loadgen
     check(r, "timed window")
 
     # reference-client mode: ONE client with 2 connections (the Rust client's
