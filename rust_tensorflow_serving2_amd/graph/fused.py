@@ -504,7 +504,18 @@ class ClassifierHead:
     def __call__(self, ctx, node, ins):
         x = O.to_torch(ins[0])
         if self.use_hip and x.is_cuda and x.dim() == 4 and x.shape[-1] == self.w.shape[1]:
-            from ..ops import hip
+            from ..ops import current_head_host_rows, hip
+            rows = current_head_host_rows()
+            if rows is not None:
+                # a serving lane's capture: the one-launch head also writes
+                # the lane's pinned output rows (ops.head_host_rows)
+                p_ptr = rows[0] if rows[1] == self.n else 0
+                c_ptr = rows[2] if self.cdt == torch.int64 else 0
+                probs, cls, wrote = hip().classifier_head_to_host(_to_bf16(x).contiguous(), self.w, self.b, self.n,
+                                                                  p_ptr, c_ptr)
+                if wrote:
+                    probs._tfs_host, cls._tfs_host = p_ptr, c_ptr
+                return [probs, cls]
             probs, cls = hip().classifier_head(_to_bf16(x).contiguous(), self.w, self.b, self.n)
         else:
             pooled = x.float().mean(dim=(1, 2))

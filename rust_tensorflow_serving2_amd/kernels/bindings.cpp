@@ -499,7 +499,19 @@ std::vector<Tensor> softmax_argmax(const Tensor& logits, bool want_probs, bool w
 }
 
 // ResNet-style head: probs, classes = softmax/argmax(mean_hw(x) @ w^T + bias)[:, :n]
+// With `probs_host` / `classes_host` (pinned host addresses of >= M rows, 0:
+// none) the one-launch head also stores its rows there; the returned flag
+// says whether it did (only the one-launch path can).
+std::tuple<Tensor, Tensor, bool> classifier_head_impl(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t n,
+                                                      int64_t probs_host, int64_t classes_host);
+
 std::vector<Tensor> classifier_head(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t n) {
+  auto r = classifier_head_impl(x, w, bias, n, 0, 0);
+  return {std::get<0>(r), std::get<1>(r)};
+}
+
+std::tuple<Tensor, Tensor, bool> classifier_head_impl(const Tensor& x, const Tensor& w, const Tensor& bias, int64_t n,
+                                                      int64_t probs_host, int64_t classes_host) {
   need(x, at::kBFloat16, "x");
   need(w, at::kBFloat16, "w");
   need(bias, at::kFloat, "bias");
@@ -523,11 +535,16 @@ std::vector<Tensor> classifier_head(const Tensor& x, const Tensor& w, const Tens
     tfsk::splitk_counters_prepare(cur_stream(x));
     counter = tfsk::splitk_counters(1, cur_stream(x));
   }
+  // host rows only where the one-launch path runs (same conditions as the launcher)
+  const bool to_host = counter != nullptr && (probs_host != 0 || classes_host != 0) && HW <= 64 && n <= 4096 &&
+                       K <= 2048;
   check(tfsk::classifier_head_launch(bf16p(x), bf16p(w), bias.data_ptr<float>(), part.data_ptr<float>(),
                                      probs.data_ptr<float>(), classes.data_ptr<int64_t>(), M, HW, K, Np, int(n),
-                                     cur_stream(x), counter),
+                                     cur_stream(x), counter,
+                                     to_host ? reinterpret_cast<float*>(probs_host) : nullptr,
+                                     to_host ? reinterpret_cast<int64_t*>(classes_host) : nullptr),
         "classifier_head");
-  return {probs, classes};
+  return {probs, classes, to_host};
 }
 
 Tensor ingest_c4(const Tensor& x, const c10::optional<Tensor>& out) {
@@ -733,6 +750,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps"), py::arg("out") = py::none());
   m.def("embed_ln", &embed_ln, py::arg("ids"), py::arg("type_ids"), py::arg("word"), py::arg("pos"),
         py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("seq"));
+  m.def("classifier_head_to_host", &classifier_head_impl, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("n"),
+        py::arg("probs_host"), py::arg("classes_host"),
+        "classifier_head that also stores its rows into pinned host memory when it runs as one launch: "
+        "(probs, classes, wrote_host)");
   m.def("attention", &attention, py::arg("qkv"), py::arg("mask_bias"), py::arg("heads"), py::arg("scale"),
         py::arg("out") = py::none(), py::arg("mask_bstride") = 0, py::arg("mask_qstride") = 0);
   m.def("splitk_counters_set_owner", [](int64_t owner) { tfsk::splitk_counters_set_owner(owner); },

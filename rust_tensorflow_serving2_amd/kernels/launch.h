@@ -137,10 +137,14 @@ hipError_t global_avgpool_nhwc_launch(const uint16_t* x, uint16_t* y, int N, int
 // workspace of classifier_head_ws_floats(M, K, Np); probs [M][N] f32 and
 // classes [M] for the first N <= Np columns.
 // `counter` (a zeroed int, re-zeroed by the kernel; nullptr: three launches):
-// M <= 16 rows and HW <= 64 run as ONE launch (misc.hip head_small_kernel).
+// M <= 16 rows and HW <= 64 run as ONE launch (misc.hip head_small_kernel),
+// which also stores the rows into pinned host buffers `probs_h` / `classes_h`
+// when given (a serving lane's output rows: no D2H copies after the graph).
+// Returns hipErrorNotSupported when host rows are asked of the 3-launch path.
 hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const float* bias, float* ws,
                                   float* probs, int64_t* classes, int M, int HW, int K, int Np, int N,
-                                  hipStream_t s, int* counter = nullptr);
+                                  hipStream_t s, int* counter = nullptr, float* probs_h = nullptr,
+                                  int64_t* classes_h = nullptr);
 size_t classifier_head_ws_floats(int M, int K, int Np);
 // BERT head: probs[r] = softmax(x[r] @ w^T + bias) over N <= 16 labels (x fp32)
 hipError_t dense_softmax_launch(const float* x, int ldx, const uint16_t* w, int ldw, const float* bias,

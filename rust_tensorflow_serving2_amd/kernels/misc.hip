@@ -804,7 +804,8 @@ __global__ __launch_bounds__(256) void head_small_kernel(const uint16_t* __restr
                                                          const float* __restrict__ bias, float* __restrict__ part,
                                                          float* __restrict__ probs, int64_t* __restrict__ classes,
                                                          int* __restrict__ counter, int M, int HW, int K, int Np,
-                                                         int N, float inv_hw) {
+                                                         int N, float inv_hw, float* __restrict__ probs_h,
+                                                         int64_t* __restrict__ classes_h) {
   constexpr int KSLICE = KSTEPS * 32 * 4;            // channels per workgroup (4 waves)
   __shared__ __attribute__((aligned(16))) uint16_t pooled[kHeadSmallM][KSLICE];
   __shared__ float quarter[4][64][9];
@@ -960,16 +961,23 @@ __global__ __launch_bounds__(256) void head_small_kernel(const uint16_t* __restr
 #pragma unroll
     for (int k = 0; k < kSmPer; ++k) {
       const int c = k * 256 + tid;
-      if (c < N) probs[long(m) * N + c] = v[k] * inv;
+      if (c < N) {
+        probs[long(m) * N + c] = v[k] * inv;
+        if (probs_h) probs_h[long(m) * N + c] = v[k] * inv;
+      }
     }
-    if (tid == 0) classes[m] = arg;
+    if (tid == 0) {
+      classes[m] = arg;
+      if (classes_h) classes_h[m] = arg;
+    }
     __syncthreads();   // smx / ssum reused by the next row
   }
+  if (probs_h || classes_h) __threadfence_system();   // host rows visible with the kernel's completion
 }
 
 hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const float* bias, float* ws, float* probs,
                                   int64_t* classes, int M, int HW, int K, int Np, int N, hipStream_t s,
-                                  int* counter) {
+                                  int* counter, float* probs_h, int64_t* classes_h) {
   if (M <= 0) return hipSuccess;
   if (K % (kHeadKS * 4 * 32) || N > Np || N <= 0 || HW <= 0) return hipErrorInvalidValue;
   const int ksteps = K / kHeadKS / 4 / 32;        // 32-deep MFMA steps per wave
@@ -981,15 +989,16 @@ hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const fl
     const float inv_hw = 1.f / float(HW);
     switch (ksteps) {
       case 1: hipLaunchKernelGGL(head_small_kernel<1>, grid, dim3(256), 0, s, x, w, bias, part, probs, classes,
-                                 counter, M, HW, K, Np, N, inv_hw); break;
+                                 counter, M, HW, K, Np, N, inv_hw, probs_h, classes_h); break;
       case 2: hipLaunchKernelGGL(head_small_kernel<2>, grid, dim3(256), 0, s, x, w, bias, part, probs, classes,
-                                 counter, M, HW, K, Np, N, inv_hw); break;
+                                 counter, M, HW, K, Np, N, inv_hw, probs_h, classes_h); break;
       case 4: hipLaunchKernelGGL(head_small_kernel<4>, grid, dim3(256), 0, s, x, w, bias, part, probs, classes,
-                                 counter, M, HW, K, Np, N, inv_hw); break;
+                                 counter, M, HW, K, Np, N, inv_hw, probs_h, classes_h); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
+  if (probs_h != nullptr || classes_h != nullptr) return hipErrorNotSupported;
   hipLaunchKernelGGL(gap_rows_kernel, dim3(M, K / 64), dim3(256), 0, s, x, pooled, HW, K, 1.f / float(HW));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

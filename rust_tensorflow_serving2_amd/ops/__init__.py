@@ -382,6 +382,28 @@ def splitk_fixup_for_bucket(bucket: int):
         h.set_splitk_fixup(-1)
 
 
+_HEAD_ROWS = threading.local()
+
+
+@contextlib.contextmanager
+def head_host_rows(rows):
+    """Around a serving lane's capture: ``rows`` = (probs_ptr, probs_width,
+    classes_ptr) of the lane's pinned output rows (0 = none), or None.  A
+    one-launch classifier head captured inside stores its rows there too and
+    tags its outputs (``_tfs_host``), so the lane can drop their D2H copies
+    (two ~4.5-us blit kernels at batch 1).  TFSERVE_HEAD_HOST=0: off."""
+    prev = getattr(_HEAD_ROWS, "rows", None)
+    _HEAD_ROWS.rows = rows if os.environ.get("TFSERVE_HEAD_HOST", "1") != "0" else None
+    try:
+        yield
+    finally:
+        _HEAD_ROWS.rows = prev
+
+
+def current_head_host_rows():
+    return getattr(_HEAD_ROWS, "rows", None)
+
+
 _OWNER_SEQ = itertools.count(1)
 _GC_HOLD = [0]
 _GC_LOCK = threading.Lock()

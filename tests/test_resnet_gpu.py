@@ -168,3 +168,31 @@ def test_bf16_ingest_is_bit_identical_to_fp32_feed(resnet50, monkeypatch):
         outs[mode] = r.run([x])
     np.testing.assert_array_equal(outs["0"][0], outs["1"][0])
     np.testing.assert_array_equal(outs["0"][1], outs["1"][1])
+
+
+def test_small_buckets_write_their_rows_to_the_host(resnet50, monkeypatch):
+    """Buckets of <= 4 rows: the one-launch classifier head stores the
+    probabilities and classes straight into the lane's pinned output rows
+    inside the graph, so the lane skips their D2H copies (two ~4.5-us blit
+    kernels at batch 1); runner outputs match TFSERVE_HEAD_HOST=0, and the
+    b32 bucket keeps its copies."""
+    from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
+    x = np.random.default_rng(11).random((4, 224, 224, 3), dtype=np.float32)
+    got, written = {}, {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("TFSERVE_HEAD_HOST", mode)
+        s = Servable("resnet", 1, resnet50, ServableOptions(
+            device="cuda:0", max_batch_size=32, allowed_batch_sizes=(1, 4, 32), lanes=1))
+        r = s.runner("serving_default", ["input"], ["classes", "probabilities"])
+        got[mode] = [r.run([x[:n]]) for n in (1, 3, 4, 1)]
+        r.run([np.concatenate([x] * 8)])                     # the b32 bucket
+        written[mode] = dict(r.lanes[0].host_written)
+        s.unload() if hasattr(s, "unload") else None
+    assert written["1"][1] == [True, True] and written["1"][4] == [True, True], written
+    assert written["1"][32] == [False, False] and not any(any(v) for v in written["0"].values()), written
+    for a, b in zip(got["0"], got["1"]):
+        np.testing.assert_allclose(a[1], b[1], atol=2e-4, rtol=0)
+        assert a[1].shape == b[1].shape and a[0].shape == b[0].shape
+        top2 = np.sort(a[1], -1)[:, -2:]
+        clear = (top2[:, 1] - top2[:, 0]) > 1e-3
+        np.testing.assert_array_equal(a[0][clear], b[0][clear])
