@@ -13,7 +13,10 @@ each rank is a full model server on its GPU:
 * load: the native gRPC load generator (C++, separate threads, real TCP
   loopback connections, HTTP/2 framing) sends batch-1 PredictRequests exactly
   as the reference Rust client builds them (alias "input", DT_FLOAT float_val,
-  224x224x3; src/lib.rs:229-263), drawn from 64 distinct synthetic images.
+  224x224x3; src/lib.rs:229-263), drawn from ``--distinct-requests``
+  (default 4; 64 until round 4) distinct synthetic images: the reference
+  client encodes each request right before sending it, so its bytes are
+  cache-hot (the JSON ``data`` field names the count).
 
 A *step* = ``--batch`` Predict RPCs (one full GPU batch per rank).  Before
 the warmup steps, ``--prewarm-s`` seconds (default 1) of untimed traffic run
@@ -21,10 +24,13 @@ through the same client and server: a step is < 1 ms, so W steps alone would
 leave the timed window inside the start-up transient (GPU/CPU clock ramp, TCP
 window growth, first touch of the transport buffers), which measured as 8-12 ms
 latency spikes and -20 % throughput in 100-step windows.  W warmup
-steps are untimed; then exactly K steps are timed between barriers with
-``torch.cuda.synchronize()`` on both sides; the max time over ranks is used
-and ``value`` = total RPCs of all ranks / that time (weak scaling: fixed work
-per GPU).  Extra fields report p50/p99 latency.
+steps are untimed; then exactly K steps are bracketed by
+``torch.cuda.synchronize()`` + a barrier on both sides.  A rank's time is
+barrier -> its K-th step's last completion (a received response implies its
+kernels finished; the closing synchronize, which waits for batches queued
+behind the window, is reported as ``end_sync_ms``); the max time over ranks
+is used and ``value`` = total RPCs of all ranks / that time (weak scaling:
+fixed work per GPU).  Extra fields report p50/p99 latency.
 
 Launch.  ``--gpus N`` with N > 1 and no ``WORLD_SIZE`` in the environment
 makes this process a launcher: it starts N child ranks (fresh subprocesses,
@@ -410,27 +416,40 @@ def main():
     diag_window = diag(dc0, topology.thread_cpu(), dio0, io_stats(), dru0, os.times(), dsecs)
     diag_window["window_s"] = round(dsecs, 3)
     diag_window["host"] = pre_contention.stop()
-    if world > 1:
-        dist.barrier()
+    # the timed bracket: synchronize + barrier, then EXACTLY K steps, then
+    # synchronize + barrier.  The timed region is barrier -> this rank's last
+    # counted completion: a received response already implies its kernels
+    # finished, and the load generator never drains, so the closing
+    # synchronize waits for batches queued BEHIND the window (3.8 of a
+    # 16.5 ms 20-step window in BENCH_r04.json).  Each rank's opening
+    # synchronize runs before the barrier, so its length (5.8 / 8.5 ms on the
+    # two ranks of a rehearsal) cannot skew the ranks' windows; both are
+    # reported as separate fields.
     t_s = time.perf_counter()
     dev_sync()
     start_sync_ms = (time.perf_counter() - t_s) * 1e3
     cpu0, io0, ru0, tid0 = topology.thread_cpu(), io_stats(), os.times(), topology.thread_cpu_by_tid()
     contention = topology.HostContention(placement.cpus).start()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     r = loadgen.window(args.steps * per_step, 600.0)
     t_last = time.perf_counter()
     dev_sync()
+    t_synced = time.perf_counter()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    t_end = time.perf_counter()
+    elapsed = t_last - t0
     cpu_report = diag(cpu0, topology.thread_cpu(), io0, io_stats(), ru0, os.times(), elapsed)
     cpu_report["top_threads"] = topology.top_threads(tid0, topology.thread_cpu_by_tid(), elapsed)
     # other tenants: busy share of this rank's node / the host, run-queue wait, quota throttling
     # the closing synchronize waits for the batches already in flight behind the
     # last counted completion (the load generator never drains): its share of
     # the window, which a short --steps window feels most
-    cpu_report["end_sync_ms"] = round((t0 + elapsed - t_last) * 1e3, 3)
+    cpu_report["end_sync_ms"] = round((t_synced - t_last) * 1e3, 3)
+    cpu_report["end_barrier_ms"] = round((t_end - t_synced) * 1e3, 3)
+    cpu_report["bracket_s"] = round(t_end - t0, 6)       # barrier -> closing sync + barrier
     cpu_report["start_sync_ms"] = round(start_sync_ms, 3)
     cpu_report["host"] = contention.stop()
     cpu_report["host"]["threads_on"] = topology.thread_llcs(("tfs-loadgen", "tfs-h2io", "tfs-nlane"))
@@ -505,6 +524,11 @@ def main():
         if r1["latency_us"]:
             p50_c1 = float(np.percentile(np.asarray(r1["latency_us"]), 50)) / 1e3
         del lg1
+    # the weight-replication group's own proof: an all-reduce of ones over it
+    # (every rank, same point, no load in flight); sum == group size, and the
+    # backend / size read from the group object (parallel/weights.py)
+    if weight_source is not None:
+        weight_source.verify_collective()
     lat = np.asarray(r["latency_us"], dtype=np.float64)
     if os.environ.get("TFSERVE_BENCH_DUMP") and rank == 0:
         np.save(os.environ["TFSERVE_BENCH_DUMP"], lat)      # completion-order latencies (diagnostics)
@@ -517,7 +541,8 @@ def main():
                "ref_client": my_ref_diag,
                "rank_timing": {"rank": rank, "ok": int(r["ok"]), "elapsed_s": round(elapsed, 6),
                                "start_sync_ms": cpu_report["start_sync_ms"],
-                               "end_sync_ms": cpu_report["end_sync_ms"]},
+                               "end_sync_ms": cpu_report["end_sync_ms"],
+                               "bracket_s": cpu_report["bracket_s"]},
                "rccl": weight_source.report() if weight_source is not None else None}
     if world > 1:
         allv = [torch.zeros_like(mine) for _ in range(world)]
@@ -572,7 +597,14 @@ def main():
             out["per_rank"] = [d["rank_timing"] for d in all_diag]
             out["rccl"] = [d["rccl"] for d in all_diag]
             rccl_bad = rccl_problems(out["rccl"], world)
-            out["rccl_ok"] = not rccl_bad
+            # rccl_ok only when the collectives really ran on RCCL (nccl) on
+            # GPUs; a gloo run (CPU, or TFSERVE_BENCH_BACKEND=gloo on shared
+            # GPUs) is flagged as a rehearsal whatever else it proves
+            backends = sorted({str(x.get("backend")) for x in out["rccl"] if x})
+            out["rccl_backend"] = backends[0] if len(backends) == 1 else backends
+            out["rehearsal"] = not (on_gpu and backends == ["nccl"])
+            out["replication_ok"] = not rccl_bad
+            out["rccl_ok"] = not rccl_bad and not out["rehearsal"]
             if rccl_bad:
                 out["rccl_problems"] = rccl_bad
         print(json.dumps(out), flush=True)
@@ -604,6 +636,8 @@ def rccl_problems(reports, world: int) -> list:
         who = f"rank {r['rank']}"
         if r["world"] != world:
             bad.append(f"{who}: group of {r['world']}")
+        if "allreduce_sum" in r and r["allreduce_sum"] != world:
+            bad.append(f"{who}: all-reduce of ones over the group summed to {r['allreduce_sum']}, not {world}")
         if r["leader"]:
             if r["broadcast_bytes"] <= 0:
                 bad.append(f"{who} (leader): broadcast nothing")

@@ -52,7 +52,11 @@ hipError_t launch_any(const tfsk::IGemmArgs& a, int a_mode, int64_t cfg, hipStre
 // profiles/round4/s13), and outside that launches of fewer than
 // kFixupAutoTiles tiles use it.
 constexpr long kFixupAutoTiles = 128;
-int g_fixup_override = -1;
+// per thread: the serving runtime sets it around ONE bucket's tuning + capture
+// on the capturing thread; eager launches of other threads (another
+// servable's warm-up / tuning) keep the default rule and never take eager
+// ring slices under a capture's mode
+thread_local int g_fixup_override = -1;
 int split_fixup_mode() {
   const char* v = std::getenv("TFSERVE_SPLITK_FIXUP");
   if (v && v[0] == '1') return 1;
@@ -536,8 +540,8 @@ std::tuple<Tensor, Tensor, bool> classifier_head_impl(const Tensor& x, const Ten
     counter = tfsk::splitk_counters(1, cur_stream(x));
   }
   // host rows only where the one-launch path runs (same conditions as the launcher)
-  const bool to_host = counter != nullptr && (probs_host != 0 || classes_host != 0) && HW <= 64 && n <= 4096 &&
-                       K <= 2048;
+  const bool to_host = counter != nullptr && (probs_host != 0 || classes_host != 0) &&
+                       tfsk::classifier_head_one_launch(M, HW, K, Np, int(n));
   check(tfsk::classifier_head_launch(bf16p(x), bf16p(w), bias.data_ptr<float>(), part.data_ptr<float>(),
                                      probs.data_ptr<float>(), classes.data_ptr<int64_t>(), M, HW, K, Np, int(n),
                                      cur_stream(x), counter,
@@ -761,6 +765,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_counters_release", [](int64_t owner) { return tfsk::splitk_counters_release(owner); },
         "return an owner's captured split-K counter slices to the pool");
   m.def("splitk_counters_captured_in_use", []() { return tfsk::splitk_counters_captured_in_use(); });
+  m.def("splitk_counters_reclaim", [](double min_age_s) { return tfsk::splitk_counters_reclaim(min_age_s); },
+        py::arg("min_age_s") = 2.0,
+        "zero released captured slices older than min_age_s and return them to the free list (call outside "
+        "any capture on this thread); returns the ints reclaimed");
+  m.def("splitk_counters_pending", []() { return tfsk::splitk_counters_pending(); });
   m.def("set_wg_trace", [](const c10::optional<Tensor>& t) {
     if (!t.has_value()) {
       g_trace = nullptr;
@@ -773,8 +782,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     g_trace_cap = int(std::min<int64_t>(t->numel() / 8, 1 << 30));
     tfsk::attention_set_trace(g_trace, g_trace_cap);
   }, "per-workgroup wall-clock stamps of the following GEMM / conv launches (None: off)");
-  m.def("set_splitk_fixup", [](int64_t mode) { g_fixup_override = mode < 0 ? -1 : (mode ? 1 : 0); },
-        "in-kernel split-K for the following launches: 1 on, 0 off, -1 default (env, else small launches)");
+  m.def("set_splitk_fixup", [](int64_t mode) {
+    const int prev = g_fixup_override;
+    g_fixup_override = mode < 0 ? -1 : (mode ? 1 : 0);
+    return prev;
+  }, "in-kernel split-K for this thread's following launches: 1 on, 0 off, -1 default (env, else small "
+     "launches); returns the previous mode (restore it when done)");
+  m.def("get_splitk_fixup", []() { return g_fixup_override; });
+  m.def("classifier_head_one_launch", [](int64_t M, int64_t HW, int64_t K, int64_t Np, int64_t n) {
+    return tfsk::classifier_head_one_launch(int(M), int(HW), int(K), int(Np), int(n));
+  });
   m.def("num_configs", []() { return tfsk::kNumIGemmConfigs; });
   m.def("cgemm_configs", []() {
     std::vector<int> v;
@@ -786,7 +803,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("halo_configs", []() {
     std::vector<int> v;
     for (int c = 0; c < tfsk::kNumHaloConfigs; ++c) v.push_back(tfsk::kHaloCfgBase + c);
-    for (int c = 0; c < tfsk::kNumHaloConfigs; ++c) v.push_back(tfsk::kHaloPfCfgBase + c);
+    for (int c = 0; c < tfsk::kNumHaloConfigs; ++c)
+      if (tfsk::halo_cfg_id(tfsk::kHaloPfCfgBase + c)) v.push_back(tfsk::kHaloPfCfgBase + c);
     return v;
   });
   m.def("config_tile", [](int cfg) {

@@ -44,9 +44,12 @@ constexpr int kHaloCfgBase = 48;
 constexpr int kNumHaloConfigs = 9;
 // the same halo tiles with the fragment-prefetch step pipeline (PF)
 constexpr int kHaloPfCfgBase = 80;
+// the PF build of tile 4 (256x128, 8 waves) does not fit the register budget
+// and is not instantiated: id 84 is not a config
+constexpr int kHaloPfMissing = 4;
 inline bool halo_cfg_id(int cfg) {
   return (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) ||
-         (cfg >= kHaloPfCfgBase && cfg < kHaloPfCfgBase + kNumHaloConfigs);
+         (cfg >= kHaloPfCfgBase && cfg < kHaloPfCfgBase + kNumHaloConfigs && cfg != kHaloPfCfgBase + kHaloPfMissing);
 }
 bool halo_supported(const IGemmArgs& a);
 int halo_config_bm(int cfg);

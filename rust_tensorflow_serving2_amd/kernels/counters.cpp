@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <map>
 #include <mutex>
@@ -20,7 +21,11 @@ constexpr int kPoolInts = 1 << 22;   // 16 MB per device
 // each graph capture) returns its slices to a free list when the runtime
 // releases the token as the graph is destroyed -- tuning candidates and
 // reload cycles no longer use the range up; slices taken without an owner
-// stay taken.  [kCapInts, kPoolInts): a ring for eager launches (autotuning,
+// stay taken.  A release only quarantines the slices (pending, stamped):
+// splitk_counters_reclaim zeroes the old-enough ones and frees them then, so
+// neither a replay still queued behind the dropped graph nor a counter left
+// non-zero by an abandoned lane can hand a later capture a live counter.
+// [kCapInts, kPoolInts): a ring for eager launches (autotuning,
 // warm-up), reused cyclically.  A maximal take (32K ints) wraps the 256K-int
 // ring after 8 launches; reuse is still safe because eager launches are
 // stream-ordered and counters return to zero when a tile's last slice
@@ -30,11 +35,17 @@ constexpr int kCapInts = 15 << 18;
 struct Range {
   int off, len;
 };
+using Clock = std::chrono::steady_clock;
+struct Pending {
+  Range r;
+  Clock::time_point at;
+};
 struct Pool {
   int* base = nullptr;
   int used = 0;
   int ring = kCapInts;
-  std::vector<Range> free_list;                     // released captured slices
+  std::vector<Range> free_list;                     // zeroed released slices, reusable
+  std::vector<Pending> pending;                     // released, not yet zeroed (quarantine)
   std::map<int64_t, std::vector<Range>> owned;      // owner token -> its captured slices
 };
 std::mutex g_mu;
@@ -115,17 +126,63 @@ int* splitk_counters(int n, hipStream_t s) {
 void splitk_counters_set_owner(int64_t owner) { g_owner = owner; }
 
 int64_t splitk_counters_release(int64_t owner) {
+  // no HIP call here: this runs from a Python finalizer on whatever thread
+  // dropped the graph (possibly one that is capturing)
   std::lock_guard<std::mutex> g(g_mu);
   int64_t n = 0;
+  const auto now = Clock::now();
   for (auto& kv : g_pools) {
     Pool& p = kv.second;
     auto it = p.owned.find(owner);
     if (it == p.owned.end()) continue;
     for (const Range& r : it->second) {
-      p.free_list.push_back(r);
+      p.pending.push_back(Pending{r, now});
       n += r.len;
     }
     p.owned.erase(it);
+  }
+  return n;
+}
+
+int64_t splitk_counters_pending() {
+  std::lock_guard<std::mutex> g(g_mu);
+  int64_t n = 0;
+  for (auto& kv : g_pools)
+    for (const Pending& q : kv.second.pending) n += q.r.len;
+  return n;
+}
+
+int64_t splitk_counters_reclaim(double min_age_s) {
+  std::lock_guard<std::mutex> g(g_mu);
+  int64_t n = 0;
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) return 0;
+  const auto now = Clock::now();
+  for (auto& kv : g_pools) {
+    Pool& p = kv.second;
+    if (p.pending.empty() || p.base == nullptr) continue;
+    std::vector<Range> ready;
+    std::vector<Pending> keep;
+    for (const Pending& q : p.pending) {
+      if (std::chrono::duration<double>(now - q.at).count() >= min_age_s) ready.push_back(q.r);
+      else keep.push_back(q);
+    }
+    if (ready.empty()) continue;
+    // zero them on a private non-blocking stream of that device and wait for
+    // that memset only (no device-wide synchronize: the lanes keep replaying)
+    if (hipSetDevice(kv.first) != hipSuccess) continue;
+    hipStream_t zs = nullptr;
+    bool ok = hipStreamCreateWithFlags(&zs, hipStreamNonBlocking) == hipSuccess;
+    for (const Range& r : ready)
+      ok = ok && hipMemsetAsync(p.base + r.off, 0, size_t(r.len) * sizeof(int), zs) == hipSuccess;
+    ok = ok && hipStreamSynchronize(zs) == hipSuccess;
+    if (zs != nullptr) hipStreamDestroy(zs);
+    if (!ok) continue;                               // stay quarantined; retried next time
+    p.pending.swap(keep);
+    for (const Range& r : ready) {
+      p.free_list.push_back(r);
+      n += r.len;
+    }
     // coalesce adjacent ranges (keeps first-fit effective over many cycles)
     std::sort(p.free_list.begin(), p.free_list.end(), [](const Range& a, const Range& b) { return a.off < b.off; });
     std::vector<Range> merged;
@@ -140,6 +197,7 @@ int64_t splitk_counters_release(int64_t owner) {
     }
     p.free_list.swap(merged);
   }
+  hipSetDevice(cur);
   return n;
 }
 
@@ -149,6 +207,7 @@ int64_t splitk_counters_captured_in_use() {
   for (auto& kv : g_pools) {
     n += kv.second.used;
     for (const Range& r : kv.second.free_list) n -= r.len;
+    for (const Pending& q : kv.second.pending) n -= q.r.len;
   }
   return n;
 }

@@ -75,8 +75,16 @@ void splitk_counters_prepare(hipStream_t s);
 // Captured slices taken on this thread while `owner` != 0 belong to that
 // owner; splitk_counters_release(owner) returns them to the pool (call it when
 // the graph captured under the token is destroyed).  Returns the ints freed.
+// Released slices are quarantined, not reused at once: a replay of the
+// dropped graph may still be queued, or a lane abandoned mid-count may have
+// left a counter non-zero.  splitk_counters_reclaim(min_age_s), called outside
+// any capture (the runtime calls it before each capture), zeroes the slices
+// released at least min_age_s ago on a private stream, waits for that memset
+// alone, and only then returns them to the free list.
 void splitk_counters_set_owner(int64_t owner);
 int64_t splitk_counters_release(int64_t owner);
+int64_t splitk_counters_reclaim(double min_age_s);
+int64_t splitk_counters_pending();
 int64_t splitk_counters_captured_in_use();
 
 // kAStem7x7x3: fp32 NHWC input with C == 3 and a 7-wide filter (the ResNet
@@ -146,6 +154,9 @@ hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const fl
                                   hipStream_t s, int* counter = nullptr, float* probs_h = nullptr,
                                   int64_t* classes_h = nullptr);
 size_t classifier_head_ws_floats(int M, int K, int Np);
+// The shapes classifier_head_launch runs as ONE launch (given a counter): the
+// only path that can store host rows.  Callers decide on host rows with it.
+bool classifier_head_one_launch(int M, int HW, int K, int Np, int N);
 // BERT head: probs[r] = softmax(x[r] @ w^T + bias) over N <= 16 labels (x fp32)
 hipError_t dense_softmax_launch(const float* x, int ldx, const uint16_t* w, int ldw, const float* bias,
                                 float* probs, int rows, int N, int K, hipStream_t s);

@@ -975,6 +975,12 @@ __global__ __launch_bounds__(256) void head_small_kernel(const uint16_t* __restr
   if (probs_h || classes_h) __threadfence_system();   // host rows visible with the kernel's completion
 }
 
+bool classifier_head_one_launch(int M, int HW, int K, int Np, int N) {
+  if (M <= 0 || HW <= 0 || N <= 0 || N > Np || K % (kHeadKS * 4 * 32)) return false;
+  const int ksteps = K / kHeadKS / 4 / 32;
+  return M <= kHeadSmallM && HW <= kHeadSmallHW && N <= kSmPer * 256 && (ksteps == 1 || ksteps == 2 || ksteps == 4);
+}
+
 hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const float* bias, float* ws, float* probs,
                                   int64_t* classes, int M, int HW, int K, int Np, int N, hipStream_t s,
                                   int* counter, float* probs_h, int64_t* classes_h) {
@@ -983,8 +989,7 @@ hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const fl
   const int ksteps = K / kHeadKS / 4 / 32;        // 32-deep MFMA steps per wave
   uint16_t* pooled = reinterpret_cast<uint16_t*>(ws);
   float* part = ws + (size_t(M) * K + 1) / 2;
-  if (counter != nullptr && M <= kHeadSmallM && HW <= kHeadSmallHW && N <= kSmPer * 256 &&
-      (ksteps == 1 || ksteps == 2 || ksteps == 4)) {
+  if (counter != nullptr && classifier_head_one_launch(M, HW, K, Np, N)) {
     const dim3 grid(kHeadKS, (Np + kHeadCols - 1) / kHeadCols);
     const float inv_hw = 1.f / float(HW);
     switch (ksteps) {

@@ -375,11 +375,13 @@ def splitk_fixup_for_bucket(bucket: int):
     except KernelsUnavailable:
         yield
         return
-    h.set_splitk_fixup(1 if bucket <= FIXUP_MAX_BUCKET else 0)
+    # thread-local in the extension (the capture runs on this thread); the
+    # previous mode is restored, so nested / re-entrant use composes
+    prev = h.set_splitk_fixup(1 if bucket <= FIXUP_MAX_BUCKET else 0)
     try:
         yield
     finally:
-        h.set_splitk_fixup(-1)
+        h.set_splitk_fixup(-1 if prev is None else int(prev))
 
 
 _HEAD_ROWS = threading.local()
@@ -405,6 +407,7 @@ def current_head_host_rows():
 
 
 _OWNER_SEQ = itertools.count(1)
+_RECLAIM_AGE_S = float(os.environ.get("TFSERVE_COUNTER_QUARANTINE_S", "2.0"))
 _GC_HOLD = [0]
 _GC_LOCK = threading.Lock()
 
@@ -445,6 +448,10 @@ def capture_owner(graph):
         except KernelsUnavailable:
             yield None
             return
+        # slices released by dropped graphs come back zeroed, after their
+        # quarantine, before this capture can take them (kernels/counters.cpp)
+        if hasattr(h, "splitk_counters_reclaim"):
+            h.splitk_counters_reclaim(_RECLAIM_AGE_S)
         tok = next(_OWNER_SEQ)
         h.splitk_counters_set_owner(tok)
         try:

@@ -117,6 +117,34 @@ _META_DT = {T.DT_FLOAT: torch.float32, T.DT_HALF: torch.float16, T.DT_BFLOAT16: 
             T.DT_DOUBLE: torch.float64}
 
 
+def pg_backend(pg) -> Optional[str]:
+    """The backend a process group actually runs ("nccl" = RCCL on ROCm,
+    "gloo"), read from the group object itself -- never inferred from the
+    device the tensors live on (a gloo rehearsal on GPUs must not report
+    itself as RCCL)."""
+    if pg is None:
+        return None
+    try:
+        return str(dist.get_backend(pg)).lower()
+    except Exception:
+        pass
+    try:
+        return str(pg.name()).lower()
+    except Exception:
+        return None
+
+
+def pg_size(pg) -> Optional[int]:
+    """Ranks in the communicator (from the group object, not the launcher's env)."""
+    try:
+        return int(pg.size())
+    except Exception:
+        try:
+            return int(dist.get_world_size(pg))
+        except Exception:
+            return None
+
+
 class _StreamMark:
     """Stream-ordered completion of a collective on ``device``: an event
     recorded on the current stream (which ``Work.wait()`` has made wait for the
@@ -261,7 +289,7 @@ class ReplicatedWeightSource:
                  load_timeout: float = 900.0, prefix: str = "tfs/wev", tuned_timeout: float = 600.0,
                  program_timeout: float = 120.0, share: Optional[bool] = None, rank: Optional[int] = None,
                  world: Optional[int] = None, restarted: bool = False, pg_timeout_s: float = 300.0,
-                 dead_after_s: float = 3.0):
+                 dead_after_s: float = 3.0, backend: Optional[str] = None):
         self.store = store
         if rank is None or world is None:
             rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -272,7 +300,18 @@ class ReplicatedWeightSource:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
                 else torch.device("cpu")
         self.device = device
-        self.backend = "nccl" if device.type == "cuda" else "gloo"
+        # the backend of the group the collectives really run on: the default
+        # group's (or ``group``'s) when one exists -- bench.py's gloo rehearsal
+        # on GPUs then stages through the host (broadcast_blob) and re-forms
+        # gloo groups in later generations; a restarted replica without a
+        # default group uses ``backend`` / TFSERVE_WEIGHT_BACKEND / the device
+        pg0 = None
+        if dist.is_initialized():
+            pg0 = group if group is not None else dist.distributed_c10d._get_default_group()
+        self.backend = (backend or pg_backend(pg0) or os.environ.get("TFSERVE_WEIGHT_BACKEND")
+                        or ("nccl" if device.type == "cuda" else "gloo"))
+        if self.backend not in ("nccl", "gloo"):
+            raise ValueError(f"weight replication needs an nccl (RCCL) or gloo group, not {self.backend!r}")
         # GPU replicas share the leader's compiled device weights; CPU replicas
         # (tests, control-plane-only deployments) read the disk each unless
         # asked to rehearse the protocol (share=True / TFSERVE_SHARE_WEIGHTS=1)
@@ -649,14 +688,40 @@ class ReplicatedWeightSource:
             time.sleep(0.02)
         return json.loads(self.store.get(sk).decode())
 
+    def verify_collective(self) -> dict:
+        """Collective (every rank of the current generation calls it at the
+        same point, with no load in flight): an all-reduce of ones over the
+        weight-replication group.  The sum must equal the group's size; the
+        backend and size are read from the group object.  bench.py's ``rccl``
+        block reports this, so a run whose "RCCL" was really gloo, or whose
+        communicator is smaller than the launch, cannot pass as RCCL."""
+        comm = self.comm
+        if comm is None:
+            comm = self._ensure_comm(max(0, self._current_gen()))
+        dev = comm._dev()
+        t = torch.ones(1, dtype=torch.float32, device=dev)
+        t0 = time.perf_counter()
+        comm.pg.allreduce([t]).wait()
+        _StreamMark(comm.device if dev.type == "cuda" else torch.device("cpu")).wait()
+        out = {"allreduce_sum": float(t.item()), "allreduce_s": round(time.perf_counter() - t0, 6),
+               "pg_backend": pg_backend(comm.pg), "pg_size": pg_size(comm.pg),
+               "allreduce_device": str(dev)}
+        self.stats["verify"] = out
+        return out
+
     def report(self) -> dict:
         """This rank's replication figures (bench.py's ``rccl`` block):
-        backend, group size, generation, bytes / seconds of device-blob
-        broadcast, loads received over the collective vs read from disk, and
-        the weight bytes this process copied host -> device itself (a
-        follower that really bound the leader's blob copies none)."""
+        the backend and size of the group the collectives ran on (read from
+        the process-group object), generation, bytes / seconds of device-blob
+        broadcast, loads received over the collective vs read from disk, the
+        weight bytes this process copied host -> device itself (a follower
+        that really bound the leader's blob copies none) and the last
+        ``verify_collective`` result."""
         st = dict(self.stats)
-        return {"backend": self.backend, "world": self.world, "rank": self.rank, "leader": self.is_leader,
+        pg = self.comm.pg if self.comm is not None else None
+        backend = pg_backend(pg) or self.backend
+        world = pg_size(pg) or self.world
+        return {"backend": backend, "world": world, "rank": self.rank, "leader": self.is_leader,
                 "gen": self.gen, "broadcast_bytes": int(st.get("broadcast_bytes", 0)),
                 "broadcast_s": round(float(st.get("broadcast_s", 0.0)), 6),
                 "programs": int(st.get("programs", 0)), "bound_bytes": int(st.get("bound_bytes", 0)),
@@ -664,7 +729,10 @@ class ReplicatedWeightSource:
                 "comm_failures": int(st.get("comm_failures", 0)),
                 "recompiles": int(st.get("recompiles", 0)),
                 "recompile_reasons": list(st.get("recompile_reasons", []))[:4],
-                "weight_h2d_bytes": int(placement.H2D_BYTES)}
+                "weight_h2d_bytes": int(placement.H2D_BYTES),
+                "blob_path": ("host-staged" if self.device.type == "cuda" and backend == "gloo" else
+                              "device-to-device" if self.device.type == "cuda" else "host"),
+                **{k: v for k, v in (st.get("verify") or {}).items()}}
 
     def close(self):
         self._stop.set()

@@ -49,9 +49,15 @@ def test_bench_gpus2_self_launch_cpu(tmp_path):
     # the weight replication the driver's scaling run depends on: the follower
     # received the leader's compiled weights over the collective (gloo here,
     # RCCL on the GPUs), read nothing from disk, copied no weight to a device
-    assert out["rccl_ok"] is True and "rccl_problems" not in out, out.get("rccl_problems")
+    # the replication protocol passed, but over gloo: a rehearsal, never "RCCL ok"
+    assert out["replication_ok"] is True and "rccl_problems" not in out, out.get("rccl_problems")
+    assert out["rehearsal"] is True and out["rccl_ok"] is False and out["rccl_backend"] == "gloo"
     lead, fol = out["rccl"]
     assert lead["leader"] and lead["backend"] == "gloo" and lead["world"] == 2
+    # backend / size read from the group object, and an all-reduce of ones over it
+    for x in (lead, fol):
+        assert x["pg_backend"] == "gloo" and x["pg_size"] == 2 and x["allreduce_sum"] == 2.0, x
+        assert x["blob_path"] == "host"
     assert lead["broadcast_bytes"] > 0 and lead["programs"] >= 1
     assert not fol["leader"] and fol["disk_loads"] == 0 and fol["weight_h2d_bytes"] == 0
     assert fol["bcast_loads"] >= 1 and fol["bound_bytes"] > 0
@@ -62,6 +68,8 @@ def test_bench_gpus2_self_launch_cpu(tmp_path):
     pr = out["per_rank"]
     assert [x["rank"] for x in pr] == [0, 1] and all(x["ok"] > 0 and x["elapsed_s"] > 0 for x in pr)
     assert all("start_sync_ms" in x and "end_sync_ms" in x for x in pr)
+    # the timed region ends at the last counted completion, inside the bracket
+    assert all(x["bracket_s"] >= x["elapsed_s"] for x in pr)
 
 
 def test_rccl_problems_flags_silent_fallbacks():
@@ -79,6 +87,9 @@ def test_rccl_problems_flags_silent_fallbacks():
     assert bench.rccl_problems([lead, dict(good, bound_bytes=0)], 2)
     assert bench.rccl_problems([dict(lead, broadcast_bytes=0), good], 2)
     assert bench.rccl_problems([lead, None], 2)
+    # the all-reduce of ones over the group must sum to the launch's world size
+    assert bench.rccl_problems([dict(lead, allreduce_sum=2.0), dict(good, allreduce_sum=2.0)], 2) == []
+    assert bench.rccl_problems([dict(lead, allreduce_sum=1.0), good], 2)
 
 
 @pytest.mark.timeout(200)

@@ -669,6 +669,39 @@ def test_splitk_counter_slices_return_with_their_graph(monkeypatch):
         del g
         gc.collect()
         assert hip().splitk_counters_captured_in_use() == base, cycle
+        # released slices are quarantined until reclaimed (zeroed, then freed)
+        assert hip().splitk_counters_pending() > 0
+        assert hip().splitk_counters_reclaim(0.0) > 0
+        assert hip().splitk_counters_pending() == 0
+        assert hip().splitk_counters_captured_in_use() == base, cycle
+
+
+def test_splitk_fixup_override_is_thread_local_and_restored():
+    """ops.splitk_fixup_for_bucket sets the in-kernel split-K mode for the
+    capturing thread only and restores the previous mode."""
+    import threading
+    from rust_tensorflow_serving2_amd import ops
+    h = hip()
+    assert h.get_splitk_fixup() == -1
+    seen = []
+    with ops.splitk_fixup_for_bucket(1):
+        assert h.get_splitk_fixup() == 1
+        with ops.splitk_fixup_for_bucket(32):
+            assert h.get_splitk_fixup() == 0
+        assert h.get_splitk_fixup() == 1
+        t = threading.Thread(target=lambda: seen.append(h.get_splitk_fixup()))
+        t.start()
+        t.join()
+    assert seen == [-1] and h.get_splitk_fixup() == -1
+
+
+def test_classifier_head_host_rows_follow_the_launcher_predicate():
+    h = hip()
+    assert h.classifier_head_one_launch(1, 49, 2048, 1001, 1001)
+    assert not h.classifier_head_one_launch(1, 49, 4096, 1001, 1001)     # 8 k-steps: three launches
+    assert not h.classifier_head_one_launch(1, 49, 1536, 1001, 1001)
+    assert not h.classifier_head_one_launch(32, 49, 2048, 1001, 1001)
+    assert 84 not in h.halo_configs() and 80 in h.halo_configs()
 
 
 # ResNet stem fused with its max pool (stem.hip): fp32 RGB in, pooled bf16 out.
