@@ -14,10 +14,14 @@ constexpr int kNumCGemmConfigs2 = 9;
 // a third range: fragment-prefetch (PF) builds of 11 of the tiles above
 constexpr int kCGemmPfCfgBase = 96;
 constexpr int kNumCGemmPfConfigs = 11;
+// a fourth range: v_mfma_f32_32x32x16_bf16 builds (wave tiles in 32x32 blocks)
+constexpr int kCGemm32CfgBase = 112;
+constexpr int kNumCGemm32Configs = 12;
 inline bool cgemm_cfg_id(int cfg) {
   return (cfg >= kCGemmCfgBase && cfg < kCGemmCfgBase + kNumCGemmConfigs) ||
          (cfg >= kCGemmCfgBase2 && cfg < kCGemmCfgBase2 + kNumCGemmConfigs2) ||
-         (cfg >= kCGemmPfCfgBase && cfg < kCGemmPfCfgBase + kNumCGemmPfConfigs);
+         (cfg >= kCGemmPfCfgBase && cfg < kCGemmPfCfgBase + kNumCGemmPfConfigs) ||
+         (cfg >= kCGemm32CfgBase && cfg < kCGemm32CfgBase + kNumCGemm32Configs);
 }
 
 // Operand requirements (else cgemm_launch returns hipErrorInvalidValue):
@@ -30,6 +34,8 @@ bool cgemm_supported(const IGemmArgs& a, int a_mode);
 int cgemm_config_bm(int cfg);
 int cgemm_config_bn(int cfg);
 hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t stream);
+// the 32x32x16 builds (cgemm32.hip), table index idx = cfg - kCGemm32CfgBase
+hipError_t cgemm32_launch(const IGemmArgs& a, int a_mode, int idx, hipStream_t stream);
 // the config can finish split-K in-kernel (IGemmArgs::counters)
 bool cgemm_fixup_ok(int cfg);
 // workgroups (= tiles) of a halo launch (its split-K counters)

@@ -155,6 +155,10 @@ CGEMM = {32: (128, 128), 33: (128, 128), 34: (64, 128), 35: (128, 64), 36: (64, 
 # fragment-prefetch (PF) builds of 11 of those tiles (kernels/cgemm.hip kPfOf)
 CGEMM_PF_OF = [32, 34, 35, 36, 39, 41, 42, 43, 44, 45, 71]
 CGEMM.update({96 + k: CGEMM[base] for k, base in enumerate(CGEMM_PF_OF)})
+# v_mfma_f32_32x32x16_bf16 builds (kernels/cgemm32.hip, ids 112..123: wave tiles in 32x32 blocks)
+CGEMM32 = {112: (64, 64), 113: (64, 64), 114: (128, 128), 115: (128, 64), 116: (64, 128), 117: (128, 256),
+           118: (256, 128), 119: (256, 64), 120: (128, 128), 121: (64, 128), 122: (128, 64), 123: (256, 192)}
+CGEMM.update(CGEMM32)
 TILES.update(CGEMM)
 # halo-tiled 3x3 stride-1 conv (kernels/halo.hip): config id -> (output pixels per tile, BN)
 HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 128), 53: (64, 128), 54: (64, 64),

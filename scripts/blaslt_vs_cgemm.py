@@ -1,9 +1,12 @@
-"""hipBLASLt (torch._addmm_activation: bias + ReLU epilogue) vs our tuned cgemm on
-the ResNet-50 1x1 convs without a residual, timed like the serving graph runs
-them: captured in a HIP graph, rotating over 8 operand copies (L2-cold).
+"""hipBLASLt (torch._addmm_activation: bias + ReLU epilogue; torch.matmul for
+the BERT shapes) vs our tuned cgemm, timed like the serving graph runs them:
+captured in a HIP graph, rotating over 8 operand copies (L2-cold).  A library
+anchor for comparison only: the serving path never calls the library.
 
-    python scripts/blaslt_vs_cgemm.py
+    python scripts/blaslt_vs_cgemm.py                 # ResNet-50 1x1 convs
+    python scripts/blaslt_vs_cgemm.py --set bert      # BERT-base b32's four GEMMs (M = 4096)
 """
+import argparse
 import json
 import os
 import sys
@@ -21,16 +24,24 @@ SHAPES = {  # name: (M, N, K) at b32
     "s4_1024_512_14": (6272, 512, 1024), "s4_2048_512": (1568, 512, 2048),
     "b1_s3_1024_256": (196, 256, 1024), "b1_s4_2048_512": (49, 512, 2048),
 }
+BERT = {"qkv": (4096, 2304, 768), "ffn1": (4096, 3072, 768), "ffn2": (4096, 768, 3072),
+        "attn_out": (4096, 768, 768)}
 
 
 def main():
-    for name, (M, N, K) in SHAPES.items():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--set", default="resnet", choices=["resnet", "bert"])
+    a = ap.parse_args()
+    for name, (M, N, K) in (BERT if a.set == "bert" else SHAPES).items():
         xs = [torch.randn(M, K, device="cuda").to(BF) for _ in range(8)]
         ws = [(torch.randn(N, K, device="cuda") * 0.05).to(BF) for _ in range(8)]
         b = torch.zeros(N, device="cuda", dtype=BF)
         bf = torch.zeros(N, device="cuda")
         outs = [torch.empty(M, N, device="cuda", dtype=BF) for _ in range(8)]
-        t_lt = time_graph(lambda i: torch._addmm_activation(b, xs[i % 8], ws[i % 8].t(), use_gelu=False))
+        if a.set == "bert":
+            t_lt = time_graph(lambda i: torch.matmul(xs[i % 8], ws[i % 8].t(), out=outs[i % 8]))
+        else:
+            t_lt = time_graph(lambda i: torch._addmm_activation(b, xs[i % 8], ws[i % 8].t(), use_gelu=False))
         best = (1e9, None)
         for cfg, sp in candidates(M, N, K, True, True):
             try:
@@ -39,8 +50,10 @@ def main():
             except RuntimeError:
                 continue
             best = min(best, (t, (cfg, sp)))
+        tf = 2 * M * N * K / 1e6
         print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "hipblaslt_us": round(t_lt, 2),
-                          "cgemm_us": round(best[0], 2), "cgemm_cfg": best[1]}), flush=True)
+                          "hipblaslt_tflops": round(tf / t_lt), "cgemm_us": round(best[0], 2),
+                          "cgemm_tflops": round(tf / best[0]), "cgemm_cfg": best[1]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -76,7 +76,7 @@ def test_conv_matches_fp32(shape, cfg, splits):
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
 
 
-CGEMM_CFGS = list(range(32, 48)) + list(range(64, 73)) + list(range(96, 107))
+CGEMM_CFGS = list(range(32, 48)) + list(range(64, 73)) + list(range(96, 107)) + list(range(112, 124))
 CGEMM_CONV_SHAPES = [s for s in CONV_SHAPES if s[3] % 64 == 0] + [
     (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)),   # tiny image: most taps hit padding at the border rows
     (1, 15, 13, 64, 192, 3, 2, (0, 1, 1, 1)),  # odd sizes, asymmetric pads, N tail
@@ -192,7 +192,7 @@ def test_cgemm_asymmetric_identity(cfg):
 
 @pytest.mark.parametrize("n,ho,c1,h,c2,s,cout", [(2, 56, 64, 56, 64, 1, 256), (2, 28, 128, 56, 256, 2, 512),
                                                  (1, 7, 512, 14, 1024, 2, 2048), (1, 5, 64, 9, 128, 2, 72)])
-@pytest.mark.parametrize("cfg", [32, 36, 42, 43, 44, 45, 47])
+@pytest.mark.parametrize("cfg", [32, 36, 42, 43, 44, 45, 47, 112, 114, 117, 121])
 def test_conv2d_dual_matches_fp32(n, ho, c1, h, c2, s, cout, cfg):
     """One GEMM for a bottleneck tail: relu(conv1x1(h) + conv1x1_stride(x) + b)."""
     hh = rnd(n, ho, ho, c1, seed=21).to(BF)
@@ -257,7 +257,7 @@ def test_rgba_stem_path(k, c):
 
 
 @pytest.mark.parametrize("k,c,s", [(7, 3, 2), (3, 3, 1), (5, 4, 2), (1, 3, 1)])
-@pytest.mark.parametrize("cfg", [36, 42, 43, 44, 32])
+@pytest.mark.parametrize("cfg", [36, 42, 43, 44, 32, 112, 114])
 def test_cgemm_padded_rgba_stem(k, c, s, cfg):
     """ingest_c4_padded (zero-bordered bf16 RGBA) + cgemm stem mode (even kh,
     8 taps: every operand chunk is two in-bounds pixels) vs the fp32 conv."""
@@ -525,6 +525,8 @@ def test_attention_matches_fp32(s):
     (44, 1, (2, 28, 28, 128, 128, 3, 2, (1, 1, 1, 1))),     # im2col, strided
     (48, 1, (2, 28, 28, 128, 128, 3, 1, (1, 1, 1, 1))),     # halo 3x3
     (51, 2, (1, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1))),       # halo, split over channel chunks
+    (117, 1, (2, 14, 14, 256, 256, 1, 1, (0, 0, 0, 0))),    # 32x32 MFMA build
+    (113, 2, (2, 28, 28, 128, 128, 3, 2, (1, 1, 1, 1))),    # 32x32 MFMA build, im2col, split-K
 ])
 def test_conv_post_activation_outputs(cfg, splits, shape):
     """ResNet v2 epilogue: one conv writes the block sum y (+bias +residual)
@@ -598,6 +600,7 @@ def test_maxpool_post_affine():
     (42, 3, (2, 14, 14, 256, 256, 1, 1, (0, 0, 0, 0)), True),     # cgemm dense 1x1, post output
     (51, 4, (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)), False),      # halo, split over channel chunks
     (54, 2, (3, 14, 14, 256, 256, 3, 1, (1, 1, 1, 1)), True),     # 9-slot halo, post output
+    (114, 2, (2, 14, 14, 256, 256, 1, 1, (0, 0, 0, 0)), True),    # 32x32 MFMA build, post output
 ])
 def test_splitk_in_kernel_fixup_inside_graph(cfg, splits, shape, post, monkeypatch):
     """Captured in a HIP graph, split-K finishes in-kernel (the last slice of a
