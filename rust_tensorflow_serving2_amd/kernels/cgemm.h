@@ -17,11 +17,15 @@ constexpr int kNumCGemmPfConfigs = 11;
 // a fourth range: v_mfma_f32_32x32x16_bf16 builds (wave tiles in 32x32 blocks)
 constexpr int kCGemm32CfgBase = 112;
 constexpr int kNumCGemm32Configs = 12;
+// a fifth range: 32-deep k-tiles (twice the ring slots in the same LDS)
+constexpr int kCGemmKt32CfgBase = 124;
+constexpr int kNumCGemmKt32Configs = 6;
 inline bool cgemm_cfg_id(int cfg) {
   return (cfg >= kCGemmCfgBase && cfg < kCGemmCfgBase + kNumCGemmConfigs) ||
          (cfg >= kCGemmCfgBase2 && cfg < kCGemmCfgBase2 + kNumCGemmConfigs2) ||
          (cfg >= kCGemmPfCfgBase && cfg < kCGemmPfCfgBase + kNumCGemmPfConfigs) ||
-         (cfg >= kCGemm32CfgBase && cfg < kCGemm32CfgBase + kNumCGemm32Configs);
+         (cfg >= kCGemm32CfgBase && cfg < kCGemm32CfgBase + kNumCGemm32Configs) ||
+         (cfg >= kCGemmKt32CfgBase && cfg < kCGemmKt32CfgBase + kNumCGemmKt32Configs);
 }
 
 // Operand requirements (else cgemm_launch returns hipErrorInvalidValue):
@@ -36,6 +40,8 @@ int cgemm_config_bn(int cfg);
 hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t stream);
 // the 32x32x16 builds (cgemm32.hip), table index idx = cfg - kCGemm32CfgBase
 hipError_t cgemm32_launch(const IGemmArgs& a, int a_mode, int idx, hipStream_t stream);
+// the 32-deep k-tile builds (cgemm_kt32.hip), idx = cfg - kCGemmKt32CfgBase
+hipError_t cgemm_kt32_launch(const IGemmArgs& a, int a_mode, int idx, hipStream_t stream);
 // the config can finish split-K in-kernel (IGemmArgs::counters)
 bool cgemm_fixup_ok(int cfg);
 // workgroups (= tiles) of a halo launch (its split-K counters)

@@ -54,9 +54,13 @@ constexpr int kPfOf[kNumCGemmPfConfigs] = {0, 2, 3, 4, 7, 9, 10, 11, 12, 13, 23}
 // 32x32x16 MFMA builds (ids kCGemm32CfgBase + i): BM x BN, wave grid, ring depth
 constexpr int k32BM[kNumCGemm32Configs] = {64, 64, 128, 128, 64, 128, 256, 256, 128, 64, 128, 256};
 constexpr int k32BN[kNumCGemm32Configs] = {64, 64, 128, 64, 128, 256, 128, 64, 128, 128, 64, 192};
+// 32-deep k-tile builds (ids kCGemmKt32CfgBase + i, cgemm_kt32.hip)
+constexpr int kK32BM[kNumCGemmKt32Configs] = {256, 256, 256, 128, 128, 128};
+constexpr int kK32BN[kNumCGemmKt32Configs] = {192, 192, 128, 256, 128, 96};
 
 // config id -> index into the tables (all id ranges; the 32x32 range indexes k32BM / k32BN)
 int cfg_index(int cfg) {
+  if (cfg >= kCGemmKt32CfgBase) return cfg - kCGemmKt32CfgBase;
   if (cfg >= kCGemm32CfgBase) return cfg - kCGemm32CfgBase;
   if (cfg >= kCGemmPfCfgBase) return kPfOf[cfg - kCGemmPfCfgBase];
   return cfg < kCGemmCfgBase2 ? cfg - kCGemmCfgBase : kNumCGemmConfigs + (cfg - kCGemmCfgBase2);
@@ -125,10 +129,12 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
 }  // namespace
 
 int cgemm_config_bm(int cfg) {
-  return cfg >= kCGemm32CfgBase ? k32BM[cfg_index(cfg)] : kBM[cfg_index(cfg)];
+  return cfg >= kCGemmKt32CfgBase ? kK32BM[cfg_index(cfg)]
+         : cfg >= kCGemm32CfgBase ? k32BM[cfg_index(cfg)] : kBM[cfg_index(cfg)];
 }
 int cgemm_config_bn(int cfg) {
-  return cfg >= kCGemm32CfgBase ? k32BN[cfg_index(cfg)] : kBN[cfg_index(cfg)];
+  return cfg >= kCGemmKt32CfgBase ? kK32BN[cfg_index(cfg)]
+         : cfg >= kCGemm32CfgBase ? k32BN[cfg_index(cfg)] : kBN[cfg_index(cfg)];
 }
 
 bool cgemm_fixup_ok(int cfg) {
@@ -156,10 +162,8 @@ bool cgemm_supported(const IGemmArgs& a, int a_mode) {
 
 hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) {
   if (!cgemm_cfg_id(cfg) || !cgemm_supported(a, a_mode)) return hipErrorInvalidValue;
-  if (cfg >= kCGemm32CfgBase) {
-    const int idx = cfg_index(cfg);
-    return cgemm32_launch(a, a_mode, idx, s);
-  }
+  if (cfg >= kCGemmKt32CfgBase) return cgemm_kt32_launch(a, a_mode, cfg_index(cfg), s);
+  if (cfg >= kCGemm32CfgBase) return cgemm32_launch(a, a_mode, cfg_index(cfg), s);
   if (cfg >= kCGemmPfCfgBase) {
     const int idx = cfg_index(cfg);
     switch (a_mode) {

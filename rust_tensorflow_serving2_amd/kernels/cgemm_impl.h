@@ -15,15 +15,27 @@ namespace cgemm_impl {
 using namespace gemm;
 constexpr int kGroupM = 8;
 
-template <int BM, int BN, int WGM, int WGN, int S, int MF = 16>
+template <int BM, int BN, int WGM, int WGN, int S, int MF = 16, int KTT = 64>
 struct CG {
   static constexpr int NW = WGM * WGN, NT = 64 * NW;
   static constexpr int WM = BM / WGM, WN = BN / WGN;
   // MF = 16: v_mfma_f32_16x16x32_bf16 tiles; MF = 32: v_mfma_f32_32x32x16_bf16
   static constexpr int TM = WM / MF, TN = WN / MF;
-  static constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW);   // 1-KB DMA pieces per wave per stage
-  static constexpr int PPW = APW + BPW;
-  static constexpr int A_ST = BM * KT, B_ST = BN * KT;            // elements per ring slot
+  // KTT: k-tile depth (LDS row = KTT * 2 bytes).  64 = one 128-B row per ring
+  // slot row; 32 halves a ring slot, so the same LDS holds twice the slots:
+  // the 256 x 192 tile then keeps 4 k-tiles in flight instead of 1
+  static constexpr int CPR = KTT / 8;                              // 16-B chunks per LDS row
+  static constexpr int RPD = 64 / CPR;                             // rows per 1-KB DMA piece
+  // 1-KB DMA pieces per stage (NAP of A, NBP of B) over NW waves.  An even
+  // split gives wave w the contiguous pieces w * APW ..; an uneven one (the
+  // 192-row B tile in 16-row pieces: 12 over 8 waves) deals piece j * NW + w,
+  // so some waves issue one piece more: every vmcnt wait then counts the
+  // fewest pieces any wave issues per stage (PPW), which over-waits, never under
+  static constexpr int NAP = BM / RPD, NBP = BN / RPD;
+  static constexpr bool A_EVEN = NAP % NW == 0, B_EVEN = NBP % NW == 0;
+  static constexpr int APW = (NAP + NW - 1) / NW, BPW = (NBP + NW - 1) / NW;   // per wave (at most)
+  static constexpr int PPW = NAP / NW + NBP / NW;
+  static constexpr int A_ST = BM * KTT, B_ST = BN * KTT;          // elements per ring slot
   static constexpr int LDS_MAIN = S * (A_ST + B_ST) * 2;
   static constexpr int CS_LD = BN + 4;
   // the fp32 tile is staged through LDS for the epilogue; a tile whose fp32
@@ -35,10 +47,11 @@ struct CG {
   static constexpr int LDS_EPI = RPP * CS_LD * 4;
   static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
   static_assert(RPP % WM == 0, "epilogue passes split the tile at wave-row boundaries");
-  static_assert(APW >= 1 && BPW >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "DMA piece split");
+  static_assert(KTT == 64 || KTT == 32, "k-tile depth");
+  static_assert(BM % RPD == 0 && BN % RPD == 0 && NAP >= NW && NBP >= NW, "DMA piece split");
   static_assert(MF == 16 || MF == 32, "MFMA shape");
   static_assert(TM >= 1 && TN >= 1 && WM % MF == 0 && WN % MF == 0, "wave tile");
-  static_assert(S >= 2 && (S - 2) * PPW < 64, "ring depth / vmcnt range");
+  static_assert(S >= 2 && (S - 2) * PPW < 64 && (S - 2) * (APW + BPW) < 64, "ring depth / vmcnt range");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
@@ -99,9 +112,9 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
 // Waves per SIMD the register allocation must leave room for: the 4-wave
 // 32-KB tiles (64x64, 2 slots) fit 5 workgroups per CU by LDS, i.e. 5 waves
 // per SIMD, which needs <= 102 VGPRs (unconstrained they took 128: 4 per CU)
-template <int BM, int BN, int WGM, int WGN, int S, bool PF, int MF = 16>
+template <int BM, int BN, int WGM, int WGN, int S, bool PF, int MF = 16, int KTT = 64>
 constexpr int cg_waves_per_eu() {
-  return (!PF && WGM * WGN == 4 && CG<BM, BN, WGM, WGN, S, MF>::LDS <= 32 * 1024) ? 5 : 1;
+  return (!PF && WGM * WGN == 4 && CG<BM, BN, WGM, WGN, S, MF, KTT>::LDS <= 32 * 1024) ? 5 : 1;
 }
 
 // LDS image swizzle: 16-B chunk c of tile row r sits in slot c ^ swz(r).  The
@@ -110,18 +123,25 @@ constexpr int cg_waves_per_eu() {
 // conflict-free with (r >> 1) & 7, which also keeps the 16x16 reads
 // conflict-free (ds_read_b128 lane groups, MI355X_MICROARCH.md LDS table;
 // checked by brute force over every group and k-subtile).
-template <int MF>
-__device__ __forceinline__ int lds_swz(int r) { return MF == 32 ? (r >> 1) & 7 : r & 7; }
+// 64-B rows (KTT = 32; 4 chunks, a 256-B bank row holds 4 rows): chunk c of
+// row r in slot c ^ (bit 3 of r) * 2 ^ (bit 4 of r), conflict-free for both
+// MFMA shapes (same brute-force check).
+template <int MF, int KTT = 64>
+__device__ __forceinline__ int lds_swz(int r) {
+  if constexpr (KTT == 32) return (((r >> 3) & 1) << 1) | ((r >> 4) & 1);
+  return MF == 32 ? (r >> 1) & 7 : r & 7;
+}
 
 // PF: fragment-prefetch step pipeline -- step t's fragments are read from LDS
 // right after its barrier while the MFMAs of step t - 1 (fragments already in
 // registers) issue, so neither the LDS read latency nor the barrier sits
 // between a k-tile landing and its MFMAs (halo.hip uses the same scheme).
-template <int BM, int BN, int WGM, int WGN, int S, int AM, bool PF, int MF = 16>
-__global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, S, PF, MF>())) void cgemm_kernel(IGemmArgs p) {
-  using G = CG<BM, BN, WGM, WGN, S, MF>;
-  static_assert(MF == 16 || !PF, "the 32x32 MFMA build has no fragment-prefetch variant");
+template <int BM, int BN, int WGM, int WGN, int S, int AM, bool PF, int MF = 16, int KTT = 64>
+__global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, S, PF, MF, KTT>())) void cgemm_kernel(IGemmArgs p) {
+  using G = CG<BM, BN, WGM, WGN, S, MF, KTT>;
+  static_assert((MF == 16 && KTT == 64) || !PF, "the fragment-prefetch variant is built for 16x16x32, 64-deep only");
   constexpr bool IM2COL = (AM == 1), DUAL = (AM == 2), STEM = (AM == 3);
+  static_assert(KTT == 64 || !STEM, "the stem operand layout packs two filter rows per 64-deep k-tile");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   char* const smem = reinterpret_cast<char*>(smem_raw);
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -149,11 +169,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WGN, wn = wid % WGN;
-  // DMA lane -> row (lane >> 3) of its 8-row piece, LDS slot (lane & 7) holding
-  // logical chunk (lane & 7) ^ swz(row); pieces start on 8-row boundaries, so
-  // the chunk depends on the piece only through bit 3 of its first row (MF 32)
-  const int prow = lane >> 3;
-  auto kc_of = [&](int piece) -> uint32_t { return uint32_t(((lane & 7) ^ lds_swz<MF>(piece * 8 + prow)) * 8); };
+  // DMA lane -> row (lane / CPR) of its RPD-row piece, LDS slot (lane % CPR)
+  // holding logical chunk (lane % CPR) ^ swz(row)
+  const int prow = lane / G::CPR;
+  auto kc_of = [&](int piece) -> uint32_t {
+    return uint32_t(((lane % G::CPR) ^ lds_swz<MF, KTT>(piece * G::RPD + prow)) * 8);
+  };
 
   // ---- buffer descriptors (wave-uniform: kernel args only)
   const char* abase = static_cast<const char*>(p.a);
@@ -173,12 +194,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
 
   // ---- per-lane DMA offsets (computed once)
   const float inv_hw = 1.f / float(p.Ho * p.Wo), inv_wo = 1.f / float(p.Wo);
+  auto a_piece = [&](int j) { return G::A_EVEN ? wid * G::APW + j : j * G::NW + wid; };
+  auto b_piece = [&](int j) { return G::B_EVEN ? wid * G::BPW + j : j * G::NW + wid; };
   uint32_t a_off[G::APW], a_msk[G::APW], a_off2[DUAL ? G::APW : 1];
 #pragma unroll
   for (int j = 0; j < G::APW; ++j) {
-    const int m = m0 + (wid * G::APW + j) * 8 + prow;
+    const int m = m0 + a_piece(j) * G::RPD + prow;
     const bool ok = m < M;
-    const uint32_t kc = kc_of(wid * G::APW + j);
+    const uint32_t kc = kc_of(a_piece(j));
     a_msk[j] = 0;
     if (STEM) {
       // pre-padded bf16 RGBA, k = kh*32 + kw*4 + c: a k-tile is filter rows
@@ -219,12 +242,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
   uint32_t b_off[G::BPW];
 #pragma unroll
   for (int j = 0; j < G::BPW; ++j) {
-    const int n = n0 + (wid * G::BPW + j) * 8 + prow;
-    b_off[j] = n < N ? (uint32_t(n) * uint32_t(p.ldb) + kc_of(wid * G::BPW + j)) * 2u : kOOB;
+    const int n = n0 + b_piece(j) * G::RPD + prow;
+    b_off[j] = n < N ? (uint32_t(n) * uint32_t(p.ldb) + kc_of(b_piece(j))) * 2u : kOOB;
   }
 
   // ---- k range of this workgroup (split-K: blockIdx.y selects a slice)
-  const int nk_all = p.K / KT;
+  const int nk_all = p.K / KTT;
   int kt0 = 0, nk = nk_all;
   if (p.splits > 1) {
     kt0 = blockIdx.y * p.kt_per_split;
@@ -232,7 +255,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
   }
 
   // ---- scalar producer walk: k element offset; im2col tap (kh, kw) + channel offset
-  int w_k = kt0 * KT;
+  int w_k = kt0 * KTT;
   int w_ci = 0, w_kh = 0, w_kw = 0, w_tap = 0;
   if (IM2COL) {
     w_tap = w_k / p.C;
@@ -250,31 +273,34 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
       const uint32_t soff2 = uint32_t(w_k - p.K1) * 2u;
 #pragma unroll
       for (int j = 0; j < G::APW; ++j) {
+        if (!G::A_EVEN && a_piece(j) >= G::NAP) continue;   // wave-uniform
         const uint32_t v = a_off2[DUAL ? j : 0];
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rsA2, (lds_ptr_t)(smem + (slot * G::A_ST + (wid * G::APW + j) * 512) * 2), 16, v, soff2, 0, 0);
+            rsA2, (lds_ptr_t)(smem + (slot * G::A_ST + a_piece(j) * 512) * 2), 16, v, soff2, 0, 0);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < G::APW; ++j) {
+        if (!G::A_EVEN && a_piece(j) >= G::NAP) continue;   // wave-uniform
         uint32_t v = a_off[j];
         if (IM2COL) v = ((a_msk[j] >> w_tap) & 1u) ? v : kOOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rsA, (lds_ptr_t)(smem + (slot * G::A_ST + (wid * G::APW + j) * 512) * 2), 16, v, a_soff, 0, 0);
+            rsA, (lds_ptr_t)(smem + (slot * G::A_ST + a_piece(j) * 512) * 2), 16, v, a_soff, 0, 0);
       }
     }
 #pragma unroll
     for (int j = 0; j < G::BPW; ++j) {
+      if (!G::B_EVEN && b_piece(j) >= G::NBP) continue;     // wave-uniform
       // (a named local, not b_off[j] in the call: with the array element as a
       // builtin argument hipcc's host pass silently drops the kernel stub)
       const uint32_t v = b_off[j];
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsB, (lds_ptr_t)(smem + (S * G::A_ST + slot * G::B_ST + (wid * G::BPW + j) * 512) * 2), 16, v, b_soff,
+          rsB, (lds_ptr_t)(smem + (S * G::A_ST + slot * G::B_ST + b_piece(j) * 512) * 2), 16, v, b_soff,
           0, 0);
     }
-    w_k += KT;
+    w_k += KTT;
     if (IM2COL) {
-      w_ci += KT;
+      w_ci += KTT;
       if (w_ci == p.C) {
         w_ci = 0;
         ++w_tap;
@@ -296,12 +322,28 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
   // (chunk 2 kk + (l >> 5)); the wave's row offsets are multiples of 32, so
   // the swizzle term depends on l only
   const int r32 = lane & 31, h32 = lane >> 5;
-  uint32_t ra32[4], rb32[4];
+  constexpr int KK32 = KTT / 16;                 // 32x32x16 k-subtiles per k-tile
+  uint32_t ra32[KK32], rb32[KK32];
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const uint32_t ch = uint32_t(((2 * kk + h32) ^ lds_swz<MF>(r32)) * 16);
-    ra32[kk] = uint32_t((wm * G::WM + r32) * KT * 2) + ch;
-    rb32[kk] = uint32_t((wn * G::WN + r32) * KT * 2) + ch;
+  for (int kk = 0; kk < KK32; ++kk) {
+    const uint32_t ch = uint32_t(((2 * kk + h32) ^ lds_swz<MF, KTT>(r32)) * 16);
+    ra32[kk] = uint32_t((wm * G::WM + r32) * KTT * 2) + ch;
+    rb32[kk] = uint32_t((wn * G::WN + r32) * KTT * 2) + ch;
+  }
+  // 16x16x32 on 64-B rows: one k-subtile per k-tile, and the swizzle reads
+  // row bits 3-4, which the fragment index i (16 rows) changes
+  uint32_t ra16[KTT == 32 ? G::TM : 1], rb16[KTT == 32 ? G::TN : 1];
+  if constexpr (KTT == 32) {
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int r = wm * G::WM + i * 16 + fr;
+      ra16[i] = uint32_t((r * KTT + ((fq ^ lds_swz<MF, KTT>(r)) * 8)) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j) {
+      const int r = wn * G::WN + j * 16 + fr;
+      rb16[j] = uint32_t((r * KTT + ((fq ^ lds_swz<MF, KTT>(r)) * 8)) * 2);
+    }
   }
 
   using AccT = typename std::conditional<MF == 32, f32x16, f32x4>::type;
@@ -316,18 +358,30 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
     const char* sb = smem + (S * G::A_ST + slot * G::B_ST) * 2;
     if constexpr (MF == 32) {
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
+      for (int kk = 0; kk < KK32; ++kk) {
         bf16x8 af[G::TM], bfr[G::TN];
 #pragma unroll
-        for (int i = 0; i < G::TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sa + ra32[kk] + i * 32 * KT * 2);
+        for (int i = 0; i < G::TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sa + ra32[kk] + i * 32 * KTT * 2);
 #pragma unroll
-        for (int j = 0; j < G::TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(sb + rb32[kk] + j * 32 * KT * 2);
+        for (int j = 0; j < G::TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(sb + rb32[kk] + j * 32 * KTT * 2);
 #pragma unroll
         for (int i = 0; i < G::TM; ++i)
 #pragma unroll
           for (int j = 0; j < G::TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
+      return;
+    } else if constexpr (KTT == 32) {
+      bf16x8 af[G::TM], bfr[G::TN];
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sa + ra16[i]);
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(sb + rb16[j]);
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       return;
     } else {
 #pragma unroll
@@ -544,18 +598,20 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
   trace_stamp(p, 3);
 }
 
-template <int BM, int BN, int WGM, int WGN, int S, int AM, bool PF = false, int MF = 16>
+template <int BM, int BN, int WGM, int WGN, int S, int AM, bool PF = false, int MF = 16, int KTT = 64>
 hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
-  using G = CG<BM, BN, WGM, WGN, S, MF>;
+  using G = CG<BM, BN, WGM, WGN, S, MF, KTT>;
   IGemmArgs a = a0;
-  const int nk = a.K / KT;
+  const int nk = a.K / KTT;
   const int splits = a.splits > 1 ? a.splits : 1;
   if (splits > 1) a.kt_per_split = (nk + splits - 1) / splits;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
-  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF>), G::LDS);
+  hipError_t e =
+      ensure_dyn_lds(reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF, KTT>), G::LDS);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF>), dim3(tiles, splits), dim3(G::NT), G::LDS, s, a);
+  hipLaunchKernelGGL((cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF, KTT>), dim3(tiles, splits), dim3(G::NT), G::LDS,
+                     s, a);
   return hipGetLastError();
 }
 

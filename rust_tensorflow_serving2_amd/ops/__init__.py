@@ -159,6 +159,9 @@ CGEMM.update({96 + k: CGEMM[base] for k, base in enumerate(CGEMM_PF_OF)})
 CGEMM32 = {112: (64, 64), 113: (64, 64), 114: (128, 128), 115: (128, 64), 116: (64, 128), 117: (128, 256),
            118: (256, 128), 119: (256, 64), 120: (128, 128), 121: (64, 128), 122: (128, 64), 123: (256, 192)}
 CGEMM.update(CGEMM32)
+# 32-deep k-tile builds (kernels/cgemm_kt32.hip, ids 124..129: deeper rings in the same LDS)
+CGEMM_KT32 = {124: (256, 192), 125: (256, 192), 126: (256, 128), 127: (128, 256), 128: (128, 128), 129: (128, 96)}
+CGEMM.update(CGEMM_KT32)
 TILES.update(CGEMM)
 # halo-tiled 3x3 stride-1 conv (kernels/halo.hip): config id -> (output pixels per tile, BN)
 HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 128), 53: (64, 128), 54: (64, 64),

@@ -76,7 +76,7 @@ def test_conv_matches_fp32(shape, cfg, splits):
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
 
 
-CGEMM_CFGS = list(range(32, 48)) + list(range(64, 73)) + list(range(96, 107)) + list(range(112, 124))
+CGEMM_CFGS = list(range(32, 48)) + list(range(64, 73)) + list(range(96, 107)) + list(range(112, 130))
 CGEMM_CONV_SHAPES = [s for s in CONV_SHAPES if s[3] % 64 == 0] + [
     (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)),   # tiny image: most taps hit padding at the border rows
     (1, 15, 13, 64, 192, 3, 2, (0, 1, 1, 1)),  # odd sizes, asymmetric pads, N tail
@@ -192,7 +192,7 @@ def test_cgemm_asymmetric_identity(cfg):
 
 @pytest.mark.parametrize("n,ho,c1,h,c2,s,cout", [(2, 56, 64, 56, 64, 1, 256), (2, 28, 128, 56, 256, 2, 512),
                                                  (1, 7, 512, 14, 1024, 2, 2048), (1, 5, 64, 9, 128, 2, 72)])
-@pytest.mark.parametrize("cfg", [32, 36, 42, 43, 44, 45, 47, 112, 114, 117, 121])
+@pytest.mark.parametrize("cfg", [32, 36, 42, 43, 44, 45, 47, 112, 114, 117, 121, 126, 128])
 def test_conv2d_dual_matches_fp32(n, ho, c1, h, c2, s, cout, cfg):
     """One GEMM for a bottleneck tail: relu(conv1x1(h) + conv1x1_stride(x) + b)."""
     hh = rnd(n, ho, ho, c1, seed=21).to(BF)
@@ -527,6 +527,7 @@ def test_attention_matches_fp32(s):
     (51, 2, (1, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1))),       # halo, split over channel chunks
     (117, 1, (2, 14, 14, 256, 256, 1, 1, (0, 0, 0, 0))),    # 32x32 MFMA build
     (113, 2, (2, 28, 28, 128, 128, 3, 2, (1, 1, 1, 1))),    # 32x32 MFMA build, im2col, split-K
+    (128, 2, (2, 28, 28, 128, 128, 3, 2, (1, 1, 1, 1))),    # 32-deep k-tiles, im2col, split-K
 ])
 def test_conv_post_activation_outputs(cfg, splits, shape):
     """ResNet v2 epilogue: one conv writes the block sum y (+bias +residual)
