@@ -203,7 +203,11 @@ class GpuRunner:
 
     def _capture(self, lane: _Lane, b: int) -> None:
         from .. import ops
-        with CAPTURE_LOCK, ops.splitk_fixup_for_bucket(b):
+        # the largest bucket runs `conc` batches at once on a loaded server:
+        # its kernels' tiles are picked (and cached) for that regime, under
+        # keys of their own (ops.tuning_regime)
+        conc = self.tune_concurrency(b) if self.servable.options.graph_autotune else 1
+        with CAPTURE_LOCK, ops.splitk_fixup_for_bucket(b), ops.tuning_regime(conc):
             self._capture_locked(lane, b)
 
     def _capture_locked(self, lane: _Lane, b: int) -> None:
