@@ -250,9 +250,16 @@ def tuning_regime(conc: int):
     it concurrently: a few large tiles that leave CUs idle alone can win there,
     because the idle CUs run the other streams' kernels
     (scripts/conc_sweep.py: the stage-4 3x3 layer 17.3 -> 11.9 us per launch
-    at 3 streams with the concurrent pick, profiles/round5/s2/conc.log)."""
+    at 3 streams with the concurrent pick, profiles/round5/s2/conc.log).
+
+    Measured, not adopted (off unless TFSERVE_CONC_TUNE=1): picks made this
+    way lost in the real serving regime, where the concurrent kernels are
+    different layers -- ResNet-50 b32 at 4 in flight 0.659 ms per batch and
+    47.8k RPC/s against 0.59 / 52.4k with the isolated screen + whole-graph
+    concurrent tuner (profiles/round5/s3/).  Big-LDS tiles that pair up well
+    with copies of themselves block other layers' workgroups from the CUs."""
     prev = getattr(_REGIME, "conc", 1)
-    _REGIME.conc = max(1, int(conc))
+    _REGIME.conc = max(1, int(conc)) if CONC_TUNE else 1
     try:
         yield
     finally:
@@ -264,6 +271,7 @@ def regime_key(key: Tuple) -> Tuple:
     return key if c <= 1 else tuple(key) + (("conc", c),)
 
 
+CONC_TUNE = os.environ.get("TFSERVE_CONC_TUNE", "0") == "1"
 CONC_TUNE_MAX = int(os.environ.get("TFSERVE_CONC_TUNE_MAX", "24"))     # candidates timed concurrently
 CONC_TUNE_RATIO = float(os.environ.get("TFSERVE_CONC_TUNE_RATIO", "3.0"))
 
