@@ -146,6 +146,12 @@ def parse():
                          "prost -> tonic), so the bytes it sends are cache-hot; 2 bodies (1.2 MB) stay in the "
                          "LLC like that, 64 cold 602-KB bodies (38.5 MB) would add a DRAM read per call that the "
                          "reference's client does not make")
+    ap.add_argument("--ref-client-llc", type=int, default=int(os.environ.get("TFSERVE_REF_CLIENT_LLC", "1")),
+                    help="during the reference-client phase, confine rank 0's threads (its server IO threads and "
+                         "the two client threads) to its least-busy last-level-cache group, so each 602 KB "
+                         "socket copy stays in one L3: runs whose client and IO threads spread over CCDs "
+                         "measured 23-35k RPC/s with recv at 25-36 us per request against 44-49k at 15 us "
+                         "(profiles/round5/s1-s4; 0 = off)")
     ap.add_argument("--cpu-report", action="store_true",
                     help="(always on now; kept for old command lines) per-thread-group CPU of the windows")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -478,7 +484,12 @@ def main():
             dist.barrier()
         s0 = served()
         rc0, rio0, rru0, rt0 = topology.thread_cpu(), io_stats(), os.times(), time.perf_counter()
+        confined = None
         if rank == 0:
+            if args.ref_client_llc and pinned:
+                grp = topology.pick_llcs(placement.cpus, 1)
+                if grp and len(grp) < len(placement.cpus):
+                    confined = (grp, topology.confine_threads(grp))
             # two connections, each driven by its own thread (a tonic channel's
             # connection task runs on one runtime thread at a time)
             # enough calls in flight to feed every GPU's batch pipeline (the
@@ -491,6 +502,8 @@ def main():
             r2 = lg2.run(args.ref_client_requests, 300.0)
             ref = {"ok": r2["ok"], "errors": r2["errors"], "elapsed_s": r2["elapsed_s"]}
             del lg2
+            if confined is not None:
+                topology.restore_threads(confined[1])
         if world > 1:
             dist.barrier()
         my_ref_diag = diag(rc0, topology.thread_cpu(), rio0, io_stats(), rru0, os.times(),
@@ -512,6 +525,7 @@ def main():
             ref = {"ref_client_rps": round(ref["ok"] / max(ref["elapsed_s"], 1e-9), 1),
                    "ref_client_errors": ref["errors"], "ref_client_in_flight": min(conc, 128) * world,
                    "ref_client_bodies": max(1, args.ref_client_bodies),
+                   "ref_client_cpus": topology.compress(confined[0]) if confined is not None else None,
                    "ref_client_gpu_share": [round(v / tot, 3) for v in share_v]}
 
     # latency mode: one client, one connection, one call in flight (the

@@ -800,6 +800,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (int c = 0; c < tfsk::kNumCGemmPfConfigs; ++c) v.push_back(tfsk::kCGemmPfCfgBase + c);
     for (int c = 0; c < tfsk::kNumCGemm32Configs; ++c) v.push_back(tfsk::kCGemm32CfgBase + c);
     for (int c = 0; c < tfsk::kNumCGemmKt32Configs; ++c) v.push_back(tfsk::kCGemmKt32CfgBase + c);
+    for (int c = 0; c < tfsk::kNumPGemmConfigs; ++c) v.push_back(tfsk::kPGemmCfgBase + c);
     return v;
   });
   m.def("halo_configs", []() {

@@ -20,12 +20,16 @@ constexpr int kNumCGemm32Configs = 12;
 // a fifth range: 32-deep k-tiles (twice the ring slots in the same LDS)
 constexpr int kCGemmKt32CfgBase = 124;
 constexpr int kNumCGemmKt32Configs = 6;
+// a sixth range: the persistent multi-tile kernel (pgemm.hip; no split-K, no stem)
+constexpr int kPGemmCfgBase = 130;
+constexpr int kNumPGemmConfigs = 8;
 inline bool cgemm_cfg_id(int cfg) {
   return (cfg >= kCGemmCfgBase && cfg < kCGemmCfgBase + kNumCGemmConfigs) ||
          (cfg >= kCGemmCfgBase2 && cfg < kCGemmCfgBase2 + kNumCGemmConfigs2) ||
          (cfg >= kCGemmPfCfgBase && cfg < kCGemmPfCfgBase + kNumCGemmPfConfigs) ||
          (cfg >= kCGemm32CfgBase && cfg < kCGemm32CfgBase + kNumCGemm32Configs) ||
-         (cfg >= kCGemmKt32CfgBase && cfg < kCGemmKt32CfgBase + kNumCGemmKt32Configs);
+         (cfg >= kCGemmKt32CfgBase && cfg < kCGemmKt32CfgBase + kNumCGemmKt32Configs) ||
+         (cfg >= kPGemmCfgBase && cfg < kPGemmCfgBase + kNumPGemmConfigs);
 }
 
 // Operand requirements (else cgemm_launch returns hipErrorInvalidValue):
@@ -42,6 +46,8 @@ hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t str
 hipError_t cgemm32_launch(const IGemmArgs& a, int a_mode, int idx, hipStream_t stream);
 // the 32-deep k-tile builds (cgemm_kt32.hip), idx = cfg - kCGemmKt32CfgBase
 hipError_t cgemm_kt32_launch(const IGemmArgs& a, int a_mode, int idx, hipStream_t stream);
+// the persistent multi-tile builds (pgemm.hip), idx = cfg - kPGemmCfgBase
+hipError_t pgemm_launch(const IGemmArgs& a, int a_mode, int idx, hipStream_t stream);
 // the config can finish split-K in-kernel (IGemmArgs::counters)
 bool cgemm_fixup_ok(int cfg);
 // workgroups (= tiles) of a halo launch (its split-K counters)

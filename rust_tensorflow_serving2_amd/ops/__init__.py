@@ -162,6 +162,11 @@ CGEMM.update(CGEMM32)
 # 32-deep k-tile builds (kernels/cgemm_kt32.hip, ids 124..129: deeper rings in the same LDS)
 CGEMM_KT32 = {124: (256, 192), 125: (256, 192), 126: (256, 128), 127: (128, 256), 128: (128, 128), 129: (128, 96)}
 CGEMM.update(CGEMM_KT32)
+# persistent multi-tile builds (kernels/pgemm.hip, ids 130..137): a resident grid loops over
+# the tiles with the DMA ring running across tile boundaries; no split-K, no stem operand
+PGEMM = {130: (64, 64), 131: (64, 64), 132: (64, 128), 133: (128, 64), 134: (128, 128), 135: (128, 128),
+         136: (64, 256), 137: (64, 64)}
+CGEMM.update(PGEMM)
 TILES.update(CGEMM)
 # halo-tiled 3x3 stride-1 conv (kernels/halo.hip): config id -> (output pixels per tile, BN)
 HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 128), 53: (64, 128), 54: (64, 64),
@@ -218,7 +223,7 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
             continue   # 96-wide tiles: only where they divide N (BERT's 768 / 2304 / 3072)
         tiles = -(-M // bm) * -(-N // bn)
         for s in (1, 2, 4, 8, 16):
-            if s > 1 and (no_split or nk // s < 2 or tiles >= 1024 or tiles * s > 4096):
+            if s > 1 and (no_split or cfg in PGEMM or nk // s < 2 or tiles >= 1024 or tiles * s > 4096):
                 continue
             out.append((cfg, s))
     return out

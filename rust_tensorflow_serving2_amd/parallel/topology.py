@@ -469,6 +469,35 @@ def thread_llcs(prefixes: Sequence[str], root: str = "/") -> Dict[str, object]:
     return {"cpus": dict(sorted(where.items())), "llcs": len(llcs)}
 
 
+def confine_threads(cpus: Sequence[int]) -> Dict[int, List[int]]:
+    """Move every thread of this process (and threads it creates later: they
+    inherit the calling thread's mask) onto ``cpus``.  Returns the previous
+    masks by thread id, for ``restore_threads``."""
+    old: Dict[int, List[int]] = {}
+    want = set(int(c) for c in cpus)
+    if not want:
+        return old
+    try:
+        tids = [int(t) for t in os.listdir(f"/proc/{os.getpid()}/task")]
+    except OSError:
+        tids = []
+    for tid in tids:
+        try:
+            old[tid] = sorted(os.sched_getaffinity(tid))
+            os.sched_setaffinity(tid, want)
+        except (OSError, ValueError):
+            continue
+    return old
+
+
+def restore_threads(old: Dict[int, List[int]]) -> None:
+    for tid, mask in old.items():
+        try:
+            os.sched_setaffinity(tid, set(mask))
+        except (OSError, ValueError):
+            continue
+
+
 def pin_hot_threads(prefixes: Sequence[str], cpus: Sequence[int], sample_s: float = 0.2,
                     root: str = "/") -> Dict[str, int]:
     """Give each thread of this process whose name starts with one of

@@ -76,7 +76,8 @@ def test_conv_matches_fp32(shape, cfg, splits):
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
 
 
-CGEMM_CFGS = list(range(32, 48)) + list(range(64, 73)) + list(range(96, 107)) + list(range(112, 130))
+PGEMM_CFGS = list(range(130, 138))      # persistent multi-tile builds (no split-K)
+CGEMM_CFGS = list(range(32, 48)) + list(range(64, 73)) + list(range(96, 107)) + list(range(112, 130)) + PGEMM_CFGS
 CGEMM_CONV_SHAPES = [s for s in CONV_SHAPES if s[3] % 64 == 0] + [
     (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)),   # tiny image: most taps hit padding at the border rows
     (1, 15, 13, 64, 192, 3, 2, (0, 1, 1, 1)),  # odd sizes, asymmetric pads, N tail
@@ -95,7 +96,7 @@ def test_cgemm_conv_matches_fp32(shape, cfg):
     wo = (w + pads[2] + pads[3] - k) // s + 1
     res = rnd(n, ho, wo, cout, seed=4).to(BF)
     ref = ref_conv(x, wt, b, s, pads, res, "relu")
-    for splits in (1, 3):
+    for splits in ((1,) if cfg in PGEMM_CFGS else (1, 3)):
         y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), k, k, s, s, *pads, act=ACT["relu"],
                          cfg=cfg, splits=splits)
         torch.cuda.synchronize()
@@ -179,6 +180,42 @@ def test_cgemm_linear_matches_fp32(m, n, k, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (act, err)
 
 
+@pytest.mark.parametrize("cfg", PGEMM_CFGS)
+@pytest.mark.parametrize("m,n,k,conv", [(32768, 256, 128, False), (20000, 72, 192, False),
+                                        (16, 56, 56, True), (9, 14, 14, True)])
+def test_pgemm_many_tiles_per_workgroup(cfg, m, n, k, conv):
+    """The persistent kernel with far more tiles than resident workgroups (each
+    loops over several, its DMA ring running across tile boundaries): dense
+    GEMMs with partial last tiles, and 3x3 im2col convs (N, H, W from the
+    tuple) whose tiles mix images and padding taps."""
+    if conv:
+        nimg, h, w = m, n, k
+        cin, cout = 64, 128
+        x = rnd(nimg, h, w, cin, seed=41).to(BF)
+        wt = rnd(3, 3, cin, cout, scale=1 / math.sqrt(9 * cin), seed=42).to(BF).float()
+        b = rnd(cout, scale=0.1, seed=43)
+        res = rnd(nimg, h, w, cout, seed=44).to(BF)
+        ref = ref_conv(x, wt, b, 1, (1, 1, 1, 1), res, "relu")
+        y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), 3, 3, 1, 1, 1, 1, 1, 1, act=ACT["relu"],
+                         cfg=cfg)
+    else:
+        x = rnd(m, k, seed=45).to(BF)
+        wm = rnd(n, k, scale=1 / math.sqrt(k), seed=46).to(BF)
+        b = rnd(n, scale=0.1, seed=47)
+        res = rnd(m, n, seed=48).to(BF)
+        ref = torch.relu(x.float() @ wm.float().t() + b + res.float())
+        y = hip().linear(x.to(DEV), wm.to(DEV), b.to(DEV), res.to(DEV), ACT["relu"], cfg, False)
+    torch.cuda.synchronize()
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
+
+
+def test_pgemm_rejects_split_k():
+    x = torch.zeros(256, 256, device=DEV, dtype=BF)
+    with pytest.raises(RuntimeError):
+        hip().linear(x, x, None, None, 0, 130, False, 1.0, None, 2)
+
+
 @pytest.mark.parametrize("cfg", CGEMM_CFGS)
 def test_cgemm_asymmetric_identity(cfg):
     """A = I, asymmetric B (exact in bf16 / fp32): catches a transposed or
@@ -192,7 +229,7 @@ def test_cgemm_asymmetric_identity(cfg):
 
 @pytest.mark.parametrize("n,ho,c1,h,c2,s,cout", [(2, 56, 64, 56, 64, 1, 256), (2, 28, 128, 56, 256, 2, 512),
                                                  (1, 7, 512, 14, 1024, 2, 2048), (1, 5, 64, 9, 128, 2, 72)])
-@pytest.mark.parametrize("cfg", [32, 36, 42, 43, 44, 45, 47, 112, 114, 117, 121, 126, 128])
+@pytest.mark.parametrize("cfg", [32, 36, 42, 43, 44, 45, 47, 112, 114, 117, 121, 126, 128, 130, 132, 134])
 def test_conv2d_dual_matches_fp32(n, ho, c1, h, c2, s, cout, cfg):
     """One GEMM for a bottleneck tail: relu(conv1x1(h) + conv1x1_stride(x) + b)."""
     hh = rnd(n, ho, ho, c1, seed=21).to(BF)
@@ -202,7 +239,7 @@ def test_conv2d_dual_matches_fp32(n, ho, c1, h, c2, s, cout, cfg):
     b = rnd(cout, scale=0.1, seed=25)
     w = torch.cat([w1, w2], 1).contiguous()
     ref = torch.relu(hh.float() @ w1.float().t() + x.float()[:, ::s, ::s, :] @ w2.float().t() + b)
-    for splits in (1, 2):
+    for splits in ((1,) if cfg in PGEMM_CFGS else (1, 2)):
         y = hip().conv2d_dual(hh.to(DEV), x.to(DEV), w.to(DEV), b.to(DEV), s, s, ACT["relu"], cfg, None, splits)
         err = (y.float().cpu() - ref).abs().max().item()
         assert y.shape == (n, ho, ho, cout)
