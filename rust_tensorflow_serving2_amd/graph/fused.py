@@ -215,7 +215,7 @@ class FusedConv:
         kw_post, outs = _post_kwargs(self, out)
         run = lambda c, s: H.conv2d(*args, cfg=c, out=out, splits=s, **kw_post)  # noqa
         cfg, splits = tuned_config(key, M, self.cout, run, K, dma, aligned, halo=halo,
-                                   cgemm_only=self.post is not None)
+                                   cgemm_only=self.post is not None, stem=self.c4)
         run(cfg, splits)
         return outs
 

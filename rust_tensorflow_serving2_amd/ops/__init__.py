@@ -187,13 +187,15 @@ def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
 
 
 def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-               halo: bool = False, no_split: bool = False):
+               halo: bool = False, no_split: bool = False, stem: bool = False):
     """(tile config, split-K) pairs worth timing for an M x N x K problem
     (``dma``: the operand mode uses the direct-to-LDS path, so the deeper
     DMA-ring configs apply; ``aligned64``: K and the conv channels are
     multiples of 64, so the pipelined cgemm configs apply; ``halo``: a 3x3
     stride-1 conv with C % 64 == 0, so the halo-tiled configs apply too —
-    their split-K granule is a 64-channel chunk of 9 taps)."""
+    their split-K granule is a 64-channel chunk of 9 taps; ``stem``: the
+    padded RGBA stem operand, which the 32-deep and persistent builds do not
+    take)."""
     nk = -(-K // 64)
     out = []
     if halo and aligned64 and K % 576 == 0 and N % 8 == 0:
@@ -214,6 +216,8 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
         if cfg in CGEMM and not (aligned64 and K % 64 == 0 and N % 8 == 0):
             continue
         if cgemm_only and cfg not in CGEMM:
+            continue
+        if stem and (cfg in CGEMM_KT32 or cfg in PGEMM):
             continue
         if K < 2 * TILE_BK.get(cfg, 64) and cfg in TILE_BK:
             continue   # deep k-tiles only pay off with several of them
@@ -333,7 +337,7 @@ def _time_concurrent(launch: Callable[[int, int], None], cands, conc: int, flush
 
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
                  dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-                 halo: bool = False, no_split: bool = False) -> Tuple[int, int]:
+                 halo: bool = False, no_split: bool = False, stem: bool = False) -> Tuple[int, int]:
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
     heuristic is used).  Inside ``tuning_regime(k > 1)`` the pick is the
@@ -363,9 +367,15 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
         best, best_t = None, float("inf")
         times = []
         flush = _flush_buffer()
-        cands = candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split)
+        cands = candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, stem)
         for c, s in cands:
-            launch(c, s)   # warm (also sets the kernel's LDS attribute)
+            try:
+                launch(c, s)   # warm (also sets the kernel's LDS attribute)
+            except RuntimeError:
+                # a host-side launch rejection (an operand mode the config does
+                # not take): not a candidate.  Device faults are not caught here
+                # -- they surface at the synchronize below and end the tuning.
+                continue
             samples = []
             for _rep in range(5):
                 # evict the L2s first: inside the serving graph a layer's weights
@@ -392,6 +402,8 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
             if t < best_t:
                 best, best_t = (c, s), t
         times.sort()
+        if best is None:
+            raise RuntimeError(f"no tile config could launch {key} (M={M} N={N} K={K})")
         if conc > 1 and times:
             # the serving regime: rank the plausible candidates (isolated time
             # within CONC_TUNE_RATIO of the best, at most CONC_TUNE_MAX) by
