@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--save-tuned", default="", help="write the tile picks (ops.save_tuned_cache format) here")
+    ap.add_argument("--only-k", type=int, default=0,
+                    help="time only k batches in flight (graphs only, no copies): a clean window for a "
+                         "rocprofv3 kernel trace of the serving regime")
     ap.add_argument("--buckets", type=int, nargs="*", default=None,
                     help="capture these batch buckets too (all tuned; only --batch is timed)")
     args = ap.parse_args()
@@ -49,6 +52,21 @@ def main():
     lanes = [r.lanes[i] for i in r.fast_lanes()]
     res = {"model": args.model, "batch": b, "capture_s": round(t_cap, 2),
            "tune_conc": r.tune_concurrency(b)}
+    if args.only_k:
+        gs = [(l.graphs[b], l.stream) for l in lanes[:args.only_k]]
+        for g, st in gs:
+            with torch.cuda.stream(st):
+                g.replay()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.iters):
+            for g, st in gs:
+                with torch.cuda.stream(st):
+                    g.replay()
+        torch.cuda.synchronize()
+        res[f"ms_per_batch_k{args.only_k}"] = round((time.perf_counter() - t) * 1e3 / (args.iters * args.only_k), 4)
+        print(json.dumps(res), flush=True)
+        return
     for k in range(1, len(lanes) + 1):
         gs = [(l.graphs[b], l.stream) for l in lanes[:k]]
         for g, st in gs:
