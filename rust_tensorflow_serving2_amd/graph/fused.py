@@ -24,6 +24,7 @@ folded parameters, which is how the passes are validated without a GPU.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence, Set, Tuple
 
 import numpy as np
@@ -288,6 +289,10 @@ class FusedMatMul:
         b = bias if bias is not None else zeros(self.n, w_kn)
         self.np = -(-self.n // 8) * 8 if (pad_n and self.n % 8 and self.k % 64 == 0) else self.n
         self.device = device
+        # the fp32 weights as given, kept until the compile passes are over
+        # (defer_layernorm folds a LayerNorm's gamma / beta into them; then
+        # release_weight_sources drops them)
+        self._w_src = w_kn if self.use_hip else None
         if self.use_hip:
             w_nk = w_kn.t().contiguous()
             if self.np != self.n:
@@ -329,6 +334,196 @@ class FusedMatMul:
         cfg, splits = tuned_config(key, M, n, run, self.k, True, self.k % 64 == 0)
         y = run(cfg, splits)
         return [y[:, :self.n] if padded else y]
+
+
+class DeferredLNMatMul(FusedMatMul):
+    """A _FusedMatMul / _FusedQKV around LayerNorms that are never stored
+    (``defer_layernorm``): ``LN(z) = (z - mean) * rstd * gamma + beta`` of a
+    GEMM output ``z`` is applied inside the GEMMs that read it, from row
+    statistics the producing GEMM's epilogue emits ([M][P][2] fp32 (sum, sum of
+    squares) partials, one per row and producer column block).
+
+    * ``emit``: this GEMM's bf16 output rows feed a deferred LayerNorm: it also
+      returns their partials (output 1).
+    * ``a_ln`` = (eps,): input 0 is a pre-LayerNorm ``z`` (statistics at input
+      ``a_pos``).  ``LN(z) @ W + b = rstd * (z @ W' - mean * colsum(W')) + b'``
+      with ``W' = diag(gamma) W`` (folded in fp32, then rounded once to bf16),
+      ``b' = b + beta @ W`` and ``colsum`` = the per-column sums of the bf16
+      ``W'`` -- the GEMM runs on ``z`` unchanged.
+    * ``r_ln`` = (gamma, beta, eps): the residual (input 1) is a pre-LayerNorm
+      ``z`` (statistics at input ``r_pos``), normalised per element in the
+      epilogue.
+
+    One kernel per GEMM (kernels/cgemm_impl.h epilogue_lnx, bindings
+    ``linear_lnx``): the 23 of 24 encoder LayerNorm launches of BERT-base
+    whose inputs and outputs are GEMMs disappear (the last one feeds the
+    pooler's strided view and stays).  Round 3's fold spilled registers in
+    the 8-wave tiles (profiles/round3/ln_fold.md); this one does not (LDS
+    column vectors, statistics fetched before the K loop, a separate LNX
+    kernel build), and still only breaks even -- see defer_layernorm."""
+
+    emit = False
+    has_res = False
+    a_ln = None
+    a_pos = None
+    r_ln = None
+    r_pos = None
+    colsum = None
+
+    @classmethod
+    def of(cls, node) -> "DeferredLNMatMul":
+        """The node's impl as a DeferredLNMatMul (converted in place the first
+        time, while its inputs are still [x] or [x, residual])."""
+        mm = node.attr("_impl")
+        if isinstance(mm, DeferredLNMatMul):
+            return mm
+        d = cls.__new__(cls)
+        d.__dict__.update(mm.__dict__)
+        d.has_res = len(node.inputs) > 1
+        node.attrs["_impl"] = d
+        return d
+
+    def fold_input_ln(self, gamma: torch.Tensor, beta: torch.Tensor, eps: float):
+        w_kn = self._w_src.float()
+        g = gamma.detach().float().reshape(-1).to(w_kn.device)
+        bt = beta.detach().float().reshape(-1).to(w_kn.device)
+        b = self.b.detach().float().to(w_kn.device)
+        wf = w_kn * g[:, None]
+        self.w = to_device(_pad_k(wf.t().contiguous(), 8).to(BF16), self.device)
+        self.b = to_device((b + bt @ w_kn).float(), self.device)
+        self.colsum = self.w.float().sum(1).contiguous()
+        self.a_ln = (float(eps),)
+
+    def _stats(self, st: torch.Tensor, length: int, eps: float):
+        s = st.float().sum(1)
+        mean = s[:, 0] / length
+        var = (s[:, 1] / length - mean * mean).clamp_min(0)
+        return mean, torch.rsqrt(var + eps)
+
+    def __call__(self, ctx, node, ins):
+        x = _to_bf16(O.to_torch(ins[0])).contiguous()
+        res = _to_bf16(O.to_torch(ins[1])).contiguous() if self.has_res else None
+        a_st = O.to_torch(ins[self.a_pos]) if self.a_ln is not None else None
+        r_st = O.to_torch(ins[self.r_pos]) if self.r_ln is not None else None
+        M = x.numel() // self.k
+        shape = list(x.shape[:-1]) + [self.n]
+        if not x.is_cuda:
+            return self._reference(x, res, a_st, r_st, M, shape)
+        from ..ops import ACT, hip, tuned_config
+        H = hip()
+        out = torch.empty(shape, device=x.device, dtype=torch.float32 if self.out_f32 else BF16)
+        ra = self.r_ln
+        key = ("mmx", M, self.n, self.k, res is not None, self.out_f32, self.act, self.a_ln is not None,
+               ra is not None, self.emit)
+
+        def run(c, _s):
+            return H.linear_lnx(x, self.w, self.b, res, ACT[self.act], c, self.out_f32, out,
+                                a_st, self.colsum, self.a_ln[0] if self.a_ln else 1e-12,
+                                r_st, ra[0] if ra else None, ra[1] if ra else None, ra[2] if ra else 1e-12,
+                                self.emit)
+        cfg, _ = tuned_config(key, M, self.n, run, self.k, True, True, no_split=True, ln=True)
+        y, st = run(cfg, 1)
+        return [y, st] if self.emit else [y]
+
+    def _reference(self, x, res, a_st, r_st, M, shape):
+        """The kernel's math in fp32 torch (CPU tensors; tests)."""
+        acc = x.float().reshape(M, self.k) @ self.w.float().cpu()[:, :self.k].t()
+        if self.a_ln is not None:
+            mean, rstd = self._stats(a_st.cpu(), self.k, self.a_ln[0])
+            acc = rstd[:, None] * (acc - mean[:, None] * self.colsum.cpu()[None, :])
+        y = acc + self.b.float().cpu()
+        if res is not None:
+            r = res.float().reshape(M, self.n)
+            if self.r_ln is not None:
+                g, b, eps = self.r_ln
+                mean, rstd = self._stats(r_st.cpu(), self.n, eps)
+                r = (r - mean[:, None]) * rstd[:, None] * g.cpu() + b.cpu()
+            y = y + r
+        y = _ref_act(y, self.act)
+        yb = y.to(BF16) if not self.out_f32 else y
+        outs = [yb.reshape(shape)]
+        if self.emit:
+            f = yb.float()
+            outs.append(torch.stack([f.sum(1), (f * f).sum(1)], 1).reshape(M, 1, 2))
+        return outs
+
+
+def _lnx_gemm_ok(impl, k: int) -> bool:
+    return isinstance(impl, FusedMatMul) and impl.use_hip and impl.np == impl.n and impl.k == k and \
+        impl.k % 64 == 0 and impl.n % 32 == 0 and getattr(impl, "_w_src", None) is not None
+
+
+def defer_layernorm(g, order, fed, fetch_refs, device, opts):
+    """_LayerNorm(z) with z = a _FusedMatMul output read by nothing else, and
+    every reader of the LayerNorm a _FusedMatMul / _FusedQKV taking it as
+    input 0 (A) or input 1 (residual): the LayerNorm node goes away -- the
+    producer emits z's row statistics, the readers take z plus the
+    statistics (DeferredLNMatMul).  Opt-in (TFSERVE_DEFER_LN=1): on
+    MI355X it measured level with the LayerNorm kernels at b32 (engine
+    1.560 / 1.568 vs 1.544 ms), behind at b1 (0.624 vs 0.585 ms) and in the
+    BERT serving bench (25.9k vs 27.1k RPC/s, profiles/round5/s15): the
+    epilogue work it adds to the four GEMMs (1.5-2.5 us each in isolation,
+    scripts/lnx_probe.py) costs about what the LayerNorm launches did."""
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    if not c.use_hip or os.environ.get("TFSERVE_DEFER_LN", "0") != "1":
+        return
+    for name in order:
+        ln_node = g.nodes.get(name)
+        if ln_node is None or ln_node.op != "_LayerNorm" or ln_node.name in c.fetch_nodes:
+            continue
+        ln = ln_node.attr("_impl")
+        if ln is None or not getattr(ln, "use_hip", False):
+            continue
+        C = ln.g.numel()
+        src, sidx = ln_node.inputs[0]
+        prod = g.nodes.get(src)
+        if prod is None or sidx != 0 or prod.op not in ("_FusedMatMul", "_FusedQKV"):
+            continue
+        pm = prod.attr("_impl")
+        if not isinstance(pm, FusedMatMul) or not pm.use_hip or pm.n != C or pm.np != C or pm.out_f32 or \
+                pm.k % 64 or C % 32 or c.only_consumer(prod.name) is not ln_node:
+            continue
+        readers = c.cons.get(ln_node.name, [])
+        ok = bool(readers)
+        for cname, pos, oidx in readers:
+            cn = g.nodes[cname]
+            ci = cn.attr("_impl")
+            if oidx != 0 or cn.op not in ("_FusedMatMul", "_FusedQKV") or ci is None:
+                ok = False
+            elif pos == 0:
+                ok = ok and _lnx_gemm_ok(ci, C) and getattr(ci, "a_ln", None) is None and \
+                    not (len(cn.inputs) > 1 and cn.inputs[1] == (ln_node.name, 0))
+            elif pos == 1:
+                ok = ok and isinstance(ci, FusedMatMul) and ci.use_hip and ci.n == C and ci.np == C and \
+                    ci.k % 64 == 0 and ci.n % 32 == 0 and getattr(ci, "r_ln", None) is None
+            else:
+                ok = False
+        if not ok:
+            continue
+        DeferredLNMatMul.of(prod).emit = True
+        z = (prod.name, 0)
+        stats = (prod.name, 1)
+        for cname, pos, _o in readers:
+            cn = g.nodes[cname]
+            d = DeferredLNMatMul.of(cn)
+            cn.inputs[pos] = z
+            if pos == 0:
+                d.fold_input_ln(ln.g, ln.b, ln.eps)
+                d.a_pos = len(cn.inputs)
+            else:
+                d.r_ln = (ln.g, ln.b, float(ln.eps))
+                d.r_pos = len(cn.inputs)
+            cn.inputs.append(stats)
+        del g.nodes[ln_node.name]
+        c.refresh()
+
+
+def release_weight_sources(g, order, fed, fetch_refs, device, opts):
+    """Drops the fp32 weight copies the GEMM ops kept for defer_layernorm."""
+    for n in g.nodes.values():
+        impl = n.attrs.get("_impl") if n.attrs else None
+        if isinstance(impl, FusedMatMul):
+            impl._w_src = None
 
 
 class DenseSoftmax:
@@ -410,7 +605,8 @@ def _impl_op(ctx, node, ins):
     return node.attrs["_impl"](ctx, node, ins)
 
 
-for _op in ("_FusedConv2D", "_FusedDualConv", "_FusedMatMul", "_GlobalAvgPool", "_MaxPool", "_SoftmaxArgMax", "_LayerNorm",
+for _op in ("_FusedConv2D", "_FusedDualConv", "_FusedMatMul", "_GlobalAvgPool", "_MaxPool",
+            "_SoftmaxArgMax", "_LayerNorm",
             "_FusedQKV", "_Attention", "_EmbeddingLN", "_KeyMaskAdder", "_DenseSoftmax"):
     O.OPS[_op] = _impl_op
 
@@ -1060,5 +1256,7 @@ def fuse_conv_chain(g, order, fed, fetch_refs, device, opts):
 def default_passes(options=None):
     from .patterns import bert_passes, late_passes
     return [fuse_pools, fuse_softmax_argmax] + bert_passes() + [fuse_conv, fuse_dual_conv, fuse_post_activation,
-                                                                 fuse_stem_pool, fuse_matmul, fuse_classifier_head,
-                                                                 fuse_dense_softmax, fuse_conv_chain] + late_passes()
+                                                                 fuse_stem_pool, fuse_matmul,
+                                                                 fuse_classifier_head, fuse_dense_softmax,
+                                                                 fuse_conv_chain] + late_passes() + \
+        [defer_layernorm, release_weight_sources]

@@ -630,9 +630,8 @@ def bert_passes():
 
 def late_passes():
     """Passes over the fused graph (after every GEMM is a _FusedMatMul).  None
-    today: the LayerNorm-folding pass of round 3 (row statistics from the
-    producing GEMM, normalisation inside the consuming GEMMs) measured slower
-    than the standalone LayerNorm kernel -- b32 engine 2.17 vs 1.58 ms, the
-    fold epilogue confined QKV / FFN1 to tiles whose registers fit it
-    (profiles/round3/ln_fold.md) -- and was removed in round 4."""
+    here; the LayerNorm fold runs last (graph/fused.py defer_layernorm: round
+    3's fold spilled registers in the 8-wave tiles and was removed in round 4,
+    profiles/round3/ln_fold.md; round 5's epilogue reads its per-column
+    vectors from LDS instead)."""
     return []

@@ -61,11 +61,10 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   uint16_t* Ps = Vt + D * VT_LD;                              // [QB/16][16][P_LD]
 
   const int qblocks = S / QB;
-  // the query blocks of one (batch, head) share its K / V: XCD-remapped ids put
-  // them on one XCD (blocks are dealt round-robin over the 8 XCDs, so ids b
-  // and b + 1 would land on two), where the second staging of K / V hits the
-  // L2 the first one filled instead of going back to HBM / MALL
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  // (an XCD remap putting a head's two query blocks on one XCD, so the second
+  // K / V staging would hit L2, measured neutral: 150.5 vs 149.6 us per 12
+  // layers at BERT-base b32, profiles/round5/s9/replay_bert_b32.txt)
+  const int bid = blockIdx.x;
   const int qb = bid % qblocks;
   const int h = (bid / qblocks) % H;
   const int b = bid / (qblocks * H);
@@ -259,7 +258,7 @@ __global__ __launch_bounds__(256) void attention_flash_kernel(const uint16_t* __
   __shared__ __attribute__((aligned(16))) uint16_t Ps[4 * 16 * P_LD]; // per-wave P / output strips
 
   const int qblocks = (S + FQB - 1) / FQB;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);     // query blocks of a head on one XCD (as above)
+  const int bid = blockIdx.x;
   const int qb = bid % qblocks;
   const int h = (bid / qblocks) % H;
   const int b = bid / (qblocks * H);

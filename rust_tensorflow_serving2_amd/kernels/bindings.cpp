@@ -313,6 +313,92 @@ Tensor linear(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
 }
 
 
+// Deferred-LayerNorm GEMM (graph/fused.py defer_layernorm): y = epilogue(x @
+// w^T) where the rows of x (a_st) and / or of the residual (r_st) are sums
+// whose LayerNorm was never stored -- their statistics come along as [M][P][2]
+// (sum, sum sq) partials and the epilogue applies the normalisation (x's via
+// the gamma-folded weights w, the beta-folded bias and a_colsum = per-column
+// sums of w; the residual's via r_gamma / r_beta) -- and, with stats, y's own
+// row partials are returned for the next consumer.  cgemm configs (not the
+// persistent ones), one K slice.  Returns {y, y's partials (empty without stats)}.
+std::vector<Tensor> linear_lnx(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
+                               const c10::optional<Tensor>& residual, int64_t act, int64_t cfg, bool out_f32,
+                               const c10::optional<Tensor>& out, const c10::optional<Tensor>& a_st,
+                               const c10::optional<Tensor>& a_colsum, double a_eps,
+                               const c10::optional<Tensor>& r_st, const c10::optional<Tensor>& r_gamma,
+                               const c10::optional<Tensor>& r_beta, double r_eps, bool stats) {
+  need(x, at::kBFloat16, "x");
+  need(w, at::kBFloat16, "w");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int K = x.size(-1);
+  const int M = x.numel() / K;
+  const int N = w.size(0), ldb = w.size(1);
+  TORCH_CHECK(ldb >= K && K % 64 == 0 && ldb % 8 == 0 && N % 8 == 0,
+              "linear_lnx: K % 64 == 0 (fitting in w), N % 8 == 0");
+  TORCH_CHECK(is_cgemm_cfg(cfg) && !(cfg >= tfsk::kPGemmCfgBase && cfg < tfsk::kPGemmCfgBase + tfsk::kNumPGemmConfigs),
+              "linear_lnx: a cgemm tile config");
+  TORCH_CHECK(!(stats && out_f32), "linear_lnx: row statistics of bf16 outputs only");
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  Tensor y = out.has_value() ? *out : torch::empty(sizes, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  need(y, out_f32 ? at::kFloat : at::kBFloat16, "out");
+  TORCH_CHECK(y.numel() == int64_t(M) * N, "out has the wrong size");
+  auto parts_of = [&](const Tensor& t, const char* what) {
+    need(t, at::kFloat, what);
+    TORCH_CHECK(t.dim() == 3 && t.size(0) == M && t.size(2) == 2 && t.size(1) >= 1,
+                "linear_lnx: ", what, " must be [M][parts][2]");
+    return int(t.size(1));
+  };
+  auto vec_n = [&](const c10::optional<Tensor>& t, const char* what) {
+    TORCH_CHECK(t.has_value(), "linear_lnx: ", what, " missing");
+    need(*t, at::kFloat, what);
+    TORCH_CHECK(t->numel() == N && aligned16(*t), "linear_lnx: ", what, " must be N floats, 16-B aligned");
+    return t->data_ptr<float>();
+  };
+  tfsk::IGemmArgs a{};
+  a.a = x.data_ptr(); a.b = bf16p(w);
+  a.a_bytes = int64_t(M) * K * 2;
+  a.b_bytes = w.numel() * 2;
+  TORCH_CHECK(a.a_bytes < 0x7ffffff0LL && a.b_bytes < 0x7ffffff0LL, "linear_lnx operands must be < 2 GiB");
+  a.M = M; a.N = N; a.K = K; a.lda = K; a.ldb = ldb;
+  if (bias.has_value()) {
+    need(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == N, "bias size");
+    a.bias = bias->data_ptr<float>();
+  }
+  if (residual.has_value()) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->numel() == y.numel(), "residual shape must match the output");
+    a.residual = bf16p(*residual);
+    a.ldr = N;
+  }
+  if (a_st.has_value()) {
+    a.a_parts = parts_of(*a_st, "a_st");
+    a.a_st = a_st->data_ptr<float>();
+    a.a_colsum = vec_n(a_colsum, "a_colsum");
+    a.a_eps = float(a_eps);
+  }
+  if (r_st.has_value()) {
+    TORCH_CHECK(residual.has_value(), "linear_lnx: r_st normalises the residual: give one");
+    a.r_parts = parts_of(*r_st, "r_st");
+    a.r_st = r_st->data_ptr<float>();
+    a.r_gamma = vec_n(r_gamma, "r_gamma");
+    a.r_beta = vec_n(r_beta, "r_beta");
+    a.r_eps = float(r_eps);
+  }
+  Tensor st;
+  if (stats) {
+    const int bn = tfsk::cgemm_config_bn(int(cfg));
+    st = torch::empty({M, (N + bn - 1) / bn, 2}, x.options().dtype(at::kFloat));
+    a.st_out = st.data_ptr<float>();
+  } else {
+    st = torch::empty({0}, x.options().dtype(at::kFloat));
+  }
+  a.act = act; a.out = y.data_ptr(); a.ldc = N; a.out_f32 = out_f32; a.alpha = 1.f;
+  run_igemm(a, tfsk::kADense, cfg, 1, x, cur_stream(x));
+  return {y, st};
+}
+
 Tensor dense_softmax(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, int64_t n) {
   need(x, at::kFloat, "x");
   need(w, at::kBFloat16, "w");
@@ -724,6 +810,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cfg") = 36, py::arg("out") = py::none(), py::arg("splits") = 1,
         py::arg("post_scale") = py::none(), py::arg("post_shift") = py::none(), py::arg("post_act") = 0,
         py::arg("out2") = py::none(), py::arg("post_only") = false);
+  m.def("linear_lnx", &linear_lnx,
+        "GEMM whose A / residual rows are LayerNorm inputs (statistics as partials), optionally "
+        "returning its own rows' partials: {y, partials}",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("residual"), py::arg("act"), py::arg("cfg"),
+        py::arg("out_f32") = false, py::arg("out") = py::none(), py::arg("a_st") = py::none(),
+        py::arg("a_colsum") = py::none(), py::arg("a_eps") = 1e-12, py::arg("r_st") = py::none(),
+        py::arg("r_gamma") = py::none(), py::arg("r_beta") = py::none(), py::arg("r_eps") = 1e-12,
+        py::arg("stats") = false);
   m.def("linear", &linear,"x @ w^T (+bias +residual +act)", py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("residual") = py::none(), py::arg("act") = 0, py::arg("cfg") = 0, py::arg("out_f32") = false,
         py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("splits") = 1);

@@ -46,6 +46,10 @@ struct CG {
   static constexpr int RPP = BM / PASSES;
   static constexpr int LDS_EPI = RPP * CS_LD * 4;
   static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+  // deferred LayerNorm: 3 x BM float2 (A stats, residual stats, output sums)
+  // and 3 x BN floats (colsum, gamma, beta of the tile's columns) past
+  // everything else (staged before the K loop); such launches ask for LDS_LNX
+  static constexpr int LDS_LNX = LDS + 24 * BM + 12 * BN;
   static_assert(RPP % WM == 0, "epilogue passes split the tile at wave-row boundaries");
   static_assert(KTT == 64 || KTT == 32, "k-tile depth");
   static_assert(BM % RPD == 0 && BN % RPD == 0 && NAP >= NW && NBP >= NW, "DMA piece split");
@@ -109,6 +113,207 @@ __device__ __forceinline__ void epilogue_rows(const IGemmArgs& p, const float* C
   }
 }
 
+// Deferred-LayerNorm epilogue (IGemmArgs::st_out / a_st / r_st; the launcher
+// admits dense, one-slice launches): `ln` = the LDS block ln_stage filled --
+// this tile's rows' (mean, rstd) of A and of the residual, the rows' output
+// (sum, sum sq) accumulators, and the tile columns' colsum / gamma / beta.
+// Register budget: round 3's fold kept the column vectors in registers over
+// the epilogue and spilled in the 8-wave tiles (256 VGPRs, 43-52 spills,
+// profiles/round3/ln_fold.md), which cost QKV / FFN1 their best tile; here
+// every chunk re-reads them from LDS (ds_read_b128; an opaque zero offset
+// keeps the compiler from merging the unrolled chunks' identical reads into
+// one hoisted, long-lived copy).  The per-row output sums: the 4 lanes of a row
+// group (CPR = BN / 8 chunk lanes per row, 4-aligned) pre-reduce by xor
+// shuffles, then one LDS float atomic per group; the loop body has no
+// `continue`, so every lane reaches the shuffles.
+template <int BM, int BN>
+struct LnLds {
+  float2* sa;      // [rows] (mean, rstd) of A
+  float2* sr;      // [rows] (mean, rstd) of the residual
+  float* red;      // [rows][2] output (sum, sum sq)
+  const float* cs; // [BN] colsum / gamma / beta of the tile's columns
+  const float* rg;
+  const float* rb;
+};
+
+template <int BM, int BN, int NT, int CS_LD, int ACT, bool USE_PRE, int TBM, int TBN>
+__device__ __forceinline__ void epilogue_lnx(const IGemmArgs& p, const float* Cs, int m0, int n0, int tid,
+                                             const uint4 (&rpre)[Epi<BM, BN, NT>::PRE > 0 ? Epi<BM, BN, NT>::PRE : 1],
+                                             const float4 b0, const float4 b1, const LnLds<TBM, TBN>& ln) {
+  using E = Epi<BM, BN, NT>;
+  constexpr int PRE = USE_PRE ? E::PRE : 0;
+  static_assert(E::CPR % 4 == 0 && E::NTE % 4 == 0, "row groups of 4 chunk lanes");
+  const int M = p.M, N = p.N;
+  const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  auto chunk = [&](int it, bool use_pre) __attribute__((always_inline)) {
+    int row, col;
+    bool in = epi_rowcol<BM, BN, NT>(tid, it, row, col);
+    const int m = m0 + row, n = n0 + col;
+    in = in && m < M && n < N;
+    float s = 0.f, q = 0.f;
+    if (in) {
+      int z;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+      const int c = col + z;
+      float v[8];
+      load8f(Cs + row * CS_LD + col, v);
+      const float alpha = p.alpha;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= alpha;
+      if (p.a_st) {
+        const float2 st = ln.sa[row];
+        float cs[8];
+        load8f(ln.cs + c, cs);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = st.y * (v[e] - st.x * cs[e]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bv[e];
+      if (p.residual) {
+        const uint4 rr = use_pre ? rpre[PRE > 0 ? it : 0]
+                                 : *reinterpret_cast<const uint4*>(p.residual + size_t(m) * p.ldr + n);
+        const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+        float r[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          r[2 * e] = __uint_as_float(w[e] << 16);
+          r[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+        }
+        if (p.r_st) {
+          const float2 st = ln.sr[row];
+          float g[8], b[8];
+          load8f(ln.rg + c, g);
+          load8f(ln.rb + c, b);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) r[e] = (r[e] - st.x) * st.y * g[e] + b[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += r[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = act_fn<ACT>(v[e]);
+      store_chunk(p, p.out, m, n, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = static_cast<float>(static_cast<__bf16>(v[e]));   // the value stored
+        s += f;
+        q += f * f;
+      }
+    }
+    if (p.st_out) {
+      s += __shfl_xor(s, 1, 64);
+      q += __shfl_xor(q, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      q += __shfl_xor(q, 2, 64);
+      if (in && (tid & 3) == 0) {
+        atomicAdd(ln.red + 2 * row, s);
+        atomicAdd(ln.red + 2 * row + 1, q);
+      }
+    }
+  };
+  // (unrolled: every chunk's residual load in flight at once.  The 8-wave
+  // 256 x 192 tile spills ~37 VGPRs with this epilogue, 10 without -- all
+  // stored after the K loop and reloaded in the epilogue, none in the MFMA
+  // loop: -Rpass-analysis=kernel-resource-usage + the ISA, round 5)
+  if constexpr (ACT != kActGeluErf) {
+#pragma unroll
+    for (int it = 0; it < E::ITERS; ++it) chunk(it, PRE > 0);
+  } else {
+#pragma unroll 1
+    for (int it = 0; it < E::ITERS; ++it) chunk(it, false);
+  }
+}
+
+// Deferred-LayerNorm staging, in two halves around the prologue's DMA issue:
+// ln_fetch (kernel start) loads this thread's row partials (thread r < BM:
+// tile row r; up to kLnPre partials per side as 16-B buffer loads, lanes past
+// a row's partials read past the resource: zeros) and column values (thread
+// c < BN); ln_stage (after the prologue's DMAs are issued) reduces them into
+// LnLds.  The loads are the oldest in flight, so the compiler's vmcnt wait
+// before the stage lets the k-tile DMAs keep flying; an epilogue-time fetch
+// stalled every workgroup for ~3 dependent memory round trips (round 5:
+// QKV / FFN1 +5-7 us each).  More partials than kLnPre: read in ln_stage.
+constexpr int kLnPre = 8;
+
+struct LnPre {
+  u32x4 a[kLnPre / 2], r[kLnPre / 2];
+  float cs, g, b;
+};
+
+__device__ __forceinline__ void ln_fetch_rows(const float* st, int parts, int M, int m, bool on, u32x4 (&v)[kLnPre / 2]) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(st), 0, int(long(M) * parts * 8), 0x00020000);
+  const uint32_t base = uint32_t(m) * uint32_t(parts) * 8u;
+#pragma unroll
+  for (int j = 0; j < kLnPre / 2; ++j)
+    v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, on && 2 * j < parts ? base + 16u * j : kOOB, 0, 0);
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void ln_fetch(const IGemmArgs& p, int m0, int n0, int tid, LnPre& f) {
+  const int m = min(m0 + tid, p.M - 1);
+  const bool row = tid < BM;
+  if (p.a_st) ln_fetch_rows(p.a_st, p.a_parts, p.M, m, row && p.a_parts <= kLnPre, f.a);
+  if (p.r_st) ln_fetch_rows(p.r_st, p.r_parts, p.M, m, row && p.r_parts <= kLnPre, f.r);
+  const uint32_t c = tid < BN && n0 + tid < p.N ? uint32_t(n0 + tid) * 4u : kOOB;
+  const int nb = p.N * 4;
+  f.cs = f.g = f.b = 0.f;
+  if (p.a_st)
+    f.cs = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.a_colsum), 0, nb, 0x00020000), c, 0, 0));
+  if (p.r_st) {
+    f.g = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.r_gamma), 0, nb, 0x00020000), c, 0, 0));
+    f.b = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.r_beta), 0, nb, 0x00020000), c, 0, 0));
+  }
+}
+
+__device__ __forceinline__ float2 ln_finish(const u32x4 (&v)[kLnPre / 2], int parts, float inv_len, float eps) {
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int j = 0; j < kLnPre / 2; ++j) {
+    a += __uint_as_float(v[j].x);
+    b += __uint_as_float(v[j].y);
+    if (2 * j + 1 < parts) {            // the upper half belongs to the next row past the last partial
+      a += __uint_as_float(v[j].z);
+      b += __uint_as_float(v[j].w);
+    }
+  }
+  const float mean = a * inv_len;
+  return make_float2(mean, rsqrtf(fmaxf(b * inv_len - mean * mean, 0.f) + eps));
+}
+
+template <int BM, int BN, int NT>
+__device__ __forceinline__ LnLds<BM, BN> ln_stage(const IGemmArgs& p, int m0, int tid, char* base, const LnPre& f) {
+  static_assert(BM <= NT && BN <= NT, "one tile row / column per thread");
+  LnLds<BM, BN> l;
+  float2* st = reinterpret_cast<float2*>(base);
+  float* vec = reinterpret_cast<float*>(st + 3 * BM);
+  l.sa = st;
+  l.sr = st + BM;
+  l.red = reinterpret_cast<float*>(st + 2 * BM);
+  l.cs = vec;
+  l.rg = vec + BN;
+  l.rb = vec + 2 * BN;
+  if (tid < BM) {
+    const int m = min(m0 + tid, p.M - 1);
+    if (p.a_st)
+      st[tid] = p.a_parts <= kLnPre ? ln_finish(f.a, p.a_parts, 1.f / float(p.K), p.a_eps)
+                                    : ln_row_stats(p.a_st, p.a_parts, m, 1.f / float(p.K), p.a_eps);
+    if (p.r_st)
+      st[BM + tid] = p.r_parts <= kLnPre ? ln_finish(f.r, p.r_parts, 1.f / float(p.N), p.r_eps)
+                                         : ln_row_stats(p.r_st, p.r_parts, m, 1.f / float(p.N), p.r_eps);
+    st[2 * BM + tid] = make_float2(0.f, 0.f);
+  }
+  if (tid < BN) {
+    vec[tid] = f.cs;
+    vec[BN + tid] = f.g;
+    vec[2 * BN + tid] = f.b;
+  }
+  return l;
+}
+
 // Waves per SIMD the register allocation must leave room for: the 4-wave
 // 32-KB tiles (64x64, 2 slots) fit 5 workgroups per CU by LDS, i.e. 5 waves
 // per SIMD, which needs <= 102 VGPRs (unconstrained they took 128: 4 per CU)
@@ -136,7 +341,12 @@ __device__ __forceinline__ int lds_swz(int r) {
 // right after its barrier while the MFMAs of step t - 1 (fragments already in
 // registers) issue, so neither the LDS read latency nor the barrier sits
 // between a k-tile landing and its MFMAs (halo.hip uses the same scheme).
-template <int BM, int BN, int WGM, int WGN, int S, int AM, bool PF, int MF = 16, int KTT = 64>
+// LNX: the deferred-LayerNorm build (dense only, launch_cfg picks it when the
+// launch carries statistics): its epilogue / staging registers would
+// otherwise count against every launch -- with the LN code in all builds the
+// 64 x 64 four-slot tiles dropped from 4 to 3 waves per SIMD (VGPRs 107 -> 109
+// next to 20 AGPRs) and ResNet-50 b1 slowed from 0.375 to 0.400 ms (round 5)
+template <int BM, int BN, int WGM, int WGN, int S, int AM, bool PF, int MF = 16, int KTT = 64, bool LNX = false>
 __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, S, PF, MF, KTT>())) void cgemm_kernel(IGemmArgs p) {
   using G = CG<BM, BN, WGM, WGN, S, MF, KTT>;
   static_assert((MF == 16 && KTT == 64) || !PF, "the fragment-prefetch variant is built for 16x16x32, 64-deep only");
@@ -433,7 +643,13 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
   uint4 rpre[Epi<BM, BN, G::NT>::PRE > 0 ? Epi<BM, BN, G::NT>::PRE : 1];
   if constexpr (G::PASSES == 1) prefetch_residual<BM, BN, G::NT>(p, m0, n0, tid, rpre);
   float4 bias0, bias1;
-  prefetch_bias<BM, BN, G::NT>(p, n0, tid, bias0, bias1);
+  // two-pass tiles run each pass's epilogue on that pass's own waves (see the
+  // epilogue): a thread's epilogue column then follows its index in its half
+  const int etid = G::PASSES == 2 ? tid - ((wm * G::WM) / G::RPP) * (G::NT / 2) : tid;
+  if constexpr (G::PASSES == 2)
+    prefetch_bias<BM, BN, G::NT / 2>(p, n0, etid, bias0, bias1);
+  else
+    prefetch_bias<BM, BN, G::NT>(p, n0, tid, bias0, bias1);
 
   if (dbg & 16) {   // ablation: setup only (keep the per-lane state live)
     uint32_t keep = 0;
@@ -445,10 +661,19 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
     return;
   }
 
+  // deferred LayerNorm (runtime-uniform; the launcher admits it for dense,
+  // one-slice tiles only): row statistics and column vectors fetched now,
+  // staged into the LDS past the ring / fp32 tile once the prologue is issued
+  const bool lnx = LNX && !STEM && (p.st_out != nullptr || p.a_st != nullptr || p.r_st != nullptr);
+  LnPre lpre;
+  if (lnx) ln_fetch<BM, BN>(p, m0, n0, tid, lpre);
+
   // ---- prologue: S-1 k-tiles in flight
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < nk && do_dma) issue(s);
+  LnLds<BM, BN> ln{};
+  if (lnx) ln = ln_stage<BM, BN, G::NT>(p, m0, tid, smem + G::LDS, lpre);
 
   // ---- main loop, unrolled by the ring depth (slot indices are immediates)
   for (int kt = 0; kt < nk; kt += S) {
@@ -490,30 +715,90 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
   // (G::PASSES row passes of G::RPP rows when the whole fp32 tile does not fit)
   float* Cs = reinterpret_cast<float*>(smem);
   constexpr int RPP = G::RPP;
+  auto stage = [&](int ps) __attribute__((always_inline)) {    // this wave's accumulators of pass ps -> Cs
+    if constexpr (MF == 32) {
+      // C/D of 32x32x16: column lane & 31, row (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            Cs[(wm * G::WM - ps * RPP + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32) * G::CS_LD + wn * G::WN +
+               j * 32 + r32] = acc[i][j][r];
+    } else {
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(wm * G::WM - ps * RPP + i * 16 + fq * 4 + r) * G::CS_LD + wn * G::WN + j * 16 + fr] = acc[i][j][r];
+    }
+  };
+  if constexpr (G::PASSES == 2) {
+    if (p.splits <= 1) {
+      // Two-pass tiles (256 x 192): pass ps's rows belong to half of the waves.
+      // Each half stages its accumulators and runs its pass's epilogue alone,
+      // on two wave-uniform paths with matching barriers: the other half's
+      // accumulators are not live during an epilogue, which kept the 8-wave
+      // tile's epilogue from spilling (10 VGPRs with the plain epilogue, 37
+      // with the deferred-LayerNorm one when all waves ran both passes).
+      constexpr int ENT = G::NT / 2;
+      using RPn = uint4[Epi<RPP, BN, ENT>::PRE > 0 ? Epi<RPP, BN, ENT>::PRE : 1];
+      const RPn& rpn = *reinterpret_cast<const RPn*>(rpre);   // not read (USE_PRE = false)
+      auto epi = [&](int ps) __attribute__((always_inline)) {
+        const int mp = m0 + ps * RPP;
+        if (lnx) {
+          LnLds<BM, BN> lp = ln;
+          lp.sa += ps * RPP;
+          lp.sr += ps * RPP;
+          lp.red += 2 * ps * RPP;
+          switch (p.act) {
+            case kActRelu: epilogue_lnx<RPP, BN, ENT, G::CS_LD, kActRelu, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1, lp); break;
+            case kActGeluTanh: epilogue_lnx<RPP, BN, ENT, G::CS_LD, kActGeluTanh, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1, lp); break;
+            case kActGeluErf: epilogue_lnx<RPP, BN, ENT, G::CS_LD, kActGeluErf, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1, lp); break;
+            case kActTanh: epilogue_lnx<RPP, BN, ENT, G::CS_LD, kActTanh, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1, lp); break;
+            default: epilogue_lnx<RPP, BN, ENT, G::CS_LD, 0, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1, lp); break;
+          }
+        } else {
+          switch (p.act) {
+            case kActRelu: epilogue_rows<RPP, BN, ENT, G::CS_LD, kActRelu, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1); break;
+            case kActGeluTanh: epilogue_rows<RPP, BN, ENT, G::CS_LD, kActGeluTanh, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1); break;
+            case kActGeluErf: epilogue_rows<RPP, BN, ENT, G::CS_LD, kActGeluErf, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1); break;
+            case kActTanh: epilogue_rows<RPP, BN, ENT, G::CS_LD, kActTanh, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1); break;
+            default: epilogue_rows<RPP, BN, ENT, G::CS_LD, 0, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1); break;
+          }
+        }
+      };
+      if (__builtin_amdgcn_readfirstlane((wm * G::WM) / RPP) == 0) {
+        stage(0);
+        __syncthreads();          // B1: pass 0 staged
+        epi(0);
+        __syncthreads();          // B2: pass 0 read
+        __syncthreads();          // B3
+        __syncthreads();          // B4
+      } else {
+        __syncthreads();          // B1
+        __syncthreads();          // B2
+        stage(1);
+        __syncthreads();          // B3: pass 1 staged
+        epi(1);
+        __syncthreads();          // B4: pass 1 done
+      }
+      if (lnx && p.st_out != nullptr) {
+        const float2* red = reinterpret_cast<const float2*>(ln.red);
+        for (int r = tid; r < BM; r += G::NT)
+          if (m0 + r < M) reinterpret_cast<float2*>(p.st_out)[size_t(m0 + r) * nbn + bn] = red[r];
+      }
+      trace_stamp(p, 3);
+      return;
+    }
+  }
 #pragma unroll
   for (int ps = 0; ps < G::PASSES; ++ps) {
     if (ps > 0) __syncthreads();    // the previous pass has read Cs
-    if (G::PASSES == 1 || (wm * G::WM) / RPP == ps) {
-      if constexpr (MF == 32) {
-        // C/D of 32x32x16: column lane & 31, row (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
-#pragma unroll
-        for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-          for (int j = 0; j < G::TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              Cs[(wm * G::WM - ps * RPP + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32) * G::CS_LD + wn * G::WN +
-                 j * 32 + r32] = acc[i][j][r];
-      } else {
-#pragma unroll
-        for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-          for (int j = 0; j < G::TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              Cs[(wm * G::WM - ps * RPP + i * 16 + fq * 4 + r) * G::CS_LD + wn * G::WN + j * 16 + fr] = acc[i][j][r];
-      }
-    }
+    if (G::PASSES == 1 || (wm * G::WM) / RPP == ps) stage(ps);
     __syncthreads();
     const int mp = m0 + ps * RPP;
 
@@ -587,6 +872,20 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
     constexpr bool P1 = G::PASSES == 1;
     using RP = uint4[Epi<RPP, BN, G::NT>::PRE > 0 ? Epi<RPP, BN, G::NT>::PRE : 1];
     const RP& rp = *reinterpret_cast<const RP*>(rpre);   // only read when PASSES == 1 (RPP == BM)
+    if (lnx) {
+      LnLds<BM, BN> lp = ln;                 // this pass's rows
+      lp.sa += ps * RPP;
+      lp.sr += ps * RPP;
+      lp.red += 2 * ps * RPP;
+      switch (p.act) {
+        case kActRelu: epilogue_lnx<RPP, BN, G::NT, G::CS_LD, kActRelu, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1, lp); break;
+        case kActGeluTanh: epilogue_lnx<RPP, BN, G::NT, G::CS_LD, kActGeluTanh, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1, lp); break;
+        case kActGeluErf: epilogue_lnx<RPP, BN, G::NT, G::CS_LD, kActGeluErf, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1, lp); break;
+        case kActTanh: epilogue_lnx<RPP, BN, G::NT, G::CS_LD, kActTanh, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1, lp); break;
+        default: epilogue_lnx<RPP, BN, G::NT, G::CS_LD, 0, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1, lp); break;
+      }
+      continue;
+    }
     switch (p.act) {
       case kActRelu: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActRelu, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1); break;
       case kActGeluTanh: epilogue_rows<RPP, BN, G::NT, G::CS_LD, kActGeluTanh, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1); break;
@@ -595,22 +894,48 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
       default: epilogue_rows<RPP, BN, G::NT, G::CS_LD, 0, P1>(p, Cs, mp, n0, tid, rp, bias0, bias1); break;
     }
   }
+  if (lnx && p.st_out != nullptr) {
+    // this tile's (sum, sum sq) of each of its rows -> slot bn of the row
+    __syncthreads();
+    const float2* red = reinterpret_cast<const float2*>(ln.red);
+    for (int r = tid; r < BM; r += G::NT)
+      if (m0 + r < M) reinterpret_cast<float2*>(p.st_out)[size_t(m0 + r) * nbn + bn] = red[r];
+  }
   trace_stamp(p, 3);
 }
 
 template <int BM, int BN, int WGM, int WGN, int S, int AM, bool PF = false, int MF = 16, int KTT = 64>
 hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
   using G = CG<BM, BN, WGM, WGN, S, MF, KTT>;
+  const bool lnx = a0.st_out != nullptr || a0.a_st != nullptr || a0.r_st != nullptr;
+  if (lnx && (AM != 0 || a0.splits > 1 || a0.out2 != nullptr || G::LDS_LNX > 160 * 1024 ||
+              (a0.st_out != nullptr && (a0.out_f32 || a0.out == nullptr)) ||
+              (a0.a_st != nullptr && (a0.a_colsum == nullptr || a0.a_parts < 1)) ||
+              (a0.r_st != nullptr && (a0.residual == nullptr || a0.r_gamma == nullptr || a0.r_beta == nullptr ||
+                                      a0.r_parts < 1)) ||
+              a0.N % 8 != 0))
+    return hipErrorInvalidValue;                    // deferred LayerNorm: dense, one K slice, bf16 sums
+  const int lds = lnx ? G::LDS_LNX : G::LDS;
   IGemmArgs a = a0;
   const int nk = a.K / KTT;
   const int splits = a.splits > 1 ? a.splits : 1;
   if (splits > 1) a.kt_per_split = (nk + splits - 1) / splits;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
+  if constexpr (AM == 0) {
+    if (lnx) {
+      hipError_t e = ensure_dyn_lds(
+          reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF, KTT, true>), lds);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL((cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF, KTT, true>), dim3(tiles, splits), dim3(G::NT),
+                         lds, s, a);
+      return hipGetLastError();
+    }
+  }
   hipError_t e =
-      ensure_dyn_lds(reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF, KTT>), G::LDS);
+      ensure_dyn_lds(reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF, KTT>), lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF, KTT>), dim3(tiles, splits), dim3(G::NT), G::LDS,
+  hipLaunchKernelGGL((cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF, KTT>), dim3(tiles, splits), dim3(G::NT), lds,
                      s, a);
   return hipGetLastError();
 }

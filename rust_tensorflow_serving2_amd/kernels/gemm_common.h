@@ -200,7 +200,7 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 }
 
 // 8 values -> one 16-B bf16 (or 2 x 16-B f32) store at row m, column n of `out`
-// (nullptr: nothing stored).
+// (nullptr: nothing stored)
 __device__ __forceinline__ void store_chunk(const IGemmArgs& p, void* out, int m, int n, const float (&v)[8]) {
   if (!out) return;
   if (p.out_f32) {
@@ -251,6 +251,31 @@ __device__ __forceinline__ void epi_chunk(const IGemmArgs& p, const float* src, 
   }
   store_chunk(p, p.out, m, n, v);
   if (p.out2) post_chunk(p, m, n, v);
+}
+
+// ---- deferred LayerNorm (IGemmArgs::st_out / a_st / r_st)
+// (mean, rstd) of row m from its `parts` (sum, sum of squares) partials.
+// One-pass variance in fp32 over bf16 values: E[x^2] - mean^2 loses
+// ~eps_f32 * E[x^2] / var relative, i.e. nothing while |mean| is within a few
+// standard deviations (LayerNorm inputs: residual streams).
+__device__ __forceinline__ float2 ln_row_stats(const float* st, int parts, int m, float inv_len, float eps) {
+  const float2* s = reinterpret_cast<const float2*>(st) + size_t(m) * parts;
+  float a = 0.f, b = 0.f;
+#pragma unroll 4
+  for (int j = 0; j < parts; ++j) {
+    const float2 v = s[j];
+    a += v.x;
+    b += v.y;
+  }
+  const float mean = a * inv_len;
+  return make_float2(mean, rsqrtf(fmaxf(b * inv_len - mean * mean, 0.f) + eps));
+}
+
+// 8 consecutive fp32 values at p (16-B aligned) into registers
+__device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
 }  // namespace gemm

@@ -62,6 +62,26 @@ struct IGemmArgs {
   // per workgroup (blockIdx.y * gridDim.x + blockIdx.x), nullptr in production
   long long* trace;
   int trace_cap;        // workgroups the trace buffer holds
+  // deferred LayerNorm (cgemm dense, one K slice; graph/fused.py
+  // defer_layernorm).  st_out: [M][ceil(N / BN)][2] fp32 -- per (row, column
+  // block) (sum, sum of squares) of the stored bf16 outputs, each slot written
+  // once by plain stores (nothing to zero between launches).  a_st / r_st:
+  // such partials (a_parts / r_parts per row) of A's rows (length K) / of the
+  // residual's rows (length N), tensors whose LayerNorm was never stored: the
+  // epilogue applies it -- v = rstd_a (acc - mean_a a_colsum[n]) + bias (the
+  // LN's gamma folded into the weights, beta into the bias, a_colsum = the
+  // per-column sums of the folded weights) and residual = (r - mean_r) rstd_r
+  // r_gamma + r_beta.  All nullptr: a plain epilogue.
+  float* st_out;
+  const float* a_st;
+  const float* a_colsum;
+  int a_parts;
+  float a_eps;
+  const float* r_st;
+  const float* r_gamma;
+  const float* r_beta;
+  int r_parts;
+  float r_eps;
 };
 
 // Per-device pool of zeroed split-K arrival counters: a launch captured into a

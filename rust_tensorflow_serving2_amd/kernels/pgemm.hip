@@ -295,7 +295,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void pgemm_kernel(IGemmArgs p) {
 template <int BM, int BN, int WGM, int WGN, int S, int AM>
 hipError_t launch_pg(const IGemmArgs& a, hipStream_t s) {
   using P = PG<BM, BN, WGM, WGN, S>;
-  if (a.splits > 1) return hipErrorInvalidValue;     // whole K loops only
+  if (a.splits > 1 || a.st_out != nullptr || a.a_st != nullptr || a.r_st != nullptr)
+    return hipErrorInvalidValue;   // whole K loops only, no deferred LayerNorm
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
   const void* fn = reinterpret_cast<const void*>(&pgemm_kernel<BM, BN, WGM, WGN, S, AM>);

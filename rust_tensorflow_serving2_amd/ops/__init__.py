@@ -187,7 +187,7 @@ def heuristic_splits(M: int, N: int, K: int, cfg: int) -> int:
 
 
 def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-               halo: bool = False, no_split: bool = False, stem: bool = False):
+               halo: bool = False, no_split: bool = False, stem: bool = False, ln: bool = False):
     """(tile config, split-K) pairs worth timing for an M x N x K problem
     (``dma``: the operand mode uses the direct-to-LDS path, so the deeper
     DMA-ring configs apply; ``aligned64``: K and the conv channels are
@@ -219,6 +219,8 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
             continue
         if stem and (cfg in CGEMM_KT32 or cfg in PGEMM):
             continue
+        if ln and (cfg not in CGEMM or cfg in PGEMM or bn % 32):
+            continue   # deferred LayerNorm: cgemm tiles (4-aligned chunk lanes per row)
         if K < 2 * TILE_BK.get(cfg, 64) and cfg in TILE_BK:
             continue   # deep k-tiles only pay off with several of them
         if bn > 64 and N <= bn // 2 or bm > 64 and M <= bm // 2:
@@ -337,7 +339,8 @@ def _time_concurrent(launch: Callable[[int, int], None], cands, conc: int, flush
 
 def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None], K: int = 64,
                  dma: bool = True, aligned64: bool = False, cgemm_only: bool = False,
-                 halo: bool = False, no_split: bool = False, stem: bool = False) -> Tuple[int, int]:
+                 halo: bool = False, no_split: bool = False, stem: bool = False,
+                 ln: bool = False) -> Tuple[int, int]:
     """Pick the fastest (tile config, split-K) for ``key`` by timing each
     candidate (eager only — never during HIP-graph capture, where the
     heuristic is used).  Inside ``tuning_regime(k > 1)`` the pick is the
@@ -367,7 +370,7 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
         best, best_t = None, float("inf")
         times = []
         flush = _flush_buffer()
-        cands = candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, stem)
+        cands = candidates(M, N, K, dma, aligned64, cgemm_only, halo, no_split, stem, ln)
         for c, s in cands:
             try:
                 launch(c, s)   # warm (also sets the kernel's LDS attribute)

@@ -20,8 +20,12 @@ def bert_base(tmp_path_factory):
     return path
 
 
-def test_bert_base_gpu_matches_cpu(bert_base):
+@pytest.mark.parametrize("defer_ln", [True, False])
+def test_bert_base_gpu_matches_cpu(bert_base, defer_ln, monkeypatch):
+    """defer_ln: the encoder LayerNorms folded into their GEMMs
+    (graph/fused.py defer_layernorm, opt-in) or run as kernels (default)."""
     from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
+    monkeypatch.setenv("TFSERVE_DEFER_LN", "1" if defer_ln else "0")
     gpu = Servable("bert", 1, bert_base, ServableOptions(device="cuda:0", max_batch_size=8))
     cpu = Servable("bert", 1, bert_base, ServableOptions(device="cpu"))
     rng = np.random.default_rng(0)
@@ -40,7 +44,8 @@ def test_bert_base_gpu_matches_cpu(bert_base):
     runner = next(iter(gpu._runners.values()))
     hist = runner.program.op_histogram()
     assert hist["_Attention"] == 12 and hist["_FusedQKV"] == 12
-    assert hist["_LayerNorm"] == 24
+    # deferred: only the last one stays (the pooler reads its output as a strided view)
+    assert hist["_LayerNorm"] == (1 if defer_ln else 24)
     assert hist["_EmbeddingLN"] == 1 and hist["_KeyMaskAdder"] == 1 and "GatherV2" not in hist
 
 

@@ -241,3 +241,95 @@ def test_capture_holds_off_gc_across_nested_and_threaded_captures():
         assert not gc.isenabled()
     finally:
         gc.enable()
+
+
+def test_defer_layernorm_pass_rewires_and_matches_unfused():
+    """defer_layernorm on a hand-built encoder slice (producer GEMM -> LN ->
+    {A of a GELU GEMM, residual of another GEMM}): the LN node goes, the
+    readers take the raw sum plus the producer's row partials, and the folded
+    math (DeferredLNMatMul._reference, the kernel's algebra in fp32) matches
+    the materialised LayerNorm.  The pass itself only runs for GPU programs;
+    it is driven here with CPU-built ops and a cuda device tag."""
+    import torch
+    import torch.nn.functional as F
+    from rust_tensorflow_serving2_amd.graph import fused as FU
+    from rust_tensorflow_serving2_amd.graph.ir import Graph, Node
+    from rust_tensorflow_serving2_amd.graph.patterns import LayerNormOp
+
+    torch.manual_seed(0)
+    cpu = torch.device("cpu")
+    C, F4 = 64, 128
+    w0, w1, w2 = torch.randn(C, C) / 8, torch.randn(C, F4) / 8, torch.randn(F4, C) / 11
+    b0, b1, b2 = torch.randn(C) / 10, torch.randn(F4) / 10, torch.randn(C) / 10
+    gam, bet = 1 + torch.randn(C) / 10, torch.randn(C) / 10
+    mm0 = FU.FusedMatMul(w0, b0, "none", False, cpu, True, "p")
+    mm1 = FU.FusedMatMul(w1, b1, "gelu_tanh", False, cpu, True, "a")
+    mm2 = FU.FusedMatMul(w2, b2, "none", False, cpu, True, "r")
+    ln = LayerNormOp(gam, bet, 1e-6, cpu, True)
+    g = Graph()
+    g.add(Node(name="x", op="Placeholder"))
+    g.add(Node(name="p", op="_FusedMatMul", inputs=[("x", 0), ("x", 0)], attrs={"_impl": mm0}))
+    g.add(Node(name="ln", op="_LayerNorm", inputs=[("p", 0)], attrs={"_impl": ln}))
+    g.add(Node(name="a", op="_FusedMatMul", inputs=[("ln", 0)], attrs={"_impl": mm1}))
+    g.add(Node(name="r", op="_FusedMatMul", inputs=[("a", 0), ("ln", 0)], attrs={"_impl": mm2}))
+    order = ["x", "p", "ln", "a", "r"]
+    x = torch.randn(16, C).to(torch.bfloat16)
+
+    # unfused: LN materialised (bf16 like the GPU program)
+    bf = torch.bfloat16
+    zp = (x.float() @ w0.to(bf).float() + b0 + x.float()).to(bf)
+    h = F.layer_norm(zp.float(), (C,), gam, bet, 1e-6)
+    a_ref = F.gelu(h.to(bf).float() @ w1 + b1, approximate="tanh")
+    r_ref = a_ref.to(bf).float() @ w2 + b2 + h
+
+    os.environ["TFSERVE_DEFER_LN"] = "1"
+    try:
+        FU.defer_layernorm(g, order, set(), [("r", 0)], torch.device("cuda"), None)
+    finally:
+        del os.environ["TFSERVE_DEFER_LN"]
+    FU.release_weight_sources(g, order, set(), [("r", 0)], torch.device("cuda"), None)
+    assert "ln" not in g.nodes
+    assert g.nodes["a"].inputs == [("p", 0), ("p", 1)]
+    assert g.nodes["r"].inputs == [("a", 0), ("p", 0), ("p", 1)]
+    P, A, R = (g.nodes[k].attrs["_impl"] for k in "par")
+    assert P.emit and A.a_ln is not None and A.a_pos == 1 and R.r_ln is not None and R.r_pos == 2
+    assert R.has_res and not A.has_res and P.has_res
+    assert all(m._w_src is None for m in (P, A, R))
+
+    zz, st = P(None, g.nodes["p"], [x, x])
+    assert st.shape == (16, 1, 2)
+    assert torch.allclose(zz.float(), zp.float(), atol=2e-2, rtol=1e-2)
+    assert torch.allclose(st[:, :, 0].sum(1), zz.float().sum(1), rtol=1e-5, atol=1e-4)
+    aa = A(None, g.nodes["a"], [zz, st])[0]
+    rr = R(None, g.nodes["r"], [aa, zz, st])[0]
+    assert (aa.float() - a_ref).abs().max() < 5e-2
+    assert (rr.float() - r_ref).abs().max() < 8e-2
+
+
+def test_defer_layernorm_leaves_other_readers_alone():
+    """A LayerNorm read by anything but GEMM inputs (here a fetch) stays."""
+    import torch
+    from rust_tensorflow_serving2_amd.graph import fused as FU
+    from rust_tensorflow_serving2_amd.graph.ir import Graph, Node
+    from rust_tensorflow_serving2_amd.graph.patterns import LayerNormOp
+
+    cpu = torch.device("cpu")
+    mm0 = FU.FusedMatMul(torch.randn(64, 64), None, "none", False, cpu, True, "p")
+    mm1 = FU.FusedMatMul(torch.randn(64, 64), None, "none", False, cpu, True, "a")
+    g = Graph()
+    g.add(Node(name="x", op="Placeholder"))
+    g.add(Node(name="p", op="_FusedMatMul", inputs=[("x", 0)], attrs={"_impl": mm0}))
+    g.add(Node(name="ln", op="_LayerNorm", inputs=[("p", 0)],
+               attrs={"_impl": LayerNormOp(torch.ones(64), torch.zeros(64), 1e-6, cpu, True)}))
+    g.add(Node(name="a", op="_FusedMatMul", inputs=[("ln", 0)], attrs={"_impl": mm1}))
+    order = ["x", "p", "ln", "a"]
+    FU.defer_layernorm(g, order, set(), [("a", 0)], torch.device("cuda"), None)    # opt-in: off by default
+    assert "ln" in g.nodes
+    os.environ["TFSERVE_DEFER_LN"] = "1"
+    try:
+        FU.defer_layernorm(g, order, set(), [("a", 0), ("ln", 0)], torch.device("cuda"), None)
+    finally:
+        del os.environ["TFSERVE_DEFER_LN"]
+    assert "ln" in g.nodes and g.nodes["a"].inputs == [("ln", 0)]
+    FU.defer_layernorm(g, order, set(), [("a", 0)], torch.device("cpu"), None)   # CPU programs: never
+    assert "ln" in g.nodes

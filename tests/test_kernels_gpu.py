@@ -893,3 +893,90 @@ def test_stem_pool_bf16_input_is_bit_identical(n, h, w, c):
     y32 = hip().stem_pool(x.to(DEV), *args)
     y16 = hip().stem_pool(x.to(BF).to(DEV), *args)
     assert torch.equal(y32, y16)
+
+
+# Deferred LayerNorm (hip().linear_lnx, graph/fused.py defer_layernorm): GEMMs
+# whose A rows / residual rows are pre-LayerNorm sums with (sum, sum sq)
+# partials, and that emit their own rows' partials -- vs fp32 references with
+# the LayerNorm materialised.
+LNX_CFGS = [36, 47, 100, 72, 123, 38, 114, 128, 129, 45]
+
+
+def _row_partials(t: torch.Tensor, parts: int) -> torch.Tensor:
+    """[M][parts][2] (sum, sum sq) over `parts` column slices of t's rows."""
+    f = t.float()
+    cols = torch.tensor_split(torch.arange(f.shape[1]), parts)
+    return torch.stack([torch.stack([f[:, c].sum(1), (f[:, c] ** 2).sum(1)], 1) for c in cols], 1).contiguous()
+
+
+@pytest.mark.parametrize("cfg", LNX_CFGS)
+@pytest.mark.parametrize("m,n,k", [(4096, 768, 768), (1000, 768, 3072), (77, 256, 128), (130, 512, 64)])
+def test_linear_lnx_residual_side_and_stats(m, n, k, cfg):
+    x = rnd(m, k, seed=61).to(BF)
+    w = rnd(n, k, scale=1 / math.sqrt(k), seed=62).to(BF)
+    b = rnd(n, scale=0.1, seed=63)
+    zr = (rnd(m, n, seed=64) * 2 + 0.5).to(BF)               # the residual before its LayerNorm
+    g, bt = 1 + rnd(n, scale=0.1, seed=65), rnd(n, scale=0.1, seed=66)
+    y_ref = x.float() @ w.float().t() + b + F.layer_norm(zr.float(), (n,), g, bt, 1e-12)
+    for parts in (1, 3):
+        y, st = hip().linear_lnx(x.to(DEV), w.to(DEV), b.to(DEV), zr.to(DEV), 0, cfg,
+                                 r_st=_row_partials(zr, parts).to(DEV), r_gamma=g.to(DEV), r_beta=bt.to(DEV),
+                                 r_eps=1e-12, stats=True)
+        torch.cuda.synchronize()
+        y = y.float().cpu()
+        assert (y - y_ref).abs().max().item() < 3e-2 * max(1.0, y_ref.abs().max().item())
+        # the emitted partials are exactly the stored rows' sums (fp32 order aside)
+        tot = st.cpu().sum(1)
+        assert st.shape[0] == m and st.shape[2] == 2
+        assert torch.allclose(tot[:, 0], y.sum(1), rtol=1e-4, atol=1e-2)
+        assert torch.allclose(tot[:, 1], (y * y).sum(1), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("cfg", LNX_CFGS)
+@pytest.mark.parametrize("m,n,k", [(4096, 768, 768), (1000, 3072, 768), (77, 256, 128), (130, 512, 64)])
+def test_linear_lnx_input_side_matches_fp32(m, n, k, cfg):
+    z = (rnd(m, k, seed=71) * 1.5 + 0.3).to(BF)                # A before its LayerNorm
+    W = rnd(k, n, scale=1 / math.sqrt(k), seed=72)
+    b = rnd(n, scale=0.1, seed=73)
+    g, bt = 1 + rnd(k, scale=0.1, seed=74), rnd(k, scale=0.1, seed=75)
+    ref = F.gelu(F.layer_norm(z.float(), (k,), g, bt, 1e-12) @ W + b, approximate="tanh")
+    wf = (W * g[:, None]).t().contiguous().to(BF)
+    colsum = wf.float().sum(1)
+    bf = b + bt @ W
+    y, st = hip().linear_lnx(z.to(DEV), wf.to(DEV), bf.to(DEV), None, ACT["gelu_tanh"], cfg,
+                             a_st=_row_partials(z, 2).to(DEV), a_colsum=colsum.to(DEV), a_eps=1e-12)
+    torch.cuda.synchronize()
+    assert st.numel() == 0
+    assert (y.float().cpu() - ref).abs().max().item() < 4e-2 * max(1.0, ref.abs().max().item())
+
+
+def test_linear_lnx_in_graph_replays_and_rejections():
+    m, n, k = 512, 768, 256
+    z = rnd(m, k, seed=81).to(BF).to(DEV)
+    w = rnd(n, k, scale=1 / math.sqrt(k), seed=82).to(BF).to(DEV)
+    zr = rnd(m, n, seed=83).to(BF).to(DEV)
+    cs = w.float().sum(1)
+    ast, rst = _row_partials(z, 2), _row_partials(zr, 4)
+    g1, b1 = torch.ones(n, device=DEV), torch.zeros(n, device=DEV)
+    y = torch.empty(m, n, device=DEV, dtype=BF)
+    kw = dict(a_st=ast, a_colsum=cs, r_st=rst, r_gamma=g1, r_beta=b1, stats=True)
+    _, st0 = hip().linear_lnx(z, w, None, zr, 0, 100, False, y, **kw)
+    torch.cuda.synchronize()
+    eager, est = y.clone(), st0.clone()
+    s = torch.cuda.Stream()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(gr, stream=s):
+        _, st = hip().linear_lnx(z, w, None, zr, 0, 100, False, y, **kw)
+    for _ in range(3):
+        y.zero_()
+        gr.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, eager) and torch.equal(st, est)
+    with pytest.raises(RuntimeError):      # persistent configs: no deferred LayerNorm
+        hip().linear_lnx(z, w, None, zr, 0, 130, **kw)
+    with pytest.raises(RuntimeError):      # igemm configs: no deferred LayerNorm
+        hip().linear_lnx(z, w, None, zr, 0, 0, **kw)
+    with pytest.raises(RuntimeError):      # statistics of fp32 outputs
+        hip().linear_lnx(z, w, None, zr, 0, 100, True, **kw)
+    with pytest.raises(RuntimeError):      # partials must be [M][P][2]
+        hip().linear_lnx(z, w, None, zr, 0, 100, r_st=rst[:100], r_gamma=g1, r_beta=b1)
