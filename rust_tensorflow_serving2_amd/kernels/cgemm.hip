@@ -43,9 +43,9 @@ using cgemm_impl::launch_cfg;
 // S * (BM + BN) * 128 B (or the fp32 epilogue tile if larger).
 constexpr int kAll = kNumCGemmConfigs + kNumCGemmConfigs2;
 constexpr int kBM[kAll] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256, 64, 64, 128, 128, 128, 64,
-                           64, 64, 64, 128, 64, 128, 64, 64, 256};
+                           64, 64, 64, 128, 64, 128, 64, 64, 256, 256};
 constexpr int kBN[kAll] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64, 64, 128, 64, 96, 96, 96,
-                           64, 64, 64, 64, 128, 64, 128, 64, 192};
+                           64, 64, 64, 64, 128, 64, 128, 64, 192, 144};
 
 // PF config ids kCGemmPfCfgBase + i: the fragment-prefetch build of table index kPfOf[i]
 // (the 8-wave 256 x 128 / 128 x 256 / 256 x 192 tiles spill with two fragment sets: not built)
@@ -126,6 +126,10 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
     // 8 waves of 64x96 (BERT's 2304 / 3072-wide projections at M = 4096: 192 /
     // 256 tiles, one per CU); 112 KB ring, epilogue in two 128-row passes
     case 24: return launch_cfg<256, 192, 4, 2, 2, AM>(a, s);
+    // 8 waves of 32x144: BERT-base's QKV projection (4096 x 2304) is exactly
+    // 256 tiles of 256 x 144, one per CU, where 256 x 192 leaves 64 CUs idle
+    // (192 tiles); 150 KB, a 3-slot ring, the fp32 epilogue in one pass
+    case 25: return launch_cfg<256, 144, 8, 1, 3, AM>(a, s);
     default: return hipErrorInvalidValue;
   }
 }

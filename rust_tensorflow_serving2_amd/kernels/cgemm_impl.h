@@ -749,7 +749,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
       const RPn& rpn = *reinterpret_cast<const RPn*>(rpre);   // not read (USE_PRE = false)
       auto epi = [&](int ps) __attribute__((always_inline)) {
         const int mp = m0 + ps * RPP;
-        if (lnx) {
+        bool done = false;
+        if constexpr (LNX) if (lnx) {
+          done = true;
           LnLds<BM, BN> lp = ln;
           lp.sa += ps * RPP;
           lp.sr += ps * RPP;
@@ -761,7 +763,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
             case kActTanh: epilogue_lnx<RPP, BN, ENT, G::CS_LD, kActTanh, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1, lp); break;
             default: epilogue_lnx<RPP, BN, ENT, G::CS_LD, 0, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1, lp); break;
           }
-        } else {
+        }
+        if (!done) {
           switch (p.act) {
             case kActRelu: epilogue_rows<RPP, BN, ENT, G::CS_LD, kActRelu, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1); break;
             case kActGeluTanh: epilogue_rows<RPP, BN, ENT, G::CS_LD, kActGeluTanh, false>(p, Cs, mp, n0, etid, rpn, bias0, bias1); break;
@@ -872,7 +875,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
     constexpr bool P1 = G::PASSES == 1;
     using RP = uint4[Epi<RPP, BN, G::NT>::PRE > 0 ? Epi<RPP, BN, G::NT>::PRE : 1];
     const RP& rp = *reinterpret_cast<const RP*>(rpre);   // only read when PASSES == 1 (RPP == BM)
-    if (lnx) {
+    if constexpr (LNX) if (lnx) {
       LnLds<BM, BN> lp = ln;                 // this pass's rows
       lp.sa += ps * RPP;
       lp.sr += ps * RPP;
@@ -908,7 +911,7 @@ template <int BM, int BN, int WGM, int WGN, int S, int AM, bool PF = false, int 
 hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
   using G = CG<BM, BN, WGM, WGN, S, MF, KTT>;
   const bool lnx = a0.st_out != nullptr || a0.a_st != nullptr || a0.r_st != nullptr;
-  if (lnx && (AM != 0 || a0.splits > 1 || a0.out2 != nullptr || G::LDS_LNX > 160 * 1024 ||
+  if (lnx && (AM != 0 || (BN / 8) % 4 != 0 || a0.splits > 1 || a0.out2 != nullptr || G::LDS_LNX > 160 * 1024 ||
               (a0.st_out != nullptr && (a0.out_f32 || a0.out == nullptr)) ||
               (a0.a_st != nullptr && (a0.a_colsum == nullptr || a0.a_parts < 1)) ||
               (a0.r_st != nullptr && (a0.residual == nullptr || a0.r_gamma == nullptr || a0.r_beta == nullptr ||
@@ -922,7 +925,7 @@ hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
   if (splits > 1) a.kt_per_split = (nk + splits - 1) / splits;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
-  if constexpr (AM == 0) {
+  if constexpr (AM == 0 && (BN / 8) % 4 == 0) {     // (epilogue_lnx row groups of 4 chunk lanes)
     if (lnx) {
       hipError_t e = ensure_dyn_lds(
           reinterpret_cast<const void*>(&cgemm_kernel<BM, BN, WGM, WGN, S, AM, PF, MF, KTT, true>), lds);
