@@ -770,11 +770,14 @@ O.OPS["_StemPool"] = _impl_op
 
 # (K1, N1, N2) shapes kernels/chain.hip is built for (ResNet-50 stages 1-2).
 # Stage 2's (N1 = 512) pairs measured no faster chained than as two launches
-# (each workgroup re-reads 256-384 KB of weights for 64 rows, one workgroup per
-# CU: profiles/round3/conv_chain.md), so by default only the stage-1 shapes are
-# chained; TFSERVE_CONV_CHAIN_SHAPES=all enables every kernel shape.
+# at b32 (each workgroup re-reads 256-384 KB of weights for 64 rows, one
+# workgroup per CU: profiles/round3/conv_chain.md); since round 5 every shape
+# is chained in the graph and ChainConv times the chain against the two
+# convs per batch bucket (ops.tuned_choice), so each bucket runs its faster
+# form.  TFSERVE_CONV_CHAIN_SHAPES=stage1 restores the stage-1-only pass.
 CHAIN_SHAPES_ALL = {(64, 256, 64), (64, 256, 128), (128, 512, 128), (128, 512, 256)}
-CHAIN_SHAPES_DEFAULT = {(64, 256, 64), (64, 256, 128)}
+CHAIN_SHAPES_STAGE1 = {(64, 256, 64), (64, 256, 128)}
+CHAIN_SHAPES_DEFAULT = CHAIN_SHAPES_ALL
 
 
 class ChainConv:
@@ -797,14 +800,25 @@ class ChainConv:
         x = O.to_torch(ins[0])
         res = O.to_torch(ins[1]) if len(ins) > 1 else None
         a, b = self.a, self.b
-        if self.use_hip and x.is_cuda and x.dim() == 4 and x.shape[-1] == a.cin:
-            from ..ops import ACT, hip
-            y1, y2 = hip().conv_chain(_to_bf16(x).contiguous(), a.w, a.b,
-                                      None if res is None else _to_bf16(res).contiguous(), ACT[a.act],
-                                      b.w, b.b, ACT[b.act])
-            return [y1, y2]
-        y1 = a(ctx, node, ins)[0]
-        return [y1, b(ctx, node, [y1])[0]]
+
+        def split():
+            y1 = a(ctx, node, ins)[0]
+            return [y1, b(ctx, node, [y1])[0]]
+        if not (self.use_hip and x.is_cuda and x.dim() == 4 and x.shape[-1] == a.cin):
+            return split()
+        from ..ops import ACT, hip, tuned_choice
+        xb = _to_bf16(x).contiguous()
+        rb = None if res is None else _to_bf16(res).contiguous()
+
+        def chained():
+            return list(hip().conv_chain(xb, a.w, a.b, rb, ACT[a.act], b.w, b.b, ACT[b.act]))
+        # one workgroup per 64 rows: the chain wins where it saves a launch
+        # boundary at small row counts or re-reads of large Y1 tiles, and loses
+        # where 64-row workgroups leave CUs idle -- timed per shape (bucket):
+        # option 1 = the chain kernel, 0 = the two convs with their own tiles
+        key = ("chain", tuple(x.shape), a.cout, b.cout, res is not None, a.act, b.act)
+        pick = tuned_choice(key, {1: chained, 0: split}, default=1)
+        return chained() if pick == 1 else split()
 
 
 O.OPS["_ChainConv"] = _impl_op
@@ -1220,7 +1234,7 @@ def fuse_conv_chain(g, order, fed, fetch_refs, device, opts):
     the op then runs both reference convs)."""
     import os
     mode = os.environ.get("TFSERVE_CONV_CHAIN", "1")
-    shapes = CHAIN_SHAPES_ALL if os.environ.get("TFSERVE_CONV_CHAIN_SHAPES") == "all" else CHAIN_SHAPES_DEFAULT
+    shapes = CHAIN_SHAPES_STAGE1 if os.environ.get("TFSERVE_CONV_CHAIN_SHAPES") == "stage1" else CHAIN_SHAPES_ALL
     c = _Ctx(g, order, fed, fetch_refs, device, opts)
     if mode == "0" or (not c.use_hip and mode != "force"):
         return

@@ -421,6 +421,65 @@ def tuned_config(key: Tuple, M: int, N: int, launch: Callable[[int, int], None],
         return best
 
 
+def tuned_choice(key: Tuple, options: Dict[int, Callable[[], None]], default: int) -> int:
+    """Pick the fastest of a few whole implementations of one op (e.g. a
+    chained two-conv kernel vs the two convs) for ``key`` -- timed like
+    tuned_config (cold L2, median of 5 single launches), stored with the tile
+    picks (``(option, 1)``: the committed table, the replicas' shared table and
+    graph_tune, which re-times the options inside the whole replay, all apply).
+    Options that raise RuntimeError are skipped; ``default`` during capture or
+    without autotuning."""
+    key = regime_key(key)
+    rec = getattr(_REC, "keys", None)
+    if rec is not None:
+        rec[key] = rec.get(key, 0) + 1
+    _ensure_cache()
+    hit = _TUNED.get(key)
+    if hit is not None:
+        return hit[0]
+    remote = _REMOTE.get(repr(key)) if _REMOTE else None
+    if remote is not None:
+        with _TUNE_LOCK:
+            _TUNED[key] = remote
+            _GRAPH_TUNED.add(key)
+        return remote[0]
+    if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
+        return default
+    ok = {}
+    for o, fn in options.items():
+        try:
+            fn()            # warm: the option's own tile picks are made here, outside the lock
+            ok[o] = fn
+        except RuntimeError:
+            continue
+    if not ok:
+        raise RuntimeError(f"no implementation could run {key}")
+    with _TUNE_LOCK:
+        hit = _TUNED.get(key)
+        if hit is not None:
+            return hit[0]
+        flush = _flush_buffer()
+        times = []
+        for o, fn in ok.items():
+            samples = []
+            for _rep in range(5):
+                flush.zero_()
+                torch.cuda._sleep(_HOST_SHADOW_CYCLES)
+                start = torch.cuda.Event(enable_timing=True)
+                end = torch.cuda.Event(enable_timing=True)
+                start.record()
+                fn()
+                end.record()
+                end.synchronize()
+                samples.append(start.elapsed_time(end))
+            samples.sort()
+            times.append((samples[len(samples) // 2], (o, 1)))
+        times.sort()
+        _TUNE_TIMES[key] = times
+        _TUNED[key] = times[0][1]
+        return times[0][1][0]
+
+
 @contextlib.contextmanager
 def record_tuned_keys():
     """Collect {key: uses} of every tuned_config lookup made on this thread

@@ -980,3 +980,29 @@ def test_linear_lnx_in_graph_replays_and_rejections():
         hip().linear_lnx(z, w, None, zr, 0, 100, True, **kw)
     with pytest.raises(RuntimeError):      # partials must be [M][P][2]
         hip().linear_lnx(z, w, None, zr, 0, 100, r_st=rst[:100], r_gamma=g1, r_beta=b1)
+
+
+def test_tuned_choice_picks_the_faster_option_and_caches_it():
+    """ops.tuned_choice (ChainConv's chain-vs-two-convs pick): times each
+    option, keeps the faster, skips options that raise, returns the cached
+    pick afterwards without running anything."""
+    from rust_tensorflow_serving2_amd import ops
+    calls = {0: 0, 1: 0, 2: 0}
+
+    def slow():
+        calls[0] += 1
+        torch.cuda._sleep(2_000_000)
+
+    def fast():
+        calls[1] += 1
+        torch.cuda._sleep(10_000)
+
+    def bad():
+        calls[2] += 1
+        raise RuntimeError("not launchable")
+    key = ("test_choice", 1)
+    assert ops.tuned_choice(key, {0: slow, 1: fast, 2: bad}, default=0) == 1
+    seen = dict(calls)
+    assert ops.tuned_choice(key, {0: slow, 1: fast, 2: bad}, default=0) == 1
+    assert calls == seen                      # cached: nothing re-run
+    assert ops._TUNED[key] == (1, 1) and [c for _t, c in ops._TUNE_TIMES[key]] == [(1, 1), (0, 1)]
