@@ -10,7 +10,7 @@ constexpr int kCGemmCfgBase = 32;
 constexpr int kNumCGemmConfigs = 16;
 // a second id range (after the halo ids): 2-wave and 3-deep variants
 constexpr int kCGemmCfgBase2 = 64;
-constexpr int kNumCGemmConfigs2 = 10;
+constexpr int kNumCGemmConfigs2 = 12;
 // a third range: fragment-prefetch (PF) builds of 11 of the tiles above
 constexpr int kCGemmPfCfgBase = 96;
 constexpr int kNumCGemmPfConfigs = 11;

@@ -43,9 +43,9 @@ using cgemm_impl::launch_cfg;
 // S * (BM + BN) * 128 B (or the fp32 epilogue tile if larger).
 constexpr int kAll = kNumCGemmConfigs + kNumCGemmConfigs2;
 constexpr int kBM[kAll] = {128, 128, 64, 128, 64, 256, 128, 128, 64, 256, 64, 64, 128, 128, 128, 64,
-                           64, 64, 64, 128, 64, 128, 64, 64, 256, 256};
+                           64, 64, 64, 128, 64, 128, 64, 64, 256, 256, 128, 128};
 constexpr int kBN[kAll] = {128, 128, 128, 64, 64, 128, 256, 128, 256, 64, 64, 128, 64, 96, 96, 96,
-                           64, 64, 64, 64, 128, 64, 128, 64, 192, 144};
+                           64, 64, 64, 64, 128, 64, 128, 64, 192, 144, 96, 96};
 
 // PF config ids kCGemmPfCfgBase + i: the fragment-prefetch build of table index kPfOf[i]
 // (the 8-wave 256 x 128 / 128 x 256 / 256 x 192 tiles spill with two fragment sets: not built)
@@ -130,6 +130,11 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
     // 256 tiles of 256 x 144, one per CU, where 256 x 192 leaves 64 CUs idle
     // (192 tiles); 150 KB, a 3-slot ring, the fp32 epilogue in one pass
     case 25: return launch_cfg<256, 144, 8, 1, 3, AM>(a, s);
+    // 8 waves of 32x48 on the 128 x 96 tile (N = 768 at M = 4096: 256 tiles):
+    // two waves per SIMD to cover the DMA latency the 4-wave 128 x 96 builds
+    // (ids 45 / 46) leave exposed over K = 3072; 4- and 5-slot rings
+    case 26: return launch_cfg<128, 96, 4, 2, 4, AM>(a, s);   // 112 KB
+    case 27: return launch_cfg<128, 96, 4, 2, 5, AM>(a, s);   // 140 KB
     default: return hipErrorInvalidValue;
   }
 }

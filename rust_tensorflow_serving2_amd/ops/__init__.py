@@ -151,7 +151,7 @@ CGEMM = {32: (128, 128), 33: (128, 128), 34: (64, 128), 35: (128, 64), 36: (64, 
          37: (256, 128), 38: (128, 256), 39: (128, 128), 40: (64, 256), 41: (256, 64),
          42: (64, 64), 43: (64, 128), 44: (128, 64), 45: (128, 96), 46: (128, 96), 47: (64, 96),
          64: (64, 64), 65: (64, 64), 66: (64, 64), 67: (128, 64), 68: (64, 128), 69: (128, 64), 70: (64, 128),
-         71: (64, 64), 72: (256, 192), 73: (256, 144)}
+         71: (64, 64), 72: (256, 192), 73: (256, 144), 74: (128, 96), 75: (128, 96)}
 # fragment-prefetch (PF) builds of 11 of those tiles (kernels/cgemm.hip kPfOf)
 CGEMM_PF_OF = [32, 34, 35, 36, 39, 41, 42, 43, 44, 45, 71]
 CGEMM.update({96 + k: CGEMM[base] for k, base in enumerate(CGEMM_PF_OF)})

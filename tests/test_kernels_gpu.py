@@ -77,7 +77,7 @@ def test_conv_matches_fp32(shape, cfg, splits):
 
 
 PGEMM_CFGS = list(range(130, 138))      # persistent multi-tile builds (no split-K)
-CGEMM_CFGS = list(range(32, 48)) + list(range(64, 74)) + list(range(96, 107)) + list(range(112, 130)) + PGEMM_CFGS
+CGEMM_CFGS = list(range(32, 48)) + list(range(64, 76)) + list(range(96, 107)) + list(range(112, 130)) + PGEMM_CFGS
 CGEMM_CONV_SHAPES = [s for s in CONV_SHAPES if s[3] % 64 == 0] + [
     (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)),   # tiny image: most taps hit padding at the border rows
     (1, 15, 13, 64, 192, 3, 2, (0, 1, 1, 1)),  # odd sizes, asymmetric pads, N tail
