@@ -59,7 +59,7 @@ long halo_tiles(const IGemmArgs& a, int cfg);
 // Config ids kHaloCfgBase .. + kNumHaloConfigs - 1; split-K splits the channel
 // chunks (kt_per_split counts 64-channel chunks).
 constexpr int kHaloCfgBase = 48;
-constexpr int kNumHaloConfigs = 9;
+constexpr int kNumHaloConfigs = 11;
 // the same halo tiles with the fragment-prefetch step pipeline (PF)
 constexpr int kHaloPfCfgBase = 80;
 // the PF build of tile 4 (256x128, 8 waves) does not fit the register budget

@@ -438,9 +438,9 @@ hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
 }
 
 // per config index (halo_cfg_index)
-constexpr int kHBM[kNumHaloConfigs] = {256, 128, 128, 64, 256, 64, 64, 128, 256};
-constexpr int kHBN[kNumHaloConfigs] = {64, 128, 64, 64, 128, 128, 64, 64, 64};
-constexpr int kHHR[kNumHaloConfigs] = {320, 192, 192, 128, 320, 128, 128, 192, 320};     // halo rows (HR)
+constexpr int kHBM[kNumHaloConfigs] = {256, 128, 128, 64, 256, 64, 64, 128, 256, 128, 128};
+constexpr int kHBN[kNumHaloConfigs] = {64, 128, 64, 64, 128, 128, 64, 64, 64, 64, 64};
+constexpr int kHHR[kNumHaloConfigs] = {320, 192, 192, 128, 320, 128, 128, 192, 320, 192, 192};     // halo rows (HR)
 
 int halo_cfg_index(int cfg) {
   if (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) return cfg - kHaloCfgBase;
@@ -484,6 +484,8 @@ hipError_t halo_launch(const IGemmArgs& a, int cfg, hipStream_t s) {
       case 6: return launch_halo_cfg<64, 64, 2, 2, 128, 9, true>(a, s);
       case 7: return launch_halo_cfg<128, 64, 2, 2, 192, 9, true>(a, s);
       case 8: return launch_halo_cfg<256, 64, 4, 1, 320, 9, true>(a, s);
+      case 9: return launch_halo_cfg<128, 64, 4, 2, 192, 3, true>(a, s);
+      case 10: return launch_halo_cfg<128, 64, 4, 2, 192, 9, true>(a, s);
       default: return hipErrorInvalidValue;
     }
   }
@@ -499,6 +501,11 @@ hipError_t halo_launch(const IGemmArgs& a, int cfg, hipStream_t s) {
     case 6: return launch_halo_cfg<64, 64, 2, 2, 128, 9>(a, s);     // 104 KB, waves 32x32
     case 7: return launch_halo_cfg<128, 64, 2, 2, 192, 9>(a, s);    // 120 KB, waves 64x32
     case 8: return launch_halo_cfg<256, 64, 4, 1, 320, 9>(a, s);    // 152 KB, waves 64x64
+    // 8 waves of 32x32 on the 128 x 64 tile: two waves per SIMD where the
+    // 4-wave build waits 40 % of its cycles (the stage-2 / 3 3x3 convs,
+    // profiles/round4/s5/pmc_r50_b32_mfma.txt)
+    case 9: return launch_halo_cfg<128, 64, 4, 2, 192, 3>(a, s);    // 72 KB
+    case 10: return launch_halo_cfg<128, 64, 4, 2, 192, 9>(a, s);   // 120 KB
     default: return hipErrorInvalidValue;
   }
 }

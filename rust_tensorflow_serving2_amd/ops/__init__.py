@@ -170,7 +170,7 @@ CGEMM.update(PGEMM)
 TILES.update(CGEMM)
 # halo-tiled 3x3 stride-1 conv (kernels/halo.hip): config id -> (output pixels per tile, BN)
 HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 128), 53: (64, 128), 54: (64, 64),
-        55: (128, 64), 56: (256, 64)}
+        55: (128, 64), 56: (256, 64), 57: (128, 64), 58: (128, 64)}
 # the same tiles with the fragment-prefetch step pipeline (halo.hip PF)
 HALO.update({cfg + 32: tile for cfg, tile in list(HALO.items()) if cfg != 52})
 TILES.update(HALO)

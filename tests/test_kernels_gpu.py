@@ -105,7 +105,7 @@ def test_cgemm_conv_matches_fp32(shape, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
 
 
-HALO_CFGS = list(range(48, 57)) + [80, 81, 82, 83, 85, 86, 87, 88]
+HALO_CFGS = list(range(48, 59)) + [80, 81, 82, 83, 85, 86, 87, 88, 89, 90]
 HALO_SHAPES = [
     # N, H, W, Cin, Cout, pads            (3x3 stride 1; ResNet-50 stages + edge cases)
     (2, 56, 56, 64, 64, (1, 1, 1, 1)),
