@@ -200,7 +200,12 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
-  __syncthreads();   // P strip (wave-private) + nothing else pending; cheap at this size
+  // the P strip is wave-private (this wave's 16 rows) and K / Vt were staged
+  // before the barrier above: only this wave's LDS writes must land before
+  // its P reads, so no workgroup barrier (waves that finish the softmax early
+  // start P V without waiting for the others)
+  __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
   attn_stamp(trace, trace_cap, 2);          // scores + softmax done
 
   // ---- ctx = P V
