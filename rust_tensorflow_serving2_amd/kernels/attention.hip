@@ -4,15 +4,16 @@
 // Q | K | V column blocks, head h at columns h*D).  One 256-thread workgroup
 // per (batch, head, 64-query block); each wave64 owns 16 query rows against
 // all S keys:
-//   scores = Q K^T          v_mfma_f32_16x16x32_bf16, K row-major in LDS
+//   scores^T = K Q^T        v_mfma_f32_16x16x32_bf16, K row-major in LDS
 //                           (XOR-swizzled 16-B chunks: conflict-free b128 reads)
-//   P = softmax(scores*scale + mask_bias)   in registers: each lane holds 4 rows
-//                           x S/16 columns; row max/sum via 16-lane xor shuffles
-//   ctx = P V               P re-laid out through a per-wave LDS strip into the
-//                           A-operand layout; V stored transposed (Vt[d][key],
-//                           rows padded by 16 B) so B fragments are 16-B reads;
-//                           the transpose is done in registers on 8x8 blocks
-//                           so staging is 16-B loads and 16-B LDS stores
+//   P = softmax(scores*scale + mask_bias)   in registers: each lane holds one
+//                           query's S/16 x 4 keys; row max/sum = 2 xor shuffles
+//   ctx^T = V^T P^T         P stays in registers as the B operand (k slots
+//                           permuted, the A side reads V^T rows to match); V
+//                           stored transposed (Vt[d][key], rows padded by 16 B),
+//                           transposed in registers on 8x8 blocks, after the
+//                           scores so its loads overlap them
+// (attention_plds_kernel: the previous layout, P through a per-wave LDS strip.)
 // S in {64, 128, 192, 256} (the whole key row in registers; D == 64), and
 // attention_flash_kernel below for any other S up to
 // kMaxAttentionSeq.  The S x S matrix never touches HBM.
@@ -44,8 +45,192 @@ __device__ __forceinline__ void attn_stamp(long long* trace, int cap, int k) {
   }
 }
 
+// Scores computed transposed (S^T = K Q^T: keys on the MFMA rows, queries on
+// the columns), so each lane ends the softmax holding, for ONE query (its
+// column fr), the 8 keys {32ks + 4fq + r, 32ks + 16 + 4fq + r} of every 32-key
+// block: exactly a B fragment of ctx^T = V^T P^T under a k-slot permutation
+// that the A side (V^T rows, two 8-B LDS reads per fragment) repeats.  P never
+// goes through LDS and the output leaves in 8-B row pieces straight from the
+// accumulators.  Staging is split: Q, K and the key mask land first (one
+// barrier), V's loads stay in flight in registers through the scores and the
+// softmax and are transposed into LDS behind a second barrier -- the V half of
+// the staging overlaps the score math instead of preceding it.
 template <int S, int QB>
 __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __restrict__ qkv,
+                                                           const float* __restrict__ mask_bias,
+                                                           uint16_t* __restrict__ ctx, int H, float scale,
+                                                           long mask_bstride, long mask_qstride,
+                                                           long long* __restrict__ trace, int trace_cap) {
+  attn_stamp(trace, trace_cap, 0);
+  constexpr int NTH = QB * 4;            // QB / 16 waves
+  constexpr int VT_LD = S + 8;           // Vt row stride (elements): +16 B pad
+  constexpr int NT = S / 16;             // key tiles
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);          // [S][64] swizzled
+  uint16_t* Vt = Ks + S * D;                                  // [64][VT_LD]
+  float* Ms = reinterpret_cast<float*>(Vt + D * VT_LD);       // [S] key mask adder
+
+  const int qblocks = S / QB;
+  const int bid = blockIdx.x;
+  const int qb = bid % qblocks;
+  const int h = (bid / qblocks) % H;
+  const int b = bid / (qblocks * H);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const long row_stride = 3L * H * D;
+  const uint16_t* base = qkv + long(b) * S * row_stride;
+
+  // ---- Q fragments (the B operand of K Q^T: column = query fr, k = d)
+  const int q0 = qb * QB + wid * 16;
+  bf16x8 qf[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+    qf[kk] = *reinterpret_cast<const bf16x8*>(base + long(q0 + fr) * row_stride + h * D + kk * 32 + fq * 8);
+  static_assert((S * 8) % NTH == 0 && S <= NTH, "staging split");
+  constexpr int KIT = S * 8 / NTH;
+  uint4 kv[KIT];
+#pragma unroll
+  for (int i = 0; i < KIT; ++i) {
+    const int c = tid + i * NTH, key = c >> 3, ch = c & 7;
+    kv[i] = *reinterpret_cast<const uint4*>(base + long(key) * row_stride + H * D + h * D + ch * 8);
+  }
+  // the [B,1,1,S] key mask (BERT's adder, mask_qstride == 0): 4 keys per
+  // thread into LDS; a 0-record descriptor (zeros) when the mask is per query
+  // row or absent
+  const bool key_mask = mask_bias != nullptr && mask_qstride == 0;
+  const __amdgpu_buffer_rsrc_t rsM = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(key_mask ? mask_bias + long(b) * mask_bstride : mask_bias), 0, key_mask ? S * 4 : 0,
+      0x00020000);
+  const u32x4 mk = __builtin_amdgcn_raw_buffer_load_b128(rsM, uint32_t(tid < S / 4 ? tid : 0) * 16u, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  // V: an 8-key x 8-dim block per thread (threads >= S load a clamped
+  // in-range block whose stores land in the rows' padding), issued now,
+  // consumed after the softmax
+  const int vblk = tid < S ? tid : S - 1;
+  const int kg = vblk >> 3, vch = vblk & 7;
+  uint32_t w[8][4];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + long(kg * 8 + k) * row_stride + 2 * H * D + h * D +
+                                                    vch * 8);
+    w[k][0] = v.x; w[k][1] = v.y; w[k][2] = v.z; w[k][3] = v.w;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < KIT; ++i) {
+    const int c = tid + i * NTH, key = c >> 3, ch = c & 7;
+    *reinterpret_cast<uint4*>(Ks + key * D + ((ch ^ (key & 7)) * 8)) = kv[i];
+  }
+  if (tid < S / 4) *reinterpret_cast<u32x4*>(Ms + tid * 4) = mk;
+  __syncthreads();
+  attn_stamp(trace, trace_cap, 1);          // Q / K / mask staged (V in flight)
+
+  // ---- S^T tiles: lane holds keys nt*16 + 4fq + r of query fr
+  f32x4 s[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int key = nt * 16 + fr;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + fq;
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + key * D + ((ch ^ (key & 7)) * 8));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], acc, 0, 0, 0);
+    }
+    s[nt] = acc;
+  }
+  // ---- softmax over keys: 32 values per lane, then the 4 lanes of a query
+  float mx = -INFINITY;
+  if (key_mask) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const f32x4 mb = *reinterpret_cast<const f32x4*>(Ms + nt * 16 + fq * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = s[nt][r] * scale + mb[r];
+        s[nt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+  } else {
+    const float* mq = mask_bias ? mask_bias + long(b) * mask_bstride + long(q0 + fr) * mask_qstride : nullptr;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = s[nt][r] * scale + (mq ? mq[nt * 16 + fq * 4 + r] : 0.f);
+        s[nt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+  bf16x8 pb[S / 32];                        // P^T B fragments, k-slot j -> tile 2ks + (j >> 2), r = j & 3
+#pragma unroll
+  for (int ks = 0; ks < S / 32; ++ks) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float e = __expf(s[2 * ks + (j >> 2)][j & 3] - mx);
+      sum += e;
+      pb[ks][j] = __builtin_bit_cast(__bf16, f32_to_bf16(e));
+    }
+  }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  attn_stamp(trace, trace_cap, 2);          // scores + softmax done
+
+  // ---- V transposed into LDS (8 x 16-B stores per thread) behind the second barrier
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = (d & 1) ? (w[2 * j][d >> 1] >> 16) : (w[2 * j][d >> 1] & 0xffffu);
+      const uint32_t hi = (d & 1) ? (w[2 * j + 1][d >> 1] & 0xffff0000u) : (w[2 * j + 1][d >> 1] << 16);
+      o[j] = lo | hi;
+    }
+    const int vcol = tid < S ? kg * 8 : S;
+    *reinterpret_cast<uint4*>(Vt + (vch * 8 + d) * VT_LD + vcol) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  __syncthreads();
+
+  // ---- ctx^T = V^T P^T: A = Vt rows dt*16 + fr at the same permuted keys
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < S / 32; ++ks) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const uint16_t* vr = Vt + (dt * 16 + fr) * VT_LD + ks * 32 + fq * 4;
+      const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+      const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+      const bf16x8 va = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb[ks], o[dt], 0, 0, 0);
+    }
+  }
+  attn_stamp(trace, trace_cap, 3);          // P V done (wave 0)
+  // ---- normalise; lane holds dims dt*16 + 4fq + [0, 4) of query q0 + fr
+  const float inv = 1.f / sum;
+  uint16_t* orow = ctx + (long(b) * S + q0 + fr) * (long(H) * D) + h * D + fq * 4;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const uint32_t lo = uint32_t(f32_to_bf16(o[dt][0] * inv)) | (uint32_t(f32_to_bf16(o[dt][1] * inv)) << 16);
+    const uint32_t hi = uint32_t(f32_to_bf16(o[dt][2] * inv)) | (uint32_t(f32_to_bf16(o[dt][3] * inv)) << 16);
+    *reinterpret_cast<uint2*>(orow + dt * 16) = make_uint2(lo, hi);
+  }
+  if (trace != nullptr) {
+    __builtin_amdgcn_s_waitcnt(0);          // this wave's stores acknowledged
+    attn_stamp(trace, trace_cap, 4);
+  }
+}
+
+// The previous layout (TFSERVE_ATTN_PLDS=1, A/B only): scores un-transposed,
+// P re-laid out through a per-wave LDS strip, all staging before one barrier.
+template <int S, int QB>
+__global__ __launch_bounds__(QB * 4) void attention_plds_kernel(const uint16_t* __restrict__ qkv,
                                                            const float* __restrict__ mask_bias,
                                                            uint16_t* __restrict__ ctx, int H, float scale,
                                                            long mask_bstride, long mask_qstride,
@@ -410,14 +595,34 @@ __global__ __launch_bounds__(256) void attention_flash_kernel(const uint16_t* __
   }
 }
 
+// -1: TFSERVE_ATTN_PLDS decides (default off); 0 / 1 forced (attention_set_plds)
+int g_attn_plds = -1;
+bool attn_plds() {
+  static const bool env = [] {
+    const char* e = getenv("TFSERVE_ATTN_PLDS");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  return g_attn_plds < 0 ? env : g_attn_plds != 0;
+}
+
 template <int S, int QB = qb_for(S)>
 hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, int H, float scale, long bs, long qs,
                     hipStream_t st) {
-  constexpr int lds = (S * D + D * (S + 8) + (QB / 16) * 16 * (S + 8)) * 2;
-  static_assert(S % QB == 0 && lds <= 160 * 1024, "attention tile");
+  static_assert(S % QB == 0, "attention tile");
+  const int grid = B * H * (S / QB);
+  if (attn_plds()) {
+    constexpr int lds = (S * D + D * (S + 8) + (QB / 16) * 16 * (S + 8)) * 2;
+    static_assert(lds <= 160 * 1024, "attention tile");
+    hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&attention_plds_kernel<S, QB>), lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((attention_plds_kernel<S, QB>), dim3(grid), dim3(QB * 4), lds, st, qkv, mb, ctx, H, scale, bs,
+                       qs, g_attn_trace, g_attn_trace_cap);
+    return hipGetLastError();
+  }
+  constexpr int lds = (S * D + D * (S + 8)) * 2 + S * 4;
+  static_assert(lds <= 160 * 1024, "attention tile");
   hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&attention_kernel<S, QB>), lds);
   if (e != hipSuccess) return e;
-  const int grid = B * H * (S / QB);
   hipLaunchKernelGGL((attention_kernel<S, QB>), dim3(grid), dim3(QB * 4), lds, st, qkv, mb, ctx, H, scale, bs, qs,
                      g_attn_trace, g_attn_trace_cap);
   return hipGetLastError();
@@ -432,6 +637,12 @@ int attn_qb() {
 }
 
 }  // namespace
+
+int attention_set_plds(int mode) {
+  const int prev = g_attn_plds;
+  g_attn_plds = mode < 0 ? -1 : (mode ? 1 : 0);
+  return prev;
+}
 
 void attention_set_trace(long long* trace, int cap) {
   g_attn_trace = trace;

@@ -876,6 +876,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     g_trace_cap = int(std::min<int64_t>(t->numel() / 8, 1 << 30));
     tfsk::attention_set_trace(g_trace, g_trace_cap);
   }, "per-workgroup wall-clock stamps of the following GEMM / conv launches (None: off)");
+  m.def("set_attention_plds", [](int64_t mode) { return tfsk::attention_set_plds(int(mode)); },
+        "fixed-S attention: 1 = the P-through-LDS kernel, 0 = P in registers (default), -1 = env; returns the "
+        "previous mode (process-wide; set it outside captures)");
   m.def("set_splitk_fixup", [](int64_t mode) {
     const int prev = g_fixup_override;
     g_fixup_override = mode < 0 ? -1 : (mode ? 1 : 0);

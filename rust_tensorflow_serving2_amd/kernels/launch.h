@@ -209,5 +209,8 @@ hipError_t attention_launch(const uint16_t* qkv, const float* mask_bias, uint16_
 // per-workgroup phase stamps of the following fixed-S attention launches
 // (entry, staged, softmax, P V, stored; [7] = CU id); nullptr: off
 void attention_set_trace(long long* trace, int cap);
+// fixed-S attention layout: 1 = P through LDS (previous kernel), 0 = P in
+// registers (default), -1 = env TFSERVE_ATTN_PLDS; returns the previous mode
+int attention_set_plds(int mode);
 
 }  // namespace tfsk

@@ -536,9 +536,20 @@ def test_classifier_head_one_launch_matches_three(monkeypatch, m, hw, k, np_, n)
         assert torch.equal(cg, c3)
 
 
-@pytest.mark.parametrize("s", [64, 128, 256,
+@pytest.mark.parametrize("s", [64, 128, 192, 256,
                                32, 100, 320, 384, 512])     # KV-block (online softmax) kernel, partial blocks
-def test_attention_matches_fp32(s):
+@pytest.mark.parametrize("plds", [0, 1])                    # P in registers (default) / through LDS (previous)
+def test_attention_matches_fp32(s, plds):
+    if plds and s not in (64, 128, 192, 256):
+        pytest.skip("the P-through-LDS layout is a fixed-S kernel")
+    prev = hip().set_attention_plds(plds)
+    try:
+        _check_attention(s)
+    finally:
+        hip().set_attention_plds(prev)
+
+
+def _check_attention(s):
     b, h, d = 3, 12, 64
     qkv = rnd(b, s, 3 * h * d, seed=21).to(BF)
     mask = torch.zeros(b, s)
@@ -554,6 +565,11 @@ def test_attention_matches_fp32(s):
     att2 = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(d) + full, -1)
     ref2 = (att2 @ v).permute(0, 2, 1, 3).reshape(b, s, h * d)
     assert (y2.float().cpu() - ref2).abs().max() < 3e-2
+    # no mask
+    y3 = hip().attention(qkv.to(DEV), None, h, 1 / math.sqrt(d), None, 0, 0)
+    att3 = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(d), -1)
+    ref3 = (att3 @ v).permute(0, 2, 1, 3).reshape(b, s, h * d)
+    assert (y3.float().cpu() - ref3).abs().max() < 3e-2
 
 
 @pytest.mark.parametrize("cfg,splits,shape", [
