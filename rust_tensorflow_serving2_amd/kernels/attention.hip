@@ -29,9 +29,10 @@ namespace {
 
 constexpr int D = 64;
 
-// query rows per workgroup (16 per wave).  64 measured faster than one
-// workgroup per (batch, head) with QB = S at BERT-base b32 S=128 (161 vs 182 us
-// per 12 layers): twice the workgroups outweigh staging K/V twice.
+// query rows per workgroup (16 per wave) for S != 128 (S = 128: attn_qb).  With
+// P through LDS, 64 measured faster than one workgroup per (batch, head) at
+// BERT-base b32 (161 vs 182 us per 12 layers); with P in registers, 128 wins
+// there (attn_qb below).
 constexpr int qb_for(int) { return 64; }
 
 // per-workgroup phase stamps (scripts/wg_trace.py --attention; null: off)
@@ -212,14 +213,28 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
     }
   }
   attn_stamp(trace, trace_cap, 3);          // P V done (wave 0)
-  // ---- normalise; lane holds dims dt*16 + 4fq + [0, 4) of query q0 + fr
+  // ---- normalise; lane holds dims dt*16 + 4fq + [0, 4) of query q0 + fr.
+  // Re-laid out through a wave-private 16 x 64 block of the K rows (every
+  // wave passed its scores before the second barrier; (wid + 1) * 16 <= S)
+  // with 16-B chunks XOR-swizzled by row, then stored as whole 128-B rows:
+  // 8-B stores straight from the accumulators touch 16 rows per instruction
+  // (0.88 vs 0.24 us for the store phase, profiles/round5/s40/wgN.log)
   const float inv = 1.f / sum;
-  uint16_t* orow = ctx + (long(b) * S + q0 + fr) * (long(H) * D) + h * D + fq * 4;
+  uint16_t* os = Ks + wid * 16 * D;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
     const uint32_t lo = uint32_t(f32_to_bf16(o[dt][0] * inv)) | (uint32_t(f32_to_bf16(o[dt][1] * inv)) << 16);
     const uint32_t hi = uint32_t(f32_to_bf16(o[dt][2] * inv)) | (uint32_t(f32_to_bf16(o[dt][3] * inv)) << 16);
-    *reinterpret_cast<uint2*>(orow + dt * 16) = make_uint2(lo, hi);
+    const int chunk = dt * 2 + (fq >> 1);
+    *reinterpret_cast<uint2*>(os + fr * D + ((chunk ^ (fr & 7)) * 8) + (fq & 1) * 4) = make_uint2(lo, hi);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): this wave's LDS writes landed
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = j * 64 + lane, row = c >> 3, ch = c & 7;
+    *reinterpret_cast<uint4*>(ctx + (long(b) * S + q0 + row) * (long(H) * D) + h * D + ch * 8) =
+        *reinterpret_cast<const uint4*>(os + row * D + ((ch ^ (row & 7)) * 8));
   }
   if (trace != nullptr) {
     __builtin_amdgcn_s_waitcnt(0);          // this wave's stores acknowledged
@@ -628,12 +643,16 @@ hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, 
   return hipGetLastError();
 }
 
-int attn_qb() {
+// query rows per workgroup at S = 128: TFSERVE_ATTN_QB (32 / 64 / 128) when
+// set, else 128 (one workgroup per (batch, head): K / V staged once) when that
+// still gives every CU a workgroup, 64 below (twice the workgroups for small
+// batches).  b32 BERT-base: 10.2 vs 11.4 us per layer (profiles/round5/s41/).
+int attn_qb(int BH) {
   static const int v = [] {
     const char* e = getenv("TFSERVE_ATTN_QB");
-    return e ? atoi(e) : 64;
+    return e ? atoi(e) : 0;
   }();
-  return v;
+  return v ? v : (BH >= 256 ? 128 : 64);
 }
 
 }  // namespace
@@ -657,7 +676,7 @@ hipError_t attention_launch(const uint16_t* qkv, const float* mask_bias, uint16_
     case 64: return launch_s<64>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
     case 128:
       // query rows per workgroup (TFSERVE_ATTN_QB: 32 / 64 / 128; experiments)
-      switch (attn_qb()) {
+      switch (attn_qb(B * H)) {
         case 32: return launch_s<128, 32>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
         case 128: return launch_s<128, 128>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);
         default: return launch_s<128>(qkv, mask_bias, ctx, B, H, scale, bs, qs, st);

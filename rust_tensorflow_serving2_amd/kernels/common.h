@@ -36,10 +36,22 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
 // a visible share of the GEMM). exp overflow -> rcp(inf) = 0: correct limits.
 __device__ __forceinline__ float sigm2(float u) { return __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u)); }
 
+// GELU-tanh as x * sigm2(u) with the constants folded into one polynomial in
+// x^2 and exp2: x * rcp(1 + exp2(x (k0 + k1 x^2))), k0 = -2 sqrt(2/pi) log2(e),
+// k1 = 0.044715 k0.  5 plain VALU ops + v_exp + v_rcp per element against 8 +
+// 2 for the textbook form (the FFN1 epilogue of BERT, 12.6 M elements per
+// forward, is VALU-bound behind the last MFMA: 32.6 vs 28.9 us without the
+// activation, profiles/round5/s41/blt.log).  Limits: x -> -inf gives
+// rcp(inf) = 0, x -> +inf gives x.
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float t = fmaf(x * x, -0.1029432395800235f, -2.302208198144325f);
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * t));
+}
+
 __device__ __forceinline__ float apply_act(float x, int act) {
   switch (act) {
     case kActRelu: return x > 0.f ? x : 0.f;
-    case kActGeluTanh: return x * sigm2(0.7978845608028654f * (x + 0.044715f * x * x * x));
+    case kActGeluTanh: return gelu_tanh(x);
     case kActGeluErf: return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
     case kActTanh: return 2.f * sigm2(x) - 1.f;
     default: return x;
@@ -53,7 +65,7 @@ __device__ __forceinline__ float act_fn(float x) {
   if constexpr (ACT == kActRelu) {
     return x > 0.f ? x : 0.f;
   } else if constexpr (ACT == kActGeluTanh) {
-    return x * sigm2(0.7978845608028654f * (x + 0.044715f * x * x * x));
+    return gelu_tanh(x);
   } else if constexpr (ACT == kActGeluErf) {
     return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
   } else if constexpr (ACT == kActTanh) {

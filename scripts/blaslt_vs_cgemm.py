@@ -31,6 +31,8 @@ BERT = {"qkv": (4096, 2304, 768), "ffn1": (4096, 3072, 768), "ffn2": (4096, 768,
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--set", default="resnet", choices=["resnet", "bert"])
+    ap.add_argument("--acts", default="", help="comma list (e.g. none,gelu_tanh): also time the best config "
+                                               "with each epilogue activation")
     a = ap.parse_args()
     for name, (M, N, K) in (BERT if a.set == "bert" else SHAPES).items():
         xs = [torch.randn(M, K, device="cuda").to(BF) for _ in range(8)]
@@ -51,9 +53,15 @@ def main():
                 continue
             best = min(best, (t, (cfg, sp)))
         tf = 2 * M * N * K / 1e6
+        by_act = {}
+        for act in filter(None, a.acts.split(",")):
+            cfg, sp = best[1]
+            by_act[act] = round(time_graph(lambda i: hip().linear(xs[i % 8], ws[i % 8], bf, None, ACT[act], cfg,
+                                                                  False, 1.0, outs[i % 8], sp)), 2)
         print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "hipblaslt_us": round(t_lt, 2),
                           "hipblaslt_tflops": round(tf / t_lt), "cgemm_us": round(best[0], 2),
-                          "cgemm_tflops": round(tf / best[0]), "cgemm_cfg": best[1]}), flush=True)
+                          "cgemm_tflops": round(tf / best[0]), "cgemm_cfg": best[1], "cgemm_us_by_act": by_act}),
+              flush=True)
 
 
 if __name__ == "__main__":
