@@ -688,6 +688,16 @@ void cast_bf16_from_host(const Tensor& x, const Tensor& out) {
         "cast_bf16_from_host");
 }
 
+void h2d_rows(const Tensor& host, const Tensor& dev) {
+  TORCH_CHECK(host.device().is_cpu() && host.is_pinned() && host.is_contiguous(), "h2d_rows: host must be a "
+              "contiguous pinned CPU tensor");
+  TORCH_CHECK(dev.is_cuda() && dev.is_contiguous(), "h2d_rows: dev must be a contiguous device tensor");
+  const int64_t bytes = host.numel() * host.element_size();
+  TORCH_CHECK(bytes == dev.numel() * dev.element_size(), "h2d_rows: size mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dev.device());
+  check(tfsk::h2d_rows_launch(host.data_ptr(), dev.data_ptr(), bytes, cur_stream(dev)), "h2d_rows");
+}
+
 Tensor cast_bf16(const Tensor& x, const c10::optional<Tensor>& out) {
   need(x, at::kFloat, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -842,6 +852,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("hp"), py::arg("wp"), py::arg("pt"), py::arg("pl"));
   m.def("ingest_c4_from_host", &ingest_c4_from_host, "ingest_c4 reading a pinned host tensor (zero-copy)",
         py::arg("x"), py::arg("out"));
+  m.def("h2d_rows", &h2d_rows, py::arg("host"), py::arg("dev"),
+        "copy a pinned host tensor into a device tensor with a kernel (system-scope loads; capturable)");
   m.def("cast_bf16_from_host", &cast_bf16_from_host, "fp32 pinned host tensor -> bf16 device tensor",
         py::arg("x"), py::arg("out"));
   m.def("layernorm", &layernorm, py::arg("x"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),

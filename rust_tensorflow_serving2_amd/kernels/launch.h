@@ -188,6 +188,9 @@ hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, 
 // fp32 -> bf16 cast (vectorized).
 hipError_t cast_f32_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t stream);
 hipError_t cast_bf16_f32_launch(const uint16_t* x, float* y, int64_t n, hipStream_t stream);
+// `bytes` (16-B multiple, 16-B aligned) of pinned host memory -> device, as a
+// kernel (system-scope loads): the small-bucket graphs' input copy
+hipError_t h2d_rows_launch(const void* host, void* dev, int64_t bytes, hipStream_t stream);
 
 // LayerNorm over the last dim (bf16 in/out, f32 gamma/beta), optional fused residual add:
 // y = LN(x + r) ; if `sum_out` != nullptr the pre-norm sum is also written.

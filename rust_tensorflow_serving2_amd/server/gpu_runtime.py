@@ -75,6 +75,9 @@ class _Lane:
         # per bucket: outputs the captured graph writes straight into host_out
         # (one-launch classifier head), whose D2H copy is skipped
         self.host_written: Dict[int, List[bool]] = {}
+        # per bucket: the captured graph copies its input rows itself (a kernel
+        # reading host_in, ops small buckets), so the lane issues no H2D
+        self.in_captured: Dict[int, bool] = {}
         # device inputs [max_bucket, ...]: every bucket graph reads a leading-row
         # view of the same buffer, so rows can be copied to the device as they
         # arrive (native lanes' eager H2D), before the batch size is known
@@ -255,9 +258,14 @@ class GpuRunner:
         if lane.pool is None and lane.share_pool:
             lane.pool = torch.cuda.graph_pool_handle()
         rows = self._head_rows(lane) if b <= 4 else None
+        h2d_in = self._graph_h2d(lane, b)
         with ops.capture_owner(graph), ops.head_host_rows(rows), \
                 torch.cuda.graph(graph, pool=lane.pool, stream=lane.stream, capture_error_mode="thread_local"):
+            if h2d_in:
+                for h, d in zip(lane.host_in, ins):
+                    ops.hip().h2d_rows(h[:b], d)
             outs = self._finish(self.program.run(ins))
+        lane.in_captured[b] = h2d_in
         lane.host_written[b] = [rows is not None and isinstance(o, torch.Tensor) and
                                 getattr(o, "_tfs_host", 0) == h.data_ptr() != 0
                                 for o, h in zip(outs, lane.host_out)]
@@ -271,6 +279,20 @@ class GpuRunner:
         lane.static_in[b] = ins
         lane.static_out[b] = outs
         log.info("captured HIP graph: %s bucket=%d (%d steps)", self.servable.name, b, len(self.program.steps))
+
+    @staticmethod
+    def _graph_h2d(lane: _Lane, b: int) -> bool:
+        """Whether bucket ``b``'s graph copies its own input rows from the
+        lane's pinned buffers (``h2d_rows``, a kernel) instead of the lane
+        issuing an SDMA copy ahead of the replay: buckets up to
+        ``TFSERVE_GRAPH_H2D_MAX`` rows (default 4; 0 = never), inputs of 16-B
+        multiple rows.  At batch 1 the copy engine's transfer plus its hand-off
+        to the graph took 21 us of the ResNet-50 request
+        (profiles/round5/s45/c1_timeline.json)."""
+        if b > int(os.environ.get("TFSERVE_GRAPH_H2D_MAX", "4")):
+            return False
+        return all(h.is_pinned() and (h[0].numel() * h.element_size()) % 16 == 0 and h.data_ptr() % 16 == 0
+                   for h in lane.host_in)
 
     @staticmethod
     def _head_rows(lane: _Lane):
@@ -353,8 +375,9 @@ class GpuRunner:
             with torch.cuda.device(self.device):
                 self._capture(lane, b)
         with torch.cuda.stream(lane.stream):
-            for h, d in zip(lane.host_in, lane.static_in[b]):
-                d[:n].copy_(h[:n], non_blocking=True)
+            if not lane.in_captured.get(b):
+                for h, d in zip(lane.host_in, lane.static_in[b]):
+                    d[:n].copy_(h[:n], non_blocking=True)
             lane.graphs[b].replay()
             written = lane.host_written.get(b) or [False] * len(lane.host_out)
             for so, ho, w in zip(lane.static_out[b], lane.host_out, written):
@@ -371,8 +394,9 @@ class GpuRunner:
         lane = self.lanes[lane_idx]
         buckets = []
         for b in self.buckets:
-            ins = [(d.data_ptr(), h.data_ptr(), d[0].numel() * d.element_size())
-                   for d, h in zip(lane.static_in[b], lane.host_in)]
+            ins = [] if lane.in_captured.get(b) else \
+                [(d.data_ptr(), h.data_ptr(), d[0].numel() * d.element_size())
+                 for d, h in zip(lane.static_in[b], lane.host_in)]
             written = lane.host_written.get(b) or [False] * len(lane.host_out)
             outs = [(h.data_ptr(), so.data_ptr(), so[0].numel() * so.element_size())
                     for so, h, w in zip(lane.static_out[b], lane.host_out, written) if not w]

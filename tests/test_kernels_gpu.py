@@ -1022,3 +1022,28 @@ def test_tuned_choice_picks_the_faster_option_and_caches_it():
     assert ops.tuned_choice(key, {0: slow, 1: fast, 2: bad}, default=0) == 1
     assert calls == seen                      # cached: nothing re-run
     assert ops._TUNED[key] == (1, 1) and [c for _t, c in ops._TUNE_TIMES[key]] == [(1, 1), (0, 1)]
+
+
+def test_h2d_rows_reads_fresh_host_rows_in_graph_replays():
+    """The small-bucket input copy: a kernel reading pinned host rows with
+    system-scope loads.  The host rewrites the SAME rows before every replay
+    of one captured graph; each replay must see that write (a line an earlier
+    replay left in L2 must not satisfy the next one)."""
+    for nbytes in (16, 512, 301056, 16 * 1024 + 16):
+        host = torch.zeros(nbytes // 2, dtype=torch.int16).pin_memory()
+        dev = torch.empty(nbytes // 2, dtype=torch.int16, device=DEV)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            hip().h2d_rows(host, dev)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            hip().h2d_rows(host, dev)
+        for i in range(12):
+            want = torch.randint(-30000, 30000, (nbytes // 2,), dtype=torch.int16, generator=torch.Generator().manual_seed(i))
+            host.copy_(want)
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(dev.cpu(), want), (nbytes, i)
+    with pytest.raises(RuntimeError):
+        hip().h2d_rows(torch.zeros(7, dtype=torch.int16).pin_memory(), torch.empty(7, dtype=torch.int16, device=DEV))

@@ -197,3 +197,31 @@ def test_small_buckets_write_their_rows_to_the_host(resnet50, monkeypatch):
         top2 = np.sort(a[1], -1)[:, -2:]
         clear = (top2[:, 1] - top2[:, 0]) > 1e-3
         np.testing.assert_array_equal(a[0][clear], b[0][clear])
+
+
+def test_small_buckets_copy_their_inputs_inside_the_graph(resnet50, monkeypatch):
+    """Buckets of <= 4 rows: the graph's first node copies the lane's pinned
+    input rows (``h2d_rows``), so the lane issues no SDMA copy ahead of the
+    replay.  Distinct inputs through the same rows, bucket after bucket, give
+    the outputs of the lane-side copy (TFSERVE_GRAPH_H2D_MAX=0); b32 keeps
+    the lane-side copy."""
+    from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
+    rng = np.random.default_rng(12)
+    xs = [rng.random((4, 224, 224, 3), dtype=np.float32) for _ in range(4)]
+    got, captured = {}, {}
+    for mode in ("0", "4"):
+        monkeypatch.setenv("TFSERVE_GRAPH_H2D_MAX", mode)
+        s = Servable("resnet", 1, resnet50, ServableOptions(
+            device="cuda:0", max_batch_size=32, allowed_batch_sizes=(1, 4, 32), lanes=1))
+        r = s.runner("serving_default", ["input"], ["classes", "probabilities"])
+        got[mode] = [r.run([x[:n]]) for x in xs for n in (1, 3, 4, 1)]
+        got[mode].append(r.run([np.concatenate([xs[0]] * 8)]))
+        captured[mode] = dict(r.lanes[0].in_captured)
+    assert captured["4"] == {1: True, 4: True, 32: False} and not any(captured["0"].values()), captured
+    for a, b in zip(got["0"], got["4"]):
+        np.testing.assert_allclose(a[1], b[1], atol=2e-4, rtol=0)
+        top2 = np.sort(a[1], -1)[:, -2:]
+        clear = (top2[:, 1] - top2[:, 0]) > 1e-3
+        np.testing.assert_array_equal(a[0][clear], b[0][clear])
+    # the four inputs differ, so a stale row would show: their outputs must too
+    assert not np.allclose(got["4"][0][1], got["4"][4][1], atol=1e-3)
