@@ -1078,18 +1078,28 @@ hipError_t key_mask_adder_launch(const void* m, int is_int, float one, float sca
 // in flight at once (4 x 16 B per thread) and carries system scope (sc0 sc1):
 // the host rewrites the same pinned rows for every batch, so a line cached in
 // L2 by an earlier replay must never satisfy a later one.
-constexpr int kH2dPer = 4;
+template <int PER>
 __global__ __launch_bounds__(256) void h2d_rows_kernel(const void* __restrict__ src, u32x4* __restrict__ dst, int n16) {
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(src), 0, n16 * 16, 0x00020000);
-  const int base = blockIdx.x * (256 * kH2dPer) + threadIdx.x;
-  u32x4 v[kH2dPer];
+  const int base = blockIdx.x * (256 * PER) + threadIdx.x;
+  u32x4 v[PER];
 #pragma unroll
-  for (int j = 0; j < kH2dPer; ++j)
+  for (int j = 0; j < PER; ++j)
     v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, uint32_t(base + j * 256) * 16u, 0, 17);   // sc0 | sc1
 #pragma unroll
-  for (int j = 0; j < kH2dPer; ++j)
+  for (int j = 0; j < PER; ++j)
     if (base + j * 256 < n16) dst[base + j * 256] = v[j];
+}
+
+// 16-B pieces per thread: TFSERVE_H2D_PER (1 / 2 / 4; A/B), default 4
+int h2d_per() {
+  static const int v = [] {
+    const char* e = getenv("TFSERVE_H2D_PER");
+    const int x = e ? atoi(e) : 4;
+    return x == 1 || x == 2 ? x : 4;
+  }();
+  return v;
 }
 
 hipError_t h2d_rows_launch(const void* host, void* dev, int64_t bytes, hipStream_t s) {
@@ -1097,9 +1107,14 @@ hipError_t h2d_rows_launch(const void* host, void* dev, int64_t bytes, hipStream
   if (bytes % 16 != 0 || bytes >= (int64_t(1) << 31) ||
       (reinterpret_cast<uintptr_t>(host) | reinterpret_cast<uintptr_t>(dev)) % 16 != 0)
     return hipErrorInvalidValue;
-  const int n16 = int(bytes / 16);
-  hipLaunchKernelGGL(h2d_rows_kernel, dim3((n16 + 256 * kH2dPer - 1) / (256 * kH2dPer)), dim3(256), 0, s, host,
-                     reinterpret_cast<u32x4*>(dev), n16);
+  const int n16 = int(bytes / 16), per = h2d_per();
+  const dim3 grid((n16 + 256 * per - 1) / (256 * per));
+  u32x4* d = reinterpret_cast<u32x4*>(dev);
+  switch (per) {
+    case 1: hipLaunchKernelGGL(h2d_rows_kernel<1>, grid, dim3(256), 0, s, host, d, n16); break;
+    case 2: hipLaunchKernelGGL(h2d_rows_kernel<2>, grid, dim3(256), 0, s, host, d, n16); break;
+    default: hipLaunchKernelGGL(h2d_rows_kernel<4>, grid, dim3(256), 0, s, host, d, n16); break;
+  }
   return hipGetLastError();
 }
 
