@@ -549,8 +549,14 @@ def test_attention_matches_fp32(s, plds):
         hip().set_attention_plds(prev)
 
 
-def _check_attention(s):
-    b, h, d = 3, 12, 64
+def test_attention_one_workgroup_per_head_at_large_batch():
+    """S = 128 with batch x heads >= 256 takes the 128-query-row workgroup
+    (8 waves, K / V staged once per (batch, head))."""
+    _check_attention(128, b=22)
+
+
+def _check_attention(s, b=3):
+    h, d = 12, 64
     qkv = rnd(b, s, 3 * h * d, seed=21).to(BF)
     mask = torch.zeros(b, s)
     mask[1, s // 2:] = -10000.0
