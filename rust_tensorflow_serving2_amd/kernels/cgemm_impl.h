@@ -15,6 +15,11 @@ namespace cgemm_impl {
 using namespace gemm;
 constexpr int kGroupM = 8;
 
+template <int A>
+struct ActC {
+  static constexpr int value = A;
+};
+
 template <int BM, int BN, int WGM, int WGN, int S, int MF = 16, int KTT = 64>
 struct CG {
   static constexpr int NW = WGM * WGN, NT = 64 * NW;
@@ -736,6 +741,61 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
             Cs[(wm * G::WM - ps * RPP + i * 16 + fq * 4 + r) * G::CS_LD + wn * G::WN + j * 16 + fr] = acc[i][j][r];
     }
   };
+  if constexpr (MF == 16 && BM * (BN + 8) * 2 <= G::LDS && (BM * (BN / 8)) % G::NT == 0) {
+    // Plain bf16 output (no residual / second output / deferred LayerNorm,
+    // activation without erf): bias and activation applied in registers and
+    // the bf16 tile staged in ONE pass by every wave, half the LDS bytes of
+    // the fp32 image.  The 256 x 192 tile's two-pass fp32 path below runs
+    // its passes on half the waves each, one after the other: its epilogue
+    // took 5.7 of 23.4 us of the workgroup's life, 2.8 us this way
+    // (profiles/round5/s2/wgt.log, s49/wgt.log).  Same arithmetic as
+    // epi_chunk (fma(acc, alpha, bias) + 0, act, RNE to bf16).
+    if (p.splits <= 1 && !lnx && p.residual == nullptr && p.out2 == nullptr && !p.out_f32 && p.out != nullptr &&
+        p.act != kActGeluErf) {
+      constexpr int CB_LD = BN + 8;
+      uint16_t* Cb = reinterpret_cast<uint16_t*>(smem);
+      const bool use_b = p.bias != nullptr && p.N % 8 == 0;
+      const __amdgpu_buffer_rsrc_t rsb =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.bias), 0, use_b ? p.N * 4 : 0, 0x00020000);
+      float bj[G::TN];
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j)
+        bj[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rsb, uint32_t(n0 + wn * G::WN + j * 16 + fr) * 4u, 0, 0));
+      const float alpha = p.alpha;
+      auto stage_bf16 = [&](auto actc) __attribute__((always_inline)) {
+        constexpr int ACT = decltype(actc)::value;
+#pragma unroll
+        for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = act_fn<ACT>(acc[i][j][r] * alpha + bj[j] + 0.f);
+              Cb[(wm * G::WM + i * 16 + fq * 4 + r) * CB_LD + wn * G::WN + j * 16 + fr] =
+                  __builtin_bit_cast(uint16_t, static_cast<__bf16>(v));
+            }
+      };
+      switch (p.act) {
+        case kActRelu: stage_bf16(ActC<kActRelu>{}); break;
+        case kActGeluTanh: stage_bf16(ActC<kActGeluTanh>{}); break;
+        case kActTanh: stage_bf16(ActC<kActTanh>{}); break;
+        default: stage_bf16(ActC<0>{}); break;
+      }
+      __syncthreads();
+      constexpr int CPRB = BN / 8;
+#pragma unroll
+      for (int it = 0; it < BM * CPRB / G::NT; ++it) {
+        const int c = tid + it * G::NT, row = c / CPRB, ch = c - row * CPRB;
+        const int m = m0 + row, n = n0 + ch * 8;
+        if (m < M && n < N)
+          *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.out) + size_t(m) * p.ldc + n) =
+              *reinterpret_cast<const uint4*>(Cb + row * CB_LD + ch * 8);
+      }
+      trace_stamp(p, 3);
+      return;
+    }
+  }
   if constexpr (G::PASSES == 2) {
     if (p.splits <= 1) {
       // Two-pass tiles (256 x 192): pass ps's rows belong to half of the waves.

@@ -128,6 +128,9 @@ def test_lane_buckets_share_one_graph_pool(resnet50, monkeypatch):
         assert len(pools) == (1 if share == "1" else len(lane.graphs))
         used[share] = _pool_bytes(pools)
         lane.dev_in[0].copy_(x.to(lane.dev_in[0].device))
+        # buckets of <= 4 rows copy their rows from the pinned host rows inside
+        # the graph (GpuRunner._graph_h2d): give them the same rows
+        lane.host_in[0].copy_(x.to(lane.host_in[0].dtype))
         probs = {}
         for b in (32, 1, 16, 2, 32, 8, 4, 1, 16):
             with torch.cuda.stream(lane.stream):
