@@ -751,7 +751,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (cg_waves_per_eu<BM, BN, WGM, WGN, 
     // (profiles/round5/s2/wgt.log, s49/wgt.log).  Same arithmetic as
     // epi_chunk (fma(acc, alpha, bias) + 0, act, RNE to bf16).
     if (p.splits <= 1 && !lnx && p.residual == nullptr && p.out2 == nullptr && !p.out_f32 && p.out != nullptr &&
-        p.act != kActGeluErf) {
+        p.act != kActGeluErf && !p.epi_f32) {
       constexpr int CB_LD = BN + 8;
       uint16_t* Cb = reinterpret_cast<uint16_t*>(smem);
       const bool use_b = p.bias != nullptr && p.N % 8 == 0;
@@ -980,6 +980,7 @@ hipError_t launch_cfg(const IGemmArgs& a0, hipStream_t s) {
     return hipErrorInvalidValue;                    // deferred LayerNorm: dense, one K slice, bf16 sums
   const int lds = lnx ? G::LDS_LNX : G::LDS;
   IGemmArgs a = a0;
+  a.epi_f32 = epi_f32_env();
   const int nk = a.K / KTT;
   const int splits = a.splits > 1 ? a.splits : 1;
   if (splits > 1) a.kt_per_split = (nk + splits - 1) / splits;

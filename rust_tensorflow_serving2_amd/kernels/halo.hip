@@ -78,6 +78,65 @@ __device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, const f32x4 (&
   const int TH = p.TH, TW = p.TW, Ho = p.Ho, Wo = p.Wo;
   const int TI = p.TI > 1 ? p.TI : 1, nimg = p.M / (Ho * Wo);
   const int lane = tid & 63, fr = lane & 15, fq = lane >> 4;
+  auto out_row = [&](int row) -> int {   // global GEMM row of tile row `row`, or -1
+    if (row >= TI * TH * TW) return -1;
+    const int ii = row / (TH * TW), r2 = row - ii * (TH * TW);
+    const int ph = r2 / TW, pw = r2 - ph * TW;
+    const int h = h0 + ph, w = w0 + pw;
+    if (h >= Ho || w >= Wo || img + ii >= nimg) return -1;
+    return ((img + ii) * Ho + h) * Wo + w;
+  };
+
+  // ---- plain bf16 output (no split, residual or second output; any
+  // activation but erf: the 3x3 convs of a bottleneck): bias and activation
+  // in registers, the bf16 tile staged once (half the LDS bytes of the fp32
+  // image), whole 16-B row chunks out.  Same arithmetic as epi_chunk (see
+  // cgemm_impl.h, the one-pass bf16 epilogue).
+  if (p.splits <= 1 && p.residual == nullptr && p.out2 == nullptr && !p.out_f32 && p.out != nullptr &&
+      p.act != kActGeluErf && !p.epi_f32) {
+    constexpr int CB_LD = BN + 8;
+    uint16_t* Cb = reinterpret_cast<uint16_t*>(smem);
+    const bool use_b = p.bias != nullptr && p.N % 8 == 0;
+    const __amdgpu_buffer_rsrc_t rsb =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.bias), 0, use_b ? p.N * 4 : 0, 0x00020000);
+    float bj[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bj[j] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(rsb, uint32_t(n0 + wn * WN + j * 16 + fr) * 4u, 0, 0));
+    const float alpha = p.alpha;
+    auto stage = [&](auto act_tag) __attribute__((always_inline)) {
+      constexpr int ACT = decltype(act_tag)::value;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = act_fn<ACT>(acc[i][j][r] * alpha + bj[j] + 0.f);
+            Cb[(wm * WM + i * 16 + fq * 4 + r) * CB_LD + wn * WN + j * 16 + fr] =
+                __builtin_bit_cast(uint16_t, static_cast<__bf16>(v));
+          }
+    };
+    switch (p.act) {
+      case kActRelu: stage(std::integral_constant<int, kActRelu>{}); break;
+      case kActGeluTanh: stage(std::integral_constant<int, kActGeluTanh>{}); break;
+      case kActTanh: stage(std::integral_constant<int, kActTanh>{}); break;
+      default: stage(std::integral_constant<int, kActNone>{}); break;
+    }
+    __syncthreads();
+    constexpr int CPRB = BN / 8;
+#pragma unroll 4
+    for (int c = tid; c < BM * CPRB; c += NT) {
+      const int row = c / CPRB, ch = c - row * CPRB;
+      const int m = out_row(row), n = n0 + ch * 8;
+      if (m >= 0 && n < p.N)
+        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.out) + size_t(m) * p.ldc + n) =
+            *reinterpret_cast<const uint4*>(Cb + row * CB_LD + ch * 8);
+    }
+    return;
+  }
+
   // ---- epilogue: fp32 tile staged in LDS; row = output pixel of the block
   float* Cs = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -88,15 +147,6 @@ __device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, const f32x4 (&
       for (int r = 0; r < 4; ++r)
         Cs[(wm * WM + i * 16 + fq * 4 + r) * CS_LD + wn * WN + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
-
-  auto out_row = [&](int row) -> int {   // global GEMM row of tile row `row`, or -1
-    if (row >= TI * TH * TW) return -1;
-    const int ii = row / (TH * TW), r2 = row - ii * (TH * TW);
-    const int ph = r2 / TW, pw = r2 - ph * TW;
-    const int h = h0 + ph, w = w0 + pw;
-    if (h >= Ho || w >= Wo || img + ii >= nimg) return -1;
-    return ((img + ii) * Ho + h) * Wo + w;
-  };
 
   using E = Epi<BM, BN, NT>;
   IGemmArgs q = p;                      // the epilogue's view (split-K fixup: splits 1, alpha 1)
@@ -418,6 +468,7 @@ template <int BM, int BN, int WGM, int WGN, int HR, int S, bool PF = false>
 hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
   using G = HG<BM, BN, WGM, WGN, HR, S>;
   IGemmArgs a = a0;
+  a.epi_f32 = epi_f32_env();
   if (!pick_block(a.Ho, a.Wo, BM, HR, a.TH, a.TW)) return hipErrorInvalidValue;
   a.TI = pick_images(a, BM, HR);
   const int nch = a.C / KT;
@@ -452,6 +503,7 @@ int halo_cfg_index(int cfg) {
 
 long halo_tiles(const IGemmArgs& a0, int cfg) {
   IGemmArgs a = a0;
+  a.epi_f32 = epi_f32_env();
   const int c = halo_cfg_index(cfg);
   if (c < 0) return 0;
   if (!pick_block(a.Ho, a.Wo, kHBM[c], kHHR[c], a.TH, a.TW)) return 0;

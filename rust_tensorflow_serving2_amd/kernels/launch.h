@@ -62,6 +62,9 @@ struct IGemmArgs {
   // per workgroup (blockIdx.y * gridDim.x + blockIdx.x), nullptr in production
   long long* trace;
   int trace_cap;        // workgroups the trace buffer holds
+  // 1: the fp32-staged epilogue even where the one-pass bf16 one applies
+  // (A/B only: TFSERVE_EPI_F32=1, set by the launchers)
+  int epi_f32;
   // deferred LayerNorm (cgemm dense, one K slice; graph/fused.py
   // defer_layernorm).  st_out: [M][ceil(N / BN)][2] fp32 -- per (row, column
   // block) (sum, sum of squares) of the stored bf16 outputs, each slot written
@@ -190,6 +193,8 @@ hipError_t cast_f32_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStrea
 hipError_t cast_bf16_f32_launch(const uint16_t* x, float* y, int64_t n, hipStream_t stream);
 // `bytes` (16-B multiple, 16-B aligned) of pinned host memory -> device, as a
 // kernel (system-scope loads): the small-bucket graphs' input copy
+// TFSERVE_EPI_F32 (read once): force the fp32-staged GEMM / conv epilogue
+int epi_f32_env();
 hipError_t h2d_rows_launch(const void* host, void* dev, int64_t bytes, hipStream_t stream);
 
 // LayerNorm over the last dim (bf16 in/out, f32 gamma/beta), optional fused residual add:

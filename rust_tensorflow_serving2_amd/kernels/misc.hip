@@ -1092,6 +1092,14 @@ __global__ __launch_bounds__(256) void h2d_rows_kernel(const void* __restrict__ 
     if (base + j * 256 < n16) dst[base + j * 256] = v[j];
 }
 
+int epi_f32_env() {
+  static const int v = [] {
+    const char* e = getenv("TFSERVE_EPI_F32");
+    return e != nullptr && atoi(e) != 0 ? 1 : 0;
+  }();
+  return v;
+}
+
 // 16-B pieces per thread: TFSERVE_H2D_PER (1 / 2 / 4; A/B), default 4
 int h2d_per() {
   static const int v = [] {
