@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
 // registers before the row arrives (their latency hides under the row's), no
 // idle lanes in the last chunk (the one-wave-per-row kernel above leaves half
 // of a wave idle for 768 columns).  Two-pass statistics from registers.
-template <int LPR, int CH>
+template <int LPR, int CH, int RG = 1>
 __global__ __launch_bounds__(256) void layernorm_fit_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ r,
                                                             const float* __restrict__ gamma,
@@ -539,7 +539,9 @@ __global__ __launch_bounds__(256) void layernorm_fit_kernel(const uint16_t* __re
   constexpr int RPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
   const int sub = lane / LPR, l = lane % LPR;
-  const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub;
+  // RG row groups per wave (TFSERVE_LN_RW): the gamma / beta registers serve
+  // RG x RPW rows instead of RPW
+  const int row0 = ((blockIdx.x * 4 + (threadIdx.x >> 6)) * RG) * RPW + sub;
   float g[CH][8], b[CH][8];
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
@@ -551,56 +553,66 @@ __global__ __launch_bounds__(256) void layernorm_fit_kernel(const uint16_t* __re
     b[k][0] = b0.x; b[k][1] = b0.y; b[k][2] = b0.z; b[k][3] = b0.w;
     b[k][4] = b1.x; b[k][5] = b1.y; b[k][6] = b1.z; b[k][7] = b1.w;
   }
-  const bool ok = row < rows;
-  const long base = long(ok ? row : 0) * COLS;
-  // every row load (x chunks and residual chunks) in flight at once: the
-  // residual goes through a buffer resource (0 records when there is none ->
-  // zeros), because `if (r) load` compiled to per-chunk conditional blocks that
-  // each waited for their load -- 2 x CH serial memory round trips per row
-  uint4 xv[CH];
-  u32x4 rv[CH];
+  // every row load (x chunks and residual chunks, all RG groups) in flight at
+  // once: the residual goes through a buffer resource (0 records when there
+  // is none -> zeros), because `if (r) load` compiled to per-chunk
+  // conditional blocks that each waited for their load -- 2 x CH serial
+  // memory round trips per row
   const __amdgpu_buffer_rsrc_t rsR = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(r), 0, r ? int(long(rows) * COLS * 2) : 0, 0x00020000);
+  uint4 xv[RG][CH];
+  u32x4 rv[RG][CH];
+  long base[RG];
+  bool ok[RG];
 #pragma unroll
-  for (int k = 0; k < CH; ++k) xv[k] = *reinterpret_cast<const uint4*>(x + base + (k * LPR + l) * 8);
+  for (int q = 0; q < RG; ++q) {
+    const int row = row0 + q * RPW;
+    ok[q] = row < rows;
+    base[q] = long(ok[q] ? row : 0) * COLS;
 #pragma unroll
-  for (int k = 0; k < CH; ++k)
-    rv[k] = __builtin_amdgcn_raw_buffer_load_b128(rsR, uint32_t(base + (k * LPR + l) * 8) * 2u, 0, 0);
+    for (int k = 0; k < CH; ++k) xv[q][k] = *reinterpret_cast<const uint4*>(x + base[q] + (k * LPR + l) * 8);
+#pragma unroll
+    for (int k = 0; k < CH; ++k)
+      rv[q][k] = __builtin_amdgcn_raw_buffer_load_b128(rsR, uint32_t(base[q] + (k * LPR + l) * 8) * 2u, 0, 0);
+  }
   // keep the gamma/beta loads above ahead of the row math (the scheduler sank
   // them below the reduction: one more serial round trip before the stores)
   __builtin_amdgcn_sched_barrier(0);
-  float v[CH][8];
-  float s = 0.f;
 #pragma unroll
-  for (int k = 0; k < CH; ++k) {
-    float rf[8];
-    unpack8(xv[k], v[k]);
-    unpack8(make_uint4(rv[k].x, rv[k].y, rv[k].z, rv[k].w), rf);
+  for (int q = 0; q < RG; ++q) {
+    float v[CH][8];
+    float s = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      v[k][e] += rf[e];
-      s += v[k][e];
+    for (int k = 0; k < CH; ++k) {
+      float rf[8];
+      unpack8(xv[q][k], v[k]);
+      unpack8(make_uint4(rv[q][k].x, rv[q][k].y, rv[q][k].z, rv[q][k].w), rf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[k][e] += rf[e];
+        s += v[k][e];
+      }
     }
-  }
 #pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  const float mean = s * (1.f / COLS);
-  float ss = 0.f;
+    for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s * (1.f / COLS);
+    float ss = 0.f;
 #pragma unroll
-  for (int k = 0; k < CH; ++k)
+    for (int k = 0; k < CH; ++k)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { const float d = v[k][e] - mean; ss += d * d; }
+      for (int e = 0; e < 8; ++e) { const float d = v[k][e] - mean; ss += d * d; }
 #pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-  const float inv = rsqrtf(ss * (1.f / COLS) + eps);
-  // no early return for rows past the end: with one, the gamma/beta loads
-  // were sunk below it and issued only after the row reduction
+    for (int o = LPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    const float inv = rsqrtf(ss * (1.f / COLS) + eps);
+    // no early return for rows past the end: with one, the gamma/beta loads
+    // were sunk below it and issued only after the row reduction
 #pragma unroll
-  for (int k = 0; k < CH; ++k) {
-    float o8[8];
+    for (int k = 0; k < CH; ++k) {
+      float o8[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o8[e] = (v[k][e] - mean) * inv * g[k][e] + b[k][e];
-    if (ok) *reinterpret_cast<uint4*>(y + base + (k * LPR + l) * 8) = pack8(o8);
+      for (int e = 0; e < 8; ++e) o8[e] = (v[k][e] - mean) * inv * g[k][e] + b[k][e];
+      if (ok[q]) *reinterpret_cast<uint4*>(y + base[q] + (k * LPR + l) * 8) = pack8(o8);
+    }
   }
 }
 
@@ -1131,15 +1143,30 @@ hipError_t cast_bf16_f32_launch(const uint16_t* x, float* y, int64_t n, hipStrea
   return hipGetLastError();
 }
 
+// row groups per wave of the exact-fit LayerNorm: TFSERVE_LN_RW (1 / 2; A/B), default 1
+int ln_rw() {
+  static const int v = [] {
+    const char* e = getenv("TFSERVE_LN_RW");
+    return e != nullptr && atoi(e) == 2 ? 2 : 1;
+  }();
+  return v;
+}
+
 template <int LPR, int CH>
 hipError_t ln_fit(const uint16_t* x, const uint16_t* r, const float* gamma, const float* beta, uint16_t* y, int rows,
                   float eps, hipStream_t s) {
-  const int per_block = 4 * (64 / LPR);
   if (long(rows) * LPR * 8 * CH * 2 >= 0x7fffffffL) {   // residual buffer offsets are 32-bit
     hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, r, gamma, beta, y, rows,
                        LPR * 8 * CH, eps);
     return hipGetLastError();
   }
+  if (ln_rw() == 2) {
+    const int per_block = 4 * 2 * (64 / LPR);
+    hipLaunchKernelGGL((layernorm_fit_kernel<LPR, CH, 2>), dim3((rows + per_block - 1) / per_block), dim3(256), 0, s,
+                       x, r, gamma, beta, y, rows, eps);
+    return hipGetLastError();
+  }
+  const int per_block = 4 * (64 / LPR);
   hipLaunchKernelGGL((layernorm_fit_kernel<LPR, CH>), dim3((rows + per_block - 1) / per_block), dim3(256), 0, s, x, r,
                      gamma, beta, y, rows, eps);
   return hipGetLastError();
