@@ -403,7 +403,8 @@ def main():
             r0, r1 = io0.get("router"), io1.get("router")
             if r0 and r1:
                 d["router"] = {k: r1[k] - r0[k] for k in ("forwarded", "streamed", "ingested", "returned",
-                                                          "reclaimed", "lost", "no_cell", "rerun")
+                                                          "reclaimed", "lost", "no_cell", "rerun", "unseen_origin",
+                                                          "orphaned")
                                if k in r1 and k in r0}
         return d
 
@@ -447,6 +448,18 @@ def main():
         dist.barrier()
     t_end = time.perf_counter()
     elapsed = t_last - t0
+    # The bracket (barrier -> last counted completion) over-reads by about
+    # 1 / (2 K) on average: the load generator never drains, so the window's
+    # first batch was mostly computed before the barrier and completes at a
+    # random phase after it (round-5 VERDICT weak item 2).  The unbiased rate
+    # counts K - 1 batch intervals: from the completion that ends the first
+    # step's worth of requests to the last one.  Both are reported; `value`
+    # is the interval one.
+    done = sorted(r.get("done_s") or [])
+    if len(done) > per_step:
+        iv_n, iv_s = len(done) - per_step, max(done[-1] - done[per_step - 1], 1e-9)
+    else:
+        iv_n, iv_s = float(r["ok"]), max(elapsed, 1e-9)
     cpu_report = diag(cpu0, topology.thread_cpu(), io0, io_stats(), ru0, os.times(), elapsed)
     cpu_report["top_threads"] = topology.top_threads(tid0, topology.thread_cpu_by_tid(), elapsed)
     # other tenants: busy share of this rank's node / the host, run-queue wait, quota throttling
@@ -547,8 +560,8 @@ def main():
     if os.environ.get("TFSERVE_BENCH_DUMP") and rank == 0:
         np.save(os.environ["TFSERVE_BENCH_DUMP"], lat)      # completion-order latencies (diagnostics)
     mine = torch.tensor([elapsed, float(r["ok"]), float(r["errors"]), np.percentile(lat, 50) if lat.size else 0,
-                         np.percentile(lat, 99) if lat.size else 0, p50_c1 or 0.0], dtype=torch.float64,
-                        device=coll_dev)
+                         np.percentile(lat, 99) if lat.size else 0, p50_c1 or 0.0, iv_s, float(iv_n)],
+                        dtype=torch.float64, device=coll_dev)
     my_diag = {"placement": dict(placement.as_dict(), pinned=pinned,
                                  bdf=gpu_info[local].bdf if local < len(gpu_info) else None),
                "gpu_busy_pct": gpu_busy, "timed": cpu_report, "prewarm": diag_window,
@@ -556,7 +569,8 @@ def main():
                "rank_timing": {"rank": rank, "ok": int(r["ok"]), "elapsed_s": round(elapsed, 6),
                                "start_sync_ms": cpu_report["start_sync_ms"],
                                "end_sync_ms": cpu_report["end_sync_ms"],
-                               "bracket_s": cpu_report["bracket_s"]},
+                               "bracket_s": cpu_report["bracket_s"],
+                               "interval_s": round(iv_s, 6), "interval_requests": int(iv_n)},
                "rccl": weight_source.report() if weight_source is not None else None}
     if world > 1:
         allv = [torch.zeros_like(mine) for _ in range(world)]
@@ -571,7 +585,11 @@ def main():
     if rank == 0:
         t_max = float(allv[:, 0].max())
         total_ok = float(allv[:, 1].sum())
-        value = total_ok / t_max
+        value_bracket = total_ok / t_max
+        # the unbiased K - 1 interval rate (see the timed bracket above), max span over ranks
+        iv_max = float(allv[:, 6].max())
+        value = float(allv[:, 7].sum()) / iv_max
+        ms_step = 1e3 * iv_max / max(1, args.steps - 1) if allv[0, 7] < allv[0, 1] else 1e3 * t_max / args.steps
         metric = METRIC if args.model != "bert-base" else \
             f"Predict RPCs/sec + p50 latency, BERT-base seq={args.seq_len} dynamic batching on MI355X"
         model_label = {"resnet50": "ResNet-50 v1.5", "resnet50-v2": "ResNet-50 v2", "tiny": "tiny-transport-probe",
@@ -583,7 +601,7 @@ def main():
             "synthetic int32 token ids / masks, random-init BERT-base weights"
         out = {
             "metric": metric, "value": round(value, 1), "unit": "Predict RPCs/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * t_max / args.steps, 3),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if on_gpu else "fp32 (cpu test mode)",
             "data": data,
@@ -593,6 +611,11 @@ def main():
                        "parallelism": f"dp{world}", "server_batch": args.batch,
                        "request_batch": args.request_batch, "image_size": args.image_size,
                        "transport": args.transport, "concurrency_per_gpu": conc},
+            "value_bracket": round(value_bracket, 1),
+            "ms_per_step_bracket": round(1e3 * t_max / args.steps, 3),
+            "timing": "value = (requests after the first step's worth) / (last completion - completion that "
+                      "ends the first step), K-1 batch intervals, max span over ranks; value_bracket = "
+                      "requests / (barrier -> last completion)",
             "images_per_s": round(value * args.request_batch, 1),
             "p50_latency_ms": round(float(np.median(allv[:, 3])) / 1e3, 3),
             "p99_latency_ms": round(float(allv[:, 4].max()) / 1e3, 3),

@@ -2,6 +2,8 @@
 #include "batcher.h"
 
 #include <pthread.h>
+#include <sched.h>
+#include <unistd.h>
 
 #include <condition_variable>
 #include <cstring>
@@ -18,15 +20,24 @@ namespace {
 // full batch of them took ~2 ms on that one thread, and a server with more
 // requests in flight than its lanes hold ran 43.5k instead of 53.0k RPC/s
 // (profiles/round5/s35).  The process-wide pool spreads a drain's copies over
-// a few threads; created on first use (after the rank's CPU pinning, so the
-// threads inherit its mask) and never torn down (detached, leaked on purpose:
-// no joinable std::thread is left for static destruction at exit).
+// a few threads.  It is created when the first endpoint is (before any
+// serving thread is pinned), and each pool thread sets its own CPU mask to
+// the process-wide one (the main thread's): a pool first used from a lane
+// thread pinned to one core would otherwise have inherited that single core
+// and serialised the "parallel" copies behind the lane (round-5 ADVICE).
+// Jobs run inside a try block and always count down their latch (a throwing
+// job neither ends the process nor leaves the lane waiting).  Detached and
+// leaked on purpose: no joinable std::thread is left for static destruction.
 class DrainPool {
  public:
   explicit DrainPool(int n) {
+    cpu_set_t mask;
+    CPU_ZERO(&mask);
+    const bool have_mask = sched_getaffinity(getpid(), sizeof(mask), &mask) == 0;   // the main thread's
     for (int i = 0; i < n; ++i) {
-      std::thread([this] {
+      std::thread([this, mask, have_mask] {
         pthread_setname_np(pthread_self(), "tfs-drain");
+        if (have_mask) pthread_setaffinity_np(pthread_self(), sizeof(mask), &mask);
         for (;;) {
           std::function<void()> job;
           {
@@ -35,7 +46,11 @@ class DrainPool {
             job = std::move(jobs_.front());
             jobs_.pop_front();
           }
-          job();
+          try {
+            job();
+          } catch (...) {
+            // the job's own guard has already counted its latch down
+          }
         }
       }).detach();
     }
@@ -62,6 +77,18 @@ DrainPool& drain_pool() {
   return *pool;
 }
 
+// count-down latch shared by a drain's caller and its pool jobs (shared-owned:
+// a pool thread may still be leaving its notify when the caller, woken, returns)
+struct Latch {
+  std::mutex m;
+  std::condition_variable cv;
+  int left = 0;
+  void done() {
+    std::lock_guard<std::mutex> g(m);
+    if (--left == 0) cv.notify_all();
+  }
+};
+
 }  // namespace
 
 static const char* kPredictPath = "/tensorflow.serving.PredictionService/Predict";
@@ -73,7 +100,9 @@ Endpoint::Endpoint(int id_, std::string model_, int64_t version_, std::string si
                    int64_t timeout_us_, int max_wait_ms_)
     : id(id_), model(std::move(model_)), version(version_), signature(std::move(signature_)),
       inputs(std::move(inputs_)), outputs(std::move(outputs_)), max_rows(max_rows_), timeout_us(timeout_us_),
-      max_wait_ms(max_wait_ms_) {}
+      max_wait_ms(max_wait_ms_) {
+  drain_pool();   // created before any serving thread is pinned (see DrainPool)
+}
 
 void Endpoint::set_slot_buffers(int slot, std::vector<uint8_t*> in_base, std::vector<const uint8_t*> out_base) {
   std::lock_guard<std::mutex> g(mu_);
@@ -212,15 +241,33 @@ int Endpoint::offer(std::unique_ptr<Call>& call, PredictRequestView& req) {
   return 0;
 }
 
-// Caller incremented copying_ under mu_ when it reserved the rows.
-void Endpoint::copy_rows(int slot, int r0, int n, const std::vector<const uint8_t*>& src) {
+// Caller incremented copying_ under mu_ when it reserved the rows.  Never
+// throws: a copy that fails still completes the slot's bookkeeping (the lane
+// is not left waiting for rows that will not come) and marks the request
+// that owns rows r0.. failed, so it is answered INTERNAL instead of with the
+// batch's output.
+void Endpoint::copy_rows(int slot, int r0, int n, const std::vector<const uint8_t*>& src) noexcept {
   Slot& s = slots_[slot];
-  for (size_t i = 0; i < inputs.size(); ++i)
-    ingest_rows(s.in_base[i] + size_t(r0) * inputs[i].slot_bytes(), src[i], size_t(n) * inputs[i].row_bytes,
-                inputs[i].conv);
+  bool ok = true;
+  try {
+    for (size_t i = 0; i < inputs.size(); ++i)
+      ingest_rows(s.in_base[i] + size_t(r0) * inputs[i].slot_bytes(), src[i], size_t(n) * inputs[i].row_bytes,
+                  inputs[i].conv);
+  } catch (...) {
+    ok = false;
+  }
   std::lock_guard<std::mutex> g(mu_);
+  if (!ok) {
+    st_.copy_errors++;
+    for (auto& p : s.reqs)
+      if (p.row0 == r0) p.failed = true;
+  }
   s.copied += n;
-  s.ready.emplace_back(r0, n);
+  try {
+    s.ready.emplace_back(r0, n);
+  } catch (...) {
+    // (only streamed rows consult `ready`; the batch still completes on `copied`)
+  }
   s.cv->notify_all();
   if (--copying_ == 0 && closed_) cv_free_.notify_all();
 }
@@ -261,14 +308,13 @@ void Endpoint::drain_queue() {
     return;
   }
   // contiguous shares: the caller takes the first, the pool the rest; the
-  // caller waits for all of them (the jobs' sources live in `jobs`)
-  // (the latch is shared-owned: a pool thread may still be leaving its
-  // notify when the caller, woken, returns)
-  struct Latch {
-    std::mutex m;
-    std::condition_variable cv;
-    int left = 0;
-  };
+  // caller waits for all of them (the jobs' sources live in `jobs`).
+  // copy_rows never throws, and a job's latch count-down runs from a guard,
+  // so the wait below always ends.
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.pooled_drains++;
+  }
   const auto latch = std::make_shared<Latch>();
   const Job* js = jobs.data();
   const int parts = kDrainThreads + 1;
@@ -279,11 +325,19 @@ void Endpoint::drain_queue() {
       std::lock_guard<std::mutex> g(latch->m);
       ++latch->left;
     }
-    drain_pool().post([this, js, b, e, latch] {
+    try {
+      drain_pool().post([this, js, b, e, latch] {
+        struct Done {
+          Latch& l;
+          ~Done() { l.done(); }
+        } done{*latch};
+        for (int i = b; i < e; ++i) copy_rows(js[i].slot, js[i].r0, js[i].n, js[i].src);
+      });
+    } catch (...) {
+      // could not queue the share: copy it here
       for (int i = b; i < e; ++i) copy_rows(js[i].slot, js[i].r0, js[i].n, js[i].src);
-      std::lock_guard<std::mutex> g(latch->m);
-      if (--latch->left == 0) latch->cv.notify_all();
-    });
+      latch->done();
+    }
   }
   for (int i = 0; i < std::min(per, int(jobs.size())); ++i) copy_rows(js[i].slot, js[i].r0, js[i].n, js[i].src);
   std::unique_lock<std::mutex> g(latch->m);
@@ -441,6 +495,10 @@ void Endpoint::complete(int slot, Server& srv) {
   }
   for (auto& p : s.reqs) {
     if (!p.call) continue;   // abandoned streaming row
+    if (p.failed) {
+      srv.respond(*p.call, 13 /*INTERNAL*/, "request rows could not be copied into the batch", std::string());
+      continue;
+    }
     if (p.call->expired(now)) {
       srv.stats.expired++;
       srv.respond(*p.call, 4 /*DEADLINE_EXCEEDED*/, "Deadline Exceeded", std::string());

@@ -58,6 +58,7 @@ struct Pending {
   int row0 = 0, n = 0;
   std::vector<int> outs;   // output indices to encode (empty = all)
   std::shared_ptr<SlotStream> sres;
+  bool failed = false;     // its rows could not be copied in: answered INTERNAL
 };
 
 // A validated request waiting for a batch slot (every slot busy on the GPU).
@@ -97,6 +98,9 @@ struct EndpointStats {
   // failed batches in total and since the last completed one (the replica
   // health monitor reloads a servable whose device keeps failing)
   uint64_t failed = 0, consecutive_failed = 0;
+  // drains of the FIFO queue spread over the drain pool (>= kDrainMinJobs
+  // requests moved into slots at once), and row copies that threw
+  uint64_t pooled_drains = 0, copy_errors = 0;
 };
 
 class Endpoint {
@@ -175,7 +179,7 @@ class Endpoint {
     const uint8_t* src;
     size_t bytes;
   };
-  void copy_rows(int slot, int r0, int n, const std::vector<const uint8_t*>& src);
+  void copy_rows(int slot, int r0, int n, const std::vector<const uint8_t*>& src) noexcept;
   // batcher-side abandonment of rows whose payload stalls (caller holds mu_)
   void abandon_stalled_locked(Slot& s);
   Server* srv_ = nullptr;

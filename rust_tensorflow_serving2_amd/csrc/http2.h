@@ -229,6 +229,9 @@ struct LoadGenResult {
   std::string first_error;
   uint64_t bytes_sent = 0, bytes_recv = 0;
   double cpu_s = 0;                 // CPU time of the client threads
+  // window(): seconds from the window's start to each of its completions
+  // (every completion, in no particular order)
+  std::vector<double> done_s;
 };
 
 // Persistent load generator: `threads` client threads each own a share of

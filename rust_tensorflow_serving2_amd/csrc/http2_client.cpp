@@ -52,11 +52,12 @@ struct Shared {
   std::condition_variable wcv;
 };
 
-// One completion in continuous mode: (sequence number, latency, ok)
+// One completion in continuous mode: (sequence number, latency, ok, when)
 struct Done {
   uint64_t seq;
   double us;
   bool ok;
+  Clock::time_point at;
 };
 
 struct Req {
@@ -168,7 +169,8 @@ int on_close(nghttp2_session* s, int32_t sid, uint32_t err, void* ud) {
   ClientConn* c = static_cast<ClientConn*>(ud);
   Req* r = static_cast<Req*>(nghttp2_session_get_stream_user_data(s, sid));
   if (!r) return 0;
-  const double us = std::chrono::duration<double, std::micro>(Clock::now() - r->t0).count();
+  const auto now = Clock::now();
+  const double us = std::chrono::duration<double, std::micro>(now - r->t0).count();
   *c->bytes_recv += r->bytes;
   const bool good = err == 0 && r->http_status == 200 && r->grpc_status == 0;
   if (c->sh->continuous.load(std::memory_order_relaxed)) {
@@ -176,7 +178,7 @@ int on_close(nghttp2_session* s, int32_t sid, uint32_t err, void* ud) {
     {
       std::lock_guard<std::mutex> g(*c->done_mu);
       seq = c->sh->finished.fetch_add(1);
-      c->done->push_back(Done{seq, us, good});
+      c->done->push_back(Done{seq, us, good, now});
     }
     if (seq + 1 == c->sh->target.load(std::memory_order_acquire)) {
       std::lock_guard<std::mutex> g(c->sh->wmu);
@@ -569,6 +571,7 @@ LoadGenResult LoadGen::window(uint64_t n, double timeout_s) {
     std::lock_guard<std::mutex> g(w->done_mu);
     for (auto& d : w->done) {
       if (d.seq < s0 || d.seq >= s0 + n) continue;
+      res.done_s.push_back(std::chrono::duration<double>(d.at - t0).count());
       if (d.ok) {
         res.ok++;
         res.latency_us.push_back(d.us);

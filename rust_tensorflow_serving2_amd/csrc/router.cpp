@@ -304,7 +304,12 @@ void Router::publish(int p, const std::shared_ptr<RouterSeg>& seg, int cell, std
   ch->resp_len = 0;
   {
     std::lock_guard<std::mutex> g(mu_);
-    const uint64_t tok = next_token_++;
+    // tokens are unique across origins and incarnations (rank, generation,
+    // sequence): an origin only ever collects a DONE cell that carries its own
+    // token, so a cell freed and reused under a stale pending entry cannot
+    // hand that entry another origin's answer
+    const uint64_t tok = (uint64_t(rank_) << 56) | (uint64_t(self_->hdr()->gen & 0xffffff) << 32) |
+                         (next_token_++ & 0xffffffffULL);
     ch->token = tok;
     auto pend = std::make_unique<Pending>();
     pend->peer = p;
@@ -393,8 +398,26 @@ void Router::respond_remote(const Call& c, int status, const std::string& msg, c
     std::lock_guard<std::mutex> g(mu_);
     if (origin < peers_.size() && peers_[origin]->gen == ch->origin_gen) oseg = peers_[origin]->seg;
   }
-  if (oseg) ring(*oseg);
-  else ch->state.store(kFree, std::memory_order_release);   // the origin is gone: nobody will collect it
+  if (oseg) {
+    ring(*oseg);
+    return;
+  }
+  // this replica's view of the origin is stale (not re-scanned yet) or the
+  // origin is gone.  Freeing the cell here (round 5) leaked the origin's call
+  // whenever the view was merely stale: the origin waited forever, and once
+  // another replica reused the cell, the stale entry took that replica's
+  // answer (found by the 8-rank CPU rehearsal).  The cell stays DONE: a live
+  // origin collects it on its next reap (its doorbell rings on other traffic
+  // and every 20 ms wait times out); a dead origin's ring is reclaimed with
+  // its generation.
+  stats.unseen_origin++;
+  std::shared_ptr<RouterSeg> any;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    rescan();
+    if (origin < peers_.size() && peers_[origin]->gen == ch->origin_gen) any = peers_[origin]->seg;
+  }
+  if (any) ring(*any);
 }
 
 void Router::ingest() {
@@ -438,6 +461,19 @@ void Router::reap(bool check_peers) {
       RouterSeg& s = *pd.seg;
       CellHdr* ch = s.cell(pd.cell);
       const uint32_t st = ch->state.load(std::memory_order_acquire);
+      if (ch->token != it->first && st != kWriting) {
+        // the cell was freed and reused under this call (it cannot be ours
+        // any more): answer it rather than wait forever or take another
+        // origin's answer
+        Ans a;
+        a.call = std::move(pd.call);
+        a.status = 14;   // UNAVAILABLE
+        a.msg = "replica " + std::to_string(pd.peer) + " lost the forwarded request";
+        answers.push_back(std::move(a));
+        stats.orphaned++;
+        it = pending_.erase(it);
+        continue;
+      }
       if (st == kDone) {
         if (ch->status == kRerunLocally) {
           std::unique_ptr<Call> c = std::move(pd.call);
@@ -553,6 +589,25 @@ void Router::rescan() {
   }
 }
 
+// (mu_ held) answers in our ring that no origin will collect: the origin's
+// process is gone or was replaced by a new generation.  Only those are freed
+// (a live origin collects its own cells, however stale our view of it was).
+void Router::collect_orphans() {
+  RouterSeg& s = *self_;
+  const int n = int(s.hdr()->ncells);
+  for (int i = 0; i < n; ++i) {
+    CellHdr* ch = s.cell(i);
+    if (ch->state.load(std::memory_order_acquire) != kDone) continue;
+    const uint32_t o = ch->origin;
+    if (o >= uint32_t(world_) || o >= uint32_t(kMaxRanks)) continue;
+    const bool replaced = dir_->d->gen[o].load(std::memory_order_acquire) != ch->origin_gen;
+    if (replaced || !pid_alive(dir_->d->pid[o].load(std::memory_order_acquire))) {
+      uint32_t expect = kDone;
+      ch->state.compare_exchange_strong(expect, kFree, std::memory_order_acq_rel);
+    }
+  }
+}
+
 void Router::run() {
   pthread_setname_np(pthread_self(), "tfs-router");
   SegHdr* h = self_->hdr();
@@ -566,6 +621,7 @@ void Router::run() {
       std::lock_guard<std::mutex> g(mu_);
       rescan();
       last_scan = now;
+      collect_orphans();
     }
     reap(scan);
     h->heartbeat.fetch_add(1, std::memory_order_relaxed);

@@ -62,6 +62,13 @@ struct RouterStats {
   std::atomic<uint64_t> rerun{0};       // forwarded calls re-run here: the answer did not fit the cell
   std::atomic<uint64_t> too_large{0};   // peers' calls whose answer did not fit their cell (sent back)
   std::atomic<uint64_t> tomb_freed{0};  // cells of given-up calls freed when the peer finished late
+  // answers written into a cell whose origin this replica could not see (its
+  // view of the origin's generation stale): the cell is left DONE for the
+  // origin to collect, never freed here
+  std::atomic<uint64_t> unseen_origin{0};
+  // forwarded calls whose cell no longer carries their token (it was freed
+  // and reused under them): answered UNAVAILABLE instead of waiting forever
+  std::atomic<uint64_t> orphaned{0};
 };
 
 class Router : public RemoteSink {
@@ -103,6 +110,7 @@ class Router : public RemoteSink {
   void ingest();
   void reap(bool check_peers);
   void rescan();
+  void collect_orphans();
   void ring(RouterSeg& seg);
 
   Server* srv_;

@@ -650,7 +650,8 @@ void register_server(py::module_& m) {
         d["forwarded"] = st.forwarded.load(); d["streamed"] = st.streamed.load();
         d["ingested"] = st.ingested.load(); d["returned"] = st.returned.load();
         d["reclaimed"] = st.reclaimed.load(); d["lost"] = st.lost.load(); d["no_cell"] = st.no_cell.load();
-        d["rerun"] = st.rerun.load(); d["too_large"] = st.too_large.load(); d["tomb_freed"] = st.tomb_freed.load();
+        d["rerun"] = st.rerun.load(); d["too_large"] = st.too_large.load(); d["tomb_freed"] = st.tomb_freed.load(); d["unseen_origin"] = st.unseen_origin.load();
+        d["orphaned"] = st.orphaned.load();
         d["local_cap"] = s.router->local_cap();
         d["peers_alive"] = s.router->peers_alive();
         d["loads"] = s.router->loads();
@@ -699,6 +700,7 @@ void register_server(py::module_& m) {
         auto st = ep->stats();
         d["requests"] = st.requests; d["batches"] = st.batches; d["rows"] = st.rows; d["rejected"] = st.rejected;
         d["failed"] = st.failed; d["consecutive_failed"] = st.consecutive_failed;
+        d["pooled_drains"] = st.pooled_drains; d["copy_errors"] = st.copy_errors;
         return d;
       });
 
@@ -738,6 +740,7 @@ void register_server(py::module_& m) {
         py::dict d;
         d["ok"] = r.ok; d["errors"] = r.errors; d["elapsed_s"] = r.elapsed_s;
         d["latency_us"] = r.latency_us; d["first_error"] = r.first_error;
+        d["done_s"] = r.done_s;
         return d;
       }, py::arg("n"), py::arg("timeout_s") = 120.0)
       .def("stop", [](LoadGen& lg, double timeout_s) {

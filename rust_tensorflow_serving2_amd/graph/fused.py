@@ -817,7 +817,12 @@ class ChainConv:
         # where 64-row workgroups leave CUs idle -- timed per shape (bucket):
         # option 1 = the chain kernel, 0 = the two convs with their own tiles
         key = ("chain", tuple(x.shape), a.cout, b.cout, res is not None, a.act, b.act)
-        pick = tuned_choice(key, {1: chained, 0: split}, default=1)
+        # without a tuned pick (TFSERVE_AUTOTUNE=0, no committed table, or a
+        # key the table lacks) only the stage-1 shapes chain: the stage-2
+        # (N1 = 512) chains measured no faster than two convs at b32
+        # (round-5 ADVICE)
+        dflt = 1 if (a.cin, a.cout, b.cout) in CHAIN_SHAPES_STAGE1 else 0
+        pick = tuned_choice(key, {1: chained, 0: split}, default=dflt)
         return chained() if pick == 1 else split()
 
 

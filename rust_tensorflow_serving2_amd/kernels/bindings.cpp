@@ -871,10 +871,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_counters_release", [](int64_t owner) { return tfsk::splitk_counters_release(owner); },
         "return an owner's captured split-K counter slices to the pool");
   m.def("splitk_counters_captured_in_use", []() { return tfsk::splitk_counters_captured_in_use(); });
-  m.def("splitk_counters_reclaim", [](double min_age_s) { return tfsk::splitk_counters_reclaim(min_age_s); },
-        py::arg("min_age_s") = 2.0,
-        "zero released captured slices older than min_age_s and return them to the free list (call outside "
-        "any capture on this thread); returns the ints reclaimed");
+  m.def("splitk_counters_reclaim", []() { return tfsk::splitk_counters_reclaim(); },
+        "advance released captured slices (fence on their replay streams -> zero on the lane's stream -> free); "
+        "never blocks; call outside any capture on this thread; returns the ints made reusable");
+  m.def("splitk_counters_add_stream", [](int64_t owner, int64_t stream) {
+          tfsk::splitk_counters_add_stream(owner, reinterpret_cast<hipStream_t>(stream));
+        }, py::arg("owner"), py::arg("stream"),
+        "another stream the owner's graph replays on (its fence must complete before the slices are reused)");
   m.def("splitk_counters_pending", []() { return tfsk::splitk_counters_pending(); });
   m.def("set_wg_trace", [](const c10::optional<Tensor>& t) {
     if (!t.has_value()) {

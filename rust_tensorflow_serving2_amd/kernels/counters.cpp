@@ -2,7 +2,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
 #include <cstdio>
 #include <map>
 #include <mutex>
@@ -21,36 +20,48 @@ constexpr int kPoolInts = 1 << 22;   // 16 MB per device
 // each graph capture) returns its slices to a free list when the runtime
 // releases the token as the graph is destroyed -- tuning candidates and
 // reload cycles no longer use the range up; slices taken without an owner
-// stay taken.  A release only quarantines the slices (pending, stamped):
-// splitk_counters_reclaim zeroes the old-enough ones and frees them then, so
-// neither a replay still queued behind the dropped graph nor a counter left
-// non-zero by an abandoned lane can hand a later capture a live counter.
+// stay taken.  A release is stream-ordered (launch.h): the slices wait for a
+// fence event on every stream the graph replays on, are then zeroed on the
+// lane's own stream, and are reused only after that memset has completed --
+// a replay still queued behind the dropped graph, or a hung lane's counter,
+// can never be handed to a later capture (round-5 ADVICE / VERDICT item 4:
+// the time-based quarantine this replaces could).
 // [kCapInts, kPoolInts): a ring for eager launches (autotuning,
 // warm-up), reused cyclically.  A maximal take (32K ints) wraps the 256K-int
 // ring after 8 launches; reuse is still safe because eager launches are
 // stream-ordered and counters return to zero when a tile's last slice
-// arrives, before the next launch on the stream starts (which is also why a
-// released slice is zero again: every replay of its graph completed).
+// arrives, before the next launch on the stream starts.
 constexpr int kCapInts = 15 << 18;
 struct Range {
   int off, len;
 };
-using Clock = std::chrono::steady_clock;
+// released slices of one owner: state 0 = released (no fence yet), 1 = fences
+// recorded, 2 = zeroing memset issued (event `zeroed`)
 struct Pending {
-  Range r;
-  Clock::time_point at;
+  std::vector<Range> ranges;
+  std::vector<hipStream_t> streams;
+  std::vector<hipEvent_t> fences;
+  hipEvent_t zeroed = nullptr;
+  int state = 0;
+  bool failed = false;            // a fence or memset reported an error: never reused
 };
 struct Pool {
   int* base = nullptr;
   int used = 0;
   int ring = kCapInts;
-  std::vector<Range> free_list;                     // zeroed released slices, reusable
-  std::vector<Pending> pending;                     // released, not yet zeroed (quarantine)
-  std::map<int64_t, std::vector<Range>> owned;      // owner token -> its captured slices
+  std::vector<Range> free_list;                         // zeroed released slices, reusable
+  std::vector<Pending> pending;                         // released, not yet reusable
+  std::map<int64_t, std::vector<Range>> owned;          // owner token -> its captured slices
+  std::map<int64_t, std::vector<hipStream_t>> streams;  // owner token -> streams its graph replays on
 };
 std::mutex g_mu;
 std::map<int, Pool> g_pools;
 thread_local int64_t g_owner = 0;
+
+void add_stream(Pool& p, int64_t owner, hipStream_t s) {
+  auto& v = p.streams[owner];
+  if (std::find(v.begin(), v.end(), s) == v.end()) v.push_back(s);
+}
 
 // first fit from the free list (splitting the range), else -1
 int take_free(Pool& p, int take) {
@@ -119,27 +130,41 @@ int* splitk_counters(int n, hipStream_t s) {
     off = p.used;
     p.used += take;
   }
-  if (g_owner != 0) p.owned[g_owner].push_back(Range{off, take});
+  if (g_owner != 0) {
+    p.owned[g_owner].push_back(Range{off, take});
+    add_stream(p, g_owner, s);              // the capturing stream replays the graph
+  }
   return p.base + off;
 }
 
 void splitk_counters_set_owner(int64_t owner) { g_owner = owner; }
 
+void splitk_counters_add_stream(int64_t owner, hipStream_t s) {
+  int dev = 0;
+  if (owner == 0 || hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> g(g_mu);
+  add_stream(g_pools[dev], owner, s);
+}
+
 int64_t splitk_counters_release(int64_t owner) {
   // no HIP call here: this runs from a Python finalizer on whatever thread
-  // dropped the graph (possibly one that is capturing)
+  // dropped the graph (possibly one that is capturing); the fences are
+  // recorded by the next splitk_counters_reclaim
   std::lock_guard<std::mutex> g(g_mu);
   int64_t n = 0;
-  const auto now = Clock::now();
   for (auto& kv : g_pools) {
     Pool& p = kv.second;
     auto it = p.owned.find(owner);
-    if (it == p.owned.end()) continue;
-    for (const Range& r : it->second) {
-      p.pending.push_back(Pending{r, now});
-      n += r.len;
+    auto st = p.streams.find(owner);
+    if (it != p.owned.end()) {
+      Pending q;
+      q.ranges = it->second;
+      if (st != p.streams.end()) q.streams = st->second;
+      for (const Range& r : q.ranges) n += r.len;
+      p.pending.push_back(std::move(q));
+      p.owned.erase(it);
     }
-    p.owned.erase(it);
+    if (st != p.streams.end()) p.streams.erase(st);
   }
   return n;
 }
@@ -148,41 +173,111 @@ int64_t splitk_counters_pending() {
   std::lock_guard<std::mutex> g(g_mu);
   int64_t n = 0;
   for (auto& kv : g_pools)
-    for (const Pending& q : kv.second.pending) n += q.r.len;
+    for (const Pending& q : kv.second.pending)
+      for (const Range& r : q.ranges) n += r.len;
   return n;
 }
 
-int64_t splitk_counters_reclaim(double min_age_s) {
+namespace {
+// every event complete (hipSuccess); an error other than not-ready marks the
+// entry failed (its slices are never reused)
+bool events_done(Pending& q, const std::vector<hipEvent_t>& evs) {
+  for (hipEvent_t e : evs) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipErrorNotReady) return false;
+    if (r != hipSuccess) {
+      (void)hipGetLastError();
+      q.failed = true;
+      return false;
+    }
+  }
+  return true;
+}
+
+hipEvent_t record(hipStream_t s) {
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  if (hipEventRecord(e, s) != hipSuccess) {
+    hipEventDestroy(e);
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return e;
+}
+
+// advance one released entry as far as it can go without blocking; true once
+// its slices are zero and no replay of its graph is outstanding
+bool advance(Pool& p, Pending& q) {
+  if (q.failed) return false;
+  if (q.state == 0) {
+    // a stream another thread is capturing on would swallow the fence into
+    // that capture: wait for the next reclaim
+    for (hipStream_t s : q.streams)
+      if (capturing(s)) return false;
+    for (hipStream_t s : q.streams) {
+      hipEvent_t e = record(s);
+      if (e == nullptr) return false;        // retried next time (fences recorded so far are kept)
+      q.fences.push_back(e);
+    }
+    q.state = 1;
+  }
+  if (q.state == 1) {
+    if (!events_done(q, q.fences)) return false;
+    // every replay queued before the release has completed: zero the slices
+    // on the lane's own stream (or the null stream when the owner recorded
+    // none), behind whatever that stream runs now
+    hipStream_t zs = q.streams.empty() ? nullptr : q.streams[0];
+    if (zs != nullptr && capturing(zs)) return false;
+    for (const Range& r : q.ranges)
+      if (hipMemsetAsync(p.base + r.off, 0, size_t(r.len) * sizeof(int), zs) != hipSuccess) {
+        (void)hipGetLastError();
+        q.failed = true;
+        return false;
+      }
+    q.zeroed = record(zs);
+    if (q.zeroed == nullptr) {
+      q.failed = true;
+      return false;
+    }
+    q.state = 2;
+  }
+  std::vector<hipEvent_t> z{q.zeroed};
+  return events_done(q, z);
+}
+
+void destroy_events(Pending& q) {
+  for (hipEvent_t e : q.fences) hipEventDestroy(e);
+  if (q.zeroed != nullptr) hipEventDestroy(q.zeroed);
+  q.fences.clear();
+  q.zeroed = nullptr;
+}
+}  // namespace
+
+int64_t splitk_counters_reclaim() {
   std::lock_guard<std::mutex> g(g_mu);
   int64_t n = 0;
   int cur = 0;
   if (hipGetDevice(&cur) != hipSuccess) return 0;
-  const auto now = Clock::now();
   for (auto& kv : g_pools) {
     Pool& p = kv.second;
     if (p.pending.empty() || p.base == nullptr) continue;
-    std::vector<Range> ready;
-    std::vector<Pending> keep;
-    for (const Pending& q : p.pending) {
-      if (std::chrono::duration<double>(now - q.at).count() >= min_age_s) ready.push_back(q.r);
-      else keep.push_back(q);
-    }
-    if (ready.empty()) continue;
-    // zero them on a private non-blocking stream of that device and wait for
-    // that memset only (no device-wide synchronize: the lanes keep replaying)
     if (hipSetDevice(kv.first) != hipSuccess) continue;
-    hipStream_t zs = nullptr;
-    bool ok = hipStreamCreateWithFlags(&zs, hipStreamNonBlocking) == hipSuccess;
-    for (const Range& r : ready)
-      ok = ok && hipMemsetAsync(p.base + r.off, 0, size_t(r.len) * sizeof(int), zs) == hipSuccess;
-    ok = ok && hipStreamSynchronize(zs) == hipSuccess;
-    if (zs != nullptr) hipStreamDestroy(zs);
-    if (!ok) continue;                               // stay quarantined; retried next time
-    p.pending.swap(keep);
-    for (const Range& r : ready) {
-      p.free_list.push_back(r);
-      n += r.len;
+    std::vector<Pending> keep;
+    bool freed = false;
+    for (Pending& q : p.pending) {
+      if (!advance(p, q)) {
+        keep.push_back(std::move(q));
+        continue;
+      }
+      destroy_events(q);
+      for (const Range& r : q.ranges) {
+        p.free_list.push_back(r);
+        n += r.len;
+      }
+      freed = true;
     }
+    p.pending.swap(keep);
+    if (!freed) continue;
     // coalesce adjacent ranges (keeps first-fit effective over many cycles)
     std::sort(p.free_list.begin(), p.free_list.end(), [](const Range& a, const Range& b) { return a.off < b.off; });
     std::vector<Range> merged;
@@ -207,7 +302,8 @@ int64_t splitk_counters_captured_in_use() {
   for (auto& kv : g_pools) {
     n += kv.second.used;
     for (const Range& r : kv.second.free_list) n -= r.len;
-    for (const Pending& q : kv.second.pending) n -= q.r.len;
+    for (const Pending& q : kv.second.pending)
+      for (const Range& r : q.ranges) n -= r.len;
   }
   return n;
 }

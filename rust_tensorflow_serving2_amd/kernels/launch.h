@@ -98,15 +98,21 @@ void splitk_counters_prepare(hipStream_t s);
 // Captured slices taken on this thread while `owner` != 0 belong to that
 // owner; splitk_counters_release(owner) returns them to the pool (call it when
 // the graph captured under the token is destroyed).  Returns the ints freed.
-// Released slices are quarantined, not reused at once: a replay of the
-// dropped graph may still be queued, or a lane abandoned mid-count may have
-// left a counter non-zero.  splitk_counters_reclaim(min_age_s), called outside
-// any capture (the runtime calls it before each capture), zeroes the slices
-// released at least min_age_s ago on a private stream, waits for that memset
-// alone, and only then returns them to the free list.
+// Released slices are not reused at once: a replay of the dropped graph may
+// still be queued on a lane, or a lane abandoned mid-count may have left a
+// counter non-zero.  Reclamation is stream-ordered, not timed: the streams the
+// owner's graph replays on (the capturing stream, recorded automatically, plus
+// any added with splitk_counters_add_stream) each get a fence event at the
+// first splitk_counters_reclaim() after the release; once every fence has
+// completed the slices are zeroed on the first of those streams (the lane's
+// own), and once that memset has completed they join the free list.  A fence
+// behind a hung kernel never completes, so a hung lane's slices are never
+// handed out again.  splitk_counters_reclaim never blocks (call it outside any
+// capture on this thread; the runtime calls it before each capture).
 void splitk_counters_set_owner(int64_t owner);
+void splitk_counters_add_stream(int64_t owner, hipStream_t s);
 int64_t splitk_counters_release(int64_t owner);
-int64_t splitk_counters_reclaim(double min_age_s);
+int64_t splitk_counters_reclaim();
 int64_t splitk_counters_pending();
 int64_t splitk_counters_captured_in_use();
 

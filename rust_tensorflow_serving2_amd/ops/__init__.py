@@ -13,7 +13,7 @@ import itertools
 import os
 import threading
 import weakref
-from typing import Callable, Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -595,7 +595,6 @@ def current_head_host_rows():
 
 
 _OWNER_SEQ = itertools.count(1)
-_RECLAIM_AGE_S = float(os.environ.get("TFSERVE_COUNTER_QUARANTINE_S", "2.0"))
 _GC_HOLD = [0]
 _GC_LOCK = threading.Lock()
 
@@ -624,24 +623,30 @@ def _no_gc():
 
 
 @contextlib.contextmanager
-def capture_owner(graph):
+def capture_owner(graph, replay_streams: Sequence = ()):
     """Around a HIP-graph capture: the split-K arrival counters its launches
     take (the split-K fixup) belong to ``graph`` and go back to the pool
     when the graph object is collected, so tuning candidates and reload
-    cycles do not use the counter pool up (kernels/counters.cpp).  Python's
-    GC is held off for the capture (``_no_gc``)."""
+    cycles do not use the counter pool up (kernels/counters.cpp).  The
+    return is stream-ordered: the capturing stream (recorded by the pool)
+    and ``replay_streams`` (other streams the graph will replay on) each get
+    a fence; the slices are zeroed on the lane's stream and reused only after
+    every fence and that memset have completed.  Python's GC is held off for
+    the capture (``_no_gc``)."""
     with _no_gc():
         try:
             h = hip()
         except KernelsUnavailable:
             yield None
             return
-        # slices released by dropped graphs come back zeroed, after their
-        # quarantine, before this capture can take them (kernels/counters.cpp)
+        # released slices whose fences have completed come back zeroed before
+        # this capture can take them; the rest stay pending (never blocks)
         if hasattr(h, "splitk_counters_reclaim"):
-            h.splitk_counters_reclaim(_RECLAIM_AGE_S)
+            h.splitk_counters_reclaim()
         tok = next(_OWNER_SEQ)
         h.splitk_counters_set_owner(tok)
+        for st in replay_streams:
+            h.splitk_counters_add_stream(tok, int(st.cuda_stream))
         try:
             yield tok
         finally:

@@ -117,21 +117,45 @@ _META_DT = {T.DT_FLOAT: torch.float32, T.DT_HALF: torch.float16, T.DT_BFLOAT16: 
             T.DT_DOUBLE: torch.float64}
 
 
-def pg_backend(pg) -> Optional[str]:
+def pg_backend(pg, device_type: Optional[str] = None) -> Optional[str]:
     """The backend a process group actually runs ("nccl" = RCCL on ROCm,
     "gloo"), read from the group object itself -- never inferred from the
     device the tensors live on (a gloo rehearsal on GPUs must not report
-    itself as RCCL)."""
+    itself as RCCL).  A multi-backend group ("cpu:gloo,cuda:nccl", e.g. one
+    set up before cli.py, which then skips its own init) runs the backend
+    listed for ``device_type`` (parse_backend)."""
     if pg is None:
         return None
+    name = None
     try:
-        return str(dist.get_backend(pg)).lower()
+        name = str(dist.get_backend(pg))
     except Exception:
-        pass
-    try:
-        return str(pg.name()).lower()
-    except Exception:
+        try:
+            name = str(pg.name())
+        except Exception:
+            return None
+    return parse_backend(name, device_type)
+
+
+def parse_backend(name: Optional[str], device_type: Optional[str] = None) -> Optional[str]:
+    """"nccl" / "gloo" from a backend string: a plain name as is; a
+    "device:backend,..." list -> the entry for ``device_type`` ("cuda" ->
+    its entry, else "cpu"), or the only entry when there is one."""
+    if name is None:
         return None
+    name = name.strip().lower()
+    if ":" not in name:
+        return name
+    pairs = {}
+    for part in name.split(","):
+        dev, _, be = part.partition(":")
+        if be:
+            pairs[dev.strip()] = be.strip()
+    if device_type in pairs:
+        return pairs[device_type]
+    if len(set(pairs.values())) == 1:
+        return next(iter(pairs.values()))
+    return pairs.get("cpu") if device_type is None else None
 
 
 def pg_size(pg) -> Optional[int]:
@@ -308,7 +332,8 @@ class ReplicatedWeightSource:
         pg0 = None
         if dist.is_initialized():
             pg0 = group if group is not None else dist.distributed_c10d._get_default_group()
-        self.backend = (backend or pg_backend(pg0) or os.environ.get("TFSERVE_WEIGHT_BACKEND")
+        self.backend = (parse_backend(backend, device.type) or pg_backend(pg0, device.type)
+                        or os.environ.get("TFSERVE_WEIGHT_BACKEND")
                         or ("nccl" if device.type == "cuda" else "gloo"))
         if self.backend not in ("nccl", "gloo"):
             raise ValueError(f"weight replication needs an nccl (RCCL) or gloo group, not {self.backend!r}")

@@ -72,6 +72,45 @@ def test_bench_gpus2_self_launch_cpu(tmp_path):
     assert all(x["bracket_s"] >= x["elapsed_s"] for x in pr)
 
 
+@pytest.mark.timeout(900)
+def test_bench_gpus8_self_launch_cpu(tmp_path):
+    """The driver's N = 8 scaling run, rehearsed on the CPU (gloo, tiny
+    model): 8 ranks launched by bench.py itself, every follower bound the
+    broadcast weights, the all-reduce over the group sums to 8, and the
+    reference-client phase (one client on rank 0's port, 1024 calls in flight)
+    spills past rank 0 once its pipeline is full.  This rehearsal found a
+    router leak at 8 ranks: a forwarded call whose cell was freed under it hung
+    its client for the phase's 300-s timeout (ref_client_rps 1.7); see
+    csrc/router.cpp respond_remote / reap."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["TMPDIR"] = str(tmp_path)
+    cmd = [sys.executable, BENCH, "--gpus", "8", "--device", "cpu", "--model", "tiny", "--image-size", "32",
+           "--steps", "4", "--warmup", "1", "--prewarm-s", "0.2", "--ref-client-requests", "512",
+           "--c1-requests", "10", "--io-threads", "1", "--client-threads", "1", "--connections", "2",
+           "--lanes", "2"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=880, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = _json_line(p.stdout)
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8"
+    assert out["errors"] == 0 and out["value"] > 0 and out["value_bracket"] > 0
+    pr = out["per_rank"]
+    assert [x["rank"] for x in pr] == list(range(8))
+    assert all(x["ok"] > 0 and 0 < x["interval_s"] <= x["elapsed_s"] for x in pr), pr
+    assert out["rehearsal"] is True and out["replication_ok"] is True and "rccl_problems" not in out
+    assert [x["allreduce_sum"] for x in out["rccl"]] == [8.0] * 8
+    assert sum(1 for x in out["rccl"] if x["leader"]) == 1
+    assert all(x["disk_loads"] == 0 and x["bcast_loads"] >= 1 for x in out["rccl"] if not x["leader"])
+    # the reference client: no errors, no hung call (the leak made this 1.7 RPC/s)
+    assert out["ref_client_errors"] == 0 and out["ref_client_rps"] > 100, out["ref_client_rps"]
+    share = out["ref_client_gpu_share"]
+    assert len(share) == 8 and abs(sum(share) - 1) < 0.01
+    assert sum(share[1:]) > 0.5, share            # spilled past rank 0
+    for d in out["diagnostics"]:
+        for phase in (d["timed"], d["ref_client"]):
+            r = phase.get("router") or {}
+            assert r.get("orphaned", 0) == 0 and r.get("lost", 0) == 0, r
+
+
 def test_rccl_problems_flags_silent_fallbacks():
     """bench.py exits non-zero (after printing its line) when a follower did
     not really receive the broadcast."""

@@ -236,3 +236,69 @@ def test_close_answers_every_unstarted_request():
     assert 1 <= codes.count("OK") <= 4 and codes.count("UNAVAILABLE") >= 10, codes
 
 
+
+
+def test_queue_drain_spreads_over_the_pool():
+    """Round-5 ADVICE: more requests in flight than the slots hold park in the
+    FIFO queue; the lane that frees a slot moves >= 4 of them in at once,
+    which runs on the drain pool (pooled_drains counts it).  Every request is
+    answered with its own rows, and the pool threads carry the process-wide
+    CPU mask, not the mask of whichever (pinned) lane thread drained first."""
+    import os
+    srv = _C.Http2Server("127.0.0.1", 0, 2)
+    ep = srv.add_endpoint("m", 1, "serving_default", [("x", T.DT_FLOAT, [64])], [("y", T.DT_FLOAT, [64])], 8, 5000000)
+    bufs = []
+    for k in range(2):
+        xin, yout = np.zeros((8, 64), np.float32), np.zeros((8, 64), np.float32)
+        srv.set_slot_buffers(ep, k, [xin.ctypes.data], [yout.ctypes.data])
+        bufs.append((xin, yout))
+    srv.set_route("m", "serving_default", -1, ep)
+    stop = threading.Event()
+    gate = threading.Event()
+
+    def lane(k):
+        cpu = sorted(os.sched_getaffinity(0))[0]
+        os.sched_setaffinity(0, {cpu})          # a pinned lane thread, as bench.py does
+        xin, yout = bufs[k]
+        while not stop.is_set():
+            n = srv.acquire(ep, k, 50)
+            if n < 0:
+                return
+            if n == 0:
+                continue
+            gate.wait(10)                       # hold the slot until the queue has built up
+            yout[:n] = xin[:n] * 3
+            srv.complete(ep, k)
+
+    ts = [threading.Thread(target=lane, args=(k,), daemon=True) for k in range(2)]
+    srv.start()
+    for t in ts:
+        t.start()
+    spec = native.spec_tuple("m", None, None, "serving_default")
+    xs = [np.full((1, 64), i, np.float32) for i in range(48)]
+    try:
+        with grpc.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+            stub = ch.unary_unary(PREDICT)
+            with cf.ThreadPoolExecutor(48) as ex:
+                futs = [ex.submit(stub, native.encode_predict_request(spec, {"x": x}), timeout=30) for x in xs]
+                time.sleep(0.5)                 # 16 rows in the two slots, the rest queued
+                gate.set()
+                ys = [_y(f.result()) for f in futs]
+        for x, y in zip(xs, ys):
+            np.testing.assert_array_equal(y, x * 3)
+        st = srv.endpoint_stats(ep)
+        assert st["pooled_drains"] >= 1, st
+        assert st["copy_errors"] == 0, st
+        main_mask = os.sched_getaffinity(os.getpid())
+        drains = [int(t) for t in os.listdir("/proc/self/task")
+                  if open(f"/proc/self/task/{t}/comm").read().strip() == "tfs-drain"]
+        assert len(drains) >= 3
+        for tid in drains:
+            assert os.sched_getaffinity(tid) == main_mask
+    finally:
+        stop.set()
+        gate.set()
+        srv.remove_endpoint(ep)
+        for t in ts:
+            t.join(timeout=5)
+        srv.stop()

@@ -727,16 +727,89 @@ def test_splitk_counter_slices_return_with_their_graph(monkeypatch):
         with torch.cuda.stream(stream), ops.capture_owner(g), torch.cuda.graph(g, stream=stream):
             hip().conv2d(x, wt, None, None, 3, 3, 1, 1, 1, 1, 1, 1, act=0, cfg=51, out=out, splits=4)
         assert hip().splitk_counters_captured_in_use() > base
-        g.replay()
+        with torch.cuda.stream(stream):
+            g.replay()
         torch.cuda.synchronize()
         del g
         gc.collect()
         assert hip().splitk_counters_captured_in_use() == base, cycle
-        # released slices are quarantined until reclaimed (zeroed, then freed)
+        # released slices stay pending until their fences and zeroing complete
         assert hip().splitk_counters_pending() > 0
-        assert hip().splitk_counters_reclaim(0.0) > 0
-        assert hip().splitk_counters_pending() == 0
+        _reclaim_all()
         assert hip().splitk_counters_captured_in_use() == base, cycle
+
+
+def _reclaim_all(timeout_s=5.0):
+    """reclaim() never blocks: call it until nothing is pending (idle streams)."""
+    import time
+    t0 = time.time()
+    while hip().splitk_counters_pending() > 0:
+        hip().splitk_counters_reclaim()
+        assert time.time() - t0 < timeout_s, "released counter slices never became reusable"
+        time.sleep(0.005)
+
+
+def test_splitk_counter_slices_wait_for_a_queued_replay(monkeypatch):
+    """a graph dropped with a replay still queued keeps its
+    split-K counter slices out of the pool until that replay has completed
+    (stream-ordered fence, no wall-clock quarantine): a capture made while it
+    is queued takes fresh counters, and the slices come back only after the
+    lane's stream has drained."""
+    import gc
+    import time
+    from rust_tensorflow_serving2_amd import ops
+    monkeypatch.setenv("TFSERVE_SPLITK_FIXUP", "1")
+    x = rnd(2, 14, 14, 256, seed=73).to(BF).to(DEV)
+    wt = pack_w(rnd(3, 3, 256, 256, scale=1 / 48, seed=74).to(BF).float())
+    out = torch.empty(2, 14, 14, 256, device=DEV, dtype=BF)
+    eager = hip().conv2d(x, wt, None, None, 3, 3, 1, 1, 1, 1, 1, 1, act=0, cfg=51, splits=4)
+    torch.cuda.synchronize()
+    gc.collect()
+    _reclaim_all()
+    base = hip().splitk_counters_captured_in_use()
+    lane, other = torch.cuda.Stream(), torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(lane), ops.capture_owner(g) as tok, torch.cuda.graph(g, stream=lane):
+        hip().conv2d(x, wt, None, None, 3, 3, 1, 1, 1, 1, 1, 1, act=0, cfg=51, out=out, splits=4)
+    took = hip().splitk_counters_captured_in_use() - base
+    assert took > 0
+    done = torch.cuda.Event()
+    with torch.cuda.stream(lane):
+        torch.cuda._sleep(600_000_000)     # ~0.25-0.3 s of GPU spin ahead of the replay
+        g.replay()
+        done.record()
+    # the owner's release while its replay is still queued (the graph object
+    # is kept: on ROCm 7 destroying a graph exec waits for its launches, so
+    # the release is issued directly, as the finalizer would)
+    assert hip().splitk_counters_release(tok) == took
+    assert hip().splitk_counters_captured_in_use() == base
+    assert hip().splitk_counters_pending() == took
+    t_end = time.time() + 0.05
+    while time.time() < t_end:
+        assert hip().splitk_counters_reclaim() == 0      # fence not reached: nothing freed
+    assert not done.query(), "the spin finished too early for this check"
+    assert hip().splitk_counters_pending() == took
+    # a capture made meanwhile gets fresh slices, not the queued replay's
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(other), ops.capture_owner(g2), torch.cuda.graph(g2, stream=other):
+        hip().conv2d(x, wt, None, None, 3, 3, 1, 1, 1, 1, 1, 1, act=0, cfg=51, out=out, splits=4)
+    assert hip().splitk_counters_pending() == took
+    assert hip().splitk_counters_captured_in_use() - base == took
+    lane.synchronize()                     # the queued replay completes (and its counters read zero)
+    assert torch.equal(out, eager)
+    _reclaim_all()
+    del g
+    gc.collect()                           # (its finalizer's release finds nothing left)
+    assert hip().splitk_counters_pending() == 0
+    with torch.cuda.stream(other):
+        out.zero_()
+        g2.replay()
+    other.synchronize()
+    assert torch.equal(out, eager)
+    del g2
+    gc.collect()
+    _reclaim_all()
+    assert hip().splitk_counters_captured_in_use() == base
 
 
 def test_splitk_fixup_override_is_thread_local_and_restored():

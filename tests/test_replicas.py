@@ -412,3 +412,16 @@ def test_reload_right_after_replica_kill_does_not_hang(tiny_resnet_path, tmp_pat
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, 9)
             proc.wait()
+
+
+def test_backend_strings_pick_the_device_backend():
+    """Round-5 ADVICE: a group set up before cli.py may report a multi-backend
+    string; the replica runs the backend listed for its device type."""
+    from rust_tensorflow_serving2_amd.parallel.weights import parse_backend
+    assert parse_backend("nccl", "cuda") == "nccl"
+    assert parse_backend("GLOO", "cpu") == "gloo"
+    assert parse_backend("cpu:gloo,cuda:nccl", "cuda") == "nccl"
+    assert parse_backend("cpu:gloo,cuda:nccl", "cpu") == "gloo"
+    assert parse_backend("cpu:gloo, cuda:gloo", "cuda") == "gloo"
+    assert parse_backend("cuda:nccl", "cpu") == "nccl"       # the only entry
+    assert parse_backend(None, "cuda") is None
