@@ -335,7 +335,7 @@ std::vector<Tensor> linear_lnx(const Tensor& x, const Tensor& w, const c10::opti
   const int N = w.size(0), ldb = w.size(1);
   TORCH_CHECK(ldb >= K && K % 64 == 0 && ldb % 8 == 0 && N % 8 == 0,
               "linear_lnx: K % 64 == 0 (fitting in w), N % 8 == 0");
-  TORCH_CHECK(is_cgemm_cfg(cfg) && !(cfg >= tfsk::kPGemmCfgBase && cfg < tfsk::kPGemmCfgBase + tfsk::kNumPGemmConfigs),
+  TORCH_CHECK(is_cgemm_cfg(cfg) && !(cfg >= tfsk::kBGemmCfgBase && cfg < tfsk::kBGemmCfgBase + tfsk::kNumBGemmConfigs),
               "linear_lnx: a cgemm tile config");
   TORCH_CHECK(!(stats && out_f32), "linear_lnx: row statistics of bf16 outputs only");
   auto sizes = x.sizes().vec();
@@ -911,8 +911,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (int c = 0; c < tfsk::kNumCGemmConfigs2; ++c) v.push_back(tfsk::kCGemmCfgBase2 + c);
     for (int c = 0; c < tfsk::kNumCGemmPfConfigs; ++c) v.push_back(tfsk::kCGemmPfCfgBase + c);
     for (int c = 0; c < tfsk::kNumCGemm32Configs; ++c) v.push_back(tfsk::kCGemm32CfgBase + c);
-    for (int c = 0; c < tfsk::kNumCGemmKt32Configs; ++c) v.push_back(tfsk::kCGemmKt32CfgBase + c);
-    for (int c = 0; c < tfsk::kNumPGemmConfigs; ++c) v.push_back(tfsk::kPGemmCfgBase + c);
+    for (int c = 0; c < tfsk::kNumBGemmConfigs; ++c) v.push_back(tfsk::kBGemmCfgBase + c);
     return v;
   });
   m.def("halo_configs", []() {

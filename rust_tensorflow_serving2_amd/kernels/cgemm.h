@@ -17,19 +17,18 @@ constexpr int kNumCGemmPfConfigs = 11;
 // a fourth range: v_mfma_f32_32x32x16_bf16 builds (wave tiles in 32x32 blocks)
 constexpr int kCGemm32CfgBase = 112;
 constexpr int kNumCGemm32Configs = 12;
-// a fifth range: 32-deep k-tiles (twice the ring slots in the same LDS)
-constexpr int kCGemmKt32CfgBase = 124;
-constexpr int kNumCGemmKt32Configs = 6;
-// a sixth range: the persistent multi-tile kernel (pgemm.hip; no split-K, no stem)
-constexpr int kPGemmCfgBase = 130;
-constexpr int kNumPGemmConfigs = 8;
+// ids 124..137 are retired: the 32-deep k-tile builds (124..129) and the
+// persistent multi-tile kernel (130..137) took 0 of 192 picks in the round-5
+// tile table (ops/tuned_mi355x.json) and were removed in round 6
+// a seventh range: the big-tile ping-pong GEMM (bgemm.hip; dense operands, no split-K fixup)
+constexpr int kBGemmCfgBase = 140;
+constexpr int kNumBGemmConfigs = 3;
 inline bool cgemm_cfg_id(int cfg) {
   return (cfg >= kCGemmCfgBase && cfg < kCGemmCfgBase + kNumCGemmConfigs) ||
          (cfg >= kCGemmCfgBase2 && cfg < kCGemmCfgBase2 + kNumCGemmConfigs2) ||
          (cfg >= kCGemmPfCfgBase && cfg < kCGemmPfCfgBase + kNumCGemmPfConfigs) ||
          (cfg >= kCGemm32CfgBase && cfg < kCGemm32CfgBase + kNumCGemm32Configs) ||
-         (cfg >= kCGemmKt32CfgBase && cfg < kCGemmKt32CfgBase + kNumCGemmKt32Configs) ||
-         (cfg >= kPGemmCfgBase && cfg < kPGemmCfgBase + kNumPGemmConfigs);
+         (cfg >= kBGemmCfgBase && cfg < kBGemmCfgBase + kNumBGemmConfigs);
 }
 
 // Operand requirements (else cgemm_launch returns hipErrorInvalidValue):
@@ -44,10 +43,8 @@ int cgemm_config_bn(int cfg);
 hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t stream);
 // the 32x32x16 builds (cgemm32.hip), table index idx = cfg - kCGemm32CfgBase
 hipError_t cgemm32_launch(const IGemmArgs& a, int a_mode, int idx, hipStream_t stream);
-// the 32-deep k-tile builds (cgemm_kt32.hip), idx = cfg - kCGemmKt32CfgBase
-hipError_t cgemm_kt32_launch(const IGemmArgs& a, int a_mode, int idx, hipStream_t stream);
-// the persistent multi-tile builds (pgemm.hip), idx = cfg - kPGemmCfgBase
-hipError_t pgemm_launch(const IGemmArgs& a, int a_mode, int idx, hipStream_t stream);
+// the big-tile ping-pong builds (bgemm.hip), idx = cfg - kBGemmCfgBase
+hipError_t bgemm_launch(const IGemmArgs& a, int a_mode, int idx, hipStream_t stream);
 // the config can finish split-K in-kernel (IGemmArgs::counters)
 bool cgemm_fixup_ok(int cfg);
 // workgroups (= tiles) of a halo launch (its split-K counters)
@@ -65,8 +62,13 @@ constexpr int kHaloPfCfgBase = 80;
 // the PF build of tile 4 (256x128, 8 waves) does not fit the register budget
 // and is not instantiated: id 84 is not a config
 constexpr int kHaloPfMissing = 4;
+// the ping-pong halo kernel (halo.hip halo_pp_kernel): 128 output pixels x
+// 128 (id 144) or 64 (id 145) channels, 8 waves in two staggered groups
+constexpr int kHaloPpCfgBase = 144;
+constexpr int kNumHaloPpConfigs = 2;
 inline bool halo_cfg_id(int cfg) {
   return (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) ||
+         (cfg >= kHaloPpCfgBase && cfg < kHaloPpCfgBase + kNumHaloPpConfigs) ||
          (cfg >= kHaloPfCfgBase && cfg < kHaloPfCfgBase + kNumHaloConfigs && cfg != kHaloPfCfgBase + kHaloPfMissing);
 }
 bool halo_supported(const IGemmArgs& a);

@@ -54,17 +54,14 @@ constexpr int kPfOf[kNumCGemmPfConfigs] = {0, 2, 3, 4, 7, 9, 10, 11, 12, 13, 23}
 // 32x32x16 MFMA builds (ids kCGemm32CfgBase + i): BM x BN, wave grid, ring depth
 constexpr int k32BM[kNumCGemm32Configs] = {64, 64, 128, 128, 64, 128, 256, 256, 128, 64, 128, 256};
 constexpr int k32BN[kNumCGemm32Configs] = {64, 64, 128, 64, 128, 256, 128, 64, 128, 128, 64, 192};
-// 32-deep k-tile builds (ids kCGemmKt32CfgBase + i, cgemm_kt32.hip)
-constexpr int kK32BM[kNumCGemmKt32Configs] = {256, 256, 256, 128, 128, 128};
-constexpr int kK32BN[kNumCGemmKt32Configs] = {192, 192, 128, 256, 128, 96};
-// persistent multi-tile builds (ids kPGemmCfgBase + i, pgemm.hip)
-constexpr int kPBM[kNumPGemmConfigs] = {64, 64, 64, 128, 128, 128, 64, 64};
-constexpr int kPBN[kNumPGemmConfigs] = {64, 64, 128, 64, 128, 128, 256, 64};
+
+// big-tile ping-pong builds (ids kBGemmCfgBase + i, bgemm.hip)
+constexpr int kBBM[kNumBGemmConfigs] = {256, 256, 256};
+constexpr int kBBN[kNumBGemmConfigs] = {256, 128, 192};
 
 // config id -> index into the tables (all id ranges; the 32x32 range indexes k32BM / k32BN)
 int cfg_index(int cfg) {
-  if (cfg >= kPGemmCfgBase) return cfg - kPGemmCfgBase;
-  if (cfg >= kCGemmKt32CfgBase) return cfg - kCGemmKt32CfgBase;
+  if (cfg >= kBGemmCfgBase) return cfg - kBGemmCfgBase;
   if (cfg >= kCGemm32CfgBase) return cfg - kCGemm32CfgBase;
   if (cfg >= kCGemmPfCfgBase) return kPfOf[cfg - kCGemmPfCfgBase];
   return cfg < kCGemmCfgBase2 ? cfg - kCGemmCfgBase : kNumCGemmConfigs + (cfg - kCGemmCfgBase2);
@@ -142,18 +139,16 @@ hipError_t launch_mode(const IGemmArgs& a, int cfg, hipStream_t s) {
 }  // namespace
 
 int cgemm_config_bm(int cfg) {
-  return cfg >= kPGemmCfgBase ? kPBM[cfg_index(cfg)]
-         : cfg >= kCGemmKt32CfgBase ? kK32BM[cfg_index(cfg)]
+  return cfg >= kBGemmCfgBase ? kBBM[cfg_index(cfg)]
          : cfg >= kCGemm32CfgBase ? k32BM[cfg_index(cfg)] : kBM[cfg_index(cfg)];
 }
 int cgemm_config_bn(int cfg) {
-  return cfg >= kPGemmCfgBase ? kPBN[cfg_index(cfg)]
-         : cfg >= kCGemmKt32CfgBase ? kK32BN[cfg_index(cfg)]
+  return cfg >= kBGemmCfgBase ? kBBN[cfg_index(cfg)]
          : cfg >= kCGemm32CfgBase ? k32BN[cfg_index(cfg)] : kBN[cfg_index(cfg)];
 }
 
 bool cgemm_fixup_ok(int cfg) {
-  if (cfg >= kPGemmCfgBase) return false;            // no split-K at all
+  if (cfg >= kBGemmCfgBase) return false;            // no in-kernel fixup (bgemm)
   // the in-kernel split-K fixup needs the whole fp32 tile in LDS at once (one pass)
   return size_t(cgemm_config_bm(cfg)) * (cgemm_config_bn(cfg) + 4) * 4 <= 160 * 1024;
 }
@@ -178,8 +173,7 @@ bool cgemm_supported(const IGemmArgs& a, int a_mode) {
 
 hipError_t cgemm_launch(const IGemmArgs& a, int a_mode, int cfg, hipStream_t s) {
   if (!cgemm_cfg_id(cfg) || !cgemm_supported(a, a_mode)) return hipErrorInvalidValue;
-  if (cfg >= kPGemmCfgBase) return pgemm_launch(a, a_mode, cfg_index(cfg), s);
-  if (cfg >= kCGemmKt32CfgBase) return cgemm_kt32_launch(a, a_mode, cfg_index(cfg), s);
+  if (cfg >= kBGemmCfgBase) return bgemm_launch(a, a_mode, cfg_index(cfg), s);
   if (cfg >= kCGemm32CfgBase) return cgemm32_launch(a, a_mode, cfg_index(cfg), s);
   if (cfg >= kCGemmPfCfgBase) {
     const int idx = cfg_index(cfg);

@@ -159,20 +159,20 @@ CGEMM.update({96 + k: CGEMM[base] for k, base in enumerate(CGEMM_PF_OF)})
 CGEMM32 = {112: (64, 64), 113: (64, 64), 114: (128, 128), 115: (128, 64), 116: (64, 128), 117: (128, 256),
            118: (256, 128), 119: (256, 64), 120: (128, 128), 121: (64, 128), 122: (128, 64), 123: (256, 192)}
 CGEMM.update(CGEMM32)
-# 32-deep k-tile builds (kernels/cgemm_kt32.hip, ids 124..129: deeper rings in the same LDS)
-CGEMM_KT32 = {124: (256, 192), 125: (256, 192), 126: (256, 128), 127: (128, 256), 128: (128, 128), 129: (128, 96)}
-CGEMM.update(CGEMM_KT32)
-# persistent multi-tile builds (kernels/pgemm.hip, ids 130..137): a resident grid loops over
-# the tiles with the DMA ring running across tile boundaries; no split-K, no stem operand
-PGEMM = {130: (64, 64), 131: (64, 64), 132: (64, 128), 133: (128, 64), 134: (128, 128), 135: (128, 128),
-         136: (64, 256), 137: (64, 64)}
-CGEMM.update(PGEMM)
+# (ids 124..137, the 32-deep k-tile and persistent multi-tile builds, were removed in round 6:
+# 0 of 192 picks in the round-5 table)
+# big-tile ping-pong builds (kernels/bgemm.hip, ids 140..142): 8 waves of 128 x 64 / 128 x 32 / 128 x 48,
+# dense operands only (other operand modes are rejected at launch and skipped by the tuner)
+BGEMM = {140: (256, 256), 141: (256, 128), 142: (256, 192)}
+CGEMM.update(BGEMM)
 TILES.update(CGEMM)
 # halo-tiled 3x3 stride-1 conv (kernels/halo.hip): config id -> (output pixels per tile, BN)
 HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 128), 53: (64, 128), 54: (64, 64),
         55: (128, 64), 56: (256, 64), 57: (128, 64), 58: (128, 64)}
 # the same tiles with the fragment-prefetch step pipeline (halo.hip PF)
 HALO.update({cfg + 32: tile for cfg, tile in list(HALO.items()) if cfg != 52})
+# the ping-pong halo kernel (halo.hip halo_pp_kernel): 8 waves in two staggered groups
+HALO.update({144: (128, 128), 145: (128, 64)})
 TILES.update(HALO)
 
 
@@ -217,9 +217,9 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
             continue
         if cgemm_only and cfg not in CGEMM:
             continue
-        if stem and (cfg in CGEMM_KT32 or cfg in PGEMM):
-            continue
-        if ln and (cfg not in CGEMM or cfg in PGEMM or bn % 32):
+        if (stem or ln) and cfg in BGEMM:
+            continue   # dense operands, plain epilogues only
+        if ln and (cfg not in CGEMM or bn % 32):
             continue   # deferred LayerNorm: cgemm tiles (4-aligned chunk lanes per row)
         if K < 2 * TILE_BK.get(cfg, 64) and cfg in TILE_BK:
             continue   # deep k-tiles only pay off with several of them
@@ -229,7 +229,7 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
             continue   # 96-wide tiles: only where they divide N (BERT's 768 / 2304 / 3072)
         tiles = -(-M // bm) * -(-N // bn)
         for s in (1, 2, 4, 8, 16):
-            if s > 1 and (no_split or cfg in PGEMM or nk // s < 2 or tiles >= 1024 or tiles * s > 4096):
+            if s > 1 and (no_split or nk // s < 2 or tiles >= 1024 or tiles * s > 4096):
                 continue
             out.append((cfg, s))
     return out

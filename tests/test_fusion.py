@@ -337,16 +337,17 @@ def test_defer_layernorm_leaves_other_readers_alone():
 
 def test_tile_candidates_respect_kernel_limits():
     """ops.candidates: the tuner is only offered tiles the launchers accept --
-    no 32-deep or persistent build for the padded RGBA stem, no split-K for the
-    persistent builds, only 4-aligned chunk-lane cgemm tiles for the deferred
-    LayerNorm, and 144- / 96-wide tiles only where they divide N."""
+    no big-tile (bgemm) build for the padded RGBA stem or the deferred
+    LayerNorm, only 4-aligned chunk-lane cgemm tiles for the deferred
+    LayerNorm, and 144- / 96-wide tiles only where they divide N; the retired
+    ids 124..137 are gone."""
     from rust_tensorflow_serving2_amd import ops
     qkv = ops.candidates(4096, 2304, 768, True, True)
-    assert (73, 1) in qkv and (72, 1) in qkv
-    assert all(not (c in ops.PGEMM and s > 1) for c, s in qkv)
+    assert (73, 1) in qkv and (72, 1) in qkv and (140, 1) in qkv and (141, 1) in qkv
+    assert all(c not in range(124, 138) for c, _s in qkv)
     assert all(c != 73 for c, _s in ops.candidates(4096, 3072, 768, True, True))    # 3072 % 144 != 0
     stem = ops.candidates(32 * 112 * 112, 64, 128, False, True, stem=True)
-    assert stem and all(c not in ops.CGEMM_KT32 and c not in ops.PGEMM for c, _s in stem)
+    assert stem and all(c not in ops.BGEMM for c, _s in stem)
     ln = ops.candidates(4096, 768, 3072, True, True, no_split=True, ln=True)
-    assert ln and all(s == 1 and c in ops.CGEMM and c not in ops.PGEMM and ops.TILES[c][1] % 32 == 0
+    assert ln and all(s == 1 and c in ops.CGEMM and c not in ops.BGEMM and ops.TILES[c][1] % 32 == 0
                       for c, s in ln)

@@ -76,8 +76,7 @@ def test_conv_matches_fp32(shape, cfg, splits):
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
 
 
-PGEMM_CFGS = list(range(130, 138))      # persistent multi-tile builds (no split-K)
-CGEMM_CFGS = list(range(32, 48)) + list(range(64, 76)) + list(range(96, 107)) + list(range(112, 130)) + PGEMM_CFGS
+CGEMM_CFGS = list(range(32, 48)) + list(range(64, 76)) + list(range(96, 107)) + list(range(112, 124))
 CGEMM_CONV_SHAPES = [s for s in CONV_SHAPES if s[3] % 64 == 0] + [
     (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)),   # tiny image: most taps hit padding at the border rows
     (1, 15, 13, 64, 192, 3, 2, (0, 1, 1, 1)),  # odd sizes, asymmetric pads, N tail
@@ -96,7 +95,7 @@ def test_cgemm_conv_matches_fp32(shape, cfg):
     wo = (w + pads[2] + pads[3] - k) // s + 1
     res = rnd(n, ho, wo, cout, seed=4).to(BF)
     ref = ref_conv(x, wt, b, s, pads, res, "relu")
-    for splits in ((1,) if cfg in PGEMM_CFGS else (1, 3)):
+    for splits in (1, 3):
         y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), k, k, s, s, *pads, act=ACT["relu"],
                          cfg=cfg, splits=splits)
         torch.cuda.synchronize()
@@ -105,7 +104,7 @@ def test_cgemm_conv_matches_fp32(shape, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
 
 
-HALO_CFGS = list(range(48, 59)) + [80, 81, 82, 83, 85, 86, 87, 88, 89, 90]
+HALO_CFGS = list(range(48, 59)) + [80, 81, 82, 83, 85, 86, 87, 88, 89, 90] + [144, 145]   # 144/145: ping-pong
 HALO_SHAPES = [
     # N, H, W, Cin, Cout, pads            (3x3 stride 1; ResNet-50 stages + edge cases)
     (2, 56, 56, 64, 64, (1, 1, 1, 1)),
@@ -180,43 +179,7 @@ def test_cgemm_linear_matches_fp32(m, n, k, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (act, err)
 
 
-@pytest.mark.parametrize("cfg", PGEMM_CFGS)
-@pytest.mark.parametrize("m,n,k,conv", [(32768, 256, 128, False), (20000, 72, 192, False),
-                                        (16, 56, 56, True), (9, 14, 14, True)])
-def test_pgemm_many_tiles_per_workgroup(cfg, m, n, k, conv):
-    """The persistent kernel with far more tiles than resident workgroups (each
-    loops over several, its DMA ring running across tile boundaries): dense
-    GEMMs with partial last tiles, and 3x3 im2col convs (N, H, W from the
-    tuple) whose tiles mix images and padding taps."""
-    if conv:
-        nimg, h, w = m, n, k
-        cin, cout = 64, 128
-        x = rnd(nimg, h, w, cin, seed=41).to(BF)
-        wt = rnd(3, 3, cin, cout, scale=1 / math.sqrt(9 * cin), seed=42).to(BF).float()
-        b = rnd(cout, scale=0.1, seed=43)
-        res = rnd(nimg, h, w, cout, seed=44).to(BF)
-        ref = ref_conv(x, wt, b, 1, (1, 1, 1, 1), res, "relu")
-        y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), 3, 3, 1, 1, 1, 1, 1, 1, act=ACT["relu"],
-                         cfg=cfg)
-    else:
-        x = rnd(m, k, seed=45).to(BF)
-        wm = rnd(n, k, scale=1 / math.sqrt(k), seed=46).to(BF)
-        b = rnd(n, scale=0.1, seed=47)
-        res = rnd(m, n, seed=48).to(BF)
-        ref = torch.relu(x.float() @ wm.float().t() + b + res.float())
-        y = hip().linear(x.to(DEV), wm.to(DEV), b.to(DEV), res.to(DEV), ACT["relu"], cfg, False)
-    torch.cuda.synchronize()
-    err = (y.float().cpu() - ref).abs().max().item()
-    assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
-
-
-def test_pgemm_rejects_split_k():
-    x = torch.zeros(256, 256, device=DEV, dtype=BF)
-    with pytest.raises(RuntimeError):
-        hip().linear(x, x, None, None, 0, 130, False, 1.0, None, 2)
-
-
-@pytest.mark.parametrize("cfg", CGEMM_CFGS)
+@pytest.mark.parametrize("cfg", CGEMM_CFGS + [140, 141, 142])
 def test_cgemm_asymmetric_identity(cfg):
     """A = I, asymmetric B (exact in bf16 / fp32): catches a transposed or
     swizzle-permuted C tile in every cgemm config."""
@@ -229,7 +192,7 @@ def test_cgemm_asymmetric_identity(cfg):
 
 @pytest.mark.parametrize("n,ho,c1,h,c2,s,cout", [(2, 56, 64, 56, 64, 1, 256), (2, 28, 128, 56, 256, 2, 512),
                                                  (1, 7, 512, 14, 1024, 2, 2048), (1, 5, 64, 9, 128, 2, 72)])
-@pytest.mark.parametrize("cfg", [32, 36, 42, 43, 44, 45, 47, 112, 114, 117, 121, 126, 128, 130, 132, 134])
+@pytest.mark.parametrize("cfg", [32, 36, 42, 43, 44, 45, 47, 112, 114, 117, 121])
 def test_conv2d_dual_matches_fp32(n, ho, c1, h, c2, s, cout, cfg):
     """One GEMM for a bottleneck tail: relu(conv1x1(h) + conv1x1_stride(x) + b)."""
     hh = rnd(n, ho, ho, c1, seed=21).to(BF)
@@ -239,7 +202,7 @@ def test_conv2d_dual_matches_fp32(n, ho, c1, h, c2, s, cout, cfg):
     b = rnd(cout, scale=0.1, seed=25)
     w = torch.cat([w1, w2], 1).contiguous()
     ref = torch.relu(hh.float() @ w1.float().t() + x.float()[:, ::s, ::s, :] @ w2.float().t() + b)
-    for splits in ((1,) if cfg in PGEMM_CFGS else (1, 2)):
+    for splits in (1, 2):
         y = hip().conv2d_dual(hh.to(DEV), x.to(DEV), w.to(DEV), b.to(DEV), s, s, ACT["relu"], cfg, None, splits)
         err = (y.float().cpu() - ref).abs().max().item()
         assert y.shape == (n, ho, ho, cout)
@@ -354,6 +317,52 @@ def test_linear_matches_fp32(m, n, k, act, cfg, splits):
            "tanh": torch.tanh(ref)}[act]
     err = (y.float().cpu() - ref).abs().max().item()
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("cfg", [140, 141, 142])
+@pytest.mark.parametrize("m,n,k,act,splits,mode", [
+    (4096, 2304, 768, "none", 1, "bf16"),          # BERT QKV (256 x 256: 16 x 9 tiles)
+    (4096, 3072, 768, "gelu_tanh", 1, "bf16"),     # FFN1
+    (4096, 768, 3072, "none", 1, "residual"),      # FFN2 + residual, the two-pass fp32 epilogue
+    (4096, 768, 3072, "none", 4, "bf16"),          # split-K slabs + reduce launch
+    (300, 264, 64, "relu", 1, "bf16"),             # one k-tile; partial tiles in M and N
+    (520, 136, 192, "tanh", 1, "f32"),             # odd k-tile count, fp32 output
+    (777, 1000, 640, "none", 3, "residual"),       # ragged everything, split-K with residual
+])
+def test_bgemm_matches_fp32(m, n, k, act, splits, mode, cfg):
+    """The big-tile ping-pong GEMM (kernels/bgemm.hip) against an fp32 matmul:
+    every epilogue path (one-pass bf16, two-pass fp32 with residual / fp32
+    output, split-K slabs), ragged M / N edges and k-tile counts of 1..48."""
+    x = rnd(m, k, seed=m + k).to(BF)
+    w = rnd(n, k, scale=1 / math.sqrt(k), seed=n + 1).to(BF)
+    b = rnd(n, scale=0.1, seed=n + 2)
+    res = rnd(m, n, seed=m + 3).to(BF) if mode == "residual" else None
+    y = hip().linear(x.to(DEV), w.to(DEV), b.to(DEV), None if res is None else res.to(DEV), ACT[act], cfg,
+                     mode == "f32", splits=splits)
+    torch.cuda.synchronize()
+    ref = x.float() @ w.float().t() + b
+    if res is not None:
+        ref = ref + res.float()
+    ref = {"none": ref, "relu": F.relu(ref), "gelu_tanh": F.gelu(ref, approximate="tanh"),
+           "tanh": torch.tanh(ref)}[act]
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
+
+
+def test_bgemm_rejects_non_dense_and_is_deterministic():
+    """bgemm takes dense operands only (a conv operand mode is a host-side
+    rejection the tuner skips), and repeated launches are bit-identical (no
+    read of a half-tile before its DMA landed)."""
+    x = rnd(1024, 512, seed=5).to(BF).to(DEV)
+    w = rnd(768, 512, scale=0.05, seed=6).to(BF).to(DEV)
+    ys = [hip().linear(x, w, None, None, 0, 140, False) for _ in range(8)]
+    torch.cuda.synchronize()
+    for y in ys[1:]:
+        assert torch.equal(y, ys[0])
+    xc = rnd(2, 8, 8, 64, seed=7).to(BF).to(DEV)
+    wc = pack_w(rnd(3, 3, 64, 64, scale=0.05, seed=8).to(BF).float())
+    with pytest.raises(RuntimeError):
+        hip().conv2d(xc, wc, None, None, 3, 3, 1, 1, 1, 1, 1, 1, act=0, cfg=140)
 
 
 @pytest.mark.parametrize("n,h,w,c,k,st,pt,pb", [(2, 9, 13, 8, 3, 2, 1, 1), (3, 17, 5, 520, 2, 2, 0, 1),
@@ -586,7 +595,7 @@ def _check_attention(s, b=3):
     (51, 2, (1, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1))),       # halo, split over channel chunks
     (117, 1, (2, 14, 14, 256, 256, 1, 1, (0, 0, 0, 0))),    # 32x32 MFMA build
     (113, 2, (2, 28, 28, 128, 128, 3, 2, (1, 1, 1, 1))),    # 32x32 MFMA build, im2col, split-K
-    (128, 2, (2, 28, 28, 128, 128, 3, 2, (1, 1, 1, 1))),    # 32-deep k-tiles, im2col, split-K
+    (144, 2, (2, 28, 28, 128, 128, 3, 1, (1, 1, 1, 1))),    # ping-pong halo, split over channel chunks
 ])
 def test_conv_post_activation_outputs(cfg, splits, shape):
     """ResNet v2 epilogue: one conv writes the block sum y (+bias +residual)
@@ -660,6 +669,8 @@ def test_maxpool_post_affine():
     (42, 3, (2, 14, 14, 256, 256, 1, 1, (0, 0, 0, 0)), True),     # cgemm dense 1x1, post output
     (51, 4, (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)), False),      # halo, split over channel chunks
     (54, 2, (3, 14, 14, 256, 256, 3, 1, (1, 1, 1, 1)), True),     # 9-slot halo, post output
+    (144, 4, (2, 7, 7, 512, 512, 3, 1, (1, 1, 1, 1)), True),      # ping-pong halo, post output
+    (145, 2, (3, 14, 14, 256, 256, 3, 1, (1, 1, 1, 1)), False),   # ping-pong halo, 64-wide
     (114, 2, (2, 14, 14, 256, 256, 1, 1, (0, 0, 0, 0)), True),    # 32x32 MFMA build, post output
 ])
 def test_splitk_in_kernel_fixup_inside_graph(cfg, splits, shape, post, monkeypatch):
