@@ -164,6 +164,20 @@ def test_tuned_cache_roundtrip(tmp_path, monkeypatch):
     assert ops.load_tuned_cache(str(p)) == 0 and not ops._REMOTE
 
 
+def test_committed_tuned_table_matches_config_schema():
+    """The shipped MI355X table (ops/tuned_mi355x.json) must carry the schema
+    of the current config tables: a stale one is silently ignored at start-up
+    and every server re-tunes its kernels (round 6 found the table stale after
+    the ping-pong config ids went in)."""
+    import json
+    from rust_tensorflow_serving2_amd import ops
+    with open(os.path.join(os.path.dirname(ops.__file__), "tuned_mi355x.json")) as f:
+        doc = json.load(f)
+    assert doc["schema"] == ops._table_schema()
+    assert doc["arch"] == "gfx950" and doc["cus"] == 256 and len(doc["picks"]) > 100
+    assert all(int(v[0]) in ops.TILES for v in doc["picks"].values())
+
+
 def test_conv_chain_pass_pairs_expand_with_next_reduce(models_dir, monkeypatch):
     """ResNet-50 stage-1/2 widths: every 1x1 expand whose output feeds the next
     block's 1x1 reduce becomes one _ChainConv with outputs [expand, reduce]
