@@ -24,9 +24,17 @@
 //     last chunk, the number of DMAs issued after B(step) is a compile-time
 //     constant per tap (a run-time switch over it cost ~12 scalar branches per
 //     step and made the kernel slower than the 2-deep original);
-//   * LDS rows are 128 B with 16-B chunks XOR-swizzled by (row & 7), the same
-//     conflict-free image as cgemm; A fragment reads re-derive the swizzle per
-//     tap from the shifted halo row (5 VALU per fragment, hidden under MFMA);
+//   * LDS rows are 128 B with 16-B chunks XOR-swizzled by a per-row key.  The
+//     key is NOT the storage row (row & 7, cgemm's image): 16 output pixels of
+//     a fragment sit on consecutive halo rows only inside one tile row, and a
+//     TW -> TW + 2 jump at each tile-row end put two lanes of an 8-lane LDS
+//     group on the same bank slot (rocprofv3: 1.4-2.3 SQ_LDS_BANK_CONFLICT
+//     cycles per LDS instruction at ResNet-50 stage 3, 9e5 per launch;
+//     profiles/round6/r6e).  halo_key uses the halo pixel's index in the
+//     tile's TW-wide numbering instead, (ii TH + h) TW + w: a fragment's 16
+//     rows then carry 16 consecutive keys at every tap (the tap adds
+//     kh TW + kw to all of them), so every 8-lane group hits 8 distinct slots.
+//     The DMA applies the key on the source address (lane-linear LDS image);
 //   * tile -> workgroup: XCD-aware remap, output-channel slices innermost so
 //     the workgroups sharing one halo run on one XCD (shared L2);
 //   * split-K over channel chunks (gridDim.y), partial slabs indexed by the
@@ -42,6 +50,10 @@ namespace tfsk {
 namespace {
 
 using namespace gemm;
+
+// XOR key of a halo row from its pixel index in the tile's TW-wide numbering
+// (see the header: conflict-free fragment reads across tile-row ends)
+__device__ __forceinline__ int halo_key(int lin) { return lin & 7; }
 
 template <int BM, int BN, int WGM, int WGN, int HR, int S_>
 struct HG {
@@ -268,7 +280,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
     const int rr = fdiv(q, HW2, inv_hw2);
     const int hh = h0 - p.PT + rr, ww = w0 - p.PL + (q - rr * HW2);
     const bool ok = r < hrows && img + ii < nimg && unsigned(hh) < unsigned(H) && unsigned(ww) < unsigned(W);
-    h_off[j] = ok ? (uint32_t(((img + ii) * H + hh) * W + ww) * uint32_t(C) + kc) * 2u : kOOB;
+    const uint32_t kh = uint32_t(((lane & 7) ^ halo_key(ii * TH * TW + rr * TW + (q - rr * HW2))) * 8);
+    h_off[j] = ok ? (uint32_t(((img + ii) * H + hh) * W + ww) * uint32_t(C) + kh) * 2u : kOOB;
   }
   uint32_t b_off[G::BPW];
 #pragma unroll
@@ -309,13 +322,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
 
   // ---- consumer fragments: A rows are output pixels -> halo rows (tap (0,0))
   const int fr = lane & 15, fq = lane >> 4;
-  int hrow0[G::TM];
+  int hrow0[G::TM], kpx0[G::TM];
 #pragma unroll
   for (int i = 0; i < G::TM; ++i) {
     const int px = wm * G::WM + i * 16 + fr;
     const int ii = px / (TH * TW), p2 = px - ii * (TH * TW);
     const int ph = p2 / TW;
     hrow0[i] = px < TI * TH * TW ? ii * HB + ph * HW2 + (p2 - ph * TW) : 0;
+    kpx0[i] = px;
   }
   const uint32_t rb0 = uint32_t(((wn * G::WN + fr) * KT + ((fq ^ (fr & 7)) * 8)) * 2);
   const uint32_t rb1 = uint32_t(((wn * G::WN + fr) * KT + (((4 + fq) ^ (fr & 7)) * 8)) * 2);
@@ -330,13 +344,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
   struct Frags {
     bf16x8 a[2][G::TM], b[2][G::TN];
   };
-  auto load_frags = [&](Frags& f, const char* hb, const char* sb, int tap_off) {
+  auto load_frags = [&](Frags& f, const char* hb, const char* sb, int tap_off, int tap_key) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
       for (int i = 0; i < G::TM; ++i) {
         const int hr = hrow0[i] + tap_off;
-        const uint32_t addr = uint32_t(hr) * 128u + ((uint32_t((kk * 4 + fq) ^ (hr & 7))) << 4);
+        const uint32_t addr = uint32_t(hr) * 128u + ((uint32_t((kk * 4 + fq) ^ halo_key(kpx0[i] + tap_key))) << 4);
         f.a[kk][i] = *reinterpret_cast<const bf16x8*>(hb + addr);
       }
 #pragma unroll
@@ -353,9 +367,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
         for (int j = 0; j < G::TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[kk][i], f.b[kk][j], acc[i][j], 0, 0, 0);
   };
-  auto compute = [&](const char* hb, const char* sb, int tap_off) {
+  auto compute = [&](const char* hb, const char* sb, int tap_off, int tap_key) {
     Frags f;
-    load_frags(f, hb, sb, tap_off);
+    load_frags(f, hb, sb, tap_off, tap_key);
     mma(f);
   };
   // PF: the fragments of step t are read from LDS right after step t's
@@ -406,13 +420,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
         // step above the barrier and sink these reads to their uses: pin both
         __builtin_amdgcn_sched_barrier(0);
         Frags cur;
-        load_frags(cur, hb, ring + (u % G::S) * G::B_B, (u / 3) * HW2 + (u % 3));
+        load_frags(cur, hb, ring + (u % G::S) * G::B_B, (u / 3) * HW2 + (u % 3), (u / 3) * TW + (u % 3));
         __builtin_amdgcn_sched_barrier(0);
         if (u > 0 || c > c0) mma(prev);
         __builtin_amdgcn_sched_barrier(0);   // (and keep them above the next step's barrier)
         prev = cur;
       } else {
-        compute(hb, ring + (u % G::S) * G::B_B, (u / 3) * HW2 + (u % 3));
+        compute(hb, ring + (u % G::S) * G::B_B, (u / 3) * HW2 + (u % 3), (u / 3) * TW + (u % 3));
       }
     }
   };
@@ -518,7 +532,8 @@ __global__ __launch_bounds__(512, 1) void halo_pp_kernel(IGemmArgs p) {
     const int rr = fdiv(q, HW2, inv_hw2);
     const int hh = h0 - p.PT + rr, ww = w0 - p.PL + (q - rr * HW2);
     const bool ok = r < hrows && img + ii < nimg && unsigned(hh) < unsigned(H) && unsigned(ww) < unsigned(W);
-    h_off[j] = ok ? (uint32_t(((img + ii) * H + hh) * W + ww) * uint32_t(C) + kc) * 2u : kOOB;
+    const uint32_t kh = uint32_t(((lane & 7) ^ halo_key(ii * TH * TW + rr * TW + (q - rr * HW2))) * 8);
+    h_off[j] = ok ? (uint32_t(((img + ii) * H + hh) * W + ww) * uint32_t(C) + kh) * 2u : kOOB;
   }
   uint32_t b_off[G::PB];
 #pragma unroll
@@ -565,13 +580,14 @@ __global__ __launch_bounds__(512, 1) void halo_pp_kernel(IGemmArgs p) {
 
   // ---- consumer fragments: A rows are output pixels -> halo rows (tap (0,0))
   const int fr = lane & 15, fq = lane >> 4;
-  int hrow0[G::TM];
+  int hrow0[G::TM], kpx0[G::TM];
 #pragma unroll
   for (int i = 0; i < G::TM; ++i) {
     const int px = wr * G::WM + i * 16 + fr;
     const int ii = px / (TH * TW), p2 = px - ii * (TH * TW);
     const int ph = p2 / TW;
     hrow0[i] = px < TI * TH * TW ? ii * HB + ph * HW2 + (p2 - ph * TW) : 0;
+    kpx0[i] = px;
   }
   const uint32_t sw0 = uint32_t((fq ^ (fr & 7)) << 4), sw1 = uint32_t(((4 + fq) ^ (fr & 7)) << 4);
   const uint32_t rb = uint32_t((wc * G::WN + fr) * 128);
@@ -589,13 +605,13 @@ __global__ __launch_bounds__(512, 1) void halo_pp_kernel(IGemmArgs p) {
   auto barrier = []() { __builtin_amdgcn_s_barrier(); };
   int rd_slot = 0;   // the ring slot of the K-step being read
   // LOAD segment of a K-step: the tap's fragments from halo buffer hb
-  auto read = [&](const char* hb, int tap_off) {
+  auto read = [&](const char* hb, int tap_off, int tap_key) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < G::TM; ++i) {
         const int hr = hrow0[i] + tap_off;
-        const uint32_t addr = uint32_t(hr) * 128u + ((uint32_t((kk * 4 + fq) ^ (hr & 7))) << 4);
+        const uint32_t addr = uint32_t(hr) * 128u + ((uint32_t((kk * 4 + fq) ^ halo_key(kpx0[i] + tap_key))) << 4);
         fa[kk][i] = *reinterpret_cast<const bf16x8*>(hb + addr);
       }
     const char* sb = ring + rd_slot * G::B_B + rb;
@@ -641,7 +657,7 @@ __global__ __launch_bounds__(512, 1) void halo_pp_kernel(IGemmArgs p) {
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
       __builtin_amdgcn_sched_barrier(0);
-      read(hb, (u / 3) * HW2 + (u % 3));
+      read(hb, (u / 3) * HW2 + (u % 3), (u / 3) * TW + (u % 3));
       if (!LAST && u == 1) issue_halo(cc + 1);
       if (!LAST || u + G::D <= 8) issue_b();
       if (!LAST || u < 8) {
