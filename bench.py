@@ -393,6 +393,13 @@ def main():
             nreq = max(1, io1["requests"] - io0["requests"])
             for k in ("io_s_recv", "io_s_h2", "io_s_dispatch", "io_s_send"):
                 d[k.replace("io_s_", "io_us_per_req_")] = round((io1[k] - io0[k]) / nreq * 1e6, 1)
+            if "recv_calls" in io1 and "recv_calls" in io0:
+                # recv() shape: syscalls per request, KB per data-returning call,
+                # empty (EAGAIN) calls per request -- names a slow recv mode
+                calls = io1["recv_calls"] - io0["recv_calls"]
+                d["recv_calls_per_req"] = round(calls / nreq, 2)
+                d["recv_kb_per_call"] = round((io1["recv_bytes"] - io0["recv_bytes"]) / max(calls, 1) / 1024, 1)
+                d["recv_empty_per_req"] = round((io1["recv_empty"] - io0["recv_empty"]) / nreq, 2)
             d["requests"] = io1["requests"] - io0["requests"]
             b = sum(e.get("batches", 0) for e in io1.get("endpoints", {}).values()) - \
                 sum(e.get("batches", 0) for e in io0.get("endpoints", {}).values())

@@ -149,6 +149,10 @@ struct ServerStats {
   // IO-thread time split (ns): recv() syscalls, nghttp2 frame processing incl.
   // body assembly, fast-path dispatch (decode + batch-slot copy), send()
   std::atomic<uint64_t> ns_recv{0}, ns_h2{0}, ns_dispatch{0}, ns_send{0};
+  // recv() shape (the reference-client slow-mode diagnostic, round-5 VERDICT
+  // item 6): calls that returned data, calls that found the socket empty
+  // (EAGAIN: one per epoll wake-up that drained it), bytes returned
+  std::atomic<uint64_t> recv_calls{0}, recv_empty{0}, recv_bytes{0};
 };
 
 class IoThread;

@@ -662,6 +662,8 @@ class IoThread {
       const auto t1 = Clock::now();
       srv_->stats.ns_recv += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
       if (n > 0) {
+        srv_->stats.recv_calls.fetch_add(1, std::memory_order_relaxed);
+        srv_->stats.recv_bytes.fetch_add(uint64_t(n), std::memory_order_relaxed);
         c->ft.advance(buf, size_t(n));
         ssize_t r = nghttp2_session_mem_recv(c->sess, buf, size_t(n));
         srv_->stats.ns_h2 +=
@@ -677,7 +679,10 @@ class IoThread {
         c->dead = true;
         return;
       }
-      if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) {
+        srv_->stats.recv_empty.fetch_add(1, std::memory_order_relaxed);
+        break;
+      }
       c->dead = true;
       return;
     }

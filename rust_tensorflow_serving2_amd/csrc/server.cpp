@@ -546,6 +546,8 @@ void register_server(py::module_& m) {
         d["bytes_in"] = st.bytes_in.load(); d["bytes_out"] = st.bytes_out.load();
         d["io_s_recv"] = st.ns_recv.load() * 1e-9; d["io_s_h2"] = st.ns_h2.load() * 1e-9;
         d["io_s_dispatch"] = st.ns_dispatch.load() * 1e-9; d["io_s_send"] = st.ns_send.load() * 1e-9;
+        d["recv_calls"] = st.recv_calls.load(); d["recv_empty"] = st.recv_empty.load();
+        d["recv_bytes"] = st.recv_bytes.load();
         d["io_connections"] = s.srv->io_connections();
         return d;
       })

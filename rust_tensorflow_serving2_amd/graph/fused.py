@@ -518,6 +518,83 @@ def defer_layernorm(g, order, fed, fetch_refs, device, opts):
         c.refresh()
 
 
+class MatMulLN:
+    """A _FusedMatMul with a residual input whose only reader is a _LayerNorm
+    over its N columns (BERT's attention-output projection + residual +
+    LayerNorm): one ``hip().linear_ln`` launch (kernels/lngemm.hip: a
+    workgroup owns whole rows, so the row statistics stay on the CU and the
+    GEMM output is never re-read), or the two launches -- timed per shape
+    (ops.tuned_choice: option 0 = split, 1 / 2 / 3 = the fused kernel with
+    32 / 64 / 16 rows per workgroup).  The weights stay in the children
+    (parallel/weights.py binds them there).  Request path: BERT Predict
+    (/root/reference/protos/tensorflow_serving/apis/predict.proto:12-40)."""
+
+    children = ("mm", "ln")
+    BM = {1: 32, 2: 64, 3: 16}
+
+    def __init__(self, mm: "FusedMatMul", ln):
+        self.mm, self.ln = mm, ln
+        self.use_hip = mm.use_hip and ln.use_hip
+        self.name = mm.name
+
+    @staticmethod
+    def fusable(mm, ln) -> bool:
+        from ..ops import hip
+        return isinstance(mm, FusedMatMul) and mm.use_hip and getattr(ln, "use_hip", False) and \
+            mm.act == "none" and not mm.out_f32 and mm.np == mm.n and mm.n == ln.g.numel() and \
+            mm.n in (512, 768, 1024) and mm.k % 128 == 0 and hip().linear_ln_supported(1, mm.n, mm.k, 32)
+
+    def __call__(self, ctx, node, ins):
+        mm, ln = self.mm, self.ln
+
+        def split():
+            return ln(ctx, node, mm(ctx, node, ins))
+        x = O.to_torch(ins[0])
+        res = O.to_torch(ins[1]) if len(ins) > 1 else None
+        if not (self.use_hip and x.is_cuda and x.shape[-1] == mm.k and (res is None or res.shape[-1] == mm.n)):
+            return split()
+        from ..ops import hip, tuned_choice
+        H = hip()
+        xb = _to_bf16(x).contiguous()
+        rb = None if res is None else _to_bf16(res).contiguous()
+        M = xb.numel() // mm.k
+        opts = {0: split}
+        for o, bm in self.BM.items():
+            if H.linear_ln_supported(M, mm.n, mm.k, bm):
+                opts[o] = (lambda bm=bm: [H.linear_ln(xb, mm.w, mm.b, rb, ln.g, ln.b, ln.eps, bm)])
+        key = ("mmln", M, mm.n, mm.k, rb is not None)
+        pick = tuned_choice(key, opts, default=0)
+        return opts.get(pick, split)()
+
+
+def fuse_matmul_layernorm(g, order, fed, fetch_refs, device, opts):
+    """_LayerNorm(_FusedMatMul(x, residual)) with the LayerNorm the GEMM
+    output's only reader -> _FusedMatMulLN (MatMulLN).  GPU only;
+    TFSERVE_MATMUL_LN=0 keeps the two nodes; the opt-in defer_layernorm
+    (TFSERVE_DEFER_LN=1) takes precedence."""
+    c = _Ctx(g, order, fed, fetch_refs, device, opts)
+    if not c.use_hip or os.environ.get("TFSERVE_MATMUL_LN", "1") == "0" or \
+            os.environ.get("TFSERVE_DEFER_LN", "0") == "1":
+        return
+    for name in order:
+        ln_node = g.nodes.get(name)
+        if ln_node is None or ln_node.op != "_LayerNorm" or len(ln_node.inputs) != 1:
+            continue
+        src, sidx = ln_node.inputs[0]
+        prod = g.nodes.get(src)
+        if prod is None or sidx != 0 or prod.op != "_FusedMatMul" or c.only_consumer(prod.name) is not ln_node:
+            continue
+        mm, ln = prod.attr("_impl"), ln_node.attr("_impl")
+        if ln is None or not MatMulLN.fusable(mm, ln):
+            continue
+        ln_node.op = "_FusedMatMulLN"
+        ln_node.attrs = {"_impl": MatMulLN(mm, ln)}
+        ln_node.inputs = list(prod.inputs)
+        ln_node.ctrl = _merge_ctrl([prod, ln_node])
+        del g.nodes[prod.name]
+        c.refresh()
+
+
 def release_weight_sources(g, order, fed, fetch_refs, device, opts):
     """Drops the fp32 weight copies the GEMM ops kept for defer_layernorm."""
     for n in g.nodes.values():
@@ -827,6 +904,7 @@ class ChainConv:
 
 
 O.OPS["_ChainConv"] = _impl_op
+O.OPS["_FusedMatMulLN"] = _impl_op
 
 _PASSTHROUGH = ("Identity", "Squeeze", "Reshape")
 
@@ -1278,4 +1356,4 @@ def default_passes(options=None):
                                                                  fuse_stem_pool, fuse_matmul,
                                                                  fuse_classifier_head, fuse_dense_softmax,
                                                                  fuse_conv_chain] + late_passes() + \
-        [defer_layernorm, release_weight_sources]
+        [fuse_matmul_layernorm, defer_layernorm, release_weight_sources]

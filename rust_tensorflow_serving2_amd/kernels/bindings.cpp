@@ -707,6 +707,43 @@ Tensor cast_bf16(const Tensor& x, const c10::optional<Tensor>& out) {
   return y;
 }
 
+// y = LN(x @ w^T + bias + residual) * gamma + beta in one launch (lngemm.hip);
+// x [.., K] contiguous bf16, w [N][ldw] bf16, bias / gamma / beta f32 [N]
+Tensor linear_ln(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
+                 const c10::optional<Tensor>& residual, const Tensor& gamma, const Tensor& beta, double eps,
+                 int64_t bm, const c10::optional<Tensor>& out) {
+  need(x, at::kBFloat16, "x");
+  need(w, at::kBFloat16, "w");
+  need(gamma, at::kFloat, "gamma");
+  need(beta, at::kFloat, "beta");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int K = x.size(-1), M = x.numel() / K, N = w.size(0), ldw = w.size(1);
+  TORCH_CHECK(ldw >= K && ldw % 8 == 0, "linear_ln: w must be [N][>= K], rows a multiple of 8");
+  TORCH_CHECK(tfsk::lngemm_supported(M, N, K, int(bm)), "linear_ln: unsupported shape M=", M, " N=", N, " K=", K,
+              " bm=", bm);
+  TORCH_CHECK(gamma.numel() == N && beta.numel() == N, "linear_ln: gamma / beta size");
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  Tensor y = out.has_value() ? *out : torch::empty(sizes, x.options());
+  need(y, at::kBFloat16, "out");
+  TORCH_CHECK(y.numel() == int64_t(M) * N, "linear_ln: out has the wrong size");
+  tfsk::LnGemmArgs a;
+  a.x = bf16p(x); a.w = bf16p(w); a.gamma = gamma.data_ptr<float>(); a.beta = beta.data_ptr<float>();
+  a.y = bf16p_mut(y); a.M = M; a.N = N; a.K = K; a.ldx = K; a.ldw = ldw; a.eps = float(eps);
+  if (bias.has_value()) {
+    need(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == N, "linear_ln: bias size");
+    a.bias = bias->data_ptr<float>();
+  }
+  if (residual.has_value()) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->numel() == y.numel(), "linear_ln: residual shape must match the output");
+    a.r = bf16p(*residual);
+  }
+  check(tfsk::lngemm_launch(a, int(bm), cur_stream(x)), "linear_ln");
+  return y;
+}
+
 Tensor layernorm(const Tensor& x, const c10::optional<Tensor>& residual, const Tensor& gamma, const Tensor& beta,
                  double eps, const c10::optional<Tensor>& out) {
   need(x, at::kBFloat16, "x");
@@ -856,6 +893,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "copy a pinned host tensor into a device tensor with a kernel (system-scope loads; capturable)");
   m.def("cast_bf16_from_host", &cast_bf16_from_host, "fp32 pinned host tensor -> bf16 device tensor",
         py::arg("x"), py::arg("out"));
+  m.def("linear_ln", &linear_ln, "LN(x @ w^T + bias + residual) * gamma + beta, whole rows per workgroup",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
+        py::arg("eps"), py::arg("bm") = 32, py::arg("out") = py::none());
+  m.def("linear_ln_supported", [](int64_t M, int64_t N, int64_t K, int64_t bm) {
+    return tfsk::lngemm_supported(int(M), int(N), int(K), int(bm));
+  });
   m.def("layernorm", &layernorm, py::arg("x"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("out") = py::none());
   m.def("embed_ln", &embed_ln, py::arg("ids"), py::arg("type_ids"), py::arg("word"), py::arg("pos"),

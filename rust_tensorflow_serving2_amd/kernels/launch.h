@@ -213,6 +213,23 @@ hipError_t embed_ln_launch(const int* ids, const int* type_ids, const uint16_t* 
                            const uint16_t* pos, const uint16_t* type, const float* gamma,
                            const float* beta, uint16_t* y, int tokens, int seq, int hidden,
                            int vocab, int ntypes, float eps, hipStream_t stream);
+// GEMM + residual + LayerNorm over whole rows (kernels/lngemm.hip):
+// y[M][N] = LN(x[M][K] w[N][K]^T + bias + r[M][N]) * gamma + beta, bf16 in/out,
+// f32 bias / gamma / beta; N in {512, 768, 1024}, K % 128 == 0; one workgroup
+// per `bm` rows (16 / 32 / 64).  r, bias may be null.
+struct LnGemmArgs {
+  const uint16_t* x = nullptr;   // [M][ldx]
+  const uint16_t* w = nullptr;   // [N][ldw]
+  const float* bias = nullptr;
+  const uint16_t* r = nullptr;   // [M][N]
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  uint16_t* y = nullptr;         // [M][N]
+  int M = 0, N = 0, K = 0, ldx = 0, ldw = 0;
+  float eps = 1e-12f;
+};
+bool lngemm_supported(int M, int N, int K, int bm);
+hipError_t lngemm_launch(const LnGemmArgs& a, int bm, hipStream_t stream);
 constexpr int kMaxAttentionSeq = 4096;
 // Fused multi-head attention over a packed QKV buffer [B*S][3*H*D] (bf16):
 // ctx[b,q,h,:] = softmax(Q K^T * scale + mask[b*bstride + q*qstride + key]) V

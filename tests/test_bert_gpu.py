@@ -45,7 +45,10 @@ def test_bert_base_gpu_matches_cpu(bert_base, defer_ln, monkeypatch):
     hist = runner.program.op_histogram()
     assert hist["_Attention"] == 12 and hist["_FusedQKV"] == 12
     # deferred: only the last one stays (the pooler reads its output as a strided view)
-    assert hist["_LayerNorm"] == (1 if defer_ln else 24)
+    # default: the 12 attention-output LayerNorms ride on their GEMM
+    # (_FusedMatMulLN, graph/fused.py fuse_matmul_layernorm), the 12 after FFN2 stay
+    assert hist["_LayerNorm"] == (1 if defer_ln else 12)
+    assert hist.get("_FusedMatMulLN", 0) == (0 if defer_ln else 12)
     assert hist["_EmbeddingLN"] == 1 and hist["_KeyMaskAdder"] == 1 and "GatherV2" not in hist
 
 
