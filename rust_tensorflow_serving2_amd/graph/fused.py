@@ -518,6 +518,15 @@ def defer_layernorm(g, order, fed, fetch_refs, device, opts):
         c.refresh()
 
 
+def ln_weight_frags(w_nk: torch.Tensor) -> torch.Tensor:
+    """[N][K] -> the fragment-major layout kernels/lngemm.hip streams: for
+    16-row n-tile nt and 32-deep K-step t, one contiguous KB whose lane l =
+    16 q + r holds w[16 nt + r][32 t + 8 q .. + 8] (a v_mfma_f32_16x16x32_bf16
+    B fragment).  Returned as a contiguous [N][K] tensor."""
+    n, k = w_nk.shape
+    return w_nk.reshape(n // 16, 16, k // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(n, k)
+
+
 class MatMulLN:
     """A _FusedMatMul with a residual input whose only reader is a _LayerNorm
     over its N columns (BERT's attention-output projection + residual +
@@ -536,6 +545,9 @@ class MatMulLN:
         self.mm, self.ln = mm, ln
         self.use_hip = mm.use_hip and ln.use_hip
         self.name = mm.name
+        # the kernel's fragment-major copy of the weights (a weight of this op:
+        # built from mm.w on its device, meta on a follower until bound)
+        self.w_frag = ln_weight_frags(mm.w[:, :mm.k])
 
     @staticmethod
     def fusable(mm, ln) -> bool:
@@ -561,7 +573,7 @@ class MatMulLN:
         opts = {0: split}
         for o, bm in self.BM.items():
             if H.linear_ln_supported(M, mm.n, mm.k, bm):
-                opts[o] = (lambda bm=bm: [H.linear_ln(xb, mm.w, mm.b, rb, ln.g, ln.b, ln.eps, bm)])
+                opts[o] = (lambda bm=bm: [H.linear_ln(xb, self.w_frag, mm.b, rb, ln.g, ln.b, ln.eps, bm)])
         key = ("mmln", M, mm.n, mm.k, rb is not None)
         pick = tuned_choice(key, opts, default=0)
         return opts.get(pick, split)()
@@ -569,11 +581,18 @@ class MatMulLN:
 
 def fuse_matmul_layernorm(g, order, fed, fetch_refs, device, opts):
     """_LayerNorm(_FusedMatMul(x, residual)) with the LayerNorm the GEMM
-    output's only reader -> _FusedMatMulLN (MatMulLN).  GPU only;
-    TFSERVE_MATMUL_LN=0 keeps the two nodes; the opt-in defer_layernorm
+    output's only reader -> _FusedMatMulLN (MatMulLN).  GPU only, opt-in
+    (TFSERVE_MATMUL_LN=1): measured slower than the two launches on MI355X.
+    BERT-base b32 attention output (4096 x 768 x 768, graph-captured, L2-cold
+    operands): fused 21.1 us (16 rows per workgroup) / 23.2 us (32) against
+    11.9 + 5.8 = 17.7 us; FFN2 (K = 3072) 63.2 against 37.5 us
+    (profiles/round6/r6j/probe.log).  A workgroup that owns whole rows must
+    stream the whole weight matrix (1.2 MB) through one CU, and one CU takes in
+    ~60 GB/s even with fragment-major weights (42-46 us per workgroup with
+    [N][K] fragment loads, profiles/round6/r6h).  The opt-in defer_layernorm
     (TFSERVE_DEFER_LN=1) takes precedence."""
     c = _Ctx(g, order, fed, fetch_refs, device, opts)
-    if not c.use_hip or os.environ.get("TFSERVE_MATMUL_LN", "1") == "0" or \
+    if not c.use_hip or os.environ.get("TFSERVE_MATMUL_LN", "0") != "1" or \
             os.environ.get("TFSERVE_DEFER_LN", "0") == "1":
         return
     for name in order:

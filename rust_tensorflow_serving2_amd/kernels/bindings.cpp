@@ -708,7 +708,8 @@ Tensor cast_bf16(const Tensor& x, const c10::optional<Tensor>& out) {
 }
 
 // y = LN(x @ w^T + bias + residual) * gamma + beta in one launch (lngemm.hip);
-// x [.., K] contiguous bf16, w [N][ldw] bf16, bias / gamma / beta f32 [N]
+// x [.., K] contiguous bf16, w_frag = w [N][K] bf16 pre-shuffled fragment-major
+// ([N/16][K/32][4][16][8]: graph/fused.py ln_weight_frags), bias / gamma / beta f32 [N]
 Tensor linear_ln(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
                  const c10::optional<Tensor>& residual, const Tensor& gamma, const Tensor& beta, double eps,
                  int64_t bm, const c10::optional<Tensor>& out) {
@@ -717,8 +718,8 @@ Tensor linear_ln(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
   need(gamma, at::kFloat, "gamma");
   need(beta, at::kFloat, "beta");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  const int K = x.size(-1), M = x.numel() / K, N = w.size(0), ldw = w.size(1);
-  TORCH_CHECK(ldw >= K && ldw % 8 == 0, "linear_ln: w must be [N][>= K], rows a multiple of 8");
+  const int K = x.size(-1), M = x.numel() / K, N = w.size(0);
+  TORCH_CHECK(w.is_contiguous() && w.numel() == int64_t(N) * K, "linear_ln: w_frag must be a contiguous [N][K]");
   TORCH_CHECK(tfsk::lngemm_supported(M, N, K, int(bm)), "linear_ln: unsupported shape M=", M, " N=", N, " K=", K,
               " bm=", bm);
   TORCH_CHECK(gamma.numel() == N && beta.numel() == N, "linear_ln: gamma / beta size");
@@ -729,7 +730,7 @@ Tensor linear_ln(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
   TORCH_CHECK(y.numel() == int64_t(M) * N, "linear_ln: out has the wrong size");
   tfsk::LnGemmArgs a;
   a.x = bf16p(x); a.w = bf16p(w); a.gamma = gamma.data_ptr<float>(); a.beta = beta.data_ptr<float>();
-  a.y = bf16p_mut(y); a.M = M; a.N = N; a.K = K; a.ldx = K; a.ldw = ldw; a.eps = float(eps);
+  a.y = bf16p_mut(y); a.M = M; a.N = N; a.K = K; a.ldx = K; a.eps = float(eps);
   if (bias.has_value()) {
     need(*bias, at::kFloat, "bias");
     TORCH_CHECK(bias->numel() == N, "linear_ln: bias size");

@@ -219,13 +219,13 @@ hipError_t embed_ln_launch(const int* ids, const int* type_ids, const uint16_t* 
 // per `bm` rows (16 / 32 / 64).  r, bias may be null.
 struct LnGemmArgs {
   const uint16_t* x = nullptr;   // [M][ldx]
-  const uint16_t* w = nullptr;   // [N][ldw]
+  const uint16_t* w = nullptr;   // fragment-major [N/16][K/32][64 lanes][8] (lngemm.hip w_off)
   const float* bias = nullptr;
   const uint16_t* r = nullptr;   // [M][N]
   const float* gamma = nullptr;
   const float* beta = nullptr;
   uint16_t* y = nullptr;         // [M][N]
-  int M = 0, N = 0, K = 0, ldx = 0, ldw = 0;
+  int M = 0, N = 0, K = 0, ldx = 0;
   float eps = 1e-12f;
 };
 bool lngemm_supported(int M, int N, int K, int bm);

@@ -1,5 +1,6 @@
 // GEMM + residual + LayerNorm in one launch for MI355X (gfx950):
 //   y[M][N] = LN(x[M][K] w[N][K]^T + bias + r[M][N]) * gamma + beta
+// (w passed fragment-major: see w_off below)
 // bf16 operands / output, fp32 accumulate and statistics.
 //
 // Why: BERT's attention-output projection (M = 128 x batch, N = K = 768) is
@@ -15,9 +16,9 @@
 //     BM/16 x TN accumulators;
 //   * the weights are read ONCE per workgroup and by one wave each (no wave
 //     shares a column), so they skip LDS: every wave streams its own [N/8][K]
-//     slice straight into VGPRs (16-B buffer loads, a DEPTH-deep register
-//     ring of K-steps; nothing else is in flight in the loop, so hipcc's own
-//     counted vmcnt waits pipeline it);
+//     slice straight into VGPRs (16-B buffer loads, a 5-slot register ring,
+//     loads issued 3 K-steps ahead and pinned above the MFMAs, one counted
+//     vmcnt per K-step);
 //   * x (BM x K) and the residual tile (BM x N, one contiguous range: whole
 //     rows) go to LDS by buffer_load ... lds in the prologue, x as k-tile
 //     images of 128-B rows with 16-B chunks XOR-swizzled by (row & 7) (the
@@ -46,7 +47,7 @@ struct LG {
   static constexpr int NW = 8, NT = 512;
   static constexpr int WN = TN * 16, N = NW * WN;   // columns per wave / per row
   static constexpr int MT = BM / 16;                // m-tiles
-  static constexpr int DEPTH = 4;                   // K-steps (32 deep) of weights in flight per wave
+  static constexpr int SLOTS = 5, AHEAD = 3;        // register ring of K-steps (32 deep); loads AHEAD steps out
   static constexpr int R_B = BM * N * 2;            // residual / output staging tile
   static constexpr int ST_B = 2 * NW * BM * 4;      // per-wave row partials (sum, then squares)
   static constexpr int MV_B = 2 * BM * 4;           // mean, rstd per row
@@ -76,22 +77,31 @@ __global__ __launch_bounds__(512, 1) void lngemm_kernel(LnGemmArgs p) {
   const __amdgpu_buffer_rsrc_t rsX =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.x), 0, int(long(M) * p.ldx * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsW =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.w), 0, int(long(G::N) * p.ldw * 2), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.w), 0, int(long(G::N) * K * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsR = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(p.r), 0, p.r ? int(long(M) * G::N * 2) : 0, 0x00020000);
 
   // ---- weights: this wave's columns n = wid * WN + j * 16 + fr, k chunk fq
   const int nks = K / 32;
+  // fragment-major weights (host pre-shuffle, graph/fused.py ln_weight_frags):
+  // the B fragment of (n-tile nt, K-step t) is one contiguous KB, lane l at
+  // ((nt * nks + t) * 64 + l) * 16 -- every load instruction reads 8 whole
+  // 128-B lines instead of 16 half lines of 16 rows (the [N][K] layout ran
+  // 42-46 us per workgroup, profiles/round6/r6h-r6i)
   uint32_t w_off[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) w_off[j] = (uint32_t(wid * G::WN + j * 16 + fr) * uint32_t(p.ldw) + fq * 8) * 2u;
-  u32x4 bq[G::DEPTH][TN];
-  auto load_b = [&](int d, int t) {
+  for (int j = 0; j < TN; ++j) w_off[j] = (uint32_t((wid * TN + j) * nks) * 64u + lane) * 16u;
+  // register ring of SLOTS K-steps: at step t the loads of step t + AHEAD go
+  // into the slot step t - 2 used (its MFMAs issued two steps back), then the
+  // wave waits for step t's own loads (vmcnt = the AHEAD younger steps)
+  u32x4 bq[G::SLOTS][TN];
+  auto load_b = [&](int slot, int t) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bq[d][j] = __builtin_amdgcn_raw_buffer_load_b128(rsW, w_off[j], t * 64, 0);
+    for (int j = 0; j < TN; ++j)
+      bq[slot][j] = __builtin_amdgcn_raw_buffer_load_b128(rsW, w_off[j], min(t, nks - 1) * 1024, 0);
   };
 #pragma unroll
-  for (int d = 0; d < G::DEPTH; ++d) load_b(d, d);
+  for (int d = 0; d < G::AHEAD; ++d) load_b(d, d);
 
   // ---- x k-tile images and the residual tile by LDS-DMA (issued after the
   // first weight loads, so both are in flight together; one vmcnt(0) below)
@@ -122,29 +132,35 @@ __global__ __launch_bounds__(512, 1) void lngemm_kernel(LnGemmArgs p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint32_t ra = uint32_t(fr * 128);
-  for (int t0 = 0; t0 < nks; t0 += G::DEPTH) {
+  for (int t0 = 0; t0 < nks; t0 += G::SLOTS) {
 #pragma unroll
-    for (int d = 0; d < G::DEPTH; ++d) {
+    for (int d = 0; d < G::SLOTS; ++d) {
       const int t = t0 + d;
-      const int kt = t >> 1, ch = (t & 1) * 4 + fq;
-      bf16x8 a[G::MT];
+      // unconditional, clamped at the tail: a branch around the loads made
+      // hipcc wait vmcnt(0) at every loop head (one K-step in flight, 38 us
+      // per workgroup, profiles/round6/r6g)
+      __builtin_amdgcn_sched_barrier(0);
+      load_b((d + G::AHEAD) % G::SLOTS, t + G::AHEAD);
+      __builtin_amdgcn_sched_barrier(0);
+      gemm::wait_vmcnt<G::AHEAD * TN>();
+      if (t < nks) {
+        const int kt = t >> 1, ch = (t & 1) * 4 + fq;
+        bf16x8 a[G::MT];
 #pragma unroll
-      for (int i = 0; i < G::MT; ++i) {
-        const int row = i * 16 + fr;
-        a[i] = *reinterpret_cast<const bf16x8*>(As + (kt * BM + i * 16) * 128 + ra + ((ch ^ (row & 7)) << 4));
+        for (int i = 0; i < G::MT; ++i) {
+          const int row = i * 16 + fr;
+          a[i] = *reinterpret_cast<const bf16x8*>(As + (kt * BM + i * 16) * 128 + ra + ((ch ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < G::MT; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], __builtin_bit_cast(bf16x8, bq[d][j]),
+                                                                acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < G::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], __builtin_bit_cast(bf16x8, bq[d][j]), acc[i][j],
-                                                              0, 0, 0);
-      // unconditional (the tail re-reads the last K-step): a branch around the
-      // loads made hipcc wait vmcnt(0) at every loop head -- one K-step in
-      // flight, 38 us per workgroup (profiles/round6/r6g)
-      load_b(d, min(t + G::DEPTH, nks - 1));
     }
   }
+  gemm::wait_vmcnt<0>();
 
   // ---- epilogue: v = acc + bias + residual; row (i, r) = i * 16 + fq * 4 + r
   const uint16_t* Rh = reinterpret_cast<const uint16_t*>(Rs);
@@ -281,7 +297,7 @@ bool lngemm_supported(int M, int N, int K, int bm) {
 }
 
 hipError_t lngemm_launch(const LnGemmArgs& a, int bm, hipStream_t s) {
-  if (!lngemm_supported(a.M, a.N, a.K, bm) || a.ldx < a.K || a.ldw < a.K || a.ldx % 8 || a.ldw % 8)
+  if (!lngemm_supported(a.M, a.N, a.K, bm) || a.ldx < a.K || a.ldx % 8)
     return hipErrorInvalidValue;
   switch (bm) {
     case 16: return launch_lg_n<16>(a, s);

@@ -4,6 +4,7 @@
 #   PASS=sq    (default) SQ / GRBM: MFMA busy, wait, active per layer
 #   PASS=fetch FETCH_SIZE (3 TCC slots) + GRBM_GUI_ACTIVE: bytes read from beyond L2
 #   PASS=write WRITE_SIZE (2 TCC slots) + GRBM_GUI_ACTIVE: bytes written
+#   PASS=lds   LDS instructions, bank-conflict cycles, LDS wait per layer
 # (FETCH_SIZE and WRITE_SIZE do not fit one pass: MI355X_MICROARCH.md PMC slots.)
 # pmc_summary.py turns the byte counters into GB/s per layer and a bound class.
 set -o pipefail
@@ -17,6 +18,7 @@ case $PASS in
   sq) CTR="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE"; TAG="";;
   fetch) CTR="FETCH_SIZE GRBM_GUI_ACTIVE"; TAG="_fetch";;
   write) CTR="WRITE_SIZE GRBM_GUI_ACTIVE"; TAG="_write";;
+  lds) CTR="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; TAG="_lds";;
   *) echo "unknown PASS=$PASS"; exit 2;;
 esac
 rm -rf /tmp/prof_pmc

@@ -15,6 +15,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from rust_tensorflow_serving2_amd.ops import candidates, hip  # noqa: E402
 from scripts.conv_sweep import time_graph  # noqa: E402
+from rust_tensorflow_serving2_amd.graph.fused import ln_weight_frags  # noqa: E402
 
 BF = torch.bfloat16
 
@@ -28,6 +29,7 @@ def main():
         M, N, K = (int(v) for v in shp.split("x"))
         xs = [torch.randn(M, K, device="cuda").to(BF) for _ in range(8)]
         ws = [(torch.randn(N, K, device="cuda") / K ** 0.5).to(BF) for _ in range(8)]
+        wf = [ln_weight_frags(w) for w in ws]
         rs = [torch.randn(M, N, device="cuda").to(BF) for _ in range(8)]
         outs = [torch.empty(M, N, device="cuda", dtype=BF) for _ in range(8)]
         b, gm, bt = (torch.randn(N, device="cuda") for _ in range(3))
@@ -35,7 +37,7 @@ def main():
         for bm in (16, 32, 64):
             if H.linear_ln_supported(M, N, K, bm):
                 res[f"fused_bm{bm}_us"] = round(time_graph(
-                    lambda i, bm=bm: H.linear_ln(xs[i % 8], ws[i % 8], b, rs[i % 8], gm, bt, 1e-12, bm,
+                    lambda i, bm=bm: H.linear_ln(xs[i % 8], wf[i % 8], b, rs[i % 8], gm, bt, 1e-12, bm,
                                                  outs[i % 8])), 2)
         best = None
         for cfg, sp in candidates(M, N, K, True, K % 64 == 0):

@@ -20,6 +20,25 @@ def bert_base(tmp_path_factory):
     return path
 
 
+def test_bert_matmul_ln_opt_in_matches_cpu(bert_base, monkeypatch):
+    """TFSERVE_MATMUL_LN=1: the 12 attention-output LayerNorms ride on their
+    GEMM (_FusedMatMulLN; each bucket still times it against the two launches)
+    and the program matches the CPU one."""
+    from rust_tensorflow_serving2_amd.server.servable import Servable, ServableOptions
+    monkeypatch.setenv("TFSERVE_MATMUL_LN", "1")
+    gpu = Servable("bert", 1, bert_base, ServableOptions(device="cuda:0", max_batch_size=8))
+    cpu = Servable("bert", 1, bert_base, ServableOptions(device="cpu"))
+    rng = np.random.default_rng(1)
+    feeds = {"input_ids": rng.integers(0, 30522, (2, 128)).astype(np.int32),
+             "input_mask": np.ones((2, 128), np.int32), "segment_ids": np.zeros((2, 128), np.int32)}
+    outs = ["pooled_output", "probabilities"]
+    g = gpu.run("serving_default", feeds, outs)
+    c = cpu.run("serving_default", feeds, outs)
+    assert np.abs(g["pooled_output"] - c["pooled_output"]).max() < 5e-2
+    hist = next(iter(gpu._runners.values())).program.op_histogram()
+    assert hist["_FusedMatMulLN"] == 12 and hist["_LayerNorm"] == 12
+
+
 @pytest.mark.parametrize("defer_ln", [True, False])
 def test_bert_base_gpu_matches_cpu(bert_base, defer_ln, monkeypatch):
     """defer_ln: the encoder LayerNorms folded into their GEMMs
@@ -45,10 +64,8 @@ def test_bert_base_gpu_matches_cpu(bert_base, defer_ln, monkeypatch):
     hist = runner.program.op_histogram()
     assert hist["_Attention"] == 12 and hist["_FusedQKV"] == 12
     # deferred: only the last one stays (the pooler reads its output as a strided view)
-    # default: the 12 attention-output LayerNorms ride on their GEMM
-    # (_FusedMatMulLN, graph/fused.py fuse_matmul_layernorm), the 12 after FFN2 stay
-    assert hist["_LayerNorm"] == (1 if defer_ln else 12)
-    assert hist.get("_FusedMatMulLN", 0) == (0 if defer_ln else 12)
+    assert hist["_LayerNorm"] == (1 if defer_ln else 24)
+    assert "_FusedMatMulLN" not in hist        # fuse_matmul_layernorm is opt-in (measured slower)
     assert hist["_EmbeddingLN"] == 1 and hist["_KeyMaskAdder"] == 1 and "GatherV2" not in hist
 
 

@@ -467,8 +467,9 @@ def test_linear_ln_matches_fp32(m, n, k, bm, res, bias):
     b = rnd(n, seed=63) if bias else None
     r = (rnd(m, n, seed=64) * 2 + 3).to(BF) if res else None
     gm, bt = rnd(n, seed=65), rnd(n, seed=66)
-    y = hip().linear_ln(x.to(DEV), w.to(DEV), None if b is None else b.to(DEV), None if r is None else r.to(DEV),
-                        gm.to(DEV), bt.to(DEV), 1e-12, bm)
+    from rust_tensorflow_serving2_amd.graph.fused import ln_weight_frags
+    y = hip().linear_ln(x.to(DEV), ln_weight_frags(w).to(DEV), None if b is None else b.to(DEV),
+                        None if r is None else r.to(DEV), gm.to(DEV), bt.to(DEV), 1e-12, bm)
     z = x.float() @ w.float().t()
     if b is not None:
         z = z + b
