@@ -62,13 +62,8 @@ constexpr int kHaloPfCfgBase = 80;
 // the PF build of tile 4 (256x128, 8 waves) does not fit the register budget
 // and is not instantiated: id 84 is not a config
 constexpr int kHaloPfMissing = 4;
-// the ping-pong halo kernel (halo.hip halo_pp_kernel): 128 output pixels x
-// 128 (id 144) or 64 (id 145) channels, 8 waves in two staggered groups
-constexpr int kHaloPpCfgBase = 144;
-constexpr int kNumHaloPpConfigs = 2;
 inline bool halo_cfg_id(int cfg) {
   return (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) ||
-         (cfg >= kHaloPpCfgBase && cfg < kHaloPpCfgBase + kNumHaloPpConfigs) ||
          (cfg >= kHaloPfCfgBase && cfg < kHaloPfCfgBase + kNumHaloConfigs && cfg != kHaloPfCfgBase + kHaloPfMissing);
 }
 bool halo_supported(const IGemmArgs& a);

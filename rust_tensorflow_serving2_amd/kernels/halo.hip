@@ -442,251 +442,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
   trace_stamp(p, 3);
 }
 
-// ---------------------------------------------------------------- ping-pong halo conv
-// halo_pp_kernel: the same halo tiling (a 128-pixel output block or whole
-// images, its (TH+2) x (TW+2) input halo DMA'd once per 64-channel chunk,
-// all nine taps against it), restructured like bgemm.hip for the 3x3 layers
-// that run 5x off their compute SOL at b32 (round-5 VERDICT item 1: stage-3/4
-// 3x3 convs 15.6-16.3 us each; halo_conv_kernel<128, 64, 4, 2> puts 32 x 32
-// outputs on a wave and its 8 waves read, wait and compute in lockstep):
-//   * 8 waves = two ping-pong groups (pixel rows 0-63 / 64-127) x 4 along
-//     Cout; wave tile 64 px x 32 (BN = 128) or x 16 (BN = 64) channels;
-//   * one phase per (chunk, tap) K-step: [LOAD: the tap's A fragments (the
-//     halo shifted by the tap), B fragments from the weight ring, DMAs,
-//     counted wait] barrier [COMPUTE: 16 / 8 MFMAs] barrier; waves 4-7 run one
-//     barrier behind, so on each SIMD one wave computes while its partner
-//     loads;
-//   * weight ring of S = 6 slots (runtime slot offset: one scalar per phase),
-//     D = 4 K-steps issued ahead; the next chunk's halo goes out at tap 1 into
-//     the other halo buffer (its last reader, the previous chunk's tap 8, is
-//     two phases back) and is waited for at tap 8 together with the next
-//     chunk's first weights;
-//   * RAW / WAR as bgemm: a slot is read one phase after the wait that
-//     retires it and refilled two phases after its last read (S >= D + 2);
-//   * the shared halo_epilogue (bf16 one-pass / fp32 staging / split-K slabs
-//     with the in-kernel fixup).
-template <int BN>
-struct HP {
-  static constexpr int BM = 128, HR = 192, NW = 8, NT = 512, WGN = 4;
-  static constexpr int WM = BM / 2, WN = BN / WGN;
-  static constexpr int TM = WM / 16, TN = WN / 16;
-  static constexpr int S = 6, D = 4;
-  static constexpr int PH = HR / 8 / NW;        // halo pieces per wave per chunk
-  static constexpr int PB = BN / 8 / NW;        // weight pieces per wave per K-step
-  static constexpr int HALO_B = HR * 128, B_B = BN * 128;
-  static constexpr int LDS_MAIN = 2 * HALO_B + S * B_B;
-  static constexpr int LDS_EPI = BM * (BN + 4) * 4;
-  static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
-  static_assert(S >= D + 2 && D <= 7, "ring depth (WAR: refill two phases after the last read)");
-  static_assert(PH * 8 * NW == HR && PB * 8 * NW == BN && TN >= 1, "DMA split");
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-};
+// (the ping-pong halo kernel, ids 144/145, was removed in round 6: 0 picks in
+// the round-6 tile tables, slower than halo_conv_kernel on every ResNet-50
+// 3x3 layer -- profiles/round6/r6f/conv.log; it stays in git history)
 
-template <int BN>
-__global__ __launch_bounds__(512, 1) void halo_pp_kernel(IGemmArgs p) {
-  using G = HP<BN>;
-  constexpr int BM = G::BM;
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  char* const smem = reinterpret_cast<char*>(smem_raw);
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-  const int TH = p.TH, TW = p.TW, HW2 = TW + 2;
-  const int Ho = p.Ho, Wo = p.Wo, H = p.H, W = p.W, C = p.C;
-  const int tph = (Ho + TH - 1) / TH, tpw = (Wo + TW - 1) / TW;
-  const int nbn = (p.N + BN - 1) / BN;
-  const int TI = p.TI > 1 ? p.TI : 1, nimg = p.M / (Ho * Wo);
-  const int HB = (TH + 2) * HW2;
-
-  // ---- tile of this workgroup: (image, tile row, tile col, channel slice)
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int bn = wg % nbn;
-  int r_ = wg / nbn;
-  const int tw = r_ % tpw;
-  r_ /= tpw;
-  const int th = r_ % tph;
-  const int img = (r_ / tph) * TI;
-  const int h0 = th * TH, w0 = tw * TW, n0 = bn * BN;
-
-  trace_stamp(p, 0);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid / G::WGN, wc = wid % G::WGN;
-  const int prow = lane >> 3;
-  const uint32_t kc = uint32_t(((lane & 7) ^ prow) * 8);
-
-  const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.a), 0, int(p.a_bytes), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.b), 0, int(p.b_bytes), 0x00020000);
-
-  // ---- per-lane halo DMA offsets (halo row r: image r / HB of the tile,
-  // pixel (h0 - PT + q / HW2, w0 - PL + q % HW2) with q = r % HB)
-  const int hrows = TI * HB;
-  const float inv_hw2 = 1.f / float(HW2), inv_hb = 1.f / float(HB);
-  uint32_t h_off[G::PH];
-#pragma unroll
-  for (int j = 0; j < G::PH; ++j) {
-    const int r = (wid * G::PH + j) * 8 + prow;
-    const int ii = TI > 1 ? fdiv(r, HB, inv_hb) : 0;
-    const int q = r - ii * HB;
-    const int rr = fdiv(q, HW2, inv_hw2);
-    const int hh = h0 - p.PT + rr, ww = w0 - p.PL + (q - rr * HW2);
-    const bool ok = r < hrows && img + ii < nimg && unsigned(hh) < unsigned(H) && unsigned(ww) < unsigned(W);
-    const uint32_t kh = uint32_t(((lane & 7) ^ halo_key(ii * TH * TW + rr * TW + (q - rr * HW2))) * 8);
-    h_off[j] = ok ? (uint32_t(((img + ii) * H + hh) * W + ww) * uint32_t(C) + kh) * 2u : kOOB;
-  }
-  uint32_t b_off[G::PB];
-#pragma unroll
-  for (int j = 0; j < G::PB; ++j) {
-    const int n = n0 + (wid * G::PB + j) * 8 + prow;
-    b_off[j] = n < p.N ? (uint32_t(n) * uint32_t(p.ldb) + kc) * 2u : kOOB;
-  }
-
-  // ---- channel-chunk range (split-K: blockIdx.y selects a slice of chunks)
-  const int nch = C / KT;
-  int c0 = 0, c1 = nch;
-  if (p.splits > 1) {
-    c0 = blockIdx.y * p.kt_per_split;
-    c1 = min(nch, c0 + p.kt_per_split);
-  }
-  const int nck = c1 - c0;
-  char* const ring = smem + 2 * G::HALO_B;
-
-  auto issue_halo = [&](int cc) {    // chunk c0 + cc -> halo buffer cc & 1
-    char* dst = smem + (cc & 1) * G::HALO_B;
-    const uint32_t soff = uint32_t(c0 + cc) * (KT * 2);
-#pragma unroll
-    for (int j = 0; j < G::PH; ++j) {
-      const uint32_t v = h_off[j];
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(dst + (wid * G::PH + j) * 1024), 16, v, soff, 0, 0);
-    }
-  };
-  // K-step t's weights: chunk c0 + t / 9, tap t % 9 (weights k = tap * C + channel) -> ring slot t % S
-  int ib_cc = 0, ib_u = 0, ib_slot = 0;   // the next K-step to issue (scalars)
-  auto issue_b = [&]() {
-    const uint32_t soff = uint32_t(ib_u * C + (c0 + ib_cc) * KT) * 2u;
-    char* dst = ring + ib_slot * G::B_B;
-#pragma unroll
-    for (int j = 0; j < G::PB; ++j) {
-      const uint32_t v = b_off[j];
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_ptr_t)(dst + (wid * G::PB + j) * 1024), 16, v, soff, 0, 0);
-    }
-    if (++ib_u == 9) {
-      ib_u = 0;
-      ++ib_cc;
-    }
-    if (++ib_slot == G::S) ib_slot = 0;
-  };
-
-  // ---- consumer fragments: A rows are output pixels -> halo rows (tap (0,0))
-  const int fr = lane & 15, fq = lane >> 4;
-  int hrow0[G::TM], kpx0[G::TM];
-#pragma unroll
-  for (int i = 0; i < G::TM; ++i) {
-    const int px = wr * G::WM + i * 16 + fr;
-    const int ii = px / (TH * TW), p2 = px - ii * (TH * TW);
-    const int ph = p2 / TW;
-    hrow0[i] = px < TI * TH * TW ? ii * HB + ph * HW2 + (p2 - ph * TW) : 0;
-    kpx0[i] = px;
-  }
-  const uint32_t sw0 = uint32_t((fq ^ (fr & 7)) << 4), sw1 = uint32_t(((4 + fq) ^ (fr & 7)) << 4);
-  const uint32_t rb = uint32_t((wc * G::WN + fr) * 128);
-
-  f32x4 acc[G::TM][G::TN];
-#pragma unroll
-  for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[2][G::TM], fb[2][G::TN];
-
-  float4 bias0, bias1;
-  prefetch_bias<BM, BN, G::NT>(p, n0, tid, bias0, bias1);
-
-  auto barrier = []() { __builtin_amdgcn_s_barrier(); };
-  int rd_slot = 0;   // the ring slot of the K-step being read
-  // LOAD segment of a K-step: the tap's fragments from halo buffer hb
-  auto read = [&](const char* hb, int tap_off, int tap_key) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < G::TM; ++i) {
-        const int hr = hrow0[i] + tap_off;
-        const uint32_t addr = uint32_t(hr) * 128u + ((uint32_t((kk * 4 + fq) ^ halo_key(kpx0[i] + tap_key))) << 4);
-        fa[kk][i] = *reinterpret_cast<const bf16x8*>(hb + addr);
-      }
-    const char* sb = ring + rd_slot * G::B_B + rb;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < G::TN; ++j) fb[kk][j] = *reinterpret_cast<const bf16x8*>(sb + j * 16 * 128 + (kk ? sw1 : sw0));
-    if (++rd_slot == G::S) rd_slot = 0;
-  };
-  auto compute = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-        for (int j = 0; j < G::TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    barrier();
-  };
-
-  // ---- prologue: chunk 0's halo, K-steps 0 .. D-1 (D < 9: all in chunk 0)
-  issue_halo(0);
-#pragma unroll
-  for (int j = 0; j < G::D; ++j) issue_b();
-  wait_vmcnt<(G::D - 1) * G::PB>();     // the halo and K-step 0 landed
-  barrier();
-  trace_stamp(p, 1);
-  if (wr == 1) barrier();               // the second group runs one barrier behind
-
-  // ---- chunks; the nine taps unrolled so every wait count is an immediate:
-  // DMAs younger than K-step t+1's weights are those of t+2 .. t+D that were
-  // issued (fewer in the last chunk's tail), plus the next chunk's halo when
-  // it went out after t+1's weights (taps 1 .. D-1)
-  auto chunk = [&](auto last_tag, int cc) {
-    constexpr bool LAST = decltype(last_tag)::value;
-    const char* hb = smem + (cc & 1) * G::HALO_B;
-#pragma unroll
-    for (int u = 0; u < 9; ++u) {
-      __builtin_amdgcn_sched_barrier(0);
-      read(hb, (u / 3) * HW2 + (u % 3), (u / 3) * TW + (u % 3));
-      if (!LAST && u == 1) issue_halo(cc + 1);
-      if (!LAST || u + G::D <= 8) issue_b();
-      if (!LAST || u < 8) {
-        const int nb = LAST ? ((G::D < 8 - u ? G::D : 8 - u) - 1) : G::D - 1;
-        const int younger = G::PB * (nb > 0 ? nb : 0) + ((!LAST && u >= 1 && u <= G::D - 1) ? G::PH : 0);
-        switch (younger) {   // folds to one immediate per unrolled tap
-#define TFSK_W(k) case k: wait_vmcnt<k>(); break;
-          TFSK_W(0) TFSK_W(1) TFSK_W(2) TFSK_W(3) TFSK_W(4) TFSK_W(5) TFSK_W(6) TFSK_W(7) TFSK_W(8) TFSK_W(9)
-          TFSK_W(10) TFSK_W(11) TFSK_W(12)
-#undef TFSK_W
-          default: wait_vmcnt<0>(); break;
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      barrier();
-      compute();
-    }
-  };
-  for (int cc = 0; cc < nck - 1; ++cc) chunk(std::false_type{}, cc);
-  chunk(std::true_type{}, nck - 1);
-  if (wr == 0) barrier();   // re-join the groups
-  wait_vmcnt<0>();
-  __syncthreads();
-  trace_stamp(p, 2);
-
-  halo_epilogue<BM, BN, G::NT, G::TM, G::TN, G::WM, G::WN>(p, acc, smem, h0, w0, img, n0, wr, wc, tid, bias0,
-                                                              bias1);
-  trace_stamp(p, 3);
-}
 
 // Output block (TH, TW) for a BM-pixel tile whose halo fits HR rows: fewest
 // tiles first, then the smallest halo (least re-read input).
@@ -748,28 +507,6 @@ hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int BN>
-hipError_t launch_halo_pp(const IGemmArgs& a0, hipStream_t s) {
-  using G = HP<BN>;
-  IGemmArgs a = a0;
-  a.epi_f32 = epi_f32_env();
-  if (!pick_block(a.Ho, a.Wo, G::BM, G::HR, a.TH, a.TW)) return hipErrorInvalidValue;
-  a.TI = pick_images(a, G::BM, G::HR);
-  const int nch = a.C / KT;
-  const int splits = a.splits > 1 ? a.splits : 1;
-  if (splits > 1 && a.kt_per_split <= 0) return hipErrorInvalidValue;
-  (void)nch;
-  const int nimg = a.M / (a.Ho * a.Wo);
-  const long tiles = long((nimg + a.TI - 1) / a.TI) * ((a.Ho + a.TH - 1) / a.TH) * ((a.Wo + a.TW - 1) / a.TW) *
-                     ((a.N + BN - 1) / BN);
-  if (tiles == 0) return hipSuccess;
-  if (tiles >= (1L << 31)) return hipErrorInvalidValue;
-  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&halo_pp_kernel<BN>), G::LDS);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((halo_pp_kernel<BN>), dim3(unsigned(tiles), splits), dim3(G::NT), G::LDS, s, a);
-  return hipGetLastError();
-}
-
 // per config index (halo_cfg_index)
 constexpr int kHBM[kNumHaloConfigs] = {256, 128, 128, 64, 256, 64, 64, 128, 256, 128, 128};
 constexpr int kHBN[kNumHaloConfigs] = {64, 128, 64, 64, 128, 128, 64, 64, 64, 64, 64};
@@ -786,14 +523,6 @@ int halo_cfg_index(int cfg) {
 long halo_tiles(const IGemmArgs& a0, int cfg) {
   IGemmArgs a = a0;
   a.epi_f32 = epi_f32_env();
-  if (cfg >= kHaloPpCfgBase && cfg < kHaloPpCfgBase + kNumHaloPpConfigs) {
-    const int bn = cfg == kHaloPpCfgBase ? 128 : 64;
-    if (!pick_block(a.Ho, a.Wo, 128, 192, a.TH, a.TW)) return 0;
-    const int nimg = a.M / (a.Ho * a.Wo);
-    const int ti = pick_images(a, 128, 192);
-    return long((nimg + ti - 1) / ti) * ((a.Ho + a.TH - 1) / a.TH) * ((a.Wo + a.TW - 1) / a.TW) *
-           ((a.N + bn - 1) / bn);
-  }
   const int c = halo_cfg_index(cfg);
   if (c < 0) return 0;
   if (!pick_block(a.Ho, a.Wo, kHBM[c], kHHR[c], a.TH, a.TW)) return 0;
@@ -810,15 +539,11 @@ bool halo_supported(const IGemmArgs& a) {
          a.M < (1 << 23) && int64_t(a.M / (a.Ho * a.Wo)) * a.H * a.W * a.C < (1LL << 30);
 }
 
-int halo_config_bm(int cfg) { return cfg >= kHaloPpCfgBase ? 128 : kHBM[halo_cfg_index(cfg)]; }
-int halo_config_bn(int cfg) {
-  return cfg >= kHaloPpCfgBase ? (cfg == kHaloPpCfgBase ? 128 : 64) : kHBN[halo_cfg_index(cfg)];
-}
+int halo_config_bm(int cfg) { return kHBM[halo_cfg_index(cfg)]; }
+int halo_config_bn(int cfg) { return kHBN[halo_cfg_index(cfg)]; }
 
 hipError_t halo_launch(const IGemmArgs& a, int cfg, hipStream_t s) {
   if (!halo_cfg_id(cfg) || !halo_supported(a)) return hipErrorInvalidValue;
-  if (cfg == kHaloPpCfgBase) return launch_halo_pp<128>(a, s);
-  if (cfg == kHaloPpCfgBase + 1) return launch_halo_pp<64>(a, s);
   if (cfg >= kHaloPfCfgBase) {
     switch (halo_cfg_index(cfg)) {   // the same tiles with the fragment-prefetch step pipeline
       case 0: return launch_halo_cfg<256, 64, 4, 1, 320, 3, true>(a, s);

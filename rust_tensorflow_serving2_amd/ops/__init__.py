@@ -171,10 +171,8 @@ HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 12
         55: (128, 64), 56: (256, 64), 57: (128, 64), 58: (128, 64)}
 # the same tiles with the fragment-prefetch step pipeline (halo.hip PF)
 HALO.update({cfg + 32: tile for cfg, tile in list(HALO.items()) if cfg != 52})
-# the ping-pong halo kernel (halo.hip halo_pp_kernel): 8 waves in two staggered groups
-HALO_PP = {144: (128, 128), 145: (128, 64)}
-HALO.update(HALO_PP)
-# TFSERVE_PINGPONG=0: leave the ping-pong builds (bgemm 140-142, halo 144/145) out of the
+# (ids 144/145, the ping-pong halo kernel, were removed in round 6: 0 picks)
+# TFSERVE_PINGPONG=0: leave the ping-pong builds (bgemm 140-142) out of the
 # tuner's candidates (A/B of the tile tables with and without them)
 PINGPONG = os.environ.get("TFSERVE_PINGPONG", "1") != "0"
 TILES.update(HALO)
@@ -205,8 +203,6 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
     if halo and aligned64 and K % 576 == 0 and N % 8 == 0:
         nch = K // 576
         for cfg, (bm, bn) in HALO.items():
-            if cfg in HALO_PP and not PINGPONG:
-                continue
             if bn > 64 and N <= bn // 2:
                 continue
             tiles = -(-M // bm) * -(-N // bn)

@@ -84,10 +84,8 @@ def main():
                     print(f"  {name} cfg {cfg} x{sp}: {str(e)[:80]}", flush=True)
         res.sort()
         flop = 2 * M * N * K
-        pp = [r for r in res if r[1] in (144, 145)]     # the ping-pong halo builds, reported apart
         print(json.dumps({"layer": name, "M": M, "N": N, "K": K, "sol_mfma_us": round(flop / 2.5e9, 2),
                           "best": [(round(t, 2), c, sp) for t, c, sp in res[:a.top]],
-                          "pingpong": [(round(t, 2), c, sp) for t, c, sp in pp[:3]],
                           "tflops": round(flop / res[0][0] / 1e6)}), flush=True)
 
 
