@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <map>
 #include <mutex>
 #include <thread>
 
@@ -149,6 +150,47 @@ double us_of(Clock::time_point t) {
   return std::chrono::duration<double, std::micro>(t.time_since_epoch()).count();
 }
 
+// Compute gate (TFSERVE_GPU_CONCURRENCY=K, 0 = off): at most K bucket graphs
+// of the lanes on one device run at once, while every lane's H2D copy still
+// goes out as soon as its batch closes.  Graph launch s makes its stream wait
+// (GPU side, hipStreamWaitEvent) for the event recorded right after graph
+// launch s - K, so no host thread blocks.  Why: ResNet-50 b32 computes a batch
+// in 0.536 ms with 3 replays in flight but 0.583 ms with 4
+// (scripts/probe_concurrency.py, profiles/round6/r6k/conc.log), while the
+// serving lanes need a fourth batch in flight to hide each batch's 175-us
+// input copy (3 lanes: 37k vs 53k RPC/s, round 5).  Launch order is a global
+// sequence taken under the gate's mutex together with the launch and the
+// record, so every wait names an event recorded by an earlier launch and the
+// dependencies are acyclic.  Measured neutral, so off by default: 2000-step
+// headline 54.1k (K = 3, 4 lanes) vs 53.0-53.8k (off) on one box; K = 2 50.1k;
+// K = 3 with 5 / 6 lanes 45.1k / 50.0k (profiles/round6/r6p/).
+struct ComputeGate {
+  std::mutex mu;
+  int cap = 0;
+  uint64_t seq = 0;
+  std::vector<void*> ring;    // cap + 16 events, reused round robin
+};
+ComputeGate* compute_gate(HipRt& rt, int device) {
+  static std::mutex mu;
+  static std::map<int, std::unique_ptr<ComputeGate>> gates;
+  static const int cap = [] {
+    const char* e = getenv("TFSERVE_GPU_CONCURRENCY");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  if (cap <= 0 || !rt.stream_wait_event) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  auto& slot = gates[device];
+  if (!slot) {
+    auto gate = std::make_unique<ComputeGate>();
+    gate->cap = cap;
+    gate->ring.assign(size_t(cap) + 16, nullptr);
+    for (auto& ev : gate->ring)
+      if (rt.event_create(&ev, kHipEventDisableTiming) != 0) return nullptr;
+    slot = std::move(gate);
+  }
+  return slot.get();
+}
+
 struct LaneCopy {
   uintptr_t dst, src;
   size_t row_bytes;
@@ -236,7 +278,16 @@ class NativeLane {
       if (rx.on()) rx.pop();
     }
     if (rx.on()) rx.push("tfs.graph_launch");
-    if (!e) e = rt.launch(b->exec, stream_);
+    if (gate_ && !e) {
+      std::lock_guard<std::mutex> g(gate_->mu);
+      const uint64_t sq = gate_->seq++;
+      const size_t R = gate_->ring.size();
+      if (sq >= uint64_t(gate_->cap)) e = rt.stream_wait_event(stream_, gate_->ring[(sq - gate_->cap) % R], 0);
+      if (!e) e = rt.launch(b->exec, stream_);
+      if (!e) e = rt.event_record(gate_->ring[sq % R], stream_);
+    } else if (!e) {
+      e = rt.launch(b->exec, stream_);
+    }
     if (rx.on()) rx.pop();
     for (auto& c : b->out)
       if (!e) e = rt.memcpy_async(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src),
@@ -311,6 +362,7 @@ class NativeLane {
     ema_us_.assign(buckets_.size(), 0.0);
     HipRt& rt = hip_rt();
     rt.set_device(device_);
+    gate_ = compute_gate(rt, device_);
     void* done = nullptr;
     if (rt.event_create(&done, kHipEventDisableTiming) != 0) done = nullptr;
     if (eager_ && (!rt.stream_create || !rt.stream_wait_event ||
@@ -387,6 +439,7 @@ class NativeLane {
   void* stream_;
   std::vector<LaneBucket> buckets_;
   bool eager_ = false;
+  ComputeGate* gate_ = nullptr;   // shared by the device's lanes (TFSERVE_GPU_CONCURRENCY)
   void* copy_stream_ = nullptr;
   void* copied_ = nullptr;
   int fault_every_ = 0;
