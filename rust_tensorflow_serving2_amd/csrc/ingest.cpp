@@ -7,6 +7,8 @@
 // one goes through the scalar path (one mask test per block otherwise).
 #include "ingest.h"
 
+#include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <immintrin.h>
 
@@ -27,9 +29,48 @@ void convert_scalar(uint16_t* dst, const uint8_t* src, size_t n) {
   }
 }
 
+// Rows of at least kNtMin values are written with non-temporal 64-B stores:
+// the pinned batch row is read next by the GPU's copy engine, never by this
+// core, so the read-for-ownership a normal store pays on each line is wasted
+// memory traffic (TFSERVE_INGEST_NT=0: plain stores).
+constexpr size_t kNtMin = 4096;
+const bool g_nt = [] {
+  const char* e = getenv("TFSERVE_INGEST_NT");
+  return !(e && std::atoi(e) == 0);
+}();
+
 __attribute__((target("avx512f,avx512bf16,avx512vl")))
 void convert_avx512(uint16_t* dst, const uint8_t* src, size_t n) {
   size_t i = 0;
+  const bool nt = g_nt && n >= kNtMin;
+  if (nt) {
+    // head: up to the first 64-B aligned output address
+    const size_t mis = (reinterpret_cast<uintptr_t>(dst) & 63) / 2;
+    const size_t head = (reinterpret_cast<uintptr_t>(dst) & 1) ? n : (mis ? 32 - mis : 0);
+    if (head >= n) {
+      convert_scalar(dst, src, n);
+      return;
+    }
+    if (head) convert_scalar(dst, src, head);
+    i = head;
+    const __m512i ex = _mm512_set1_epi32(0x7f800000), mt = _mm512_set1_epi32(0x007fffff);
+    for (; i + 32 <= n; i += 32) {
+      const __m512 a = _mm512_loadu_ps(reinterpret_cast<const float*>(src + 4 * i));
+      const __m512 b = _mm512_loadu_ps(reinterpret_cast<const float*>(src + 4 * i + 64));
+      const __m512i ia = _mm512_castps_si512(a), ib = _mm512_castps_si512(b);
+      const __mmask16 da = _mm512_mask_test_epi32_mask(_mm512_testn_epi32_mask(ia, ex), ia, mt);
+      const __mmask16 db = _mm512_mask_test_epi32_mask(_mm512_testn_epi32_mask(ib, ex), ib, mt);
+      if (__builtin_expect((da | db) != 0, 0)) {
+        convert_scalar(dst + i, src + 4 * i, 32);
+        continue;
+      }
+      const __m512bh r = _mm512_cvtne2ps_pbh(b, a);
+      _mm512_stream_si512(reinterpret_cast<__m512i*>(dst + i), reinterpret_cast<__m512i>(r));
+    }
+    if (i < n) convert_scalar(dst + i, src + 4 * i, n - i);
+    _mm_sfence();   // the row is handed to another thread / the copy engine next
+    return;
+  }
   for (; i + 32 <= n; i += 32) {
     const __m512 a = _mm512_loadu_ps(reinterpret_cast<const float*>(src + 4 * i));
     const __m512 b = _mm512_loadu_ps(reinterpret_cast<const float*>(src + 4 * i + 64));
