@@ -160,7 +160,9 @@ def parse():
     ap.add_argument("--pin-threads", action="store_true",
                     default=os.environ.get("TFSERVE_PIN_THREADS", "0") == "1",
                     help="after start-up, give each IO / load-generator / lane thread a physical core of "
-                         "its own among the rank's CPUs, least-busy cores first (default off)")
+                         "its own among the rank's CPUs, least-busy cores first (default off: with the CPUs "
+                         "narrowed to two LLC groups there are fewer cores than hot threads, and pinned runs "
+                         "measured 45-53k vs 54-56k RPC/s, profiles/round6/r6s/)")
     ap.add_argument("--llc-groups", type=int, default=None,
                     help="narrow the rank's CPUs to its N least-busy last-level-cache groups (CCDs) "
                          "before pinning (0 = the whole NUMA-node share; default 2, 0 for --model multi; "
