@@ -963,6 +963,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (int c = 0; c < tfsk::kNumHaloConfigs; ++c) v.push_back(tfsk::kHaloCfgBase + c);
     for (int c = 0; c < tfsk::kNumHaloConfigs; ++c)
       if (tfsk::halo_cfg_id(tfsk::kHaloPfCfgBase + c)) v.push_back(tfsk::kHaloPfCfgBase + c);
+    v.push_back(tfsk::kHaloPersistCfg);
     return v;
   });
   m.def("config_tile", [](int cfg) {

@@ -62,8 +62,11 @@ constexpr int kHaloPfCfgBase = 80;
 // the PF build of tile 4 (256x128, 8 waves) does not fit the register budget
 // and is not instantiated: id 84 is not a config
 constexpr int kHaloPfMissing = 4;
+// the persistent halo kernel (halo.hip halo_persist_kernel): 128 pixels x 64
+// channels, C == 64 only, the whole filter resident in LDS
+constexpr int kHaloPersistCfg = 146;
 inline bool halo_cfg_id(int cfg) {
-  return (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) ||
+  return (cfg >= kHaloCfgBase && cfg < kHaloCfgBase + kNumHaloConfigs) || cfg == kHaloPersistCfg ||
          (cfg >= kHaloPfCfgBase && cfg < kHaloPfCfgBase + kNumHaloConfigs && cfg != kHaloPfCfgBase + kHaloPfMissing);
 }
 bool halo_supported(const IGemmArgs& a);

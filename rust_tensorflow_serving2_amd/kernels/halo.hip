@@ -442,6 +442,222 @@ __global__ __launch_bounds__(64 * WGM * WGN) void halo_conv_kernel(IGemmArgs p) 
   trace_stamp(p, 3);
 }
 
+// ---------------------------------------------------------------- persistent halo conv
+// halo_persist_kernel (id kHaloPersistCfg): the 3x3 layers whose whole filter
+// fits in LDS -- one 64-channel input chunk and 64 output channels (ResNet-50
+// stage 1, 56x56x64 -> 64: 9 taps x 64 x 64 bf16 = 72 KB).  halo_conv_kernel
+// runs them as ~1.75 waves of workgroups that all wait for their first halo at
+// once, compute, then all store at once: 17-18 us at b32 for 7.4 GFLOP
+// (profiles/round6/r6n/replay_r50_b32.txt), the halo latency and the store
+// tail exposed in every workgroup.  Here one workgroup per CU:
+//   * the 9 taps' weights are DMA'd ONCE into 9 resident slots (the image of
+//     halo_conv_kernel's B ring), so the K loop of a tile has no barrier;
+//   * the workgroup walks its tiles (tile = blockIdx.x + k * gridDim.x) with
+//     two halo buffers: tile k+1's halo goes out right after tile k's opening
+//     barrier and lands while tile k computes;
+//   * epilogue: bias + act in registers, the bf16 tile staged in its own LDS
+//     region, 16-B buffer stores -- unconditional (rows past the output go to
+//     an out-of-range offset and are dropped), so each lane has exactly
+//     kStores stores in flight and the next tile's opening wait is the counted
+//     vmcnt(kStores): the stores drain while the next tile computes;
+//   * raw s_barrier (lds_barrier) only: a __syncthreads() would drain vmcnt.
+// Plain bf16 output only (bias, act != erf; no residual / second output /
+// split): the launcher rejects the rest, which the tuner skips.
+constexpr int kPersistBM = 128, kPersistBN = 64, kPersistHR = 192;
+struct HPs {
+  static constexpr int BM = kPersistBM, BN = kPersistBN, HR = kPersistHR;
+  static constexpr int WGM = 4, WGN = 2, NW = 8, NT = 512;
+  static constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+  static constexpr int HPW = HR / (8 * NW), BPW = BN / (8 * NW);
+  static constexpr int B_B = BN * 128, HALO_B = HR * 128;
+  static constexpr int CB_LD = BN + 8;
+  static constexpr int STG_B = BM * CB_LD * 2;
+  static constexpr int OFF_HALO = 9 * B_B, OFF_STG = OFF_HALO + 2 * HALO_B;
+  static constexpr int LDS = OFF_STG + STG_B;
+  static constexpr int kStores = BM * (BN / 8) / NT;     // 16-B stores per thread per tile
+  static_assert(HPW * 8 * NW == HR && BPW == 1 && kStores * NT == BM * (BN / 8), "persistent halo split");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+__global__ __launch_bounds__(512, 1) void halo_persist_kernel(IGemmArgs p, int ntiles) {
+  using G = HPs;
+  constexpr int BM = G::BM, BN = G::BN;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  char* const smem = reinterpret_cast<char*>(smem_raw);
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+  const int TH = p.TH, TW = p.TW, HW2 = TW + 2;
+  const int Ho = p.Ho, Wo = p.Wo, H = p.H, W = p.W, C = p.C;
+  const int tph = (Ho + TH - 1) / TH, tpw = (Wo + TW - 1) / TW;
+  const int TI = p.TI > 1 ? p.TI : 1, nimg = p.M / (Ho * Wo);
+  const int HB = (TH + 2) * HW2, hrows = TI * HB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / G::WGN, wn = wid % G::WGN;
+  const int prow = lane >> 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.a), 0, int(p.a_bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.b), 0, int(p.b_bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsO =
+      __builtin_amdgcn_make_buffer_rsrc(p.out, 0, int(long(p.M) * p.ldc * 2), 0x00020000);
+  const bool use_b = p.bias != nullptr;
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.bias), 0, use_b ? BN * 4 : 0, 0x00020000);
+
+  // bias first (a VGPR-destination load: issued and used before any DMA, so
+  // no wait on it lands inside the DMA pipeline)
+  float bj[G::TN];
+#pragma unroll
+  for (int j = 0; j < G::TN; ++j)
+    bj[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsb, uint32_t(wn * G::WN + j * 16 + fr) * 4u, 0, 0));
+  const float alpha = p.alpha;
+  gemm::wait_vmcnt<0>();
+
+  // ---- the filter: 9 resident slots, slot u = tap u (k = u * C + channel), rows n swizzled by n & 7
+  {
+    const uint32_t kc = uint32_t(((lane & 7) ^ prow) * 8);
+    const int n = wid * 8 + prow;
+    const uint32_t boff = (uint32_t(n) * uint32_t(p.ldb) + kc) * 2u;
+#pragma unroll
+    for (int u = 0; u < 9; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_ptr_t)(smem + u * G::B_B + wid * 1024), 16, boff,
+                                               uint32_t(u * C) * 2u, 0, 0);
+  }
+  // ---- halo DMA of tile t into buffer b (halo_key swizzle, as halo_conv_kernel)
+  const float inv_hw2 = 1.f / float(HW2), inv_hb = 1.f / float(HB);
+  auto issue_halo = [&](int t, int b) {
+    int r_ = t;
+    const int tw = r_ % tpw;
+    r_ /= tpw;
+    const int th = r_ % tph;
+    const int img = (r_ / tph) * TI;
+    const int h0 = th * TH, w0 = tw * TW;
+    char* dst = smem + G::OFF_HALO + b * G::HALO_B;
+#pragma unroll
+    for (int j = 0; j < G::HPW; ++j) {
+      const int r = (wid * G::HPW + j) * 8 + prow;
+      const int ii = TI > 1 ? fdiv(r, HB, inv_hb) : 0;
+      const int q = r - ii * HB;
+      const int rr = fdiv(q, HW2, inv_hw2);
+      const int hh = h0 - p.PT + rr, ww = w0 - p.PL + (q - rr * HW2);
+      const bool ok = r < hrows && img + ii < nimg && unsigned(hh) < unsigned(H) && unsigned(ww) < unsigned(W);
+      const uint32_t kh = uint32_t(((lane & 7) ^ halo_key(ii * TH * TW + rr * TW + (q - rr * HW2))) * 8);
+      const uint32_t off = ok ? (uint32_t(((img + ii) * H + hh) * W + ww) * uint32_t(C) + kh) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(dst + (wid * G::HPW + j) * 1024), 16, off, 0, 0, 0);
+    }
+  };
+
+  // ---- consumer fragment rows (tile-invariant): output pixel -> halo row, swizzle key
+  int hrow0[G::TM], kpx0[G::TM];
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i) {
+    const int px = wm * G::WM + i * 16 + fr;
+    const int ii = px / (TH * TW), p2 = px - ii * (TH * TW);
+    const int ph = p2 / TW;
+    hrow0[i] = px < TI * TH * TW ? ii * HB + ph * HW2 + (p2 - ph * TW) : 0;
+    kpx0[i] = px;
+  }
+  const uint32_t rb0 = uint32_t(((wn * G::WN + fr) * KT + ((fq ^ (fr & 7)) * 8)) * 2);
+  const uint32_t rb1 = uint32_t(((wn * G::WN + fr) * KT + (((4 + fq) ^ (fr & 7)) * 8)) * 2);
+  // epilogue store rows of this thread (tile-invariant): chunk c = tid + it * NT
+  constexpr int CPRB = BN / 8;
+  uint16_t* const Cb = reinterpret_cast<uint16_t*>(smem + G::OFF_STG);
+
+  int t = blockIdx.x;
+  if (t < ntiles) issue_halo(t, 0);
+  for (int k = 0; t < ntiles; t += gridDim.x, ++k) {
+    const int b = k & 1;
+    // tile t's halo (and, on the first tile, the filter) landed; the previous
+    // tile's kStores stores stay in flight
+    if (k == 0) gemm::wait_vmcnt<0>();
+    else gemm::wait_vmcnt<G::kStores>();
+    gemm::lds_barrier();   // every wave's DMAs landed; halo buffer b^1 and the staging tile are read-free
+    const int tn = t + gridDim.x;
+    if (tn < ntiles) issue_halo(tn, b ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+
+    f32x4 acc[G::TM][G::TN];
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* hb = smem + G::OFF_HALO + b * G::HALO_B;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      const int tap_off = (u / 3) * HW2 + (u % 3), tap_key = (u / 3) * TW + (u % 3);
+      const char* sb = smem + u * G::B_B;
+      bf16x8 fa[2][G::TM], fb[2][G::TN];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < G::TM; ++i) {
+          const int hr = hrow0[i] + tap_off;
+          const uint32_t addr = uint32_t(hr) * 128u + ((uint32_t((kk * 4 + fq) ^ halo_key(kpx0[i] + tap_key))) << 4);
+          fa[kk][i] = *reinterpret_cast<const bf16x8*>(hb + addr);
+        }
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j)
+          fb[kk][j] = *reinterpret_cast<const bf16x8*>(sb + (kk ? rb1 : rb0) + j * 16 * KT * 2);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < G::TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+    }
+
+    // ---- epilogue: bias + act -> bf16 staging -> 16-B buffer stores
+    auto stage = [&](auto act_tag) __attribute__((always_inline)) {
+      constexpr int ACT = decltype(act_tag)::value;
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = act_fn<ACT>(acc[i][j][r] * alpha + bj[j] + 0.f);
+            Cb[(wm * G::WM + i * 16 + fq * 4 + r) * G::CB_LD + wn * G::WN + j * 16 + fr] =
+                __builtin_bit_cast(uint16_t, static_cast<__bf16>(v));
+          }
+    };
+    switch (p.act) {
+      case kActRelu: stage(std::integral_constant<int, kActRelu>{}); break;
+      case kActGeluTanh: stage(std::integral_constant<int, kActGeluTanh>{}); break;
+      case kActTanh: stage(std::integral_constant<int, kActTanh>{}); break;
+      default: stage(std::integral_constant<int, kActNone>{}); break;
+    }
+    gemm::lds_barrier();
+    {
+      int r_ = t;
+      const int tw = r_ % tpw;
+      r_ /= tpw;
+      const int th = r_ % tph;
+      const int img = (r_ / tph) * TI;
+      const int h0 = th * TH, w0 = tw * TW;
+#pragma unroll
+      for (int it = 0; it < G::kStores; ++it) {
+        const int c = tid + it * G::NT, row = c / CPRB, ch = c - row * CPRB;
+        int m = -1;
+        if (row < TI * TH * TW) {
+          const int ii = row / (TH * TW), r2 = row - ii * (TH * TW);
+          const int ph = r2 / TW, pw = r2 - ph * TW;
+          const int h = h0 + ph, w = w0 + pw;
+          if (h < Ho && w < Wo && img + ii < nimg) m = ((img + ii) * Ho + h) * Wo + w;
+        }
+        const uint32_t off = m >= 0 ? (uint32_t(m) * uint32_t(p.ldc) + uint32_t(ch * 8)) * 2u : kOOB;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(Cb + row * G::CB_LD + ch * 8);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsO, off, 0, 0);
+      }
+    }
+  }
+  gemm::wait_vmcnt<0>();
+}
+
 // (the ping-pong halo kernel, ids 144/145, was removed in round 6: 0 picks in
 // the round-6 tile tables, slower than halo_conv_kernel on every ResNet-50
 // 3x3 layer -- profiles/round6/r6f/conv.log; it stays in git history)
@@ -507,6 +723,36 @@ hipError_t launch_halo_cfg(const IGemmArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
+hipError_t launch_halo_persist(const IGemmArgs& a0, hipStream_t s) {
+  using G = HPs;
+  IGemmArgs a = a0;
+  // the configuration it is built for: one 64-channel chunk, 64 output
+  // channels, plain bf16 output (see halo_persist_kernel)
+  if (a.C != KT || a.N != G::BN || a.splits > 1 || a.residual != nullptr || a.out2 != nullptr || a.out_f32 ||
+      a.out == nullptr || a.act == kActGeluErf || epi_f32_env() || a.counters != nullptr || a.ldc % 8)
+    return hipErrorInvalidValue;
+  if (long(a.M) * a.ldc * 2 >= 0x7fffffffL) return hipErrorInvalidValue;
+  if (!pick_block(a.Ho, a.Wo, G::BM, G::HR, a.TH, a.TW)) return hipErrorInvalidValue;
+  a.TI = pick_images(a, G::BM, G::HR);
+  const int nimg = a.M / (a.Ho * a.Wo);
+  const long tiles = long((nimg + a.TI - 1) / a.TI) * ((a.Ho + a.TH - 1) / a.TH) * ((a.Wo + a.TW - 1) / a.TW);
+  if (tiles == 0) return hipSuccess;
+  if (tiles >= (1L << 30)) return hipErrorInvalidValue;
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
+  }
+  const int grid = int(tiles < cus ? tiles : cus);
+  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&halo_persist_kernel), G::LDS);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(halo_persist_kernel, dim3(unsigned(grid)), dim3(G::NT), G::LDS, s, a, int(tiles));
+  return hipGetLastError();
+}
+
 // per config index (halo_cfg_index)
 constexpr int kHBM[kNumHaloConfigs] = {256, 128, 128, 64, 256, 64, 64, 128, 256, 128, 128};
 constexpr int kHBN[kNumHaloConfigs] = {64, 128, 64, 64, 128, 128, 64, 64, 64, 64, 64};
@@ -523,6 +769,7 @@ int halo_cfg_index(int cfg) {
 long halo_tiles(const IGemmArgs& a0, int cfg) {
   IGemmArgs a = a0;
   a.epi_f32 = epi_f32_env();
+  if (cfg == kHaloPersistCfg) return 0;   // no split-K (no fixup counters)
   const int c = halo_cfg_index(cfg);
   if (c < 0) return 0;
   if (!pick_block(a.Ho, a.Wo, kHBM[c], kHHR[c], a.TH, a.TW)) return 0;
@@ -539,11 +786,12 @@ bool halo_supported(const IGemmArgs& a) {
          a.M < (1 << 23) && int64_t(a.M / (a.Ho * a.Wo)) * a.H * a.W * a.C < (1LL << 30);
 }
 
-int halo_config_bm(int cfg) { return kHBM[halo_cfg_index(cfg)]; }
-int halo_config_bn(int cfg) { return kHBN[halo_cfg_index(cfg)]; }
+int halo_config_bm(int cfg) { return cfg == kHaloPersistCfg ? kPersistBM : kHBM[halo_cfg_index(cfg)]; }
+int halo_config_bn(int cfg) { return cfg == kHaloPersistCfg ? kPersistBN : kHBN[halo_cfg_index(cfg)]; }
 
 hipError_t halo_launch(const IGemmArgs& a, int cfg, hipStream_t s) {
   if (!halo_cfg_id(cfg) || !halo_supported(a)) return hipErrorInvalidValue;
+  if (cfg == kHaloPersistCfg) return launch_halo_persist(a, s);
   if (cfg >= kHaloPfCfgBase) {
     switch (halo_cfg_index(cfg)) {   // the same tiles with the fragment-prefetch step pipeline
       case 0: return launch_halo_cfg<256, 64, 4, 1, 320, 3, true>(a, s);

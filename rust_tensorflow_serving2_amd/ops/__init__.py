@@ -172,6 +172,10 @@ HALO = {48: (256, 64), 49: (128, 128), 50: (128, 64), 51: (64, 64), 52: (256, 12
 # the same tiles with the fragment-prefetch step pipeline (halo.hip PF)
 HALO.update({cfg + 32: tile for cfg, tile in list(HALO.items()) if cfg != 52})
 # (ids 144/145, the ping-pong halo kernel, were removed in round 6: 0 picks)
+# the persistent halo kernel (halo.hip halo_persist_kernel): C == 64 and N == 64, the whole
+# filter resident in LDS, plain bf16 output; other operand modes are rejected at launch
+HALO_PERSIST = 146
+HALO[HALO_PERSIST] = (128, 64)
 # TFSERVE_PINGPONG=0: leave the ping-pong builds (bgemm 140-142) out of the
 # tuner's candidates (A/B of the tile tables with and without them)
 PINGPONG = os.environ.get("TFSERVE_PINGPONG", "1") != "0"
@@ -204,6 +208,10 @@ def candidates(M: int, N: int, K: int, dma: bool = True, aligned64: bool = False
         nch = K // 576
         for cfg, (bm, bn) in HALO.items():
             if bn > 64 and N <= bn // 2:
+                continue
+            if cfg == HALO_PERSIST:
+                if K == 576 and N == 64:
+                    out.append((cfg, 1))     # one chunk, no split-K
                 continue
             tiles = -(-M // bm) * -(-N // bn)
             for s in (1, 2, 4, 8):

@@ -141,6 +141,43 @@ def test_halo_conv_matches_fp32(shape, cfg):
         assert err < 3e-2 * max(1.0, ref.abs().max().item()), (splits, err)
 
 
+@pytest.mark.parametrize("shape", [
+    (32, 56, 56, (1, 1, 1, 1)),      # ResNet-50 stage 1 at b32: 896 tiles, 3-4 per workgroup
+    (3, 56, 56, (1, 1, 1, 1)),       # fewer tiles than CUs
+    (5, 7, 7, (1, 1, 1, 1)),         # whole-image tiles (several images per tile, last tile partial)
+    (2, 13, 17, (0, 2, 1, 1)),       # odd image, asymmetric pads
+])
+@pytest.mark.parametrize("act", ["relu", "none"])
+def test_halo_persist_matches_fp32(shape, act):
+    """Persistent halo conv (config 146: the 64 x 64 x 3 x 3 filter resident in
+    LDS, each workgroup walking several tiles with double-buffered halos and its
+    stores draining under the next tile) vs fp32; it takes the plain bf16
+    output only and rejects residual / other channel counts."""
+    n, h, w, pads = shape
+    x = rnd(n, h, w, 64, seed=21).to(BF)
+    wt = rnd(3, 3, 64, 64, scale=1 / math.sqrt(9 * 64), seed=22).to(BF).float()
+    b = rnd(64, scale=0.1, seed=23)
+    ho, wo = h + pads[0] + pads[1] - 2, w + pads[2] + pads[3] - 2
+    ref = ref_conv(x, wt, b, 1, pads, None, act)
+    y = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), None, 3, 3, 1, 1, *pads, act=ACT[act], cfg=146)
+    y2 = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), None, 3, 3, 1, 1, *pads, act=ACT[act], cfg=146)
+    torch.cuda.synchronize()
+    assert y.shape == (n, ho, wo, 64)
+    assert (y.float().cpu() - ref).abs().max().item() < 3e-2 * max(1.0, ref.abs().max().item())
+    assert torch.equal(y, y2)
+    res = rnd(n, ho, wo, 64, seed=24).to(BF)
+    with pytest.raises(RuntimeError):
+        hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), res.to(DEV), 3, 3, 1, 1, *pads, act=ACT[act], cfg=146)
+    # a split request over the single 64-channel chunk runs unsplit (the binding clamps it)
+    y3 = hip().conv2d(x.to(DEV), pack_w(wt), b.to(DEV), None, 3, 3, 1, 1, *pads, act=ACT[act], cfg=146, splits=2)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y3)
+    x2 = rnd(1, 8, 8, 128, seed=25).to(BF)
+    w2 = rnd(3, 3, 128, 64, scale=0.03, seed=26).to(BF).float()
+    with pytest.raises(RuntimeError):
+        hip().conv2d(x2.to(DEV), pack_w(w2), b.to(DEV), None, 3, 3, 1, 1, 1, 1, 1, 1, act=ACT[act], cfg=146)
+
+
 def test_halo_exact_identity_taps():
     """Integer-valued operands (exact in bf16 and fp32): every output pixel of
     every tile position, tap and channel chunk must match bit for bit — catches
