@@ -585,31 +585,45 @@ __global__ __launch_bounds__(512, 1) void halo_persist_kernel(IGemmArgs p, int n
 #pragma unroll
       for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const char* hb = smem + G::OFF_HALO + b * G::HALO_B;
-#pragma unroll
-    for (int u = 0; u < 9; ++u) {
+    // the nine taps, software-pipelined: tap u + 1's fragment reads are issued
+    // ahead of tap u's MFMAs (pinned by sched_barrier), so the LDS latency of a
+    // tap runs under the previous tap's matrix work
+    struct TapFrags {
+      bf16x8 a[2][G::TM], b[2][G::TN];
+    };
+    auto load_tap = [&](TapFrags& f, int u) __attribute__((always_inline)) {
       const int tap_off = (u / 3) * HW2 + (u % 3), tap_key = (u / 3) * TW + (u % 3);
       const char* sb = smem + u * G::B_B;
-      bf16x8 fa[2][G::TM], fb[2][G::TN];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
         for (int i = 0; i < G::TM; ++i) {
           const int hr = hrow0[i] + tap_off;
           const uint32_t addr = uint32_t(hr) * 128u + ((uint32_t((kk * 4 + fq) ^ halo_key(kpx0[i] + tap_key))) << 4);
-          fa[kk][i] = *reinterpret_cast<const bf16x8*>(hb + addr);
+          f.a[kk][i] = *reinterpret_cast<const bf16x8*>(hb + addr);
         }
 #pragma unroll
         for (int j = 0; j < G::TN; ++j)
-          fb[kk][j] = *reinterpret_cast<const bf16x8*>(sb + (kk ? rb1 : rb0) + j * 16 * KT * 2);
+          f.b[kk][j] = *reinterpret_cast<const bf16x8*>(sb + (kk ? rb1 : rb0) + j * 16 * KT * 2);
       }
+    };
+    TapFrags fr2[2];
+    load_tap(fr2[0], 0);
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (u < 8) load_tap(fr2[(u + 1) & 1], u + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const TapFrags& f = fr2[u & 1];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int i = 0; i < G::TM; ++i)
 #pragma unroll
           for (int j = 0; j < G::TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[kk][i], f.b[kk][j], acc[i][j], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
 
     // ---- epilogue: bias + act -> bf16 staging -> 16-B buffer stores
     auto stage = [&](auto act_tag) __attribute__((always_inline)) {
