@@ -76,34 +76,49 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   const int qb = bid % qblocks;
   const int h = (bid / qblocks) % H;
   const int b = bid / (qblocks * H);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
   const long row_stride = 3L * H * D;
   const uint16_t* base = qkv + long(b) * S * row_stride;
 
+  // ---- K rows and the key mask by LDS-DMA: each wave instruction lands 1 KB
+  // (8 keys x 128 B) with lane l at chunk l & 7 of key row l >> 3, so lane l
+  // fetches chunk (l & 7) ^ (key & 7) -- the XOR-swizzled row.  (Loads into
+  // registers were sunk by the compiler to their LDS stores, one serial round
+  // trip per chunk, and the mask's behind them.)
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  constexpr int NW = NTH / 64;
+  const __amdgpu_buffer_rsrc_t rsQ =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, int(S * row_stride * 2), 0x00020000);
+  static_assert((S / 8) % NW == 0, "K staging split");
+  constexpr int KDMA = S / 8 / NW;
+#pragma unroll
+  for (int i = 0; i < KDMA; ++i) {
+    const int pc = wid + i * NW, key = pc * 8 + (lane >> 3);
+    const uint32_t src = uint32_t(long(key) * row_stride + H * D + h * D + (((lane & 7) ^ (key & 7)) * 8)) * 2u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsQ, (lds_ptr_t)(Ks + pc * 512), 16, src, 0, 0, 0);
+  }
+  // the [B,1,1,S] key mask (BERT's adder, mask_qstride == 0); a 0-record
+  // descriptor (zeros) when the mask is per query row or absent.  Lanes past
+  // S / 4 land zeros in the region's padding.
+  const bool key_mask = mask_bias != nullptr && mask_qstride == 0;
+  const __amdgpu_buffer_rsrc_t rsM = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(key_mask ? mask_bias + long(b) * mask_bstride : mask_bias), 0, key_mask ? S * 4 : 0,
+      0x00020000);
+  static_assert(S * 4 <= 1024, "mask staging");
+  if (wid == 0)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsM, (lds_ptr_t)Ms, 16, lane * 16 < S * 4 ? uint32_t(lane * 16) : gemm::kOOB,
+                                             0, 0, 0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
   // ---- Q fragments (the B operand of K Q^T: column = query fr, k = d)
   const int q0 = qb * QB + wid * 16;
   bf16x8 qf[2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
-    qf[kk] = *reinterpret_cast<const bf16x8*>(base + long(q0 + fr) * row_stride + h * D + kk * 32 + fq * 8);
-  static_assert((S * 8) % NTH == 0 && S <= NTH, "staging split");
-  constexpr int KIT = S * 8 / NTH;
-  uint4 kv[KIT];
-#pragma unroll
-  for (int i = 0; i < KIT; ++i) {
-    const int c = tid + i * NTH, key = c >> 3, ch = c & 7;
-    kv[i] = *reinterpret_cast<const uint4*>(base + long(key) * row_stride + H * D + h * D + ch * 8);
-  }
-  // the [B,1,1,S] key mask (BERT's adder, mask_qstride == 0): 4 keys per
-  // thread into LDS; a 0-record descriptor (zeros) when the mask is per query
-  // row or absent
-  const bool key_mask = mask_bias != nullptr && mask_qstride == 0;
-  const __amdgpu_buffer_rsrc_t rsM = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(key_mask ? mask_bias + long(b) * mask_bstride : mask_bias), 0, key_mask ? S * 4 : 0,
-      0x00020000);
-  const u32x4 mk = __builtin_amdgcn_raw_buffer_load_b128(rsM, uint32_t(tid < S / 4 ? tid : 0) * 16u, 0, 0);
-  __builtin_amdgcn_sched_barrier(0);
+    qf[kk] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rsQ, uint32_t(long(q0 + fr) * row_stride + h * D + kk * 32 + fq * 8) * 2u, 0, 0));
+  static_assert(S <= NTH, "V staging split");
   // V: an 8-key x 8-dim block per thread (threads >= S load a clamped
   // in-range block whose stores land in the rows' padding), issued now,
   // consumed after the softmax
@@ -112,17 +127,14 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   uint32_t w[8][4];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const uint4 v = *reinterpret_cast<const uint4*>(base + long(kg * 8 + k) * row_stride + 2 * H * D + h * D +
-                                                    vch * 8);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+        rsQ, uint32_t(long(kg * 8 + k) * row_stride + 2 * H * D + h * D + vch * 8) * 2u, 0, 0);
     w[k][0] = v.x; w[k][1] = v.y; w[k][2] = v.z; w[k][3] = v.w;
   }
+  asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < KIT; ++i) {
-    const int c = tid + i * NTH, key = c >> 3, ch = c & 7;
-    *reinterpret_cast<uint4*>(Ks + key * D + ((ch ^ (key & 7)) * 8)) = kv[i];
-  }
-  if (tid < S / 4) *reinterpret_cast<u32x4*>(Ms + tid * 4) = mk;
+  // K, the mask and Q landed (in order: only the 8 V loads may be younger)
+  gemm::wait_vmcnt<8>();
   __syncthreads();
   attn_stamp(trace, trace_cap, 1);          // Q / K / mask staged (V in flight)
 
@@ -175,7 +187,7 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
     for (int j = 0; j < 8; ++j) {
       const float e = __expf(s[2 * ks + (j >> 2)][j & 3] - mx);
       sum += e;
-      pb[ks][j] = __builtin_bit_cast(__bf16, f32_to_bf16(e));
+      pb[ks][j] = static_cast<__bf16>(e);
     }
   }
   sum += __shfl_xor(sum, 16, 64);
@@ -201,16 +213,29 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   f32x4 o[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < S / 32; ++ks) {
+  // the V^T fragments read two 32-key steps ahead of their MFMAs (the
+  // compiler's own order left an LDS round trip in front of every MFMA;
+  // sched_barriers pin this one)
+  constexpr int KS = S / 32;
+  bf16x8 va[KS][4];
+  auto read_v = [&](int ks) {
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const uint16_t* vr = Vt + (dt * 16 + fr) * VT_LD + ks * 32 + fq * 4;
       const uint2 lo = *reinterpret_cast<const uint2*>(vr);
       const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
-      const bf16x8 va = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb[ks], o[dt], 0, 0, 0);
+      va[ks][dt] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
     }
+  };
+  read_v(0);
+  if (KS > 1) read_v(1);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (ks + 2 < KS) read_v(ks + 2);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[ks][dt], pb[ks], o[dt], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
   attn_stamp(trace, trace_cap, 3);          // P V done (wave 0)
   // ---- normalise; lane holds dims dt*16 + 4fq + [0, 4) of query q0 + fr.
@@ -223,8 +248,8 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   uint16_t* os = Ks + wid * 16 * D;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    const uint32_t lo = uint32_t(f32_to_bf16(o[dt][0] * inv)) | (uint32_t(f32_to_bf16(o[dt][1] * inv)) << 16);
-    const uint32_t hi = uint32_t(f32_to_bf16(o[dt][2] * inv)) | (uint32_t(f32_to_bf16(o[dt][3] * inv)) << 16);
+    const uint32_t lo = gemm::pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv);
+    const uint32_t hi = gemm::pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv);
     const int chunk = dt * 2 + (fq >> 1);
     *reinterpret_cast<uint2*>(os + fr * D + ((chunk ^ (fr & 7)) * 8) + (fq & 1) * 4) = make_uint2(lo, hi);
   }
@@ -634,7 +659,7 @@ hipError_t launch_s(const uint16_t* qkv, const float* mb, uint16_t* ctx, int B, 
                        qs, g_attn_trace, g_attn_trace_cap);
     return hipGetLastError();
   }
-  constexpr int lds = (S * D + D * (S + 8)) * 2 + S * 4;
+  constexpr int lds = (S * D + D * (S + 8)) * 2 + 1024;          // + the key mask's 1-KB DMA image
   static_assert(lds <= 160 * 1024, "attention tile");
   hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&attention_kernel<S, QB>), lds);
   if (e != hipSuccess) return e;
