@@ -79,9 +79,22 @@ __device__ __forceinline__ uint32_t okey(uint32_t u) {
   const s16x2 v = __builtin_bit_cast(s16x2, u);
   return __builtin_bit_cast(uint32_t, v ^ ((v >> 15) & (s16x2){0x7fff, 0x7fff}));
 }
+// key pair of two bf16 -inf (0xff80): what conv pixels outside the output hold
+constexpr uint32_t kNegInfKey2 = 0x807f807fu;
 __device__ __forceinline__ uint32_t kmax(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, a),
                                                                 __builtin_bit_cast(s16x2, b)));
+}
+
+// s_waitcnt vmcnt(N) only (gfx9 encoding: expcnt / lgkmcnt at their maxima)
+template <int N>
+__device__ __forceinline__ void stem_wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+__device__ __forceinline__ u32x4 make_u32x4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  u32x4 v;
+  v.x = a; v.y = b; v.z = c; v.w = d;
+  return v;
 }
 
 template <int NCG, bool XB16>
@@ -100,19 +113,6 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
   const int t_begin = int(long(wg) * p.tiles / gridDim.x);
   const int t_end = int(long(wg + 1) * p.tiles / gridDim.x);
   if (t_begin >= t_end) return;
-
-  // ---- weights (MFMA A operand: rows = output channels) and bias in registers
-  // for the whole run.  C = W x patch^T, so a lane's accumulator holds 4
-  // CONSECUTIVE channels of one conv pixel: one packed 8-B LDS store each.
-  bf16x8 wf[kKSteps][NCG];
-  float4 bias[NCG];
-#pragma unroll
-  for (int j = 0; j < NCG; ++j) {
-    const uint16_t* wr = p.w + long(j * 16 + fr) * p.ldw + fq * 8;
-#pragma unroll
-    for (int kh = 0; kh < kKSteps; ++kh) wf[kh][j] = *reinterpret_cast<const bf16x8*>(wr + kh * 32);
-    bias[j] = *reinterpret_cast<const float4*>(p.bias + j * 16 + fq * 4);
-  }
 
   // ---- this lane's conv pixel in each of the wave's row groups (B operand
   // columns); pixels past 153 clamp their reads and store to scratch rows
@@ -182,10 +182,47 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
   // ablations (timing only, results are garbage): bit 0 skips the patch
   // loads, bit 1 the MFMAs, bit 2 the pool phase, bit 3 the conv-tile stores
   const int dbg = p.dbg;
+  // the conv activation's floor as a packed key pair (ReLU: +0 -> key 0;
+  // none: -inf -> the smallest key, a no-op under the max)
+  const uint32_t lokey = okey(cvt2(p.lo, p.lo));
+  // pooled-tile stores: with COUT = 64 every thread stores exactly SPT 16-B
+  // items per tile (out-of-range items to an out-of-range offset: dropped), so
+  // the next tile's patch wait is an exact vmcnt(SPT) -- the stores stay in
+  // flight.  (vmcnt counts stores too on gfx950: the plain vmcnt(0) there
+  // waited for the previous tile's write acknowledgements every tile.)
+  constexpr int C8 = COUT / 8;
+  constexpr int kItems = kTPY * kTPX * C8;
+  constexpr bool kExactStores = kItems % 256 == 0;
+  constexpr int SPT = kItems / 256;
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
+      p.y, 0, int(long(p.N) * p.Hp * p.Wp * COUT * 2), 0x00020000);
   if (!(dbg & 1)) load_patch(t_begin);
+  // ---- weights (MFMA A operand: rows = output channels) and bias in registers
+  // for the whole run.  C = W x patch^T, so a lane's accumulator holds 4
+  // CONSECUTIVE channels of one conv pixel: one packed 8-B LDS store each.
+  bf16x8 wf[kKSteps][NCG];
+  float4 bias[NCG];
+#pragma unroll
+  for (int j = 0; j < NCG; ++j) {
+    const uint16_t* wr = p.w + long(j * 16 + fr) * p.ldw + fq * 8;
+#pragma unroll
+    for (int kh = 0; kh < kKSteps; ++kh) wf[kh][j] = *reinterpret_cast<const bf16x8*>(wr + kh * 32);
+    bias[j] = *reinterpret_cast<const float4*>(p.bias + j * 16 + fq * 4);
+  }
+
+  // the weights, the bias and the first patch, one round trip; the explicit
+  // wait also tells the compiler's wait-count pass that the weight / bias
+  // registers are complete.  (Without it the loop body waited for them --
+  // vmcnt(4) in the MFMAs, vmcnt(0) in the epilogue -- and so for most of the
+  // next tile's patch prefetch, every tile.)
+  stem_wait_vmcnt<0>();
   for (int t = t_begin; t < t_end; ++t) {
     // ---- stage the prefetched patch (the previous tile's MFMA reads ended at
     // its post-epilogue barrier)
+    if constexpr (kExactStores) {
+      if (t == t_begin) stem_wait_vmcnt<0>();
+      else stem_wait_vmcnt<SPT>();
+    }
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
       const int q = tid + s * 256;
@@ -207,16 +244,28 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
 #pragma unroll
     for (int i = 0; i < kRGW; ++i)
 #pragma unroll
-      for (int j = 0; j < NCG; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NCG; ++j) acc[i][j] = f32x4{bias[j].x, bias[j].y, bias[j].z, bias[j].w};   // bias in the accumulator
     const char* pb = reinterpret_cast<const char*>(patch);
+    // patch fragments read one filter row ahead, unconditionally (a wave's
+    // missing third row group reads a clamped pixel, never used): with the
+    // read inside each group's wave-uniform branch every group waited
+    // lgkmcnt(0) for its own read, 21 LDS round trips per tile
+    bf16x8 afr[2][kRGW];
+#pragma unroll
+    for (int i = 0; i < kRGW; ++i) afr[0][i] = *reinterpret_cast<const bf16x8*>(pb + size_t(aoff[i]) * 8);
 #pragma unroll
     for (int kh = 0; kh < kKSteps; ++kh) {
+      if (kh + 1 < kKSteps) {
+#pragma unroll
+        for (int i = 0; i < kRGW; ++i)
+          afr[(kh + 1) & 1][i] = *reinterpret_cast<const bf16x8*>(pb + size_t(aoff[i] + (kh + 1) * kIC) * 8);
+      }
 #pragma unroll
       for (int i = 0; i < kRGW; ++i) {
         if (wid + 4 * i >= kNRG || (dbg & 2)) continue;   // wave-uniform
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(pb + size_t(aoff[i] + kh * kIC) * 8);
 #pragma unroll
-        for (int j = 0; j < NCG; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kh][j], a, acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NCG; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kh][j], afr[kh & 1][i], acc[i][j], 0, 0, 0);
       }
     }
 
@@ -233,12 +282,13 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
       const bool in = (unsigned)(cy0 + pcy[i]) < (unsigned)p.Hc && (unsigned)(cx0 + pcx[i]) < (unsigned)p.Wc;
 #pragma unroll
       for (int j = 0; j < NCG; ++j) {
-        float v[4];
-        const float b[4] = {bias[j].x, bias[j].y, bias[j].z, bias[j].w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = in ? fmaxf(acc[i][j][r] + b[r], p.lo) : -INFINITY;
+        // keys of the biased conv values; -inf keys outside the conv output.
+        // The activation floor is applied after the max (max and ReLU
+        // commute; bf16 rounding is monotonic): ~10 fewer VALU ops per 4 values
+        const uint32_t k01 = okey(cvt2(acc[i][j][0], acc[i][j][1]));
+        const uint32_t k23 = okey(cvt2(acc[i][j][2], acc[i][j][3]));
         *reinterpret_cast<uint2*>(ctile + px * CS + j * 16 + fq * 4) =
-            make_uint2(okey(cvt2(v[0], v[1])), okey(cvt2(v[2], v[3])));
+            make_uint2(in ? k01 : kNegInfKey2, in ? k23 : kNegInfKey2);
       }
     }
     __syncthreads();
@@ -248,11 +298,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
     // pixels 2 apart (288 B = bank offset 8 for COUT 64), so 8 lanes x 16 B
     // cover all 64 banks; channel-chunk-fastest order had 2-way conflicts
     // (SQ_LDS_BANK_CONFLICT 2.1M cycles per launch at b32)
-    constexpr int C8 = COUT / 8;
-    for (int idx = tid; idx < kTPY * kTPX * C8 && !(dbg & 4); idx += 256) {
-      const int qx = idx % kTPX, c8 = (idx / kTPX) % C8, qy = idx / (kTPX * C8);
-      const int py = ty * kTPY + qy, px = tx * kTPX + qx;
-      if (py >= p.Hp || px >= p.Wp) continue;
+    auto pool_item = [&](int idx, bool out_ok, int qx, int c8, int qy, int py, int px) {
       const uint16_t* c0 = ctile + (2 * qy * kCC + 2 * qx) * CS + c8 * 8;
       uint4 m = *reinterpret_cast<const uint4*>(c0);
 #pragma unroll
@@ -260,6 +306,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
         const uint4 v = *reinterpret_cast<const uint4*>(c0 + ((tap / 3) * kCC + tap % 3) * CS);
         m = make_uint4(kmax(m.x, v.x), kmax(m.y, v.y), kmax(m.z, v.z), kmax(m.w, v.w));
       }
+      m = make_uint4(kmax(m.x, lokey), kmax(m.y, lokey), kmax(m.z, lokey), kmax(m.w, lokey));   // the conv's act
       uint32_t o[4] = {okey(m.x), okey(m.y), okey(m.z), okey(m.w)};
       if (p.pscale) {
 #pragma unroll
@@ -270,8 +317,31 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemArgs p) {
           o[e] = cvt2(lo, hi);
         }
       }
-      *reinterpret_cast<uint4*>(p.y + ((long(n) * p.Hp + py) * p.Wp + px) * COUT + c8 * 8) =
-          make_uint4(o[0], o[1], o[2], o[3]);
+      if constexpr (kExactStores) {
+        const uint32_t yoff = out_ok ? uint32_t(((long(n) * p.Hp + py) * p.Wp + px) * COUT + c8 * 8) * 2u : kOff;
+        __builtin_amdgcn_raw_buffer_store_b128(make_u32x4(o[0], o[1], o[2], o[3]), rsY, yoff, 0, 0);
+      } else {
+        *reinterpret_cast<uint4*>(p.y + ((long(n) * p.Hp + py) * p.Wp + px) * COUT + c8 * 8) =
+            make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    };
+    if constexpr (kExactStores) {
+      // exactly SPT items per thread, no branch around the stores (the wait
+      // count above relies on it; TFSK_STEM_DBG bit 2 does not apply here)
+#pragma unroll
+      for (int it = 0; it < SPT; ++it) {
+        const int idx = tid + it * 256;
+        const int qx = idx % kTPX, c8 = (idx / kTPX) % C8, qy = idx / (kTPX * C8);
+        const int py = ty * kTPY + qy, px = tx * kTPX + qx;
+        pool_item(idx, py < p.Hp && px < p.Wp, qx, c8, qy, py, px);
+      }
+    } else {
+      for (int idx = tid; idx < kItems && !(dbg & 4); idx += 256) {
+        const int qx = idx % kTPX, c8 = (idx / kTPX) % C8, qy = idx / (kTPX * C8);
+        const int py = ty * kTPY + qy, px = tx * kTPX + qx;
+        if (py >= p.Hp || px >= p.Wp) continue;
+        pool_item(idx, true, qx, c8, qy, py, px);
+      }
     }
     // the next iteration's barrier (after its patch store) orders these ctile
     // reads before its epilogue's writes
@@ -314,6 +384,7 @@ hipError_t stem_pool_launch(const void* x, bool x_bf16, const uint16_t* w, int l
   const long tiles = long(N) * a.tiles_y * a.tiles_x;
   if (tiles > (1L << 30)) return hipErrorInvalidValue;
   if (long(N) * H * W * C * (x_bf16 ? 2 : 4) >= 0x7fffffffL) return hipErrorInvalidValue;   // 32-bit buffer offsets
+  if (long(N) * Hp * Wp * cout * 2 >= 0x7fffffffL) return hipErrorInvalidValue;
   a.tiles = int(tiles);
   const int grid = int(tiles < 2L * cu_count() ? tiles : 2L * cu_count());
   if (x_bf16) {
