@@ -1,6 +1,8 @@
 // Memory-bound companion kernels (gfx950): pooling, classifier head, casts,
 // LayerNorm, embedding+LN.  All bf16 traffic is 16-B vectorised (8 elements
 // per lane), reductions are wave64 shuffles.
+#include <type_traits>
+
 #include "common.h"
 #include "gemm_common.h"
 #include "launch.h"
@@ -524,6 +526,25 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
   }
 }
 
+// Sum over aligned groups of LPR lanes, every lane of a group getting the
+// total: DPP lane swaps within 16-lane rows (quad xor 1 / 2, half-row mirror,
+// row mirror: a few cycles each) and ds_bpermute only across rows.  The
+// __shfl_xor butterfly was 5 LDS round trips per sum, each waited for alone.
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+  static_assert(LPR == 16 || LPR == 32 || LPR == 64, "lane group");
+  auto dpp = [](float x, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value, 0xf, 0xf, false));
+  };
+  v += dpp(v, std::integral_constant<int, 0xb1>{});    // quad_perm [1, 0, 3, 2]
+  v += dpp(v, std::integral_constant<int, 0x4e>{});    // quad_perm [2, 3, 0, 1]
+  v += dpp(v, std::integral_constant<int, 0x141>{});   // row_half_mirror: quad 0 <-> 1
+  v += dpp(v, std::integral_constant<int, 0x140>{});   // row_mirror: half-row 0 <-> 1
+  if constexpr (LPR >= 32) v += __shfl_xor(v, 16, 64);
+  if constexpr (LPR >= 64) v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
 // Exact-fit rows (cols == LPR * 8 * CH, e.g. BERT-base 768 = 32 lanes x 3
 // chunks): LPR lanes per row, 64 / LPR rows per wave, gamma / beta loaded into
 // registers before the row arrives (their latency hides under the row's), no
@@ -542,16 +563,26 @@ __global__ __launch_bounds__(256) void layernorm_fit_kernel(const uint16_t* __re
   // RG row groups per wave (TFSERVE_LN_RW): the gamma / beta registers serve
   // RG x RPW rows instead of RPW
   const int row0 = ((blockIdx.x * 4 + (threadIdx.x >> 6)) * RG) * RPW + sub;
+  // gamma / beta through buffer loads: plain loads of the restrict-const
+  // pointers were rematerialised by the register allocator next to their use,
+  // after the row reduction (one more serial round trip per row group)
   float g[CH][8], b[CH][8];
+  const __amdgpu_buffer_rsrc_t rsG =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gamma), 0, COLS * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(beta), 0, COLS * 4, 0x00020000);
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
-    const int c = (k * LPR + l) * 8;
-    const float4 g0 = *reinterpret_cast<const float4*>(gamma + c), g1 = *reinterpret_cast<const float4*>(gamma + c + 4);
-    const float4 b0 = *reinterpret_cast<const float4*>(beta + c), b1 = *reinterpret_cast<const float4*>(beta + c + 4);
-    g[k][0] = g0.x; g[k][1] = g0.y; g[k][2] = g0.z; g[k][3] = g0.w;
-    g[k][4] = g1.x; g[k][5] = g1.y; g[k][6] = g1.z; g[k][7] = g1.w;
-    b[k][0] = b0.x; b[k][1] = b0.y; b[k][2] = b0.z; b[k][3] = b0.w;
-    b[k][4] = b1.x; b[k][5] = b1.y; b[k][6] = b1.z; b[k][7] = b1.w;
+    const uint32_t c4 = uint32_t((k * LPR + l) * 8) * 4u;
+    const u32x4 g0 = __builtin_amdgcn_raw_buffer_load_b128(rsG, c4, 0, 0);
+    const u32x4 g1 = __builtin_amdgcn_raw_buffer_load_b128(rsG, c4 + 16u, 0, 0);
+    const u32x4 b0 = __builtin_amdgcn_raw_buffer_load_b128(rsB, c4, 0, 0);
+    const u32x4 b1 = __builtin_amdgcn_raw_buffer_load_b128(rsB, c4 + 16u, 0, 0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      g[k][e] = __uint_as_float(g0[e]); g[k][4 + e] = __uint_as_float(g1[e]);
+      b[k][e] = __uint_as_float(b0[e]); b[k][4 + e] = __uint_as_float(b1[e]);
+    }
   }
   // every row load (x chunks and residual chunks, all RG groups) in flight at
   // once: the residual goes through a buffer resource (0 records when there
@@ -560,6 +591,7 @@ __global__ __launch_bounds__(256) void layernorm_fit_kernel(const uint16_t* __re
   // memory round trips per row
   const __amdgpu_buffer_rsrc_t rsR = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(r), 0, r ? int(long(rows) * COLS * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(y, 0, int(long(rows) * COLS * 2), 0x00020000);
   uint4 xv[RG][CH];
   u32x4 rv[RG][CH];
   long base[RG];
@@ -593,25 +625,29 @@ __global__ __launch_bounds__(256) void layernorm_fit_kernel(const uint16_t* __re
         s += v[k][e];
       }
     }
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    s = group_sum<LPR>(s);
     const float mean = s * (1.f / COLS);
     float ss = 0.f;
 #pragma unroll
     for (int k = 0; k < CH; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) { const float d = v[k][e] - mean; ss += d * d; }
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    ss = group_sum<LPR>(ss);
     const float inv = rsqrtf(ss * (1.f / COLS) + eps);
-    // no early return for rows past the end: with one, the gamma/beta loads
-    // were sunk below it and issued only after the row reduction
+    // no branch around the stores (rows past the end store to an out-of-range
+    // offset, dropped): with `if (ok) store` the gamma / beta loads above were
+    // sunk into that branch -- issued after the row reduction, one more serial
+    // memory round trip (seen in the gfx950 ISA, scripts/isa_audit.py)
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       float o8[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) o8[e] = (v[k][e] - mean) * inv * g[k][e] + b[k][e];
-      if (ok[q]) *reinterpret_cast<uint4*>(y + base[q] + (k * LPR + l) * 8) = pack8(o8);
+      const uint4 pk = pack8(o8);
+      u32x4 pv;
+      pv.x = pk.x; pv.y = pk.y; pv.z = pk.z; pv.w = pk.w;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          pv, rsY, ok[q] ? uint32_t(base[q] + (k * LPR + l) * 8) * 2u : 0x80000000u, 0, 0);
     }
   }
 }
