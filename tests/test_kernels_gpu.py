@@ -925,6 +925,10 @@ STEM_CASES = [
     (2, 37, 53, 3, 32, (2, 3, 2, 3), (0, 1, 1, 1), "relu", False),     # odd sizes, partial tiles
     (1, 41, 29, 1, 48, (0, 0, 0, 0), (0, 0, 0, 0), "none", False),     # VALID conv + VALID pool, 1 channel
     (2, 64, 64, 4, 64, (3, 3, 3, 3), (1, 1, 1, 1), "relu", True),      # RGBA, symmetric pool padding
+    # COUT = 64 with partial pooled tiles: the exact-store path's out-of-range
+    # items go to a dropped offset (stem.hip kExactStores)
+    (2, 37, 53, 3, 64, (2, 3, 2, 3), (0, 1, 1, 1), "relu", False),
+    (1, 45, 71, 3, 64, (3, 3, 3, 3), (0, 1, 0, 1), "none", True),
 ]
 
 
