@@ -232,6 +232,24 @@ __global__ __launch_bounds__(256, 1) void conv_chain_kernel(ChainArgs p) {
   const uint32_t rb0 = uint32_t(((wn2 * G::WN2 + fr) * KT + ((fq ^ (fr & 7)) * 8)) * 2);
   const uint32_t rb1 = uint32_t(((wn2 * G::WN2 + fr) * KT + (((4 + fq) ^ (fr & 7)) * 8)) * 2);
   constexpr int S = G::S2;
+  // ---- epilogue-2 bias values of this lane's items, issued here so the
+  // ring's first wait covers them (plain loads of p.b2 were reloaded next to
+  // each store: one serial memory round trip per epilogue item, seen in the
+  // gfx950 ISA, scripts/isa_audit.py); buffer loads are not rematerialised
+  constexpr int CPR2 = G::UW2 / 8;                  // chunks per slab row (4 or 8)
+  constexpr int IT2 = 16 * CPR2 / 64;               // items per lane (1 or 2)
+  const __amdgpu_buffer_rsrc_t rsB2 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.b2), 0, N2 * 4, 0x00020000);
+  u32x4 b2v[G::U2][IT2][2];
+#pragma unroll
+  for (int c = 0; c < G::U2; ++c)
+#pragma unroll
+    for (int k = 0; k < IT2; ++k) {
+      const int cc = (lane + 64 * k) % CPR2;
+      const uint32_t n = uint32_t(wn2 * G::WN2 + c * G::UW2 + cc * 8);
+      b2v[c][k][0] = __builtin_amdgcn_raw_buffer_load_b128(rsB2, n * 4u, 0, 0);
+      b2v[c][k][1] = __builtin_amdgcn_raw_buffer_load_b128(rsB2, n * 4u + 16u, 0, 0);
+    }
   // ---- W2 ring prologue, once every wave is done with its slab (same region)
   __syncthreads();
 #pragma unroll
@@ -276,8 +294,8 @@ __global__ __launch_bounds__(256, 1) void conv_chain_kernel(ChainArgs p) {
 
   // ---- epilogue 2 (its slabs overlay the ring: every wave is done reading it)
   __syncthreads();
-  constexpr int CPR2 = G::UW2 / 8;                  // chunks per slab row (4 or 8)
-  constexpr int IT2 = 16 * CPR2 / 64;               // items per lane (1 or 2)
+  const __amdgpu_buffer_rsrc_t rsY2 =
+      __builtin_amdgcn_make_buffer_rsrc(p.y2, 0, int(long(M) * N2 * 2), 0x00020000);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -296,14 +314,16 @@ __global__ __launch_bounds__(256, 1) void conv_chain_kernel(ChainArgs p) {
         const float4 lo = *reinterpret_cast<const float4*>(src);
         const float4 hi = *reinterpret_cast<const float4*>(src + 4);
         const int n = wn2 * G::WN2 + c * G::UW2 + cc * 8;
-        const float4 b0 = *reinterpret_cast<const float4*>(p.b2 + n);
-        const float4 b1 = *reinterpret_cast<const float4*>(p.b2 + n + 4);
-        const uint4 ov = make_uint4(pack_bf16x2(fmaxf(lo.x + b0.x, p.lo2), fmaxf(lo.y + b0.y, p.lo2)),
-                                    pack_bf16x2(fmaxf(lo.z + b0.z, p.lo2), fmaxf(lo.w + b0.w, p.lo2)),
-                                    pack_bf16x2(fmaxf(hi.x + b1.x, p.lo2), fmaxf(hi.y + b1.y, p.lo2)),
-                                    pack_bf16x2(fmaxf(hi.z + b1.z, p.lo2), fmaxf(hi.w + b1.w, p.lo2)));
+        const u32x4 b0 = b2v[c][k][0], b1 = b2v[c][k][1];
+        auto f = [](uint32_t u) { return __uint_as_float(u); };
+        u32x4 ov;
+        ov.x = pack_bf16x2(fmaxf(lo.x + f(b0.x), p.lo2), fmaxf(lo.y + f(b0.y), p.lo2));
+        ov.y = pack_bf16x2(fmaxf(lo.z + f(b0.z), p.lo2), fmaxf(lo.w + f(b0.w), p.lo2));
+        ov.z = pack_bf16x2(fmaxf(hi.x + f(b1.x), p.lo2), fmaxf(hi.y + f(b1.y), p.lo2));
+        ov.w = pack_bf16x2(fmaxf(hi.z + f(b1.z), p.lo2), fmaxf(hi.w + f(b1.w), p.lo2));
         const int m = m0 + wm2 * 32 + i * 16 + rloc;
-        if (m < M) *reinterpret_cast<uint4*>(p.y2 + size_t(m) * N2 + n) = ov;
+        // unconditional store: rows past M go to a dropped out-of-range offset
+        __builtin_amdgcn_raw_buffer_store_b128(ov, rsY2, m < M ? (uint32_t(m) * N2 + uint32_t(n)) * 2u : kOOB, 0, 0);
       }
       __builtin_amdgcn_wave_barrier();
     }
