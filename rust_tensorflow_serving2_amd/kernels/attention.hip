@@ -181,11 +181,15 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   float sum = 0.f;
   bf16x8 pb[S / 32];                        // P^T B fragments, k-slot j -> tile 2ks + (j >> 2), r = j & 3
+  // exp(v - mx) as exp2(v log2e - mx log2e): one fma + v_exp_f32 per value
+  // (__expf is a subtract, a multiply and the v_exp)
+  constexpr float kLog2e = 1.4426950408889634f;
+  const float mxl = mx * kLog2e;
 #pragma unroll
   for (int ks = 0; ks < S / 32; ++ks) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float e = __expf(s[2 * ks + (j >> 2)][j & 3] - mx);
+      const float e = __builtin_amdgcn_exp2f(fmaf(s[2 * ks + (j >> 2)][j & 3], kLog2e, -mxl));
       sum += e;
       pb[ks][j] = static_cast<__bf16>(e);
     }
