@@ -183,17 +183,25 @@ __global__ __launch_bounds__(QB * 4) void attention_kernel(const uint16_t* __res
   bf16x8 pb[S / 32];                        // P^T B fragments, k-slot j -> tile 2ks + (j >> 2), r = j & 3
   // exp(v - mx) as exp2(v log2e - mx log2e): one fma + v_exp_f32 per value
   // (__expf is a subtract, a multiply and the v_exp)
+  // (pairs: the arguments and the running sum as packed fp32, v_pk_fma_f32 /
+  // v_pk_add_f32, two values per instruction)
   constexpr float kLog2e = 1.4426950408889634f;
   const float mxl = mx * kLog2e;
+  typedef __attribute__((ext_vector_type(2))) float f32x2;
+  f32x2 sum2 = {0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < S / 32; ++ks) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float e = __builtin_amdgcn_exp2f(fmaf(s[2 * ks + (j >> 2)][j & 3], kLog2e, -mxl));
-      sum += e;
-      pb[ks][j] = static_cast<__bf16>(e);
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 v = {s[2 * ks + (j >> 2)][j & 3], s[2 * ks + (j >> 2)][(j & 3) + 1]};
+      const f32x2 a = v * kLog2e - mxl;
+      const f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+      sum2 += e;
+      pb[ks][j] = static_cast<__bf16>(e.x);
+      pb[ks][j + 1] = static_cast<__bf16>(e.y);
     }
   }
+  sum = sum2.x + sum2.y;
   sum += __shfl_xor(sum, 16, 64);
   sum += __shfl_xor(sum, 32, 64);
   attn_stamp(trace, trace_cap, 2);          // scores + softmax done
