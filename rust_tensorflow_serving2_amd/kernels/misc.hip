@@ -149,8 +149,12 @@ __global__ __launch_bounds__(256) void gap_nhwc_kernel(const uint16_t* __restric
 // + LDS).  ArgMax ties resolve to the smallest index (TF semantics).
 // With `parts`, a logit is bias[c] + the sum of `nparts` split-K partial rows
 // (parts[p * part_stride + row * ld + c]): the classifier head's reduction.
-constexpr int kSmPer = 16;
-template <int NPARTS>
+// PER = register-tile logits per thread: 4 for rows of <= 1024 classes (the
+// ResNet head's 1001), so a thread issues 4 x (NPARTS + 1) loads instead of 16
+// x (NPARTS + 1) mostly-clamped duplicates (80 loads > the 63 vmcnt slots at
+// NPARTS = 4: the wave stalled on a second round trip).
+constexpr int kSmPer = 16, kSmPerSmall = 4;
+template <int NPARTS, int PER = kSmPer>
 __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restrict__ logits, int in_bf16,
                                                              float* __restrict__ probs,
                                                              int64_t* __restrict__ classes, int rows, int cols,
@@ -173,28 +177,28 @@ __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restr
     return in_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(logits)[long(row) * ld + c])
                    : static_cast<const float*>(logits)[long(row) * ld + c];
   };
-  float v[kSmPer];
+  float v[PER];
   float mx = -INFINITY;
   int arg = 0x7fffffff;
   // every load of the register tile issued before any compare: unconditional
   // loads of clamped columns, masked afterwards (`if (c < cols) x = load(c)`
   // compiled to one conditional block per k that waited for its loads, i.e.
-  // kSmPer serial memory round trips per row)
+  // PER serial memory round trips per row)
 #pragma unroll
-  for (int k = 0; k < kSmPer; ++k) {
+  for (int k = 0; k < PER; ++k) {
     const int c = k * 256 + tid;
     v[k] = load(c < cols ? c : cols - 1);
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int k = 0; k < kSmPer; ++k) {
+  for (int k = 0; k < PER; ++k) {
     const int c = k * 256 + tid;
     const float x = c < cols ? v[k] : -INFINITY;
     v[k] = x;
     if (c < cols && (x > mx || (x == mx && c < arg))) { mx = x; arg = c; }
   }
   // columns beyond the register tile (cols > 4096): strided tail, recomputed below
-  for (int c = kSmPer * 256 + tid; c < cols; c += 256) {
+  for (int c = PER * 256 + tid; c < cols; c += 256) {
     const float x = load(c);
     if (x > mx || (x == mx && c < arg)) { mx = x; arg = c; }
   }
@@ -214,22 +218,22 @@ __global__ __launch_bounds__(256) void softmax_argmax_kernel(const void* __restr
   }
   float s = 0.f;
 #pragma unroll
-  for (int k = 0; k < kSmPer; ++k) {
+  for (int k = 0; k < PER; ++k) {
     v[k] = (k * 256 + tid < cols) ? __expf(v[k] - mx) : 0.f;
     s += v[k];
   }
-  for (int c = kSmPer * 256 + tid; c < cols; c += 256) s += __expf(load(c) - mx);
+  for (int c = PER * 256 + tid; c < cols; c += 256) s += __expf(load(c) - mx);
   s = wave_sum(s);
   if (lane == 0) ssum[w] = s;
   __syncthreads();
   const float inv = 1.f / (ssum[0] + ssum[1] + ssum[2] + ssum[3]);
   if (probs) {
 #pragma unroll
-    for (int k = 0; k < kSmPer; ++k) {
+    for (int k = 0; k < PER; ++k) {
       const int c = k * 256 + tid;
       if (c < cols) probs[long(row) * cols + c] = v[k] * inv;
     }
-    for (int c = kSmPer * 256 + tid; c < cols; c += 256) probs[long(row) * cols + c] = __expf(load(c) - mx) * inv;
+    for (int c = PER * 256 + tid; c < cols; c += 256) probs[long(row) * cols + c] = __expf(load(c) - mx) * inv;
   }
   if (classes && tid == 0) classes[row] = arg;
 }
@@ -829,8 +833,13 @@ hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, 
                                  int cols, long ld, hipStream_t s) {
   if (rows <= 0) return hipSuccess;
   if (ld < cols) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(softmax_argmax_kernel<0>, dim3(rows), dim3(256), 0, s, logits, in_bf16, probs, classes, rows,
-                     cols, ld, static_cast<const float*>(nullptr), 0L, static_cast<const float*>(nullptr));
+  if (cols <= kSmPerSmall * 256)
+    hipLaunchKernelGGL((softmax_argmax_kernel<0, kSmPerSmall>), dim3(rows), dim3(256), 0, s, logits, in_bf16, probs,
+                       classes, rows, cols, ld, static_cast<const float*>(nullptr), 0L,
+                       static_cast<const float*>(nullptr));
+  else
+    hipLaunchKernelGGL(softmax_argmax_kernel<0>, dim3(rows), dim3(256), 0, s, logits, in_bf16, probs, classes, rows,
+                       cols, ld, static_cast<const float*>(nullptr), 0L, static_cast<const float*>(nullptr));
   return hipGetLastError();
 }
 
@@ -847,7 +856,7 @@ hipError_t softmax_argmax_launch(const void* logits, int in_bf16, float* probs, 
 //     (the split-K fixup's hand-off, kernels/gemm_common.h), and re-zeroes
 //     the counter for the next launch.
 constexpr int kHeadSmallM = 16, kHeadSmallHW = 64;
-template <int KSTEPS>
+template <int KSTEPS, int PER>
 __global__ __launch_bounds__(256) void head_small_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                          const float* __restrict__ bias, float* __restrict__ part,
                                                          float* __restrict__ probs, int64_t* __restrict__ classes,
@@ -879,9 +888,9 @@ __global__ __launch_bounds__(256) void head_small_kernel(const uint16_t* __restr
       bfr[t][j] = n < Np ? *reinterpret_cast<const bf16x8*>(w + long(n) * K + kbase + kl + t * 32 + fq * 8)
                          : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
-  float bv[kSmPer];
+  float bv[PER];
 #pragma unroll
-  for (int k = 0; k < kSmPer; ++k) {
+  for (int k = 0; k < PER; ++k) {
     const int c = k * 256 + tid;
     bv[k] = bias[c < N ? c : N - 1];
   }
@@ -969,11 +978,11 @@ __global__ __launch_bounds__(256) void head_small_kernel(const uint16_t* __restr
   __syncthreads();
   if (!s_last) return;
   for (int m = 0; m < M; ++m) {
-    float v[kSmPer];
+    float v[PER];
     float mx = -INFINITY;
     int arg = 0x7fffffff;
 #pragma unroll
-    for (int k = 0; k < kSmPer; ++k) {
+    for (int k = 0; k < PER; ++k) {
       const int c = k * 256 + tid, cc = c < N ? c : N - 1;
       float a = bv[k];
 #pragma unroll
@@ -998,7 +1007,7 @@ __global__ __launch_bounds__(256) void head_small_kernel(const uint16_t* __restr
     }
     float sum = 0.f;
 #pragma unroll
-    for (int k = 0; k < kSmPer; ++k) {
+    for (int k = 0; k < PER; ++k) {
       v[k] = (k * 256 + tid < N) ? __expf(v[k] - mx) : 0.f;
       sum += v[k];
     }
@@ -1007,7 +1016,7 @@ __global__ __launch_bounds__(256) void head_small_kernel(const uint16_t* __restr
     __syncthreads();
     const float inv = 1.f / (ssum[0] + ssum[1] + ssum[2] + ssum[3]);
 #pragma unroll
-    for (int k = 0; k < kSmPer; ++k) {
+    for (int k = 0; k < PER; ++k) {
       const int c = k * 256 + tid;
       if (c < N) {
         probs[long(m) * N + c] = v[k] * inv;
@@ -1040,15 +1049,19 @@ hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const fl
   if (counter != nullptr && classifier_head_one_launch(M, HW, K, Np, N)) {
     const dim3 grid(kHeadKS, (Np + kHeadCols - 1) / kHeadCols);
     const float inv_hw = 1.f / float(HW);
+    // the last workgroup's softmax tile: 4 logits per thread for N <= 1024
+    // (see softmax_argmax_kernel), 16 otherwise
+    const bool small = N <= kSmPerSmall * 256;
+#define TFSK_HEAD_SMALL(KS, PER)                                                                               \
+  hipLaunchKernelGGL((head_small_kernel<KS, PER>), grid, dim3(256), 0, s, x, w, bias, part, probs, classes,   \
+                     counter, M, HW, K, Np, N, inv_hw, probs_h, classes_h)
     switch (ksteps) {
-      case 1: hipLaunchKernelGGL(head_small_kernel<1>, grid, dim3(256), 0, s, x, w, bias, part, probs, classes,
-                                 counter, M, HW, K, Np, N, inv_hw, probs_h, classes_h); break;
-      case 2: hipLaunchKernelGGL(head_small_kernel<2>, grid, dim3(256), 0, s, x, w, bias, part, probs, classes,
-                                 counter, M, HW, K, Np, N, inv_hw, probs_h, classes_h); break;
-      case 4: hipLaunchKernelGGL(head_small_kernel<4>, grid, dim3(256), 0, s, x, w, bias, part, probs, classes,
-                                 counter, M, HW, K, Np, N, inv_hw, probs_h, classes_h); break;
+      case 1: if (small) TFSK_HEAD_SMALL(1, kSmPerSmall); else TFSK_HEAD_SMALL(1, kSmPer); break;
+      case 2: if (small) TFSK_HEAD_SMALL(2, kSmPerSmall); else TFSK_HEAD_SMALL(2, kSmPer); break;
+      case 4: if (small) TFSK_HEAD_SMALL(4, kSmPerSmall); else TFSK_HEAD_SMALL(4, kSmPer); break;
       default: return hipErrorInvalidValue;
     }
+#undef TFSK_HEAD_SMALL
     return hipGetLastError();
   }
   if (probs_h != nullptr || classes_h != nullptr) return hipErrorNotSupported;
@@ -1065,8 +1078,13 @@ hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const fl
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(softmax_argmax_kernel<kHeadKS>, dim3(M), dim3(256), 0, s, static_cast<const void*>(nullptr), 0,
-                     probs, classes, M, N, long(Np), static_cast<const float*>(part), long(M) * Np, bias);
+  if (N <= kSmPerSmall * 256)
+    hipLaunchKernelGGL((softmax_argmax_kernel<kHeadKS, kSmPerSmall>), dim3(M), dim3(256), 0, s,
+                       static_cast<const void*>(nullptr), 0, probs, classes, M, N, long(Np),
+                       static_cast<const float*>(part), long(M) * Np, bias);
+  else
+    hipLaunchKernelGGL(softmax_argmax_kernel<kHeadKS>, dim3(M), dim3(256), 0, s, static_cast<const void*>(nullptr),
+                       0, probs, classes, M, N, long(Np), static_cast<const float*>(part), long(M) * Np, bias);
   return hipGetLastError();
 }
 

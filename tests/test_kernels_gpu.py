@@ -558,7 +558,8 @@ def test_embedding_out_of_range_rows_are_zero(hd):
 
 
 @pytest.mark.parametrize("m,hw,k,np_,n", [(32, 49, 2048, 1001, 1001), (32, 49, 2048, 1008, 1001), (1, 49, 2048, 1001, 1001),
-                                         (3, 4, 512, 10, 10), (70, 9, 1024, 300, 257), (5, 1, 4096, 33, 33)])
+                                         (3, 4, 512, 10, 10), (70, 9, 1024, 300, 257), (5, 1, 4096, 33, 33),
+                                         (3, 4, 512, 2000, 1500)])   # > 1024 classes: the 16-per-thread softmax tile
 def test_classifier_head_matches_fp32(m, hw, k, np_, n):
     """mean_hw -> dense -> softmax/argmax in two launches (split-K partial rows,
     then bias + partial sums + softmax) vs fp32; rows in several 32-row chunks,
@@ -578,7 +579,8 @@ def test_classifier_head_matches_fp32(m, hw, k, np_, n):
 
 
 @pytest.mark.parametrize("m,hw,k,np_,n", [(1, 49, 2048, 1001, 1001), (2, 49, 2048, 1008, 1001), (4, 64, 1024, 300, 257),
-                                         (7, 3, 512, 10, 10), (16, 49, 2048, 1001, 1001)])
+                                         (7, 3, 512, 10, 10), (16, 49, 2048, 1001, 1001),
+                                         (2, 9, 512, 2000, 2000)])   # > 1024 classes: the 16-per-thread tile
 def test_classifier_head_one_launch_matches_three(monkeypatch, m, hw, k, np_, n):
     """The small-batch head (pool + dense + arrival-counter hand-off + softmax
     in ONE launch, misc.hip head_small_kernel) vs the three-launch head and
