@@ -294,7 +294,7 @@ __global__ __launch_bounds__(256) void gap_rows_kernel(const uint16_t* __restric
 
 // K slice = K / kHeadKS channels, split over the 4 waves (kw = K slice / 4 each,
 // a multiple of 32); a wave holds 2 x 2 16x16 accumulators (32 rows x 32 cols).
-template <int KSTEPS>
+template <int KSTEPS, int KS>
 __global__ __launch_bounds__(256) void fc_partial_kernel(const uint16_t* __restrict__ pooled,
                                                          const uint16_t* __restrict__ w, float* __restrict__ part,
                                                          int M, int K, int Np) {
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void fc_partial_kernel(const uint16_t* __restr
   const int ks = blockIdx.x, ns = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int kslice = K / kHeadKS, kw = kslice / 4;
+  const int kslice = K / KS, kw = kslice / 4;
   const int k0 = ks * kslice + wid * kw;
   const int n0 = ns * kHeadCols;
   // B fragments of this wave's K range: rows n0 + j*16 + fr (zero past Np)
@@ -1038,6 +1038,12 @@ bool classifier_head_one_launch(int M, int HW, int K, int Np, int N) {
   return M <= kHeadSmallM && HW <= kHeadSmallHW && N <= kSmPer * 256 && (ksteps == 1 || ksteps == 2 || ksteps == 4);
 }
 
+static int head_ks(int K) {   // read per launch (captured once into a graph; tests flip it)
+  const char* e = getenv("TFSERVE_HEAD_KS");
+  const int want = e && std::atoi(e) == 8 ? 8 : kHeadKS;
+  return (want == 2 * kHeadKS && K % (2 * kHeadKS * 4 * 32) == 0 && K / (2 * kHeadKS * 4 * 32) <= 4) ? want : kHeadKS;
+}
+
 hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const float* bias, float* ws, float* probs,
                                   int64_t* classes, int M, int HW, int K, int Np, int N, hipStream_t s,
                                   int* counter, float* probs_h, int64_t* classes_h) {
@@ -1068,28 +1074,47 @@ hipError_t classifier_head_launch(const uint16_t* x, const uint16_t* w, const fl
   hipLaunchKernelGGL(gap_rows_kernel, dim3(M, K / 64), dim3(256), 0, s, x, pooled, HW, K, 1.f / float(HW));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const dim3 grid(kHeadKS, (Np + kHeadCols - 1) / kHeadCols);
-  switch (ksteps) {
-    case 1: hipLaunchKernelGGL(fc_partial_kernel<1>, grid, dim3(256), 0, s, pooled, w, part, M, K, Np); break;
-    case 2: hipLaunchKernelGGL(fc_partial_kernel<2>, grid, dim3(256), 0, s, pooled, w, part, M, K, Np); break;
-    case 4: hipLaunchKernelGGL(fc_partial_kernel<4>, grid, dim3(256), 0, s, pooled, w, part, M, K, Np); break;
-    case 8: hipLaunchKernelGGL(fc_partial_kernel<8>, grid, dim3(256), 0, s, pooled, w, part, M, K, Np); break;
-    default: return hipErrorInvalidValue;
+  // K split: kHeadKS (4) slices, or 8 (TFSERVE_HEAD_KS=8, K a multiple of
+  // 1024) for twice the workgroups on the weight stream (A/B switch)
+  const int KS = head_ks(K);
+  const int ks_steps = K / KS / 4 / 32;
+  const dim3 grid(KS, (Np + kHeadCols - 1) / kHeadCols);
+#define TFSK_FC(T, KSV) hipLaunchKernelGGL((fc_partial_kernel<T, KSV>), grid, dim3(256), 0, s, pooled, w, part, M, K, Np)
+  if (KS == kHeadKS) {
+    switch (ks_steps) {
+      case 1: TFSK_FC(1, kHeadKS); break;
+      case 2: TFSK_FC(2, kHeadKS); break;
+      case 4: TFSK_FC(4, kHeadKS); break;
+      case 8: TFSK_FC(8, kHeadKS); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (ks_steps) {
+      case 1: TFSK_FC(1, 2 * kHeadKS); break;
+      case 2: TFSK_FC(2, 2 * kHeadKS); break;
+      case 4: TFSK_FC(4, 2 * kHeadKS); break;
+      default: return hipErrorInvalidValue;
+    }
   }
+#undef TFSK_FC
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (N <= kSmPerSmall * 256)
-    hipLaunchKernelGGL((softmax_argmax_kernel<kHeadKS, kSmPerSmall>), dim3(M), dim3(256), 0, s,
-                       static_cast<const void*>(nullptr), 0, probs, classes, M, N, long(Np),
-                       static_cast<const float*>(part), long(M) * Np, bias);
-  else
-    hipLaunchKernelGGL(softmax_argmax_kernel<kHeadKS>, dim3(M), dim3(256), 0, s, static_cast<const void*>(nullptr),
-                       0, probs, classes, M, N, long(Np), static_cast<const float*>(part), long(M) * Np, bias);
+#define TFSK_SM(NP, PER)                                                                                   \
+  hipLaunchKernelGGL((softmax_argmax_kernel<NP, PER>), dim3(M), dim3(256), 0, s,                          \
+                     static_cast<const void*>(nullptr), 0, probs, classes, M, N, long(Np),                \
+                     static_cast<const float*>(part), long(M) * Np, bias)
+  const bool small = N <= kSmPerSmall * 256;
+  if (KS == kHeadKS) {
+    if (small) TFSK_SM(kHeadKS, kSmPerSmall); else TFSK_SM(kHeadKS, kSmPer);
+  } else {
+    if (small) TFSK_SM(2 * kHeadKS, kSmPerSmall); else TFSK_SM(2 * kHeadKS, kSmPer);
+  }
+#undef TFSK_SM
   return hipGetLastError();
 }
 
 size_t classifier_head_ws_floats(int M, int K, int Np) {
-  return (size_t(M) * K + 1) / 2 + size_t(kHeadKS) * M * Np;   // bf16 pooled rows + f32 partials
+  return (size_t(M) * K + 1) / 2 + size_t(2 * kHeadKS) * M * Np;   // bf16 pooled rows + f32 partials (<= 8 slices)
 }
 
 hipError_t cast_f32_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t s) {

@@ -560,10 +560,14 @@ def test_embedding_out_of_range_rows_are_zero(hd):
 @pytest.mark.parametrize("m,hw,k,np_,n", [(32, 49, 2048, 1001, 1001), (32, 49, 2048, 1008, 1001), (1, 49, 2048, 1001, 1001),
                                          (3, 4, 512, 10, 10), (70, 9, 1024, 300, 257), (5, 1, 4096, 33, 33),
                                          (3, 4, 512, 2000, 1500)])   # > 1024 classes: the 16-per-thread softmax tile
-def test_classifier_head_matches_fp32(m, hw, k, np_, n):
+@pytest.mark.parametrize("head_ks", ["4", "8"])
+def test_classifier_head_matches_fp32(monkeypatch, head_ks, m, hw, k, np_, n):
     """mean_hw -> dense -> softmax/argmax in two launches (split-K partial rows,
     then bias + partial sums + softmax) vs fp32; rows in several 32-row chunks,
-    a weight matrix padded past the n classes read."""
+    a weight matrix padded past the n classes read.  TFSERVE_HEAD_KS=8 splits K
+    eight ways where K is a multiple of 1024 (four elsewhere)."""
+    monkeypatch.setenv("TFSERVE_HEAD_KS", head_ks)
+    monkeypatch.setenv("TFSERVE_HEAD_FUSED", "0")            # the three-launch path at every m
     x = rnd(m, hw, 1, k, seed=41).to(BF)
     w = rnd(np_, k, scale=0.05, seed=42).to(BF)
     b = rnd(np_, scale=0.1, seed=43)
